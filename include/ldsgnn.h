@@ -1,0 +1,171 @@
+/*
+ * ldsgnn.h — C-ABI of the MI355X-native LDS bilevel hot path.
+ *
+ * The reference (andreas-grafberger/lds-gnn) is pure Python/PyTorch and has no
+ * FFI: its "interface" for this path is a handful of Python functions whose
+ * dense ATen calls these entry points replace.  Each entry point below names
+ * the reference function (file:line under /root/reference) it stands in for.
+ *
+ * Conventions (every function):
+ *   - all array arguments are DEVICE pointers owned by the caller (PyTorch);
+ *     nothing is allocated inside, workspaces are passed in explicitly;
+ *   - `stream` is a hipStream_t passed as void*; NULL = the legacy stream;
+ *     every launch is asynchronous and graph-capturable (no host sync, no
+ *     hipMalloc, no memcpy to host);
+ *   - the return value is a hipError_t cast to int (0 = hipSuccess);
+ *     argument errors return hipErrorInvalidValue (1) before any launch;
+ *     lds_error_string() turns a code into text.
+ *   - θ ("theta") is the reference's BernoulliGraphModel.probs: the row-major
+ *     upper triangle INCLUDING the diagonal of an n×n matrix, n(n+1)/2 fp32
+ *     values (torch.triu_indices(n, n) order, src/utils/graph.py:41-45).
+ *     Index of (i, j), i <= j:  i*(2n - i + 1)/2 + (j - i).
+ *   - sampled graphs are exchanged as a symmetric bit matrix (`bits`,
+ *     n rows × `words` uint64, bit j%64 of word j/64 of row i = edge (i, j),
+ *     diagonal = self-loop set) and as CSR (row_ptr[n+1], col[nnz], int32,
+ *     columns ascending, self-loop included) plus s = deg^-1/2 (fp32).
+ */
+#ifndef LDSGNN_H
+#define LDSGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDS_ABI_VERSION 1
+
+/* ABI version of the loaded library (== LDS_ABI_VERSION). */
+int lds_abi_version(void);
+
+/* Text for a return code (hipGetErrorString). Never NULL. */
+const char* lds_error_string(int err);
+
+/* Number of uint64 words per bitmask row for n nodes (ceil(n/64) rounded up
+ * to an even count so every row starts 16-byte aligned). Host-only. */
+int lds_bitmask_words(int n);
+
+/* ---------------------------------------------------------------------------
+ * RNG contract.  All randomness on the path is counter-based Philox4x32-10:
+ *   key  = (seed & 0xffffffff, seed >> 32)
+ *   ctr  = (column, row >> 2, tag, counter)
+ *   u(row, column) = ((out[row & 3] >> 8) * 2^-24)        in [0, 1), exact fp32
+ * `tag` names the consumer (graph sample, dropout site, replica), `counter`
+ * the draw index.  The CPU oracle (oracle/philox.py) implements the same map.
+ * Writes u for a rows×cols row-major block (ld = cols).  Test hook.
+ * ------------------------------------------------------------------------- */
+int lds_philox_uniform(uint64_t seed, uint32_t tag, uint32_t counter,
+                       int rows, int cols, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Graph sampling.  Replaces
+ *   BernoulliGraphModel.forward -> triu_values_to_symmetric_matrix
+ *       (src/models/graph.py:66-67, src/utils/graph.py:166-181)
+ *   Sampler.sample -> sample_graph(undirected=True, NONE, dense=False)
+ *       (src/models/sampling.py:106-138, 47-79): Bernoulli(P).sample() over
+ *       the upper triangle, to_undirected(from_triu_only=True)
+ *       (src/utils/graph.py:27-38)
+ *   add_self_loops (src/utils/graph.py:123-133) — diagonal SET to 1.
+ * Edge (i, j), i < j, iff u(i, j) < clamp(theta_ij, 0, 1).  With `u_inject`
+ * non-NULL, u(i, j) = u_inject[i*n + j] (an n×n row-major fp32 array, e.g.
+ * torch.rand(n, n) — reproduces torch.bernoulli(P) bit-exactly).
+ * Writes the full symmetric `bits` (n × words); no memset needed.
+ * ------------------------------------------------------------------------- */
+int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint32_t tag,
+                       uint32_t counter, const float* u_inject,
+                       uint64_t* bits, int words, void* stream);
+
+/* Degree of every row of `bits` (self-loop included) and s = 1/sqrt(deg),
+ * i.e. the degree half of normalize_adjacency_matrix
+ * (src/utils/graph.py:146-149).  deg has n entries. */
+int lds_bitmask_degree(const uint64_t* bits, int n, int words, int* deg,
+                       float* s, void* stream);
+
+/* row_ptr[0] = 0, row_ptr[i+1] = row_ptr[i] + deg[i] (n+1 entries).
+ * Single-workgroup scan; n <= 2^24. */
+int lds_exclusive_scan(const int* deg, int n, int* row_ptr, void* stream);
+
+/* Column indices of every row of `bits`, ascending, at col[row_ptr[i]...].
+ * `col_capacity` bounds the writes (entries past it are dropped and
+ * *overflow is set to 1 when overflow != NULL). */
+int lds_bitmask_fill_csr(const uint64_t* bits, int n, int words,
+                         const int* row_ptr, int* col, int64_t col_capacity,
+                         int* overflow, void* stream);
+
+/* deg[i] = row_ptr[i+1] - row_ptr[i] and s = 1/sqrt(deg) for a CSR built
+ * elsewhere (e.g. a fixed dataset graph, src/scripts/gcn.py:78).  deg may be
+ * NULL. */
+int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* s,
+                         void* stream);
+
+/* The four launches above in order: sample -> degree/s -> scan -> fill.
+ * deg_ws: n ints of workspace. */
+int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32_t tag,
+                     uint32_t counter, const float* u_inject, uint64_t* bits,
+                     int words, int* deg_ws, int* row_ptr, int* col,
+                     int64_t col_capacity, int* overflow, float* s,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Normalised aggregation (the north-star kernel).  Replaces
+ *   torch.mm(normalize_adjacency_matrix(A), Z)
+ *       (src/models/layers.py:44 with src/utils/graph.py:136-153)
+ * Y[i, :f] = s_i * sum_{j in row i} s_j * Z[j, :f]   (beta = 0)
+ * Y[i, :f] += ...                                     (beta = 1)
+ * Â = diag(s)·Ã·diag(s) is symmetric, so the same call gives the backward
+ * dZ = Â·dY.  f <= 64.  z/y row strides ldz/ldy in elements.
+ * ------------------------------------------------------------------------- */
+int lds_spmm_norm(const int* row_ptr, const int* col, const float* s, int n,
+                  const float* z, int f, int ldz, float* y, int ldy, int beta,
+                  void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Hypergradient assembly.  Replaces the autograd of
+ *   normalize_adjacency_matrix -> straight_through_estimator ->
+ *   triu_values_to_symmetric_matrix w.r.t. BernoulliGraphModel.probs
+ *       (src/utils/graph.py:136-153, src/models/sampling.py:82-85,
+ *        src/utils/graph.py:166-181)
+ * For a cotangent dL/dÂ = sum_c G_c Z_cᵀ on one sampled graph, with
+ * U = s⊙[G_1|G_2|..], V = s⊙[Z_1|Z_2|..] (n×k, row stride ld) and
+ * R_i = sum_{c} r[i, c] (r: n×nr, row stride ldr; r_c,i = -½ s_i² (G_i·(ÂZ)_i + Z_i·(ÂG)_i)):
+ *   g_ij = mask_ij * ( U_i·V_j + V_i·U_j + R_i + R_j )   for i < j
+ *   g_ii = 0                                             (fill_diagonal_)
+ * mask_ij = (0 <= theta_ij <= 1) (clamp backward) when theta != NULL, else 1.
+ * accumulate = 0: grad = g;  accumulate = 1: grad += g.
+ * ------------------------------------------------------------------------- */
+int lds_theta_grad(const float* u, const float* v, int ld, int k,
+                   const float* r, int ldr, int nr, const float* theta, int n,
+                   float* grad, int accumulate, void* stream);
+
+/* Slot factors for lds_theta_grad from one aggregation Y = ÂZ and its
+ * cotangent G (dZ = ÂG):  U = s⊙G, V = s⊙Z, r = -½ s² (G·Y + Z·dZ) rowwise.
+ * Columns [f, fpad) of U and V are zero-filled. */
+int lds_slot_factors(const float* g, int ldg, const float* z, int ldz,
+                     const float* y, int ldy, const float* dz, int lddz,
+                     const float* s, int n, int f, int fpad, float* u, int ldu,
+                     float* v, int ldv, float* r, int ldr, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Outer update.  Replaces SGD.step (no momentum) + ParameterClamper
+ *   (src/trainers/outer.py:78-83, src/models/graph.py:16-20, 63-64):
+ *   theta = clamp(theta - lr * grad, 0, 1)
+ * ------------------------------------------------------------------------- */
+int lds_sgd_clamp(float* theta, const float* grad, float lr, int64_t count,
+                  void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Keyed dropout.  Replaces F.dropout (src/models/gcn.py:27,29):
+ *   y = x * (u(i, j) < 1 - p ? 1/(1-p) : 0)     element (i, j) of a rows×cols
+ * block (row strides ldx, ldy).  Linear in x, so the same call with the same
+ * key is its own backward.  `scale` = float(1) / float(1 - p).
+ * ------------------------------------------------------------------------- */
+int lds_dropout(const float* x, int ldx, float* y, int ldy, int rows, int cols,
+                float keep_prob, float scale, uint64_t seed, uint32_t tag,
+                uint32_t counter, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LDSGNN_H */

@@ -1,0 +1,256 @@
+// Graph sampling: θ (packed triu) -> symmetric bitmask -> degree / s -> CSR.
+//
+// Replaces, for the LDS configuration (undirected=True, sparsification NONE,
+// dense=False), the dense chain
+//   triu_values_to_symmetric_matrix   src/utils/graph.py:166-181
+//   Bernoulli(probs=P).sample()       src/models/sampling.py:68
+//   to_undirected(from_triu_only)     src/utils/graph.py:35-37
+//   add_self_loops + degree           src/utils/graph.py:123-149
+// which the reference runs over all N² entries with four dense temporaries.
+// Here θ is read once, the graph is born as a 1-bit-per-pair symmetric mask
+// (N²/8 bytes) and compacted into CSR; P is never materialised.
+#include "common.hpp"
+#include "../../include/ldsgnn.h"
+
+namespace lds {
+
+// One wave per 64×64 tile (bi <= bj) of the upper triangle.  Lane l owns
+// column j = 64*bj + l; the wave walks the tile's 64 rows four at a time (one
+// Philox call yields the four rows' uniforms for that column).  Row words come
+// out of __ballot, the transposed (lower-triangle) words accumulate one bit
+// per row in each lane: every word of `bits` has exactly one writer, so the
+// kernel needs neither atomics nor a memset.
+__global__ __launch_bounds__(256) void sample_tiles_kernel(
+    const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
+    uint32_t counter, const float* __restrict__ u_inj, uint64_t* __restrict__ bits,
+    int words, int ntiles) {
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;  // wave-uniform
+    const int lane = wave_lane();
+    int a, b;
+    tri_tile(tile, a, b);
+    const int bi = b, bj = a;  // bi <= bj
+    const int j = bj * 64 + lane;
+    const bool diag_tile = (bi == bj);
+    const int64_t nn = n;
+
+    uint64_t colword = 0, myrow = 0;
+    for (int q = 0; q < 16; ++q) {
+        const int i0 = bi * 64 + 4 * q;
+        if (i0 >= n) break;  // wave-uniform
+        float u[4];
+        if (u_inj != nullptr) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + r;
+                u[r] = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
+            }
+        } else {
+            philox_quad(k0, k1, tag, counter, (uint32_t)j, (uint32_t)(i0 >> 2), u);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + r;
+            bool e = false;
+            if (i < j && j < n) {  // i < n follows from i < j < n
+                float t = theta[tri_index(i, j, nn)];
+                t = fminf(fmaxf(t, 0.0f), 1.0f);  // clamp(0, 1), src/utils/graph.py:180
+                e = u[r] < t;
+            }
+            const uint64_t w = __ballot(e);
+            if (i < n) {
+                if (!diag_tile) {
+                    if (lane == 0) bits[(int64_t)i * words + bj] = w;
+                } else if (lane == i - bi * 64) {
+                    myrow = w;
+                }
+            }
+            if (e) colword |= 1ull << (i - bi * 64);
+        }
+    }
+    if (j < n) {
+        uint64_t out = colword;
+        if (diag_tile) out |= myrow | (1ull << lane);  // self-loop: diagonal set to 1
+        bits[(int64_t)j * words + bi] = out;
+    }
+}
+
+// One wave per row: popcount of the row's words.
+__global__ __launch_bounds__(256) void degree_kernel(const uint64_t* __restrict__ bits, int n,
+                                                      int words, int* __restrict__ deg,
+                                                      float* __restrict__ s) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = wave_lane();
+    const int nbw = (n + 63) / 64;
+    const uint64_t* rb = bits + (int64_t)row * words;
+    int c = 0;
+    for (int w = lane; w < nbw; w += 64) c += __popcll(rb[w]);
+    c = wave_sum(c);
+    if (lane == 0) {
+        deg[row] = c;
+        s[row] = inv_sqrt_degree(c);
+    }
+}
+
+// Single-workgroup exclusive scan of n ints into n+1 row pointers.
+__global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ deg, int n,
+                                                     int* __restrict__ row_ptr) {
+    __shared__ int partial[1024];
+    const int t = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int beg = min(n, t * per), end = min(n, beg + per);
+    int sum = 0;
+    for (int i = beg; i < end; ++i) sum += deg[i];
+    partial[t] = sum;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over the 1024 thread totals.
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? partial[t - o] : 0;
+        __syncthreads();
+        partial[t] += v;
+        __syncthreads();
+    }
+    int run = t > 0 ? partial[t - 1] : 0;
+    for (int i = beg; i < end; ++i) {
+        row_ptr[i] = run;
+        run += deg[i];
+    }
+    if (t == 1023) row_ptr[n] = partial[1023];
+}
+
+// One wave per row: ascending column indices of the set bits.
+__global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restrict__ bits, int n,
+                                                        int words, const int* __restrict__ row_ptr,
+                                                        int* __restrict__ col, int64_t capacity,
+                                                        int* __restrict__ overflow) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = wave_lane();
+    const int nbw = (n + 63) / 64;
+    const uint64_t* rb = bits + (int64_t)row * words;
+    int64_t base = row_ptr[row];
+    bool over = false;
+    for (int w0 = 0; w0 < nbw; w0 += 64) {
+        const int w = w0 + lane;
+        uint64_t word = w < nbw ? rb[w] : 0ull;
+        const int cnt = __popcll(word);
+        // inclusive wave scan of cnt
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        int64_t pos = base + (incl - cnt);
+        while (word) {
+            const int bit = __ffsll((unsigned long long)word) - 1;
+            if (pos < capacity) col[pos] = w * 64 + bit;
+            else over = true;
+            ++pos;
+            word &= word - 1;
+        }
+        base += __shfl(incl, 63);
+    }
+    if (over && overflow != nullptr) *overflow = 1;
+}
+
+__global__ void csr_degree_scale_kernel(const int* __restrict__ row_ptr, int n,
+                                        int* __restrict__ deg, float* __restrict__ s) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int d = row_ptr[i + 1] - row_ptr[i];
+    if (deg != nullptr) deg[i] = d;
+    s[i] = inv_sqrt_degree(d);
+}
+
+__global__ void philox_uniform_kernel(uint32_t k0, uint32_t k1, uint32_t tag, uint32_t counter,
+                                      int rows, int cols, float* __restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int rq = blockIdx.y;
+    if (j >= cols) return;
+    float u[4];
+    philox_quad(k0, k1, tag, counter, (uint32_t)j, (uint32_t)rq, u);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = rq * 4 + r;
+        if (i < rows) out[(int64_t)i * cols + j] = u[r];
+    }
+}
+
+}  // namespace lds
+
+using namespace lds;
+
+extern "C" int lds_bitmask_words(int n) {
+    int w = (n + 63) / 64;
+    return (w + 1) & ~1;
+}
+
+extern "C" int lds_philox_uniform(uint64_t seed, uint32_t tag, uint32_t counter, int rows,
+                                  int cols, float* out, void* stream) {
+    LDS_CHECK_ARG(rows > 0 && cols > 0 && out != nullptr && rows <= 4 * 65535);
+    dim3 grid((cols + 255) / 256, (rows + 3) / 4);
+    hipLaunchKernelGGL(philox_uniform_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter, rows, cols, out);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint32_t tag,
+                                  uint32_t counter, const float* u_inject, uint64_t* bits,
+                                  int words, void* stream) {
+    LDS_CHECK_ARG(theta != nullptr && bits != nullptr && n > 0 && n <= (1 << 20));
+    LDS_CHECK_ARG(words >= (n + 63) / 64);
+    const int nb = (n + 63) / 64;
+    const int ntiles = nb * (nb + 1) / 2;
+    hipLaunchKernelGGL(sample_tiles_kernel, dim3((ntiles + 3) / 4), dim3(256), 0,
+                       (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                       counter, u_inject, bits, words, ntiles);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_bitmask_degree(const uint64_t* bits, int n, int words, int* deg, float* s,
+                                  void* stream) {
+    LDS_CHECK_ARG(bits != nullptr && deg != nullptr && s != nullptr && n > 0);
+    LDS_CHECK_ARG(words >= (n + 63) / 64);
+    hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, bits,
+                       n, words, deg, s);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_exclusive_scan(const int* deg, int n, int* row_ptr, void* stream) {
+    LDS_CHECK_ARG(deg != nullptr && row_ptr != nullptr && n > 0 && n <= (1 << 24));
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, deg, n, row_ptr);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_bitmask_fill_csr(const uint64_t* bits, int n, int words, const int* row_ptr,
+                                    int* col, int64_t col_capacity, int* overflow,
+                                    void* stream) {
+    LDS_CHECK_ARG(bits != nullptr && row_ptr != nullptr && col != nullptr && n > 0);
+    LDS_CHECK_ARG(words >= (n + 63) / 64 && col_capacity >= 0);
+    hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                       bits, n, words, row_ptr, col, col_capacity, overflow);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* s,
+                                    void* stream) {
+    LDS_CHECK_ARG(row_ptr != nullptr && s != nullptr && n > 0);
+    hipLaunchKernelGGL(csr_degree_scale_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                       (hipStream_t)stream, row_ptr, n, deg, s);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32_t tag,
+                                uint32_t counter, const float* u_inject, uint64_t* bits, int words,
+                                int* deg_ws, int* row_ptr, int* col, int64_t col_capacity,
+                                int* overflow, float* s, void* stream) {
+    int e = lds_sample_bitmask(theta, n, seed, tag, counter, u_inject, bits, words, stream);
+    if (e) return e;
+    e = lds_bitmask_degree(bits, n, words, deg_ws, s, stream);
+    if (e) return e;
+    e = lds_exclusive_scan(deg_ws, n, row_ptr, stream);
+    if (e) return e;
+    return lds_bitmask_fill_csr(bits, n, words, row_ptr, col, col_capacity, overflow, stream);
+}

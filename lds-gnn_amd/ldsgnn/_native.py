@@ -1,0 +1,96 @@
+"""ctypes binding of the C-ABI hot-path library (include/ldsgnn.h).
+
+The library is built in-tree (lds-gnn_amd/csrc/Makefile -> ldsgnn/libldsgnn.so)
+and loaded AFTER torch so that it binds to the HIP runtime torch already
+loaded (same SONAME libamdhip64.so.7): our kernels then run on torch's
+streams and inside torch's HIP graphs.  There is no fallback: if the library
+is missing, importing ldsgnn raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
+ABI_VERSION = 1
+
+c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
+    ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
+P = c_void_p  # device pointers travel as integers
+
+# name -> argtypes (restype is always int = hipError_t, except where noted)
+SIGNATURES = {
+    "lds_abi_version": [],
+    "lds_bitmask_words": [c_int],
+    "lds_philox_uniform": [c_uint64, c_uint32, c_uint32, c_int, c_int, P, P],
+    "lds_sample_bitmask": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P],
+    "lds_bitmask_degree": [P, c_int, c_int, P, P, P],
+    "lds_exclusive_scan": [P, c_int, P, P],
+    "lds_bitmask_fill_csr": [P, c_int, c_int, P, P, c_int64, P, P],
+    "lds_csr_degree_scale": [P, c_int, P, P, P],
+    "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
+                         P, P],
+    "lds_spmm_norm": [P, P, P, c_int, P, c_int, c_int, P, c_int, c_int, P],
+    "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
+    "lds_slot_factors": [P, c_int, P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, P, c_int, P,
+                         c_int, P, c_int, P],
+    "lds_sgd_clamp": [P, P, c_float, c_int64, P],
+    "lds_dropout": [P, c_int, P, c_int, c_int, c_int, c_float, c_float, c_uint64, c_uint32, c_uint32,
+                    P],
+}
+
+
+class NativeError(RuntimeError):
+    """A hot-path entry point returned a HIP error."""
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"ldsgnn native library not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (make -C lds-gnn_amd/csrc). "
+            "There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    lib.lds_error_string.argtypes = [c_int]
+    lib.lds_error_string.restype = ctypes.c_char_p
+    v = lib.lds_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"libldsgnn ABI {v} != expected {ABI_VERSION}; rebuild")
+    return lib
+
+
+lib = _load()
+
+
+def check(err: int, what: str = "") -> None:
+    if err != 0:
+        msg = lib.lds_error_string(err).decode(errors="replace")
+        raise NativeError(f"{what or 'ldsgnn'} failed: hip error {err} ({msg})")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib, name)(*args), name)
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return 0
+    return t.data_ptr()
+
+
+def stream_of(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"ldsgnn {what}: tensors must live on a HIP device (got {t.device}); "
+            "the hot path has no CPU implementation")

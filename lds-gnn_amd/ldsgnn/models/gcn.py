@@ -1,0 +1,64 @@
+"""2-layer dense-API GCN (src/models/gcn.py:9-34).
+
+forward(x, graph, params) = log_softmax(Â·(drop(relu(Â·(drop(x)W0ᵀ + b0)))W1ᵀ + b1))
+
+With a hot-path graph (ldsgnn.ops.CsrGraph / SampledGraph) normalisation is
+implicit in the graph (s = deg^-1/2, self-loops set) and both aggregations run
+on the lds_spmm_norm HIP kernel; dropout is keyed (ldsgnn.rng) and runs on the
+lds_dropout kernel.  A dense tensor graph keeps the reference semantics
+(normalize_adjacency_matrix + torch.mm) on its device.
+"""
+from __future__ import annotations
+
+import torch.nn.functional as F
+
+from .. import rng as _rng
+from ..ops import CsrGraph, keyed_dropout
+from ..utils.graph import normalize_adjacency_matrix
+from .layers import MetaDenseGraphConvolution
+from .meta import MetaModule, get_subdict
+
+
+class MetaDenseGCN(MetaModule):
+
+    def __init__(self, in_features, hidden_features, out_features, dropout, normalize_adj: bool = True,
+                 generator: "_rng.Generator" = None):
+        super().__init__()
+        self.layer_in = MetaDenseGraphConvolution(in_features, hidden_features)
+        self.layer_out = MetaDenseGraphConvolution(hidden_features, out_features)
+        self.dropout = dropout
+        self.normalize_adj = normalize_adj
+        self.generator = generator  # None -> ldsgnn.rng.default_generator
+
+    def reset_weights(self):
+        self.layer_in.reset_weights()
+        self.layer_out.reset_weights()
+
+    def _dropout_keys(self):
+        if not self.training or self.dropout == 0.0:
+            return None, None
+        gen = self.generator or _rng.default_generator
+        c = gen.next_forward()
+        return gen.dropout_key(_rng.TAG_DROP_X, c), gen.dropout_key(_rng.TAG_DROP_H, c)
+
+    def _drop(self, x, key):
+        if key is None:
+            return x
+        return keyed_dropout(x, self.dropout, key)  # HIP kernel; raises for CPU tensors
+
+    def forward_to_last_layer(self, node_features, dense_adj, params=None):
+        if isinstance(dense_adj, CsrGraph):
+            if not self.normalize_adj:
+                raise NotImplementedError("hot-path graphs are normalised by construction "
+                                          "(normalize_adj=False needs a dense graph)")
+        elif self.normalize_adj:
+            dense_adj = normalize_adjacency_matrix(dense_adj)
+        kx, kh = self._dropout_keys()
+        embeddings = self._drop(node_features, kx)
+        embeddings = F.relu(self.layer_in(embeddings, dense_adj, params=get_subdict(params, "layer_in")))
+        embeddings = self._drop(embeddings, kh)
+        return self.layer_out(embeddings, dense_adj, params=get_subdict(params, "layer_out"))
+
+    def forward(self, node_features, dense_adj, params=None):
+        embeddings = self.forward_to_last_layer(node_features, dense_adj, params=params)
+        return F.log_softmax(embeddings, dim=1)

@@ -1,0 +1,101 @@
+"""Outer problem: the hypergradient step on θ (src/trainers/outer.py:19-129).
+
+`train_step` samples a fresh graph, predicts with the inner model's current
+(differentiable) parameters, and backpropagates the NLL on `opt_mask` through
+the outer graph and every unrolled inner step since the last detach.  The
+θ-gradient arrives through the sampled graphs' tokens (ldsgnn.ops), assembled
+by the lds_theta_grad HIP kernel; then SGD → StepLR → clamp as the reference.
+Regularisation / refinement / pre-training branches are out of scope
+(defaults off for LDS, src/trainers/outer.py:121-129 — pretrain is "next").
+"""
+from __future__ import annotations
+
+from typing import Callable, List
+
+import torch.nn.functional as F
+from torch import Tensor
+from torch.optim.lr_scheduler import StepLR
+from torch.optim.optimizer import Optimizer
+
+from ..models.graph import GraphGenerativeModel
+from ..utils.evaluation import accuracy
+from . import Metrics
+
+
+def get_lr(optimizer: Optimizer) -> List[float]:
+    """src/utils/tracking.py:54-55"""
+    return [group["lr"] for group in optimizer.param_groups]
+
+
+class OuterProblemTrainer:
+
+    def __init__(self, optimizer: Optimizer, data, opt_mask: Tensor, model: GraphGenerativeModel,
+                 smoothness_factor: float = 0.0, disconnection_factor: float = 0.0,
+                 sparsity_factor: float = 0.0, regularize: bool = False, lr_decay: float = None,
+                 lr_decay_step_size: int = 1, refine_embeddings: bool = False, pretrain: bool = False):
+        if regularize:
+            raise NotImplementedError("graph regularisation is outside the LDS hot path (default off)")
+        if pretrain:
+            raise NotImplementedError("θ pre-training is not implemented yet (SURVEY §8(f)3)")
+        self.lr_decay = lr_decay
+        self.lr_decay_step_size = lr_decay_step_size
+        self.dataset = data
+        self.opt_mask = opt_mask
+        self.model = model
+        self.regularize = regularize
+        self.smoothness_factor = smoothness_factor
+        self.disconnection_factor = disconnection_factor
+        self.sparsity_factor = sparsity_factor
+        self.optimizer: Optimizer = optimizer
+        self.lr_decayer = StepLR(self.optimizer, step_size=self.lr_decay_step_size,
+                                 gamma=self.lr_decay) if self.lr_decay is not None else None
+        self.refine_embeddings = refine_embeddings
+
+    def train_step(self, gcn_predict_fct: Callable, mask: Tensor = None,
+                   retain_graph: bool = True) -> Metrics:
+        self.model.train()
+        self.optimizer.zero_grad()
+        graph = self.model.sample()
+        predictions = gcn_predict_fct(graph)
+        mask = mask if mask is not None else self.opt_mask
+        loss = F.nll_loss(predictions[mask], self.dataset.y[mask])
+        acc = accuracy(predictions[mask], self.dataset.y[mask])
+        loss.backward(retain_graph=retain_graph)
+        self.optimizer.step()
+        if self.lr_decayer is not None:
+            self.lr_decayer.step()
+        self.model.project_parameters()
+        if self.refine_embeddings:
+            self.model.refine()
+        return Metrics(loss=loss.item(), acc=acc)
+
+    def sample(self):
+        return self.model.sample()
+
+    def detach(self):
+        self.model.load_state_dict(self.model.state_dict())
+        self.optimizer.load_state_dict(self.optimizer.state_dict())
+
+    def get_learning_rates(self) -> List[float]:
+        if self.optimizer is None:
+            raise ValueError("Can't get optimizer learning rate, no optimizer initialized yet.")
+        return get_lr(self.optimizer)
+
+    def train(self, mode: bool = True):
+        self.model.train(mode=mode)
+
+    def eval(self):
+        self.model.eval()
+
+
+class OuterProblemTrainerFactory:
+    """Defaults of the sacred ingredient (src/trainers/outer.py:120-129),
+    with pretrain off (not implemented yet)."""
+    config = dict(lr_decay=1.0, lr_decay_step_size=1, refine_embeddings=False, pretrain=False,
+                  regularize=False, smoothness_factor=0.0, disconnection_factor=0.0, sparsity_factor=0.0)
+
+    @staticmethod
+    def trainer(optimizer, data, opt_mask, model, **overrides) -> OuterProblemTrainer:
+        cfg = dict(OuterProblemTrainerFactory.config)
+        cfg.update(overrides)
+        return OuterProblemTrainer(optimizer=optimizer, data=data, opt_mask=opt_mask, model=model, **cfg)

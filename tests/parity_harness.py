@@ -1,0 +1,87 @@
+"""Test infrastructure: run the product (ldsgnn on cuda:0) and the CPU oracle
+on the same seeded synthetic LDS problem and report the largest differences.
+Used by tests/ and __graft_entry__.smoke()."""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from oracle import lds_oracle as O
+
+
+def synthetic_problem(n: int, f_in: int, classes: int, seed: int, p_edge: float = 0.05):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(n, f_in, generator=g) * (torch.rand(n, f_in, generator=g) < 0.3)
+    x = x / x.sum(1, keepdim=True).clamp(min=1e-12)  # NormalizeFeatures
+    y = torch.randint(0, classes, (n,), generator=g)
+    perm = torch.randperm(n, generator=g)
+    ntr, nva = max(2, n // 5), max(2, (3 * n) // 10)
+    masks = []
+    for idx in (perm[:ntr], perm[ntr:ntr + nva // 2], perm[ntr + nva // 2:ntr + nva], perm[ntr + nva:]):
+        m = torch.zeros(n, dtype=torch.bool)
+        m[idx] = True
+        masks.append(m)
+    train, val, opt, test = masks
+    a = (torch.rand(n, n, generator=g) < p_edge).float().triu(1)
+    adj = a + a.t()
+    return dict(x=x, y=y, train=train, val=val, opt=opt, test=test, adj=adj)
+
+
+def build_product(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1,
+                  lr_decay=0.99, seed=0, device="cuda"):
+    import ldsgnn
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from ldsgnn.models.graph import BernoulliGraphModel
+    from ldsgnn.trainers.bilevel import BilevelProblemRunner
+    from ldsgnn.trainers.inner import InnerProblemTrainer
+    from ldsgnn.trainers.outer import OuterProblemTrainer
+    from ldsgnn.utils.graph import DenseData
+
+    data = DenseData(x=prob["x"], y=prob["y"], dense_adj=prob["adj"], train_mask=prob["train"],
+                     val_mask=prob["val"], test_mask=prob["test"],
+                     num_classes=int(prob["y"].max()) + 1).to(device)
+    ldsgnn.rng.manual_seed(seed, 0)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.num_features, hidden, data.num_classes, dropout=dropout).to(device)
+    inner = InnerProblemTrainer(gcn, data, lr=gcn_lr, weight_decay=gcn_wd)
+    gm = BernoulliGraphModel(data.dense_adj)
+    opt = torch.optim.SGD(gm.parameters(), lr=outer_lr)
+    outer = OuterProblemTrainer(opt, data, prob["opt"].to(device), gm, lr_decay=lr_decay)
+    runner = BilevelProblemRunner(inner, outer, data)
+    return runner
+
+
+def build_oracle(prob, runner, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1,
+                 lr_decay=0.99, seed=0):
+    params = OrderedDict((k, v.detach().cpu()) for k, v in runner.inner_trainer.model_params.items())
+    theta = O.get_triu_values(prob["adj"])
+    return O.LdsProblem(prob["x"], prob["y"], prob["train"], prob["val"], prob["test"], prob["opt"],
+                        theta, hidden=hidden, dropout_p=dropout, gcn_lr=gcn_lr, gcn_wd=gcn_wd,
+                        outer_lr=outer_lr, lr_decay=lr_decay, rnd=O.Randomness(seed, 0), params=params)
+
+
+def run_product_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5, seed=0,
+                           hidden=16, p_edge=0.05):
+    prob = synthetic_problem(n, f_in, classes, seed, p_edge)
+    runner = build_product(prob, hidden=hidden, dropout=dropout, seed=seed)
+    oracle = build_oracle(prob, runner, hidden=hidden, dropout=dropout, seed=seed)
+    p_losses, o_losses, p_outer, o_outer = [], [], [], []
+    for step in range(steps):
+        p_losses.append(runner.inner_opt_step().loss)
+        o_losses.append(oracle.inner_step(oracle.sample())[0])
+        if tau == 0 or step % tau == 0:
+            p_outer.append(runner.hyper_opt_step(step).loss)
+            o_outer.append(oracle.hyper_step()[0])
+    theta_p = runner.outer_trainer.model.probs.detach().cpu()
+    theta_o = oracle.theta.detach()
+    perr = max(float((a.detach().cpu() - b.detach()).abs().max())
+               for a, b in zip(runner.inner_trainer.model_params.values(), oracle.params.values()))
+    return dict(
+        max_theta_err=float((theta_p - theta_o).abs().max()),
+        max_param_err=perr,
+        max_loss_err=float(np.max(np.abs(np.array(p_losses + p_outer) - np.array(o_losses + o_outer)))),
+        theta_changed=float((theta_o - O.get_triu_values(prob["adj"])).abs().max()),
+        losses=p_losses, outer=p_outer,
+    )

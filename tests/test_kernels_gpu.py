@@ -1,0 +1,192 @@
+"""Kernel-level parity of the HIP hot path against the CPU oracle.
+
+Bit-exact for integer / index / RNG work (Philox uniforms, sampled edge sets,
+CSR, degrees, s = deg^-1/2, dropout masks); fp32 kernels within the tolerance
+BASELINE.json's north_star states (1e-5), stated per test.
+"""
+import numpy as np
+import pytest
+import torch
+
+import ldsgnn
+from ldsgnn import _native as nat
+from ldsgnn import ops
+from ldsgnn.rng import Generator, TAG_GRAPH, tag_for
+from oracle import philox
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def expected_graph(theta_np: np.ndarray, n: int, u: np.ndarray):
+    """Oracle: A_ij = u_ij < clamp(θ_ij) for i < j, symmetric, self-loops set."""
+    iu = np.triu_indices(n)
+    p = np.zeros((n, n), dtype=np.float32)
+    p[iu] = np.clip(theta_np, 0.0, 1.0)
+    a = (u < p)
+    a = np.triu(a, 1)
+    a = a | a.T
+    np.fill_diagonal(a, True)
+    deg = a.sum(1).astype(np.int32)
+    row_ptr = np.zeros(n + 1, dtype=np.int64)
+    row_ptr[1:] = np.cumsum(deg)
+    col = np.nonzero(a)[1].astype(np.int32)
+    s = np.float32(1.0) / np.sqrt(deg.astype(np.float32))
+    return a, deg, row_ptr, col, s
+
+
+def bits_to_dense(bits: torch.Tensor, n: int) -> np.ndarray:
+    b = bits.cpu().numpy().view(np.uint64)
+    out = np.zeros((n, n), dtype=bool)
+    for w in range((n + 63) // 64):
+        word = b[:, w]
+        for k in range(64):
+            j = 64 * w + k
+            if j < n:
+                out[:, j] = (word >> np.uint64(k)) & np.uint64(1)
+    return out
+
+
+def test_philox_uniform_bit_exact(device):
+    for rows, cols, seed, tag, ctr in [(37, 101, 123, 5, 0), (4, 4, 2**40 + 7, 1 << 24, 9), (130, 3, 0, 0, 77)]:
+        got = ops.philox_uniform(seed, tag, ctr, rows, cols, device).cpu().numpy()
+        want = philox.uniform(seed, tag, ctr, rows, cols)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 130, 300])
+def test_sampler_bit_exact_vs_oracle(device, n):
+    g = torch.Generator().manual_seed(n)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    gen = Generator(seed=1234 + n, replica=3)
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=gen, track_grad=False)
+    u = philox.uniform(1234 + n, tag_for(TAG_GRAPH, 3), 0, n, n)
+    a, deg, row_ptr, col, s = expected_graph(theta.numpy(), n, u)
+    assert np.array_equal(bits_to_dense(graph.bits, n), a)
+    assert np.array_equal(graph.deg.cpu().numpy(), deg)
+    assert np.array_equal(graph.row_ptr.cpu().numpy(), row_ptr)
+    assert graph.nnz() == len(col)
+    assert np.array_equal(graph.col[: len(col)].cpu().numpy(), col)
+    assert np.array_equal(graph.s.cpu().numpy().view(np.uint32), s.view(np.uint32))
+    assert gen.graph_counter == 1
+
+
+def test_sampler_injected_uniforms_match_torch_bernoulli(device):
+    """Injected-U mode reproduces the reference's own draw:
+    Bernoulli(P).sample() under torch.manual_seed (src/models/sampling.py:68)."""
+    n = 200
+    g = torch.Generator().manual_seed(7)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    iu = torch.triu_indices(n, n)
+    p = torch.zeros(n, n)
+    p[iu[0], iu[1]] = theta
+    p = (p.triu(1) + p.triu(1).t() + torch.diag(p.diag())).clamp(0, 1)
+    torch.manual_seed(99)
+    ref = torch.distributions.Bernoulli(probs=p).sample()
+    ref = ref.triu(1) + ref.triu(1).t()
+    ref.fill_diagonal_(1.0)
+    torch.manual_seed(99)
+    u = torch.rand(n, n)
+    graph = ops.sample_graph_from_triu(theta.to(device), n, u_inject=u.to(device), track_grad=False)
+    assert torch.equal(graph.to_dense().cpu(), ref)
+
+
+def test_sampler_known_answers(device):
+    """θ ∈ {0, 1} is deterministic (tst/models/test_sampling.py:149-160)."""
+    n = 70
+    ones = torch.ones(n * (n + 1) // 2, device=device)
+    full = ops.sample_graph_from_triu(ones, n, generator=Generator(5), track_grad=False)
+    assert torch.equal(full.to_dense().cpu(), torch.ones(n, n))
+    assert full.num_edges() == n * (n - 1) // 2
+    zeros = torch.zeros_like(ones)
+    empty = ops.sample_graph_from_triu(zeros, n, generator=Generator(5), track_grad=False)
+    assert torch.equal(empty.to_dense().cpu(), torch.eye(n))
+    assert torch.equal(empty.s.cpu(), torch.ones(n))
+    # out-of-range θ is clamped like triu_values_to_symmetric_matrix
+    big = ops.sample_graph_from_triu(ones * 3.0, n, generator=Generator(5), track_grad=False)
+    assert big.num_edges() == n * (n - 1) // 2
+
+
+@pytest.mark.parametrize("f", [1, 7, 16, 33, 64])
+def test_spmm_norm_vs_dense(device, f):
+    n = 333
+    g = torch.Generator().manual_seed(f)
+    theta = torch.rand(n * (n + 1) // 2, generator=g) * 0.2
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(f), track_grad=False)
+    z = torch.randn(n, f, generator=g)
+    y = graph.spmm(z.to(device)).cpu().double()
+    a_hat = graph.normalized_dense().cpu().double()
+    ref = a_hat @ z.double()
+    assert torch.allclose(y, ref, rtol=RTOL, atol=RTOL)
+    # strided input / beta=1 accumulate
+    zz = torch.randn(n, f + 5, generator=g).to(device)
+    out = torch.ones(n, f + 3, device=device)
+    graph.spmm(zz[:, :f], out=out[:, :f], beta=1)
+    ref2 = a_hat @ zz[:, :f].cpu().double() + 1.0
+    assert torch.allclose(out[:, :f].cpu().double(), ref2, rtol=RTOL, atol=RTOL)
+    assert torch.equal(out[:, f:].cpu(), torch.ones(n, 3))
+
+
+@pytest.mark.parametrize("n,k,nr", [(1, 4, 1), (64, 16, 2), (150, 20, 3), (257, 64, 4)])
+def test_theta_grad_vs_dense(device, n, k, nr):
+    g = torch.Generator().manual_seed(n + k)
+    u = torch.randn(n, k, generator=g)
+    v = torch.randn(n, k, generator=g)
+    r = torch.randn(n, nr, generator=g)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    theta[::7] = 1.5  # outside [0,1]: clamp backward masks these
+    out = ops.theta_grad(u.to(device), v.to(device), r.to(device), n, theta=theta.to(device)).cpu().double()
+    ud, vd, rd = u.double(), v.double(), r.double().sum(1)
+    m = ud @ vd.t() + vd @ ud.t() + rd[:, None] + rd[None, :]
+    iu = torch.triu_indices(n, n)
+    ref = m[iu[0], iu[1]]
+    ref[iu[0] == iu[1]] = 0.0
+    ref[(theta.double() < 0) | (theta.double() > 1)] = 0.0
+    assert torch.allclose(out, ref, rtol=RTOL, atol=1e-4)
+    # accumulate
+    base = torch.randn(n * (n + 1) // 2, generator=g)
+    acc = base.clone().to(device)
+    ops.theta_grad(u.to(device), v.to(device), r.to(device), n, theta=theta.to(device), out=acc, accumulate=True)
+    assert torch.allclose(acc.cpu().double(), base.double() + ref, rtol=RTOL, atol=1e-4)
+
+
+def test_dropout_bit_exact(device):
+    rows, cols = 37, 50
+    x = torch.randn(rows, cols)
+    key = (99, tag_for(2 << 24, 1), 4)
+    y = ops.keyed_dropout(x.to(device), 0.5, key).cpu()
+    u = philox.uniform(99, key[1], 4, rows, cols)
+    ref = x * torch.from_numpy((u < 0.5).astype(np.float32)) * 2.0
+    assert torch.equal(y, ref)
+
+
+def test_sgd_clamp(device):
+    g = torch.Generator().manual_seed(0)
+    for count in [1, 5, 1000, 4097]:
+        th = torch.rand(count, generator=g)
+        gr = torch.randn(count, generator=g)
+        t = th.to(device)
+        ops.sgd_clamp_(t, gr.to(device), 0.3)
+        ref = (th - 0.3 * gr).clamp(0, 1)
+        assert torch.allclose(t.cpu(), ref, atol=1e-6)
+
+
+def test_native_errors_are_raised(device):
+    with pytest.raises(nat.NativeError):
+        nat.call("lds_spmm_norm", 0, 0, 0, 10, 0, 4, 4, 0, 4, 0, 0)
+
+
+def test_degree_scale_is_correctly_rounded(device):
+    """s = fl32(1/fl32(sqrt(d))) bit-exact for every degree 1..20000."""
+    n = 20000
+    deg = torch.arange(1, n + 1, dtype=torch.int64)
+    row_ptr = torch.zeros(n + 1, dtype=torch.int64)
+    row_ptr[1:] = torch.cumsum(deg, 0)
+    rp = row_ptr.to(torch.int32).to(device)
+    s = torch.empty(n, device=device)
+    d = torch.empty(n, dtype=torch.int32, device=device)
+    nat.call("lds_csr_degree_scale", nat.ptr(rp), n, nat.ptr(d), nat.ptr(s), nat.stream_of(s.device))
+    want = np.float32(1.0) / np.sqrt(deg.numpy().astype(np.float32))
+    assert np.array_equal(d.cpu().numpy(), deg.numpy())
+    assert np.array_equal(s.cpu().numpy().view(np.uint32), want.view(np.uint32))
