@@ -1,0 +1,196 @@
+"""Benchmark: LDS inner-loop steps/s on Cora-sized LDS (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): Cora-shaped LDS bilevel, kNN-initialised
+θ (k=10, cosine, symmetrised), 1 sampled graph per inner step, hidden 16,
+dropout 0.5, Adam 0.01 / wd 5e-4, hyper step every τ=5 inner steps (SGD
+lr 0.1, decay 0.99), fp32.  Early stopping disabled: W untimed warm-up inner
+steps, then exactly K timed inner steps with their hyper steps inside the
+timed region.  Synthetic data of Cora's shape (no network).
+
+N>1 (torchrun, one process per GPU): every rank runs its own Monte-Carlo
+replica (keyed RNG stream = rank) and the ranks all-reduce θ.grad once per
+hyper step over RCCL — per-GPU work fixed ("weak"); value = inner steps of all
+ranks / max-over-ranks wall time.
+
+Also reported: `roofline` of the dominant kernel (HIP-event average launch
+time over a second, instrumented pass of the same K steps) and
+`cpu_baseline` — the CPU oracle (dense PyTorch restatement of the reference)
+timed on this host over a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "lds-gnn_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
+
+
+def build(args, rank, device):
+    import ldsgnn
+    from ldsgnn.data.synthetic import knn_init, make_dataset
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from ldsgnn.models.graph import BernoulliGraphModel
+    from ldsgnn.replicas import allreduce_mean
+    from ldsgnn.trainers.bilevel import BilevelProblemRunner
+    from ldsgnn.trainers.inner import InnerProblemTrainer
+    from ldsgnn.trainers.outer import OuterProblemTrainer
+    from ldsgnn.utils.graph import split_mask
+
+    data = knn_init(make_dataset(args.dataset, seed=args.seed), k=10)
+    np.random.seed(args.seed)
+    data.val_mask, opt_mask = split_mask(data.val_mask, 0.5, shuffle=True)
+    data = data.to(device)
+    opt_mask = opt_mask.to(device)
+    ldsgnn.rng.manual_seed(args.seed, replica=rank)
+    torch.manual_seed(args.seed)
+    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(device)
+    inner = InnerProblemTrainer(gcn, data, lr=0.01, weight_decay=5e-4)
+    gm = BernoulliGraphModel(data.dense_adj)
+    outer = OuterProblemTrainer(torch.optim.SGD(gm.parameters(), lr=0.1), data, opt_mask, gm,
+                                lr_decay=0.99, grad_reducer=allreduce_mean)
+    return data, BilevelProblemRunner(inner, outer, data), opt_mask
+
+
+def run_steps(runner, start: int, count: int, tau: int) -> int:
+    step = start
+    for _ in range(count):
+        runner.inner_opt_step()
+        if tau == 0 or step % tau == 0:
+            runner.hyper_opt_step(step)
+        step += 1
+    return step
+
+
+def cpu_baseline(args, data, opt_mask):
+    """The oracle (dense CPU restatement of the reference) on a bounded sample:
+    `cpu_steps` inner steps incl. their τ-hyper steps, host threads."""
+    from oracle import lds_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cpu = data.to("cpu")
+    theta = O.get_triu_values(cpu.dense_adj)
+    prob = O.LdsProblem(cpu.x, cpu.y, cpu.train_mask, cpu.val_mask, cpu.test_mask, opt_mask.cpu(), theta,
+                        hidden=16, dropout_p=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99,
+                        rnd=O.Randomness(args.seed, 0), init_generator=torch.Generator().manual_seed(args.seed))
+    prob.run_steps(1, args.tau)  # warm-up (allocations, first hyper step)
+    t0 = time.perf_counter()
+    prob.run_steps(args.cpu_steps, args.tau)
+    dt = time.perf_counter() - t0
+    return {"value": args.cpu_steps / dt, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} inner steps incl. hyper steps every tau={args.tau} "
+                      f"(oracle/lds_oracle.py, dense torch-CPU fp32, {threads} threads), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--tau", type=int, default=5)
+    ap.add_argument("--dataset", default="cora")
+    ap.add_argument("--seed", type=int, default=597905255 % (2 ** 31))
+    ap.add_argument("--cpu-steps", type=int, default=11)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", default="lds_theta_grad", help="kernel for the roofline leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import ldsgnn
+    from ldsgnn import _native as nat
+
+    data, runner, opt_mask = build(args, rank, device)
+    n = data.num_nodes
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    step = run_steps(runner, 0, args.warmup, args.tau)
+    barrier_sync()
+    t0 = time.perf_counter()
+    step = run_steps(runner, step, args.steps, args.tau)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * args.steps / elapsed
+
+    # roofline leg: the same K steps again with HIP events around the kernel
+    nat.timer.enable(args.kernel)
+    step = run_steps(runner, step, args.steps, args.tau)
+    ksum = nat.timer.summary()[args.kernel]
+    nat.timer.disable()
+    g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
+    nnz = g.nnz()
+    tri = n * (n + 1) // 2
+    if args.kernel == "lds_spmm_norm":
+        f = 16
+        algo = 4 * (n + 1) + 4 * nnz + 4 * n + 8 * n * f
+        achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
+    elif args.kernel == "lds_sample_bitmask":
+        words = nat.lib.lds_bitmask_words(n)
+        algo = 4 * tri + 8 * n * words
+        achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
+    else:  # lds_theta_grad: rank-2k update of the packed triangle (k = 48 at C=7)
+        k = 16 + 8 + 8 + 16
+        flops = 4.0 * k * tri
+        achieved = flops / (ksum["avg_us"] * 1e-6) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None}
+    roof.update(kernel=args.kernel, avg_us=ksum["avg_us"], launches=ksum["launches"])
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, data, opt_mask)
+
+    if rank == 0:
+        out = {
+            "metric": "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X",
+            "value": value, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": f"synthetic {args.dataset}-shaped (N={n}, F_in={data.num_features}, "
+                    f"C={data.num_classes}), kNN-initialised theta",
+            "config": {"workload": f"{args.dataset}-lds-knn-init-S1-tau{args.tau}", "nodes": n,
+                       "features": data.num_features, "classes": data.num_classes, "hidden": 16,
+                       "tau": args.tau, "samples_per_rank": 1, "parallelism": f"replicas{world}",
+                       "sampled_nnz": nnz},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -74,7 +74,44 @@ def check(err: int, what: str = "") -> None:
         raise NativeError(f"{what or 'ldsgnn'} failed: hip error {err} ({msg})")
 
 
+class KernelTimer:
+    """Optional HIP-event timing of selected entry points on the current
+    stream (bench.py's roofline leg): start/end events around each launch."""
+
+    def __init__(self):
+        self.names = set()
+        self.events = {}
+
+    def enable(self, *names):
+        self.names = set(names)
+        self.events = {n: [] for n in names}
+
+    def disable(self):
+        self.names = set()
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for n, evs in self.events.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            out[n] = dict(launches=len(ms), total_ms=float(sum(ms)),
+                          avg_us=float(1000.0 * sum(ms) / len(ms)) if ms else 0.0)
+        return out
+
+
+timer = KernelTimer()
+
+
 def call(name: str, *args) -> None:
+    if name in timer.names:
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        err = getattr(lib, name)(*args)
+        b.record()
+        timer.events[name].append((a, b))
+        check(err, name)
+        return
     check(getattr(lib, name)(*args), name)
 
 

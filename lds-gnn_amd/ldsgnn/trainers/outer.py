@@ -32,7 +32,8 @@ class OuterProblemTrainer:
     def __init__(self, optimizer: Optimizer, data, opt_mask: Tensor, model: GraphGenerativeModel,
                  smoothness_factor: float = 0.0, disconnection_factor: float = 0.0,
                  sparsity_factor: float = 0.0, regularize: bool = False, lr_decay: float = None,
-                 lr_decay_step_size: int = 1, refine_embeddings: bool = False, pretrain: bool = False):
+                 lr_decay_step_size: int = 1, refine_embeddings: bool = False, pretrain: bool = False,
+                 grad_reducer: Callable = None):
         if regularize:
             raise NotImplementedError("graph regularisation is outside the LDS hot path (default off)")
         if pretrain:
@@ -50,6 +51,10 @@ class OuterProblemTrainer:
         self.lr_decayer = StepLR(self.optimizer, step_size=self.lr_decay_step_size,
                                  gamma=self.lr_decay) if self.lr_decay is not None else None
         self.refine_embeddings = refine_embeddings
+        # Sample parallelism: called with the model after the
+        # backward and before the SGD step — e.g. ldsgnn.replicas.allreduce_mean
+        # to average θ.grad over ranks (one RCCL all-reduce per hyper step).
+        self.grad_reducer = grad_reducer
 
     def train_step(self, gcn_predict_fct: Callable, mask: Tensor = None,
                    retain_graph: bool = True) -> Metrics:
@@ -61,6 +66,8 @@ class OuterProblemTrainer:
         loss = F.nll_loss(predictions[mask], self.dataset.y[mask])
         acc = accuracy(predictions[mask], self.dataset.y[mask])
         loss.backward(retain_graph=retain_graph)
+        if self.grad_reducer is not None:
+            self.grad_reducer(self.model)
         self.optimizer.step()
         if self.lr_decayer is not None:
             self.lr_decayer.step()
