@@ -137,13 +137,30 @@ PARAM_NAMES = ("layer_in.fc.weight", "layer_in.fc.bias", "layer_out.fc.weight", 
 def init_params(in_features: int, hidden: int, out_features: int,
                 generator: Optional[torch.Generator] = None) -> "OrderedDict[str, torch.Tensor]":
     """reset_weights (src/models/layers.py:38-40): xavier_uniform_ W, zero b —
-    drawn in the order layer_in then layer_out from the CPU generator."""
+    drawn in the order layer_in then layer_out (torch's global CPU generator
+    when `generator` is None, exactly as the reference consumes it)."""
     p = OrderedDict()
     for name, (fo, fi) in (("layer_in", (hidden, in_features)), ("layer_out", (out_features, hidden))):
         w = torch.empty(fo, fi)
-        bound = math.sqrt(6.0 / float(fi + fo))
         with torch.no_grad():
-            w.uniform_(-bound, bound, generator=generator)
+            if generator is None:
+                torch.nn.init.xavier_uniform_(w)
+            else:
+                a = math.sqrt(3.0) * math.sqrt(2.0 / float(fi + fo))
+                w.uniform_(-a, a, generator=generator)
+        p[f"{name}.fc.weight"] = w
+        p[f"{name}.fc.bias"] = torch.zeros(fo)
+    return p
+
+
+def reference_construction_params(in_features: int, hidden: int, out_features: int):
+    """MetaDenseGCN.__init__'s draws (src/models/gcn.py:11-17): each
+    MetaLinear is an nn.Linear (kaiming weight + uniform bias draws), then
+    reset_weights (xavier) — layer_in then layer_out, global CPU generator."""
+    p = OrderedDict()
+    for name, (fi, fo) in (("layer_in", (in_features, hidden)), ("layer_out", (hidden, out_features))):
+        lin = torch.nn.Linear(fi, fo)
+        w = torch.nn.init.xavier_uniform_(lin.weight.detach().clone())
         p[f"{name}.fc.weight"] = w
         p[f"{name}.fc.bias"] = torch.zeros(fo)
     return p
@@ -412,9 +429,19 @@ class LdsProblem:
             (vl, va), (tl, ta) = self.empirical_mean_loss(n_samples_empirical_mean, best)
             if log is not None:
                 log.append(("empirical", step, vl, va, tl, ta))
-            outer_stop.update(vl, model_params=[best, self.theta.detach().clone()])
+            # the reference stores outer_trainer.model.state_dict(): live views
+            # of θ, not copies (src/trainers/bilevel.py:96-98) — kept as such.
+            outer_stop.update(vl, model_params=[best, self.theta.detach()])
         self.best_params, self.best_theta = outer_stop.model_params
+        self.n_samples_empirical_mean = n_samples_empirical_mean
         return step
+
+    def evaluate(self):
+        """BilevelProblemRunner.evaluate (src/trainers/bilevel.py:128-145)."""
+        with torch.no_grad():
+            self.theta.copy_(self.best_theta)
+        (vl, va), (tl, ta) = self.empirical_mean_loss(self.n_samples_empirical_mean, self.best_params)
+        return {"loss.val.final": vl, "acc.val.final": va, "loss.test.final": tl, "acc.test.final": ta}
 
     def run_steps(self, inner_steps: int, hyper_gradient_interval: int):
         """Fixed-count inner loop with hyper steps every τ (benchmark protocol,

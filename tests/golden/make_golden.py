@@ -1,0 +1,474 @@
+"""Generate the golden vectors in tests/golden/*.npz from the REFERENCE CODE.
+
+Run in the development container only (needs /root/reference; the GPU box
+never sees the reference):  python tests/golden/make_golden.py
+
+How the reference is run here
+  * /root/reference/src is imported as-is.  Its third-party imports that are
+    not installed are satisfied by stubs written to a temporary directory
+    outside the repository:
+      - import-only placeholders (never called on this path): sacred,
+        torch_geometric, torch_scatter;
+      - functional stand-ins for the two libraries whose arithmetic IS on the
+        path, loaded from this repository's restatements:
+          torchmeta.modules{,.utils}  <- lds-gnn_amd/ldsgnn/models/meta.py
+          higher.optim                <- lds-gnn_amd/ldsgnn/optim.py
+        (higher's first-order values are additionally pinned against
+        torch.optim.Adam, golden `adam_first_order`).
+  * Randomness: `Bernoulli` in src.models.sampling and `F.dropout` in
+    src.models.gcn are replaced by draws from the keyed Philox map
+    (oracle/philox.py) on the product's schedule (ldsgnn/rng.py), so the GPU
+    product and the reference see identical edge sets and dropout masks.  One
+    golden (`sampling_native`) keeps torch's own RNG to pin the injected-U mode.
+Nothing from the reference is copied into the repository: only inputs and
+outputs (arrays) are stored.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+from oracle import philox  # noqa: E402
+
+TAG_GRAPH, TAG_DROP_X, TAG_DROP_H = philox.TAG_GRAPH, philox.TAG_DROP_X, philox.TAG_DROP_H
+
+
+# ---------------------------------------------------------------------------
+# stubs
+# ---------------------------------------------------------------------------
+
+def _load_file_module(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def install_stubs():
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        sys.modules[name] = m
+        return m
+
+    class Ingredient:
+        def __init__(self, *a, **k):
+            pass
+
+        def config(self, f):
+            return f
+
+        def capture(self, f):
+            return f
+
+    class _Placeholder:
+        def __init__(self, *a, **k):
+            raise RuntimeError("stub placeholder called: not on the golden path")
+
+    class Data:
+        def __init__(self, **kwargs):
+            for k, v in kwargs.items():
+                setattr(self, k, v)
+
+    mod("sacred", Ingredient=Ingredient, Experiment=_Placeholder)
+    mod("sacred.observers", TelegramObserver=_Placeholder)
+    mod("sacred.run", Run=object)
+    mod("torch_geometric")
+    mod("torch_geometric.data", Data=Data)
+    mod("torch_geometric.datasets", Planetoid=_Placeholder)
+    mod("torch_geometric.nn")
+    mod("torch_geometric.nn.models", GAE=_Placeholder)
+    mod("torch_geometric.transforms", NormalizeFeatures=_Placeholder, Compose=_Placeholder)
+    mod("torch_geometric.utils", to_scipy_sparse_matrix=_Placeholder, to_undirected=_Placeholder)
+    mod("torch_scatter", scatter_add=_Placeholder)
+    meta = _load_file_module("ldsgnn_meta_standin", os.path.join(ROOT, "lds-gnn_amd/ldsgnn/models/meta.py"))
+    mod("torchmeta")
+    mod("torchmeta.modules", MetaModule=meta.MetaModule, MetaLinear=meta.MetaLinear)
+    mod("torchmeta.modules.utils", get_subdict=meta.get_subdict)
+    opt = _load_file_module("ldsgnn_optim_standin", os.path.join(ROOT, "lds-gnn_amd/ldsgnn/optim.py"))
+    mod("higher")
+    mod("higher.optim", DifferentiableOptimizer=opt.DifferentiableOptimizer,
+        DifferentiableAdam=opt.DifferentiableAdam)
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+
+
+# ---------------------------------------------------------------------------
+# keyed randomness patched into the reference
+# ---------------------------------------------------------------------------
+
+class KeyedRandomness:
+    """The product's draw schedule (ldsgnn/rng.py) as patches on the reference."""
+
+    def __init__(self, seed: int, replica: int = 0):
+        self.seed, self.replica = seed, replica
+        self.graph_counter = 0
+        self.forward_counter = 0
+        self._pending_h = None
+
+    def bernoulli_class(self):
+        outer = self
+
+        class Bernoulli:
+            def __init__(self, probs):
+                self.probs = probs
+
+            def sample(self):
+                n = self.probs.size(0)
+                c = outer.graph_counter
+                outer.graph_counter += 1
+                u = philox.uniform(outer.seed, philox.tag_for(TAG_GRAPH, outer.replica), c, n, n)
+                return (torch.from_numpy(u) < self.probs.detach()).to(self.probs.dtype)
+
+        return Bernoulli
+
+    def functional(self):
+        import torch.nn.functional as F
+        outer = self
+
+        def dropout(x, p=0.5, training=True, inplace=False):
+            if not training or p == 0.0:
+                return x
+            if outer._pending_h is None:
+                c = outer.forward_counter
+                outer.forward_counter += 1
+                tag = philox.tag_for(TAG_DROP_X, outer.replica)
+                outer._pending_h = c
+            else:
+                c = outer._pending_h
+                tag = philox.tag_for(TAG_DROP_H, outer.replica)
+                outer._pending_h = None
+            u = torch.from_numpy(philox.uniform(outer.seed, tag, c, x.size(0), x.size(1)))
+            keep = np.float32(1.0) - np.float32(p)
+            return x * ((u < float(keep)).to(x.dtype) * float(np.float32(1.0) / keep))
+
+        proxy = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith("__")})
+        proxy.dropout = dropout
+        return proxy
+
+
+def patch_reference(rnd: KeyedRandomness):
+    import src.models.gcn as gcn_mod
+    import src.models.sampling as sampling_mod
+    sampling_mod.Bernoulli = rnd.bernoulli_class()
+    gcn_mod.F = rnd.functional()
+    # sacred would inject the sampler config (src/models/sampling.py:96-102)
+    sampling_mod.Sampler.sample = staticmethod(_sampler_with_config(sampling_mod))
+
+
+def _sampler_with_config(sampling_mod):
+    def sample(edge_probs, undirected=True, sparsification="NONE", k=20, eps=0.9, embeddings=None,
+               dense=False, knn_metric="cosine"):
+        return sampling_mod.sample_graph(edge_probs=edge_probs, embeddings=embeddings, undirected=undirected,
+                                         sparsification=sampling_mod.SPARSIFICATION[sparsification],
+                                         dense=dense, k=k, eps=eps, knn_metric=knn_metric)
+    return sample
+
+
+# ---------------------------------------------------------------------------
+# problems
+# ---------------------------------------------------------------------------
+
+def synthetic(n, f_in, classes, seed, p_edge=0.05):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(n, f_in, generator=g) * (torch.rand(n, f_in, generator=g) < 0.3)
+    x = x / x.sum(1, keepdim=True).clamp(min=1e-12)
+    y = torch.randint(0, classes, (n,), generator=g)
+    perm = torch.randperm(n, generator=g)
+    ntr, nva = max(2, n // 5), max(2, (3 * n) // 10)
+    masks = []
+    for idx in (perm[:ntr], perm[ntr:ntr + nva // 2], perm[ntr + nva // 2:ntr + nva], perm[ntr + nva:]):
+        m = torch.zeros(n, dtype=torch.bool)
+        m[idx] = True
+        masks.append(m)
+    a = (torch.rand(n, n, generator=g) < p_edge).float().triu(1)
+    return dict(x=x, y=y, train=masks[0], val=masks[1], opt=masks[2], test=masks[3], adj=a + a.t())
+
+
+def dense_data(prob):
+    from src.utils.graph import DenseData
+    d = DenseData.__new__(DenseData)
+    d.x, d.y, d.dense_adj = prob["x"], prob["y"], prob["adj"]
+    d.train_mask, d.val_mask, d.test_mask = prob["train"], prob["val"], prob["test"]
+    d.num_classes = int(prob["y"].max()) + 1
+    return d
+
+
+def np_prob(prob, prefix=""):
+    return {prefix + k: (v.numpy() if isinstance(v, torch.Tensor) else v) for k, v in prob.items()}
+
+
+def build_reference(prob, seed, dropout, hidden=16, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99):
+    from src.models.gcn import MetaDenseGCN
+    from src.models.graph import BernoulliGraphModel
+    from src.trainers.bilevel import BilevelProblemRunner
+    from src.trainers.inner import InnerProblemTrainer
+    from src.trainers.outer import OuterProblemTrainer
+    data = dense_data(prob)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.x.size(1), hidden, data.num_classes, dropout=dropout)
+    inner = InnerProblemTrainer(gcn, data, lr=gcn_lr, weight_decay=gcn_wd)
+    gm = BernoulliGraphModel(data.dense_adj)
+    opt = torch.optim.SGD(gm.parameters(), lr=outer_lr)
+    outer = OuterProblemTrainer(opt, data, prob["opt"], gm, smoothness_factor=0.0, disconnection_factor=0.0,
+                                sparsity_factor=0.0, regularize=False, lr_decay=lr_decay, pretrain=False)
+    runner = BilevelProblemRunner(inner, outer, data, n_samples_empirical_mean=16)
+    runner.logger = types.SimpleNamespace(info=lambda *a, **k: None, warn=lambda *a, **k: None)
+    return runner
+
+
+class Log:
+    def __init__(self):
+        self.rows = []
+
+    def log_scalar(self, name, value, step=None):
+        self.rows.append((name, float(value), -1 if step is None else int(step)))
+
+
+# ---------------------------------------------------------------------------
+# goldens
+# ---------------------------------------------------------------------------
+
+def g_graph_math(out):
+    from src.models.sampling import sample_graph, SPARSIFICATION
+    from src.utils.graph import normalize_adjacency_matrix, triu_values_to_symmetric_matrix
+    g = torch.Generator().manual_seed(1)
+    theta8 = torch.rand(36, generator=g) * 1.4 - 0.2
+    out["theta8"] = theta8.numpy()
+    out["p8"] = triu_values_to_symmetric_matrix(theta8).numpy()
+    a = (torch.rand(16, 16, generator=g) < 0.3).float().triu(1)
+    a = a + a.t()
+    out["adj16"] = a.numpy()
+    out["norm16"] = normalize_adjacency_matrix(a).numpy()
+    # θ-gradient through P -> sample (STE) -> normalise, reference autograd
+    n = 30
+    theta = torch.rand(n * (n + 1) // 2, generator=g).requires_grad_(True)
+    w = torch.randn(n, n, generator=g)
+    p = triu_values_to_symmetric_matrix(theta)
+    rnd = KeyedRandomness(seed=4242)
+    import src.models.sampling as sm
+    old = sm.Bernoulli
+    sm.Bernoulli = rnd.bernoulli_class()
+    try:
+        a30 = sample_graph(p, undirected=True, sparsification=SPARSIFICATION.NONE, dense=False)
+    finally:
+        sm.Bernoulli = old
+    loss = (w * normalize_adjacency_matrix(a30)).sum()
+    loss.backward()
+    out["theta30"] = theta.detach().numpy()
+    out["w30"] = w.numpy()
+    out["sample30"] = a30.detach().numpy()
+    out["grad30"] = theta.grad.numpy()
+    out["seed30"] = np.int64(4242)
+
+
+def g_sampling_native(out):
+    """torch's own RNG: Bernoulli(P).sample() under torch.manual_seed."""
+    from src.models.sampling import sample_graph, SPARSIFICATION
+    from src.utils.graph import triu_values_to_symmetric_matrix
+    import src.models.sampling as sm
+    from torch.distributions import Bernoulli as TorchBernoulli
+    old = sm.Bernoulli
+    sm.Bernoulli = TorchBernoulli
+    try:
+        n = 64
+        g = torch.Generator().manual_seed(2)
+        theta = torch.rand(n * (n + 1) // 2, generator=g)
+        p = triu_values_to_symmetric_matrix(theta)
+        torch.manual_seed(77)
+        a = sample_graph(p, undirected=True, sparsification=SPARSIFICATION.NONE, dense=False)
+        torch.manual_seed(77)
+        u = torch.rand(n, n)
+    finally:
+        sm.Bernoulli = old
+    out["theta"] = theta.numpy()
+    out["u"] = u.numpy()
+    out["sample"] = a.detach().numpy()
+
+
+def g_gcn_forward(out):
+    from src.models.gcn import MetaDenseGCN
+    from src.models.graph import BernoulliGraphModel
+    prob = synthetic(64, 20, 5, seed=3, p_edge=0.2)
+    rnd = KeyedRandomness(seed=31)
+    patch_reference(rnd)
+    torch.manual_seed(5)
+    gcn = MetaDenseGCN(20, 16, 5, dropout=0.5)
+    gm = BernoulliGraphModel(prob["adj"])
+    with torch.no_grad():
+        gm.probs.mul_(0.5).add_(0.25)  # fractional θ
+    graph = gm.sample()
+    gcn.train()
+    train_out = gcn(prob["x"], graph)
+    gcn.eval()
+    eval_out = gcn(prob["x"], graph)
+    out.update(np_prob(prob, "prob_"))
+    out["theta"] = gm.probs.detach().numpy()
+    out["params"] = np.concatenate([p.detach().numpy().ravel() for p in gcn.parameters()])
+    out["train_logp"] = train_out.detach().numpy()
+    out["eval_logp"] = eval_out.detach().numpy()
+    out["seed"] = np.int64(31)
+    out["torch_seed"] = np.int64(5)
+
+
+def g_adam_first_order(out):
+    """torch.optim.Adam (real torch arithmetic) with the reference's groups on
+    the reference GCN: pins the differentiable-Adam restatement's values."""
+    from src.models.gcn import MetaDenseGCN
+    from src.utils.graph import DenseData  # noqa: F401
+    import torch.nn.functional as F
+    prob = synthetic(48, 16, 4, seed=4, p_edge=0.1)
+    torch.manual_seed(6)
+    gcn = MetaDenseGCN(16, 16, 4, dropout=0.0)
+    opt = torch.optim.Adam([{"params": gcn.layer_in.parameters(), "weight_decay": 5e-4},
+                            {"params": gcn.layer_out.parameters()}], lr=0.01)
+    out["params0"] = np.concatenate([p.detach().numpy().ravel() for p in gcn.parameters()])
+    traj = []
+    for _ in range(5):
+        opt.zero_grad()
+        pred = gcn(prob["x"], prob["adj"])
+        F.nll_loss(pred[prob["train"]], prob["y"][prob["train"]]).backward()
+        opt.step()
+        traj.append(np.concatenate([p.detach().numpy().ravel() for p in gcn.parameters()]))
+    out.update(np_prob(prob, "prob_"))
+    out["trajectory"] = np.stack(traj)
+    out["torch_seed"] = np.int64(6)
+
+
+def g_bilevel(out, n=80, f_in=24, classes=4, seed=11, dropout=0.5):
+    """The reference's own BilevelProblemRunner.train + evaluate, early
+    stopping included, with keyed randomness; θ-gradients of every hyper step."""
+    prob = synthetic(n, f_in, classes, seed=seed, p_edge=0.06)
+    rnd = KeyedRandomness(seed=seed)
+    patch_reference(rnd)
+    runner = build_reference(prob, seed=seed, dropout=dropout)
+    grads = []
+    orig = runner.outer_trainer.train_step
+
+    def spy(*a, **k):
+        m = orig(*a, **k)
+        grads.append(runner.outer_trainer.model.probs.grad.detach().clone().numpy())
+        return m
+
+    runner.outer_trainer.train_step = spy
+    log = Log()
+    runner.train(patience=3, hyper_gradient_interval=5, inner_loop_max_epochs=12, outer_loop_max_epochs=2,
+                 sacred_runner=log)
+    res = runner.evaluate()
+    out.update(np_prob(prob, "prob_"))
+    out["seed"] = np.int64(seed)
+    out["dropout"] = np.float64(dropout)
+    out["log_names"] = np.array([r[0] for r in log.rows])
+    out["log_values"] = np.array([r[1] for r in log.rows])
+    out["log_steps"] = np.array([r[2] for r in log.rows])
+    out["theta_final"] = runner.outer_trainer.model.probs.detach().numpy()
+    out["theta_grads"] = np.stack(grads)
+    out["final"] = np.array([res["loss.val.final"], res["acc.val.final"], res["loss.test.final"],
+                             res["acc.test.final"]])
+    out["graph_draws"] = np.int64(rnd.graph_counter)
+    out["forward_draws"] = np.int64(rnd.forward_counter)
+
+
+def g_conditioning_probe(out):
+    """bilevel_small again, with the reference's aggregation torch.mm
+    (src/models/layers.py:44) accumulated in fp64 and rounded once — a pure
+    rounding change.  Shows how much the reference's own hypergradients move
+    under reordered fp32 arithmetic (used to justify whole-loop tolerances)."""
+    import src.models.layers as layers
+    orig_mm = torch.mm
+
+    class TorchProxy:
+        def __getattr__(self, k):
+            return getattr(torch, k)
+
+        @staticmethod
+        def mm(a, b):
+            return orig_mm(a.double(), b.double()).float()
+
+    layers.torch = TorchProxy()
+    try:
+        g_bilevel(out)
+    finally:
+        layers.torch = torch
+
+
+def g_hypergrad_cora(out, seed=7):
+    """One τ=5 window on a Cora-shaped problem (N=2708, F_in=1433, C=7):
+    5 inner steps + the hyper step, reference code; θ-gradient summary."""
+    sys.path.insert(0, os.path.join(ROOT, "lds-gnn_amd"))
+    from ldsgnn.data.synthetic import knn_init, make_dataset
+    data = knn_init(make_dataset("cora", seed=seed), k=10)
+    gperm = torch.Generator().manual_seed(seed)
+    val_idx = data.val_mask.nonzero().squeeze(1)
+    val_idx = val_idx[torch.randperm(val_idx.numel(), generator=gperm)]
+    opt_mask = torch.zeros_like(data.val_mask)
+    opt_mask[val_idx[: val_idx.numel() // 2]] = True
+    prob = dict(x=data.x, y=data.y, train=data.train_mask, val=data.val_mask & ~opt_mask, opt=opt_mask,
+                test=data.test_mask, adj=data.dense_adj)
+    rnd = KeyedRandomness(seed=seed)
+    patch_reference(rnd)
+    runner = build_reference(prob, seed=seed, dropout=0.5)
+    losses = []
+    for step in range(6):
+        losses.append(runner.inner_opt_step().loss)
+        if step % 5 == 0:
+            runner.hyper_opt_step(step)
+    grad = runner.outer_trainer.model.probs.grad.detach().numpy().astype(np.float64)
+    theta = runner.outer_trainer.model.probs.detach().numpy()
+    pick = np.random.default_rng(seed).choice(grad.size, 20000, replace=False)
+    out["seed"] = np.int64(seed)
+    out["opt_mask"] = opt_mask.numpy()
+    # the data itself travels (kNN near-ties and row sums are machine-dependent)
+    xs = data.x.to_sparse_csr()
+    out["x_indptr"] = xs.crow_indices().numpy().astype(np.int64)
+    out["x_indices"] = xs.col_indices().numpy().astype(np.int32)
+    out["x_values"] = xs.values().numpy()
+    out["x_shape"] = np.array(data.x.shape)
+    iu = torch.triu_indices(data.x.shape[0], data.x.shape[0], 1)
+    keep = data.dense_adj[iu[0], iu[1]] != 0
+    out["adj_edges"] = iu[:, keep].numpy().astype(np.int32)
+    out["y"] = data.y.numpy()
+    out["train_mask"] = data.train_mask.numpy()
+    out["val_mask"] = data.val_mask.numpy()
+    out["test_mask"] = data.test_mask.numpy()
+    out["inner_losses"] = np.array(losses)
+    out["grad_idx"] = pick.astype(np.int64)
+    out["grad_val"] = grad[pick].astype(np.float32)
+    out["grad_sum"] = grad.sum()
+    out["grad_l2"] = np.sqrt((grad ** 2).sum())
+    out["theta_idx"] = pick.astype(np.int64)
+    out["theta_val"] = theta[pick]
+    out["theta_sum"] = theta.astype(np.float64).sum()
+
+
+def main():
+    install_stubs()
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    jobs = [("graph_math", g_graph_math), ("sampling_native", g_sampling_native),
+            ("gcn_forward", g_gcn_forward), ("adam_first_order", g_adam_first_order),
+            ("bilevel_small", g_bilevel),
+            ("bilevel_nodrop", lambda o: g_bilevel(o, n=64, f_in=16, classes=3, seed=12, dropout=0.0)),
+            ("hypergrad_cora", g_hypergrad_cora), ("conditioning_probe", g_conditioning_probe)]
+    only = set(sys.argv[1:])
+    for name, fn in jobs:
+        if only and name not in only:
+            continue
+        out = {}
+        fn(out)
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **out)
+        print(f"wrote {path} ({os.path.getsize(path) / 1024:.1f} KiB)")
+
+
+if __name__ == "__main__":
+    main()
