@@ -164,6 +164,122 @@ int lds_dropout(const float* x, int ldx, float* y, int ldy, int rows, int cols,
                 float keep_prob, float scale, uint64_t seed, uint32_t tag,
                 uint32_t counter, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Fused engine (lds-gnn_amd/csrc/engine.hip; orchestrated by
+ * lds-gnn_amd/ldsgnn/engine.py).  Replaces, for the LDS configuration, the
+ * autograd work of
+ *   InnerProblemTrainer.train_step + higher.DifferentiableAdam.step
+ *       (src/trainers/inner.py:55-74, create_graph=True)
+ *   OuterProblemTrainer.train_step's loss.backward through the unrolled
+ *       window (src/trainers/outer.py:57-87) and the SGD/StepLR/clamp that
+ *       follow (src/trainers/outer.py:78-83, src/models/graph.py:63-64)
+ * with hand-derived forward / backward / reverse kernels.
+ * Per-node arrays are n × 16 fp32 (hidden width 16; c <= 16 classes padded to
+ * 16 columns).  `scalars` points to the engine's device-resident
+ * EngineScalars {u32 graph_ctr, u32 fwd_ctr, i32 adam_step, i32 hyper_steps,
+ * f64 outer_lr, f64 lr_decay} (lds_engine_scalars_size() bytes); kernels read
+ * the RNG counters / Adam step / lr from it so one captured HIP graph of a
+ * whole τ-window replays with advancing state.  `fwd_off`, `step_off` are
+ * offsets added to those counters.  Factor outputs (U, V, R) feed
+ * lds_theta_grad with ld = ldk.
+ * ------------------------------------------------------------------------- */
+int lds_engine_scalars_size(void);
+
+/* lds_sample_bitmask with the draw counter read from device memory:
+ * counter = *counter_base + counter_offset. */
+int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, uint32_t tag,
+                           const uint32_t* counter_base, uint32_t counter_offset,
+                           uint64_t* bits, int words, void* stream);
+
+/* H0 = dropout(X) W0ᵀ + b0 (X in CSR; wt = W0ᵀ as [fin][16]). */
+int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int n,
+                        const float* wt, const float* bias, float* out, uint64_t seed,
+                        uint32_t tag_x, const void* scalars, int fwd_off, int train,
+                        float keep, float scale, void* stream);
+/* out[f][:] (+)= Σ_i dropout(X)[i][f] · d[i][:]  (+ wd · w)   (X in CSC). */
+int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int fin,
+                         const float* d, float* out, const float* w, float wd,
+                         int accumulate, uint64_t seed, uint32_t tag_x,
+                         const void* scalars, int fwd_off, int train, float keep,
+                         float scale, void* stream);
+/* Y0 = ÂH0; H1d = dropout(relu(Y0)); H2 = H1d W1ᵀ + b1. */
+int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, int n,
+                          const float* h0, float* y0, float* h1d, float* h2,
+                          const float* w1, const float* b1, int c, uint64_t seed,
+                          uint32_t tag_h, const void* scalars, int fwd_off, int train,
+                          float keep, float scale, void* stream);
+/* O = ÂH2; P = softmax(O); dO = (P - onehot) ⊙ mask · inv_count; per-row
+ * NLL and correctness where mask. */
+int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, int n,
+                          const float* h2, float* o, float* p, float* d_o,
+                          const int* label, const uint8_t* mask, float inv_count,
+                          float* lossrow, float* corrrow, int c, void* stream);
+/* dH2 = ÂdO; dY0 = (dH2 W1) ⊙ dropout' ⊙ relu'.  U != NULL: emit the outer
+ * graph's factor (dO, H2) at columns [foff, foff + fwidth). */
+int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, int n,
+                          const float* d_o, const float* y0, float* dh2, float* dy0,
+                          const float* w1, int c, uint64_t seed, uint32_t tag_h,
+                          const void* scalars, int fwd_off, int train, float keep,
+                          float scale, const float* o, const float* h2, float* U,
+                          float* V, int ldk, float* R, int foff, int fwidth,
+                          void* stream);
+/* dH0 = ÂdY0.  U != NULL: emit the outer graph's factor (dY0, H0). */
+int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, int n,
+                          const float* dy0, float* dh0, const float* y0,
+                          const float* h0, float* U, float* V, int ldk, float* R,
+                          int foff, void* stream);
+/* Deterministic two-stage column reductions over nodes (see engine.hip). */
+int lds_engine_colreduce(int n, int c_n, const float* a1, const float* b1,
+                         const float* a2, const float* b2, const float* x1,
+                         const float* x2, const float* l, const float* q,
+                         float* partials, int nblocks, float* dst_a, float* dst_v1,
+                         int v1_width, float* dst_v2, int v2_width, float* dst_l,
+                         int accumulate, void* stream);
+/* higher's differentiable-Adam step, forward and reverse, per parameter.
+ * hyper = {lr, beta1, beta2, eps, weight_decay} (host doubles); betas_dev =
+ * {beta1, beta2, lr} (device doubles); params [0, n_wd) carry weight decay. */
+int lds_engine_adam(int np, const float* w0, const float* g, const float* m0,
+                    const float* v0, float* w1, float* m1, float* v1, float* gp_out,
+                    const double* hyper, const double* betas_dev, int n_wd,
+                    const void* scalars, int step_off, void* stream);
+int lds_engine_adam_reverse(int np, float* wbar, float* mbar, float* vbar,
+                            const float* m1, const float* v1, const float* gp,
+                            float* gbar, const double* hyper, const double* betas_dev,
+                            int n_wd, const void* scalars, int step_off, void* stream);
+/* Reverse of the inner backward (Hessian-vector part): aggregation kernels
+ * a (dY0bar = ÂdH0bar), b (dObar = ÂdH2bar), c (H2bar = ÂObar),
+ * d (H0bar = ÂY0bar), each emitting its use's factor pair. */
+int lds_engine_rev_a(const int* rp, const int* col, const float* s, int n,
+                     const float* dh0bar, const float* dy0, const float* dh0,
+                     const float* y0, const float* h1d, const float* dh2, const float* w1,
+                     const float* gw1bar, const float* gb1bar, int c, float* dh1dbar,
+                     float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
+                     const void* scalars, int fwd_off, int train, float keep, float scale,
+                     float* U, float* V, int ldk, float* R, int foff, void* stream);
+int lds_engine_rev_b(const int* rp, const int* col, const float* s, int n,
+                     const float* dh2bar, const float* d_o, const float* dh2,
+                     const float* p, const uint8_t* mask, float inv_count, int c,
+                     float* obar, float* U, float* V, int ldk, float* R, int foff,
+                     int cw, void* stream);
+int lds_engine_rev_c(const int* rp, const int* col, const float* s, int n,
+                     const float* obar, const float* h2, const float* o,
+                     const float* h1dbar_part, const float* y0, const float* w1, int c,
+                     float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
+                     const void* scalars, int fwd_off, int train, float keep, float scale,
+                     float* U, float* V, int ldk, float* R, int foff, int cw,
+                     void* stream);
+int lds_engine_rev_d(const int* rp, const int* col, const float* s, int n,
+                     const float* y0bar, const float* h0, const float* y0,
+                     float* h0bar, float* U, float* V, int ldk, float* R, int foff,
+                     void* stream);
+/* θ = clamp(θ - lr·grad, 0, 1) with lr = scalars->outer_lr. */
+int lds_engine_sgd_clamp(float* theta, const float* grad, int64_t count,
+                         const void* scalars, void* stream);
+/* Advance the scalars: counters += (graphs, forwards), adam_step +=
+ * adam_steps, and `hypers` times {hyper_steps += 1; outer_lr *= lr_decay}. */
+int lds_engine_advance(void* scalars, int graphs, int forwards, int adam_steps,
+                       int hypers, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

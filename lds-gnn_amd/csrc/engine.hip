@@ -1,0 +1,759 @@
+// Fused LDS bilevel engine: forward / backward / differentiable-Adam / reverse
+// (hypergradient) kernels for the 2-layer GCN of src/models/gcn.py:23-34 on a
+// sampled graph, written for 16-lane row groups (hidden width H = 16; class
+// count C <= 16 padded to 16 columns).  Every per-node array is N × 16 fp32.
+//
+// Replaces, for the LDS configuration, the autograd machinery the reference
+// runs per inner step (src/trainers/inner.py:55-74 with higher's
+// DifferentiableAdam, create_graph=True) and per hyper step
+// (src/trainers/outer.py:57-87: loss.backward through <= τ unrolled steps).
+// The reverse pass is derived by hand; each aggregation's
+// θ-gradient factor pair (s⊙G, s⊙Z) and r term is emitted by the epilogue of
+// the kernel that has the pair in registers, so one rank-K update
+// (lds_theta_grad) assembles the whole window's dθ.
+//
+// RNG counters, the Adam step and the outer learning rate are read from device
+// memory (EngineScalars) so a whole τ-window is capturable as one HIP graph and
+// replays advance them.
+#include "common.hpp"
+#include "../../include/ldsgnn.h"
+
+namespace lds {
+
+constexpr int HID = 16;   // hidden width / row-group width
+constexpr int RG = 256 / HID;  // row groups per 256-thread block
+
+__device__ __forceinline__ float gsum16(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, HID);
+    return v;
+}
+__device__ __forceinline__ float gmax16(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, HID));
+    return v;
+}
+__device__ __forceinline__ float bcast16(float v, int src) { return __shfl(v, src, HID); }
+
+// Device-resident scalars of an engine (one per replica).
+struct EngineScalars {
+    uint32_t graph_ctr;   // next graph draw counter
+    uint32_t fwd_ctr;     // next training-forward counter
+    int32_t adam_step;    // Adam steps taken so far (state['step'])
+    int32_t hyper_steps;  // hyper steps taken so far
+    double outer_lr;      // current SGD lr on θ (StepLR applied after each hyper step)
+    double lr_decay;      // StepLR gamma (1.0 = none)
+};
+
+struct Keys {
+    uint32_t k0, k1, tag_x, tag_h;
+};
+
+__device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr, int row, int col) {
+    const U32x4 o = philox4x32_10(U32x4{(uint32_t)col, (uint32_t)(row >> 2), tag, ctr}, k.k0, k.k1);
+    const uint32_t w = (row & 3) == 0 ? o.x : (row & 3) == 1 ? o.y : (row & 3) == 2 ? o.z : o.w;
+    return u01(w);
+}
+
+// Normalised aggregation of one 16-wide row: s_i Σ_j s_j Z[j][lane].
+__device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* __restrict__ col,
+                                         const float* __restrict__ s, const float* __restrict__ z,
+                                         int row, int lane) {
+    const int beg = rp[row], end = rp[row + 1];
+    float acc = 0.f;
+    int p = beg;
+    for (; p + 4 <= end; p += 4) {
+        const int j0 = col[p], j1 = col[p + 1], j2 = col[p + 2], j3 = col[p + 3];
+        const float z0 = z[j0 * HID + lane], z1 = z[j1 * HID + lane];
+        const float z2 = z[j2 * HID + lane], z3 = z[j3 * HID + lane];
+        acc = fmaf(s[j0], z0, acc);
+        acc = fmaf(s[j1], z1, acc);
+        acc = fmaf(s[j2], z2, acc);
+        acc = fmaf(s[j3], z3, acc);
+    }
+    for (; p < end; ++p) {
+        const int j = col[p];
+        acc = fmaf(s[j], z[j * HID + lane], acc);
+    }
+    return s[row] * acc;
+}
+
+// Write one factor pair (U = s⊙G, V = s⊙Z) into columns [off, off+width) of the
+// window's factor matrices and add r = -½ s² (G·Y + Z·ÂG) into R[row].
+__device__ __forceinline__ void emit_factor(float* __restrict__ U, float* __restrict__ V, int ldk,
+                                            float* __restrict__ R, int off, int width, int row,
+                                            int lane, float si, float g, float z, float y, float ag) {
+    const float d = gsum16(g * y + z * ag);
+    if (lane < width) {
+        U[(int64_t)row * ldk + off + lane] = si * g;
+        V[(int64_t)row * ldk + off + lane] = si * z;
+    }
+    if (lane == 0) R[row] += -0.5f * si * si * d;
+}
+
+// ---------------------------------------------------------------------------
+// X-side products (X is CSR / CSC, dropout keyed per (node, feature))
+// ---------------------------------------------------------------------------
+
+// out[i][h] = bias[h] + Σ_f Xd[i][f] · Wt[f][h]      (H0 = Xd W0ᵀ + b0)
+// Xd = dropout(X) with key (tag_x, fwd counter) when `train`, else X.
+__global__ __launch_bounds__(256) void x_linear_kernel(
+    const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
+    const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
+    const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const uint32_t ctr = sc->fwd_ctr + fwd_off;
+    float acc = bias != nullptr ? bias[lane] : 0.f;
+    const int beg = xrp[row], end = xrp[row + 1];
+    for (int p0 = beg; p0 < end; p0 += HID) {
+        const int p = p0 + lane;
+        int f = 0;
+        float x = 0.f;
+        if (p < end) {
+            f = xcol[p];
+            x = xval[p];
+            if (train) x = u_at(keys, keys.tag_x, ctr, row, f) < keep ? x * scale : 0.f;
+        }
+        const int cnt = min(HID, end - p0);
+        for (int k = 0; k < cnt; ++k) {
+            const int fk = __shfl(f, k, HID);
+            const float xk = __shfl(x, k, HID);
+            acc = fmaf(xk, wt[fk * HID + lane], acc);
+        }
+    }
+    out[row * HID + lane] = acc;
+}
+
+// out[f][h] (= or +=) Σ_i Xd[i][f] · D[i][h]  (+ wd · w[f][h])   via CSC of X.
+__global__ __launch_bounds__(256) void xt_linear_kernel(
+    const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
+    const float* __restrict__ d, float* __restrict__ out, const float* __restrict__ w, float wd,
+    int accumulate, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
+    float scale) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int f = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (f >= fin) return;
+    const uint32_t ctr = sc->fwd_ctr + fwd_off;
+    float acc = 0.f;
+    const int beg = xcp[f], end = xcp[f + 1];
+    for (int p0 = beg; p0 < end; p0 += HID) {
+        const int p = p0 + lane;
+        int i = 0;
+        float x = 0.f;
+        if (p < end) {
+            i = xrow[p];
+            x = xval[p];
+            if (train) x = u_at(keys, keys.tag_x, ctr, i, f) < keep ? x * scale : 0.f;
+        }
+        const int cnt = min(HID, end - p0);
+        for (int k = 0; k < cnt; ++k) {
+            const int ik = __shfl(i, k, HID);
+            const float xk = __shfl(x, k, HID);
+            acc = fmaf(xk, d[ik * HID + lane], acc);
+        }
+    }
+    float* o = out + f * HID + lane;
+    if (w != nullptr) acc = acc + wd * w[f * HID + lane];
+    *o = accumulate ? *o + acc : acc;
+}
+
+// ---------------------------------------------------------------------------
+// Forward
+// ---------------------------------------------------------------------------
+
+struct GcnW {  // pointers into a flat parameter vector (layout in engine.py)
+    const float* w0t;  // [fin][16]
+    const float* b0;   // [16]
+    const float* w1;   // [C][16]
+    const float* b1;   // [C]
+};
+
+// Y0 = Â H0;  H1d = relu(Y0) ⊙ D1;  H2 = H1d W1ᵀ + b1  (16-padded, zeros past C)
+__global__ __launch_bounds__(256) void fwd_layer1_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
+    GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
+    float scale) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const float y = agg_row(rp, col, s, h0, row, lane);
+    float hd = fmaxf(y, 0.f);
+    if (train) hd = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? hd * scale : 0.f;
+    y0[row * HID + lane] = y;
+    h1d[row * HID + lane] = hd;
+    float out = 0.f;
+    for (int k = 0; k < c; ++k) {
+        const float t = gsum16(hd * w.w1[k * HID + lane]);
+        if (lane == k) out = t + w.b1[k];
+    }
+    h2[row * HID + lane] = out;
+}
+
+// O = Â H2; P = softmax(O) (over c classes); dO = (P - onehot(y)) ⊙ m / |m|;
+// per-row loss -log P[y] and correctness (argmax == y) where m.
+__global__ __launch_bounds__(256) void fwd_layer2_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ h2, float* __restrict__ o_out, float* __restrict__ p_out,
+    float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
+    float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const float o = agg_row(rp, col, s, h2, row, lane);
+    const bool act = lane < c;
+    const float m = gmax16(act ? o : -INFINITY);
+    const float e = act ? expf(o - m) : 0.f;
+    const float sum = gsum16(e);
+    const float lse = logf(sum);
+    const float logp = o - m - lse;
+    const float p = act ? expf(logp) : 0.f;
+    const int y = label[row];
+    const bool sel = mask != nullptr && mask[row];
+    if (o_out) o_out[row * HID + lane] = act ? o : 0.f;
+    if (p_out) p_out[row * HID + lane] = p;
+    if (d_o) d_o[row * HID + lane] = (sel && act) ? (p - (lane == y ? 1.f : 0.f)) * inv_count : 0.f;
+    // argmax with first-index tie-break (torch.argmax)
+    float best = act ? o : -INFINITY;
+    int bi = lane;
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+        const float ob = __shfl_xor(best, off, HID);
+        const int oi = __shfl_xor(bi, off, HID);
+        if (ob > best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+        }
+    }
+    const float logpy = bcast16(logp, y);
+    if (lane == 0) {
+        lossrow[row] = sel ? -logpy : 0.f;
+        corrrow[row] = (sel && bi == y) ? 1.f : 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Backward (first order)
+// ---------------------------------------------------------------------------
+
+// dH2 = Â dO;  dY0 = (dH2 W1) ⊙ D1 ⊙ [Y0 > 0].  Outer mode: emit factor (dO, H2).
+__global__ __launch_bounds__(256) void bwd_layer2_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ d_o, const float* __restrict__ y0, float* __restrict__ dh2,
+    float* __restrict__ dy0, GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off,
+    int train, float keep, float scale, const float* __restrict__ o_in, const float* __restrict__ h2,
+    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const float g2 = agg_row(rp, col, s, d_o, row, lane);  // zero past c (dO is)
+    dh2[row * HID + lane] = g2;
+    float dh1d = 0.f;
+    for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
+    float mask = y0[row * HID + lane] > 0.f ? 1.f : 0.f;
+    if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    dy0[row * HID + lane] = dh1d * mask;
+    if (U != nullptr)  // outer graph, use 2: G = dO, Z = H2, Y = O, ÂG = dH2
+        emit_factor(U, V, ldk, R, foff, fwidth, row, lane, s[row], d_o[row * HID + lane],
+                    h2[row * HID + lane], o_in[row * HID + lane], g2);
+}
+
+// dH0 = Â dY0.  Outer mode: emit factor (dY0, H0).
+__global__ __launch_bounds__(256) void bwd_layer1_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ dy0, float* __restrict__ dh0, const float* __restrict__ y0,
+    const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
+    float* __restrict__ R, int foff) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const float g = agg_row(rp, col, s, dy0, row, lane);
+    dh0[row * HID + lane] = g;
+    if (U != nullptr)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
+        emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dy0[row * HID + lane],
+                    h0[row * HID + lane], y0[row * HID + lane], g);
+}
+
+// ---------------------------------------------------------------------------
+// Column reductions over nodes (deterministic two-stage): per block partials of
+//   A[c][h] = Σ_i (a1[i][c] b1[i][h] + a2[i][c] b2[i][h])   (c < c_n, h < 16)
+//   v1[h]   = Σ_i x1[i][h],  v2[h] = Σ_i x2[i][h]
+//   l0 = Σ_i l[i], l1 = Σ_i q[i]
+// Layout of a partial: [A (16×16) | v1 (16) | v2 (16) | l0 | l1 | pad to 304].
+// ---------------------------------------------------------------------------
+constexpr int kRedLen = 16 * 16 + 16 + 16 + 16;  // 304 floats per partial
+
+__global__ __launch_bounds__(256) void colreduce_kernel(
+    int n, int c_n, const float* __restrict__ a1, const float* __restrict__ b1,
+    const float* __restrict__ a2, const float* __restrict__ b2, const float* __restrict__ x1,
+    const float* __restrict__ x2, const float* __restrict__ l, const float* __restrict__ q,
+    float* __restrict__ partials, int rows_per_block) {
+    __shared__ float red[RG][kRedLen];
+    const int lane = threadIdx.x & (HID - 1);
+    const int grp = threadIdx.x / HID;
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(n, r0 + rows_per_block);
+    float acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+    float s1 = 0.f, s2 = 0.f, sl = 0.f, sq = 0.f;
+    for (int i = r0 + grp; i < r1; i += RG) {
+        const float bh1 = b1 ? b1[i * HID + lane] : 0.f;
+        const float bh2 = b2 ? b2[i * HID + lane] : 0.f;
+        const float av1 = a1 ? a1[i * HID + lane] : 0.f;
+        const float av2 = a2 ? a2[i * HID + lane] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k < c_n) {
+                acc[k] = fmaf(bcast16(av1, k), bh1, acc[k]);
+                acc[k] = fmaf(bcast16(av2, k), bh2, acc[k]);
+            }
+        }
+        if (x1) s1 += x1[i * HID + lane];
+        if (x2) s2 += x2[i * HID + lane];
+        if (lane == 0) {
+            if (l) sl += l[i];
+            if (q) sq += q[i];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[grp][k * 16 + lane] = acc[k];
+    red[grp][256 + lane] = s1;
+    red[grp][272 + lane] = s2;
+    if (lane >= 2) red[grp][288 + lane] = 0.f;
+    if (lane == 0) {
+        red[grp][288] = sl;
+        red[grp][289] = sq;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kRedLen; e += 256) {
+        float t = 0.f;
+        for (int g = 0; g < RG; ++g) t += red[g][e];
+        partials[(int64_t)blockIdx.x * kRedLen + e] = t;
+    }
+}
+
+// Sum the partials in block order; scatter into destinations (+= or =).
+//   A -> dst_a[c][h] (c < c_n), v1 -> dst_v1[h], v2 -> dst_v2[c] (c < c_n
+//   when v2_is_class else 16), l0 -> dst_l[0], l1 -> dst_l[1].
+__global__ __launch_bounds__(320) void colreduce_final_kernel(
+    const float* __restrict__ partials, int nblocks, int c_n, float* __restrict__ dst_a,
+    float* __restrict__ dst_v1, int v1_width, float* __restrict__ dst_v2, int v2_width,
+    float* __restrict__ dst_l, int accumulate) {
+    const int e = threadIdx.x;
+    if (e >= kRedLen) return;
+    float t = 0.f;
+    for (int b = 0; b < nblocks; ++b) t += partials[(int64_t)b * kRedLen + e];
+    float* dst = nullptr;
+    if (e < 256) {
+        const int k = e / 16;
+        if (dst_a && k < c_n) dst = dst_a + e;
+    } else if (e < 272) {
+        if (dst_v1 && e - 256 < v1_width) dst = dst_v1 + (e - 256);
+    } else if (e < 288) {
+        if (dst_v2 && e - 272 < v2_width) dst = dst_v2 + (e - 272);
+    } else if (e < 290) {
+        if (dst_l) dst = dst_l + (e - 288);
+    }
+    if (dst) *dst = accumulate ? *dst + t : t;
+}
+
+// ---------------------------------------------------------------------------
+// Differentiable Adam (higher's rule) forward and reverse, per parameter.
+//   g' = g + wd·w (first n_wd entries);  m1 = β1 m0 + (1-β1) g';
+//   v1 = β2 v0 + (1-β2) g'²;  w1 = w0 - (lr/bc1) m1 / (sqrt(v1)/sqrt(bc2) + eps)
+// ---------------------------------------------------------------------------
+struct AdamHyper {
+    float lr, beta1, beta2, eps, wd;
+    float omb1, omb2;  // float(1 - β) computed in double, as Python evaluates `1 - beta`
+    int n_wd;          // parameters [0, n_wd) carry weight decay (group 0)
+};
+
+// bias corrections in double from the double β's, as Python computes them
+__device__ __forceinline__ void adam_consts(const EngineScalars* sc, int step_off, const AdamHyper& hp,
+                                            const double* betas, float& step_size, float& c2, int& step) {
+    step = sc->adam_step + step_off + 1;
+    const double bc1 = 1.0 - pow(betas[0], (double)step);
+    const double bc2 = 1.0 - pow(betas[1], (double)step);
+    step_size = (float)(betas[2] / bc1);
+    c2 = (float)sqrt(bc2);
+}
+
+__global__ __launch_bounds__(256) void adam_fwd_kernel(
+    int np, const float* __restrict__ w0, const float* __restrict__ g, const float* __restrict__ m0,
+    const float* __restrict__ v0, float* __restrict__ w1, float* __restrict__ m1, float* __restrict__ v1,
+    float* __restrict__ gp_out, AdamHyper hp, const double* __restrict__ betas,
+    const EngineScalars* __restrict__ sc, int step_off) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= np) return;
+    float step_size, c2;
+    int step;
+    adam_consts(sc, step_off, hp, betas, step_size, c2, step);
+    const float w = w0[e];
+    float gp = g[e];
+    if (e < hp.n_wd && hp.wd != 0.f) gp = gp + hp.wd * w;
+    const float m = m0[e] * hp.beta1 + hp.omb1 * gp;
+    const float v = v0[e] * hp.beta2 + (hp.omb2 * gp) * gp;
+    const float denom = sqrtf(v) / c2 + hp.eps;
+    // torch CPU addcdiv: self + (value * t1) / t2
+    w1[e] = w + ((-step_size) * m) / denom;
+    m1[e] = m;
+    v1[e] = v;
+    if (gp_out) gp_out[e] = gp;
+}
+
+// Reverse of one Adam step.  In: wbar (adjoint of w1, updated in place to the
+// adjoint of w0's direct + weight-decay paths), mbar/vbar (adjoints of m1/v1,
+// updated in place to those of m0/v0), m1, v1, g' of the step.  Out: gbar
+// (adjoint of the data gradient g — fed to the Hessian-vector reverse).
+__global__ __launch_bounds__(256) void adam_rev_kernel(
+    int np, float* __restrict__ wbar, float* __restrict__ mbar, float* __restrict__ vbar,
+    const float* __restrict__ m1, const float* __restrict__ v1, const float* __restrict__ gp,
+    float* __restrict__ gbar, AdamHyper hp, const double* __restrict__ betas,
+    const EngineScalars* __restrict__ sc, int step_off) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= np) return;
+    float step_size, c2;
+    int step;
+    adam_consts(sc, step_off, hp, betas, step_size, c2, step);
+    const float wb = wbar[e];
+    const float m = m1[e], v = v1[e], g = gp[e];
+    const float sq = sqrtf(v);
+    const float denom = sq / c2 + hp.eps;
+    // w1 = w0 + (α m) / denom,  α = -step_size  (torch's addcdiv backward formulas)
+    const float alpha = -step_size;
+    const float mb = mbar[e] + wb * alpha / denom;            // total adjoint of m1
+    const float db = -wb * alpha * m / (denom * denom);       // adjoint of denom
+    float vb = vbar[e] + (db / c2) / (2.f * sq);               // sqrt backward: grad / (2 result)
+    if (v == 0.f) vb = 0.f;  // higher's _maybe_mask hook on exp_avg_sq
+    const float gb = hp.omb1 * mb + 2.f * (hp.omb2 * g) * vb;
+    gbar[e] = gb;
+    mbar[e] = hp.beta1 * mb;
+    vbar[e] = hp.beta2 * vb;
+    if (e < hp.n_wd && hp.wd != 0.f) wbar[e] = wb + hp.wd * gb;
+}
+
+// ---------------------------------------------------------------------------
+// Reverse of the inner backward (Hessian-vector part), three aggregation
+// kernels; see DESIGN.md §4 for the adjoint equations.
+// ---------------------------------------------------------------------------
+
+// dY0bar = Â dH0bar.  Factor use 4 (G = dH0bar, Z = dY0, Y = dH0, ÂG = dY0bar).
+// dH1dbar = dY0bar ⊙ D1 ⊙ [Y0 > 0]
+// dH2bar  = dH1dbar W1ᵀ + H1d ḡW1ᵀ + ḡb1
+// H1dbar_part = dH2 ḡW1
+__global__ __launch_bounds__(256) void rev_a_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ dh0bar, const float* __restrict__ dy0, const float* __restrict__ dh0,
+    const float* __restrict__ y0, const float* __restrict__ h1d, const float* __restrict__ dh2,
+    GcnW w, const float* __restrict__ gw1bar, const float* __restrict__ gb1bar, int c,
+    float* __restrict__ dh1dbar, float* __restrict__ dh2bar, float* __restrict__ h1dbar,
+    Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
+    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const int ix = row * HID + lane;
+    const float ag = agg_row(rp, col, s, dh0bar, row, lane);  // dY0bar
+    emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
+    float mask = y0[ix] > 0.f ? 1.f : 0.f;
+    if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    const float a = ag * mask;  // dH1dbar
+    dh1dbar[ix] = a;
+    const float hd = h1d[ix];
+    float out = 0.f;
+    for (int k = 0; k < c; ++k) {
+        const float t = gsum16(a * w.w1[k * HID + lane] + hd * gw1bar[k * HID + lane]);
+        if (lane == k) out = t + gb1bar[k];
+    }
+    dh2bar[ix] = out;
+    const float g2 = dh2[ix];
+    float hb = 0.f;
+    for (int k = 0; k < c; ++k) hb = fmaf(bcast16(g2, k), gw1bar[k * HID + lane], hb);
+    h1dbar[ix] = hb;
+}
+
+// dObar = Â dH2bar.  Factor use 3 (G = dH2bar, Z = dO, Y = dH2, ÂG = dObar).
+// Obar = P ⊙ (ū - P·ū), ū = dObar ⊙ m / |m|   (softmax Jacobian of dO = (P - E) m/|m|)
+__global__ __launch_bounds__(256) void rev_b_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ dh2bar, const float* __restrict__ d_o, const float* __restrict__ dh2,
+    const float* __restrict__ p, const uint8_t* __restrict__ mask, float inv_count, int c,
+    float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
+    float* __restrict__ R, int foff, int cw) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const int ix = row * HID + lane;
+    const float ag = agg_row(rp, col, s, dh2bar, row, lane);  // dObar
+    emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
+    const bool sel = mask[row] != 0;
+    const float ub = (sel && lane < c) ? ag * inv_count : 0.f;
+    const float pv = p[ix];
+    const float dot = gsum16(ub * pv);
+    obar[ix] = (lane < c) ? pv * (ub - dot) : 0.f;
+}
+
+// H2bar = Â Obar.  Factor use 2 (G = Obar, Z = H2, Y = O, ÂG = H2bar).
+// H1dbar = H1dbar_part + H2bar W1;  Y0bar = H1dbar ⊙ D1 ⊙ [Y0 > 0]
+__global__ __launch_bounds__(256) void rev_c_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ obar, const float* __restrict__ h2, const float* __restrict__ o,
+    const float* __restrict__ h1dbar_part, const float* __restrict__ y0, GcnW w, int c,
+    float* __restrict__ h2bar, float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc,
+    int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
+    int ldk, float* __restrict__ R, int foff, int cw) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const int ix = row * HID + lane;
+    const float ag = agg_row(rp, col, s, obar, row, lane);  // H2bar (zero past c)
+    emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
+    h2bar[ix] = ag;
+    float hb = h1dbar_part[ix];
+    for (int k = 0; k < c; ++k) hb = fmaf(bcast16(ag, k), w.w1[k * HID + lane], hb);
+    float mask = y0[ix] > 0.f ? 1.f : 0.f;
+    if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    y0bar[ix] = hb * mask;
+}
+
+// H0bar = Â Y0bar.  Factor use 1 (G = Y0bar, Z = H0, Y = Y0, ÂG = H0bar).
+__global__ __launch_bounds__(256) void rev_d_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ y0bar, const float* __restrict__ h0, const float* __restrict__ y0,
+    float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
+    float* __restrict__ R, int foff) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    if (row >= n) return;
+    const int ix = row * HID + lane;
+    const float ag = agg_row(rp, col, s, y0bar, row, lane);
+    emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
+    h0bar[ix] = ag;
+}
+
+// θ <- clamp(θ - lr·g, 0, 1) with lr from the scalars, then StepLR: lr *= γ.
+__global__ void sgd_clamp_dev_kernel(float* __restrict__ theta, const float* __restrict__ grad,
+                                     int64_t count, const EngineScalars* __restrict__ sc) {
+    const float lr = (float)sc->outer_lr;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count; e += stride)
+        theta[e] = fminf(fmaxf(fmaf(-lr, grad[e], theta[e]), 0.f), 1.f);
+}
+
+// Advance the device scalars after a window: graph/forward counters, Adam
+// step, hyper step count and the StepLR learning rate.
+__global__ void advance_kernel(EngineScalars* sc, int graphs, int forwards, int adam_steps, int hypers) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        sc->graph_ctr += graphs;
+        sc->fwd_ctr += forwards;
+        sc->adam_step += adam_steps;
+        for (int h = 0; h < hypers; ++h) {
+            sc->hyper_steps += 1;
+            sc->outer_lr = sc->outer_lr * sc->lr_decay;
+        }
+    }
+}
+
+}  // namespace lds
+
+using namespace lds;
+
+// ---------------------------------------------------------------------------
+// C-ABI (see include/ldsgnn.h, "Fused engine")
+// ---------------------------------------------------------------------------
+static inline int rows_blocks(int n) { return (n + RG - 1) / RG; }
+static inline Keys mk_keys(uint64_t seed, uint32_t tag_x, uint32_t tag_h) {
+    return Keys{(uint32_t)seed, (uint32_t)(seed >> 32), tag_x, tag_h};
+}
+
+extern "C" int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int n,
+                                   const float* wt, const float* bias, float* out, uint64_t seed,
+                                   uint32_t tag_x, const void* scalars, int fwd_off, int train,
+                                   float keep, float scale, void* stream) {
+    LDS_CHECK_ARG(xrp && xcol && xval && wt && out && scalars && n > 0);
+    hipLaunchKernelGGL(x_linear_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, xrp,
+                       xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0),
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int fin,
+                                    const float* d, float* out, const float* w, float wd,
+                                    int accumulate, uint64_t seed, uint32_t tag_x, const void* scalars,
+                                    int fwd_off, int train, float keep, float scale, void* stream) {
+    LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && fin > 0);
+    hipLaunchKernelGGL(xt_linear_kernel, dim3(rows_blocks(fin)), dim3(256), 0, (hipStream_t)stream,
+                       xcp, xrow, xval, fin, d, out, w, wd, accumulate, mk_keys(seed, tag_x, 0),
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, int n,
+                                     const float* h0, float* y0, float* h1d, float* h2,
+                                     const float* w1, const float* b1, int c, uint64_t seed,
+                                     uint32_t tag_h, const void* scalars, int fwd_off, int train,
+                                     float keep, float scale, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && h0 && y0 && h1d && h2 && w1 && b1 && scalars && n > 0);
+    LDS_CHECK_ARG(c > 0 && c <= HID);
+    GcnW w{nullptr, nullptr, w1, b1};
+    hipLaunchKernelGGL(fwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+                       col, s, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, int n,
+                                     const float* h2, float* o, float* p, float* d_o,
+                                     const int* label, const uint8_t* mask, float inv_count,
+                                     float* lossrow, float* corrrow, int c, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && h2 && label && lossrow && corrrow && n > 0 && c > 0 && c <= HID);
+    hipLaunchKernelGGL(fwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+                       col, s, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, int n,
+                                     const float* d_o, const float* y0, float* dh2, float* dy0,
+                                     const float* w1, int c, uint64_t seed, uint32_t tag_h,
+                                     const void* scalars, int fwd_off, int train, float keep,
+                                     float scale, const float* o, const float* h2, float* U, float* V,
+                                     int ldk, float* R, int foff, int fwidth, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && d_o && y0 && dh2 && dy0 && w1 && scalars && n > 0);
+    LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && o && h2 && fwidth <= HID)));
+    GcnW w{nullptr, nullptr, w1, nullptr};
+    hipLaunchKernelGGL(bwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+                       col, s, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
+                       foff, fwidth);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, int n,
+                                     const float* dy0, float* dh0, const float* y0, const float* h0,
+                                     float* U, float* V, int ldk, float* R, int foff, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && n > 0);
+    LDS_CHECK_ARG(U == nullptr || (V && R && y0 && h0));
+    hipLaunchKernelGGL(bwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+                       col, s, n, dy0, dh0, y0, h0, U, V, ldk, R, foff);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_colreduce(int n, int c_n, const float* a1, const float* b1, const float* a2,
+                                    const float* b2, const float* x1, const float* x2, const float* l,
+                                    const float* q, float* partials, int nblocks, float* dst_a,
+                                    float* dst_v1, int v1_width, float* dst_v2, int v2_width,
+                                    float* dst_l, int accumulate, void* stream) {
+    LDS_CHECK_ARG(partials && n > 0 && nblocks > 0 && c_n >= 0 && c_n <= HID);
+    const int rpb = (n + nblocks - 1) / nblocks;
+    hipLaunchKernelGGL(colreduce_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, n, c_n, a1,
+                       b1, a2, b2, x1, x2, l, q, partials, rpb);
+    hipLaunchKernelGGL(colreduce_final_kernel, dim3(1), dim3(320), 0, (hipStream_t)stream, partials,
+                       nblocks, c_n, dst_a, dst_v1, v1_width, dst_v2, v2_width, dst_l, accumulate);
+    LDS_RETURN_LAST_ERROR();
+}
+
+// `hyper` = {lr, beta1, beta2, eps, weight_decay} as doubles (Python floats); the
+// kernels use float(x) of each, float(1 - beta) and the double bias corrections.
+static AdamHyper mk_adam(const double* h, int n_wd) {
+    return AdamHyper{(float)h[0], (float)h[1], (float)h[2], (float)h[3], (float)h[4],
+                     (float)(1.0 - h[1]), (float)(1.0 - h[2]), n_wd};
+}
+
+extern "C" int lds_engine_adam(int np, const float* w0, const float* g, const float* m0,
+                               const float* v0, float* w1, float* m1, float* v1, float* gp_out,
+                               const double* hyper, const double* betas_dev, int n_wd,
+                               const void* scalars, int step_off, void* stream) {
+    LDS_CHECK_ARG(np > 0 && w0 && g && m0 && v0 && w1 && m1 && v1 && scalars && hyper && betas_dev);
+    hipLaunchKernelGGL(adam_fwd_kernel, dim3((np + 255) / 256), dim3(256), 0, (hipStream_t)stream, np,
+                       w0, g, m0, v0, w1, m1, v1, gp_out, mk_adam(hyper, n_wd), betas_dev,
+                       (const EngineScalars*)scalars, step_off);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_adam_reverse(int np, float* wbar, float* mbar, float* vbar, const float* m1,
+                                       const float* v1, const float* gp, float* gbar,
+                                       const double* hyper, const double* betas_dev, int n_wd,
+                                       const void* scalars, int step_off, void* stream) {
+    LDS_CHECK_ARG(np > 0 && wbar && mbar && vbar && m1 && v1 && gp && gbar && scalars && hyper);
+    LDS_CHECK_ARG(betas_dev != nullptr);
+    hipLaunchKernelGGL(adam_rev_kernel, dim3((np + 255) / 256), dim3(256), 0, (hipStream_t)stream, np,
+                       wbar, mbar, vbar, m1, v1, gp, gbar, mk_adam(hyper, n_wd), betas_dev,
+                       (const EngineScalars*)scalars, step_off);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, int n,
+                                const float* dh0bar, const float* dy0, const float* dh0,
+                                const float* y0, const float* h1d, const float* dh2, const float* w1,
+                                const float* gw1bar, const float* gb1bar, int c, float* dh1dbar,
+                                float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
+                                const void* scalars, int fwd_off, int train, float keep, float scale,
+                                float* U, float* V, int ldk, float* R, int foff, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && dh0bar && dy0 && dh0 && y0 && h1d && dh2 && w1 && gw1bar && gb1bar);
+    LDS_CHECK_ARG(dh1dbar && dh2bar && h1dbar && scalars && U && V && R && n > 0 && c > 0 && c <= HID);
+    GcnW w{nullptr, nullptr, w1, nullptr};
+    hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar, h1dbar,
+                       mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
+                       scale, U, V, ldk, R, foff);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, int n,
+                                const float* dh2bar, const float* d_o, const float* dh2, const float* p,
+                                const uint8_t* mask, float inv_count, int c, float* obar, float* U,
+                                float* V, int ldk, float* R, int foff, int cw, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && dh2bar && d_o && dh2 && p && mask && obar && U && V && R && n > 0);
+    LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID);
+    hipLaunchKernelGGL(rev_b_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, int n,
+                                const float* obar, const float* h2, const float* o,
+                                const float* h1dbar_part, const float* y0, const float* w1, int c,
+                                float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
+                                const void* scalars, int fwd_off, int train, float keep, float scale,
+                                float* U, float* V, int ldk, float* R, int foff, int cw, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && obar && h2 && o && h1dbar_part && y0 && w1 && h2bar && y0bar);
+    LDS_CHECK_ARG(scalars && U && V && R && n > 0 && c > 0 && c <= HID && cw >= c && cw <= HID);
+    GcnW w{nullptr, nullptr, w1, nullptr};
+    hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar, mk_keys(seed, 0, tag_h),
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff,
+                       cw);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_rev_d(const int* rp, const int* col, const float* s, int n,
+                                const float* y0bar, const float* h0, const float* y0, float* h0bar,
+                                float* U, float* V, int ldk, float* R, int foff, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && n > 0);
+    hipLaunchKernelGGL(rev_d_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_sgd_clamp(float* theta, const float* grad, int64_t count, const void* scalars,
+                                    void* stream) {
+    LDS_CHECK_ARG(theta && grad && scalars && count >= 0);
+    if (count == 0) return 0;
+    const int64_t b = (count + 255) / 256;
+    hipLaunchKernelGGL(sgd_clamp_dev_kernel, dim3((unsigned)(b < 8192 ? b : 8192)), dim3(256), 0,
+                       (hipStream_t)stream, theta, grad, count, (const EngineScalars*)scalars);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_advance(void* scalars, int graphs, int forwards, int adam_steps, int hypers,
+                                  void* stream) {
+    LDS_CHECK_ARG(scalars != nullptr);
+    hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       (EngineScalars*)scalars, graphs, forwards, adam_steps, hypers);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_scalars_size(void) { return (int)sizeof(EngineScalars); }

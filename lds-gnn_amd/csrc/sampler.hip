@@ -22,10 +22,11 @@ namespace lds {
 // kernel needs neither atomics nor a memset.
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
-    uint32_t counter, const float* __restrict__ u_inj, uint64_t* __restrict__ bits,
-    int words, int ntiles) {
+    uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
+    uint64_t* __restrict__ bits, int words, int ntiles) {
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= ntiles) return;  // wave-uniform
+    if (counter_base != nullptr) counter += *counter_base;  // device-resident draw counter
     const int lane = wave_lane();
     int a, b;
     tri_tile(tile, a, b);
@@ -205,7 +206,20 @@ extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint
     const int ntiles = nb * (nb + 1) / 2;
     hipLaunchKernelGGL(sample_tiles_kernel, dim3((ntiles + 3) / 4), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter, u_inject, bits, words, ntiles);
+                       counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, uint32_t tag,
+                                      const uint32_t* counter_base, uint32_t counter_offset,
+                                      uint64_t* bits, int words, void* stream) {
+    LDS_CHECK_ARG(theta != nullptr && bits != nullptr && counter_base != nullptr);
+    LDS_CHECK_ARG(n > 0 && n <= (1 << 20) && words >= (n + 63) / 64);
+    const int nb = (n + 63) / 64;
+    const int ntiles = nb * (nb + 1) / 2;
+    hipLaunchKernelGGL(sample_tiles_kernel, dim3((ntiles + 3) / 4), dim3(256), 0,
+                       (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles);
     LDS_RETURN_LAST_ERROR();
 }
 

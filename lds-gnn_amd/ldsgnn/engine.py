@@ -1,0 +1,450 @@
+"""Fused LDS engine: the bilevel hot path as hand-written HIP kernels.
+
+What it replaces (LDS configuration of the reference):
+  * an inner step — InnerProblemTrainer.train_step (src/trainers/inner.py:55-74):
+    sample A ~ θ, GCN forward, NLL on the train mask, create_graph backward,
+    higher's differentiable Adam step;
+  * a hyper step — OuterProblemTrainer.train_step (src/trainers/outer.py:57-87):
+    fresh sample, forward with the current weights, NLL on opt_mask,
+    loss.backward through the outer graph and every unrolled inner step since
+    the last detach, SGD on θ, StepLR, clamp; then both trainers detach
+    (src/trainers/bilevel.py:109-114).
+
+How: autograd is replaced by a hand-derived reverse pass.  Each
+inner step records a tape slot (graph CSR + s, 10 n×16 activation arrays,
+w/m/v/g' of the Adam step).  The hyper step runs the outer forward/backward,
+then walks the tape backwards: Adam reverse → Hessian-vector reverse of the
+backward (4 aggregations, 2 X-products, 1 reduction); every aggregation emits
+its θ-gradient factor pair, and ONE lds_theta_grad call (rank K = 48 per inner
+graph + 24 outer at C = 7) assembles the window's dθ, followed by SGD + clamp
+with the device-resident learning rate.  RNG counters, the Adam step and the
+learning rate live on the device, so `capture_window()` records a whole
+τ-window (τ inner steps + the hyper step) as one HIP graph that replays with
+advancing state.
+
+Layout: per-node arrays are n × 16 fp32 (hidden 16; classes padded to 16);
+parameters are one flat vector [W0ᵀ (fin×16) | b0 (16) | W1 (C×16) | b1 (C)].
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .rng import TAG_DROP_H, TAG_DROP_X, TAG_GRAPH, Generator, tag_for
+
+HID = 16
+_RED_LEN = 304
+_ACT = ("h0", "y0", "h1d", "h2", "o", "p", "d_o", "dh2", "dy0", "dh0")
+
+
+class _Graph:
+    """Device buffers of one sampled graph (CSR with self-loops + s)."""
+
+    def __init__(self, n: int, cap: int, dev):
+        self.row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        self.col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        self.s = torch.empty(n, dtype=torch.float32, device=dev)
+
+
+class _Slot:
+    """Tape of one inner step (or the outer step): graph + activations."""
+
+    def __init__(self, n: int, cap: int, dev):
+        self.g = _Graph(n, cap, dev)
+        for a in _ACT:
+            setattr(self, a, torch.zeros((n, HID), dtype=torch.float32, device=dev))
+        self.lossrow = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.corrrow = torch.zeros(n, dtype=torch.float32, device=dev)
+
+
+def _csr_of(dense: torch.Tensor):
+    sp = dense.to_sparse_csr()
+    return (sp.crow_indices().to(torch.int32).contiguous(), sp.col_indices().to(torch.int32).contiguous(),
+            sp.values().to(torch.float32).contiguous())
+
+
+class LdsEngine:
+    """One replica of the LDS bilevel problem, resident on one GPU."""
+
+    def __init__(self, x: torch.Tensor, y: torch.Tensor, train_mask: torch.Tensor, opt_mask: torch.Tensor,
+                 theta: torch.Tensor, num_classes: int, dropout: float = 0.5, gcn_lr: float = 0.01,
+                 gcn_wd: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8, outer_lr: float = 1.0,
+                 lr_decay: Optional[float] = None, tau: int = 5, generator: Optional[Generator] = None,
+                 params: Optional["OrderedDict[str, torch.Tensor]"] = None):
+        nat.require_device(x, "LdsEngine")
+        dev = x.device
+        self.dev = dev
+        self.n, self.fin = int(x.shape[0]), int(x.shape[1])
+        self.c = int(num_classes)
+        if not (0 < self.c <= HID):
+            raise NotImplementedError(f"LdsEngine supports 1..{HID} classes")
+        n, fin, c = self.n, self.fin, self.c
+        if theta.numel() != n * (n + 1) // 2 or theta.dtype != torch.float32 or not theta.is_contiguous():
+            raise ValueError("theta must be the contiguous float32 packed upper triangle of an n×n matrix")
+        self.theta = theta  # updated in place (the BernoulliGraphModel.probs storage)
+        self.dropout = float(dropout)
+        self.keep = float(np.float32(1.0) - np.float32(self.dropout))
+        self.scale = float(np.float32(1.0) / np.float32(self.keep)) if self.keep > 0 else 0.0
+        self.train_flag = 1 if self.dropout > 0.0 else 0
+        self.hyper_np = np.array([gcn_lr, betas[0], betas[1], eps, gcn_wd], dtype=np.float64)
+        self.betas_dev = torch.tensor([betas[0], betas[1], gcn_lr], dtype=torch.float64, device=dev)
+        self.gen = generator or Generator(0, 0)
+        rep = self.gen.replica
+        self.seed = self.gen.seed
+        self.tag_graph = tag_for(TAG_GRAPH, rep)
+        self.tag_x = tag_for(TAG_DROP_X, rep)
+        self.tag_h = tag_for(TAG_DROP_H, rep)
+
+        # data
+        self.xrp, self.xcol, self.xval = _csr_of(x.float())
+        self.xcp, self.xrow, self.xtval = _csr_of(x.float().t().contiguous())
+        self.label = y.to(device=dev, dtype=torch.int32).contiguous()
+        self.train_mask = train_mask.to(device=dev, dtype=torch.uint8).contiguous()
+        self.opt_mask = opt_mask.to(device=dev, dtype=torch.uint8).contiguous()
+        self.inv_train = float(np.float32(1.0) / np.float32(int(train_mask.sum())))
+        self.inv_opt = float(np.float32(1.0) / np.float32(int(opt_mask.sum())))
+
+        # parameter layout
+        self.np = fin * HID + HID + c * HID + c
+        self.off_b0 = fin * HID
+        self.off_w1 = self.off_b0 + HID
+        self.off_b1 = self.off_w1 + c * HID
+        self.n_wd = self.off_w1  # group 0 = layer_in (weight + bias)
+
+        # device scalars {u32 graph_ctr, u32 fwd_ctr, i32 adam_step, i32 hyper, f64 lr, f64 decay}
+        assert nat.lib.lds_engine_scalars_size() == 32
+        self.scalars = torch.zeros(32, dtype=torch.uint8, device=dev)
+        self._i32 = self.scalars[:16].view(torch.int32)
+        self._f64 = self.scalars[16:].view(torch.float64)
+        self._i32.copy_(torch.tensor([self.gen.graph_counter, self.gen.forward_counter, 0, 0], dtype=torch.int32))
+        self._f64.copy_(torch.tensor([outer_lr, 1.0 if lr_decay is None else lr_decay], dtype=torch.float64))
+
+        # graph buffers
+        self.cap = n * n if n * n <= (1 << 27) else None
+        if self.cap is None:
+            raise NotImplementedError("LdsEngine at n > 11585 needs exact CSR sizing (not yet)")
+        self.words = nat.lib.lds_bitmask_words(n)
+        self.bits = torch.empty((n, self.words), dtype=torch.int64, device=dev)
+        self.deg = torch.empty(n, dtype=torch.int32, device=dev)
+
+        # tape
+        self.tau = max(1, int(tau))
+        self.cw = (c + 3) & ~3
+        self.kg = 2 * HID + 2 * self.cw  # factor columns per inner graph
+        self.slots: List[_Slot] = []
+        self.w: List[torch.Tensor] = []
+        self.m: List[torch.Tensor] = []
+        self.v: List[torch.Tensor] = []
+        self.gp: List[torch.Tensor] = []
+        self._grow(self.tau)
+        self.outer = _Slot(n, self.cap, dev)
+        self.t = 0  # inner steps in the current window
+        self.pending_graph = 0
+        self.pending_fwd = 0
+
+        # reverse-pass buffers
+        z = lambda: torch.zeros((n, HID), dtype=torch.float32, device=dev)  # noqa: E731
+        self.dh0bar, self.dh1dbar, self.dh2bar, self.h1dbar = z(), z(), z(), z()
+        self.obar, self.h2bar, self.y0bar, self.h0bar = z(), z(), z(), z()
+        zp = lambda: torch.zeros(self.np, dtype=torch.float32, device=dev)  # noqa: E731
+        self.wbar, self.mbar, self.vbar, self.gbar, self.g = zp(), zp(), zp(), zp(), zp()
+        self.nblocks = max(1, min(64, (n + 15) // 16))
+        self.partials = torch.zeros((self.nblocks, _RED_LEN), dtype=torch.float32, device=dev)
+        self._alloc_factors()
+        self.grad = torch.zeros_like(theta)
+        self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=dev)
+        self.eval_metrics = torch.zeros((64, 4), dtype=torch.float32, device=dev)
+        self._graph_capture = None
+        if params is not None:
+            self.set_params(params)
+        self.reset_optimizer()
+
+    # ------------------------------------------------------------------ setup
+    def _alloc_factors(self):
+        self.ktot = self.tau * self.kg + HID + self.cw
+        self.ldk = (self.ktot + 3) & ~3
+        self.U = torch.zeros((self.n, self.ldk), dtype=torch.float32, device=self.dev)
+        self.V = torch.zeros_like(self.U)
+        self.R = torch.zeros(self.n, dtype=torch.float32, device=self.dev)
+
+    def _grow(self, slots: int):
+        while len(self.slots) < slots:
+            self.slots.append(_Slot(self.n, self.cap, self.dev))
+        while len(self.w) < slots + 1:
+            for lst in (self.w, self.m, self.v):
+                lst.append(torch.zeros(self.np, dtype=torch.float32, device=self.dev))
+        while len(self.gp) < slots:
+            self.gp.append(torch.zeros(self.np, dtype=torch.float32, device=self.dev))
+
+    def _stream(self) -> int:
+        return nat.stream_of(self.dev)
+
+    def _views(self, flat: torch.Tensor):
+        c = self.c
+        return (flat[: self.off_b0], flat[self.off_b0:self.off_w1], flat[self.off_w1:self.off_b1],
+                flat[self.off_b1:self.off_b1 + c])
+
+    def set_params(self, params):
+        """Load reference-layout params (layer_in.fc.weight [16, fin], ...)."""
+        w = self.w[0]
+        w0t, b0, w1, b1 = self._views(w)
+        with torch.no_grad():
+            w0t.view(self.fin, HID).copy_(params["layer_in.fc.weight"].detach().t())
+            b0.copy_(params["layer_in.fc.bias"].detach())
+            w1.view(self.c, HID).copy_(params["layer_out.fc.weight"].detach())
+            b1.copy_(params["layer_out.fc.bias"].detach())
+        self.t = 0
+
+    def get_params(self) -> "OrderedDict[str, torch.Tensor]":
+        w0t, b0, w1, b1 = self._views(self.w[self.t])
+        return OrderedDict([
+            ("layer_in.fc.weight", w0t.view(self.fin, HID).t().contiguous()),
+            ("layer_in.fc.bias", b0.clone()),
+            ("layer_out.fc.weight", w1.view(self.c, HID).clone()),
+            ("layer_out.fc.bias", b1.clone()),
+        ])
+
+    def reset_optimizer(self):
+        """InnerProblemTrainer.reset_optimizer: fresh Adam state, step 0."""
+        self._flush()
+        cur = self.t
+        if cur != 0:
+            self.w[0].copy_(self.w[cur])
+        self.m[0].zero_()
+        self.v[0].zero_()
+        self._i32[2:3].zero_()
+        self.t = 0
+
+    def _flush(self, hypers: int = 0):
+        """Apply pending counter offsets to the device scalars."""
+        if self.pending_graph or self.pending_fwd or self.t or hypers:
+            nat.call("lds_engine_advance", nat.ptr(self.scalars), self.pending_graph, self.pending_fwd, self.t,
+                     hypers, self._stream())
+        self.pending_graph = 0
+        self.pending_fwd = 0
+
+    def sync_generator(self):
+        """Write the device draw counters back to the host Generator (sync)."""
+        self._flush_counters_only()
+        vals = self._i32.cpu().tolist()
+        self.gen.graph_counter, self.gen.forward_counter = int(vals[0]), int(vals[1])
+
+    def _flush_counters_only(self):
+        if self.pending_graph or self.pending_fwd:
+            nat.call("lds_engine_advance", nat.ptr(self.scalars), self.pending_graph, self.pending_fwd, 0, 0,
+                     self._stream())
+        self.pending_graph = 0
+        self.pending_fwd = 0
+
+    # --------------------------------------------------------------- pieces
+    def _sample(self, g: _Graph):
+        st = self._stream()
+        nat.call("lds_sample_bitmask_dev", nat.ptr(self.theta), self.n, self.seed, self.tag_graph,
+                 nat.ptr(self.scalars), self.pending_graph, nat.ptr(self.bits), self.words, st)
+        nat.call("lds_bitmask_degree", nat.ptr(self.bits), self.n, self.words, nat.ptr(self.deg), nat.ptr(g.s), st)
+        nat.call("lds_exclusive_scan", nat.ptr(self.deg), self.n, nat.ptr(g.row_ptr), st)
+        nat.call("lds_bitmask_fill_csr", nat.ptr(self.bits), self.n, self.words, nat.ptr(g.row_ptr),
+                 nat.ptr(g.col), self.cap, 0, st)
+        self.pending_graph += 1
+
+    def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int):
+        st, n, c = self._stream(), self.n, self.c
+        w0t, b0, w1, b1 = self._views(w)
+        g = sl.g
+        nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
+                 nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
+                 fwd_off, train, self.keep, self.scale, st)
+        nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.h0),
+                 nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
+                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, st)
+        nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.h2),
+                 nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
+                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, st)
+
+    def _backward(self, sl: _Slot, w: torch.Tensor, gout: torch.Tensor, train: int, fwd_off: int,
+                  metrics_row: torch.Tensor, outer_factors: bool):
+        """First-order backward into `gout` (data gradient, no weight decay)."""
+        st, n, c = self._stream(), self.n, self.c
+        _, _, w1, _ = self._views(w)
+        g = sl.g
+        go0t, gob0, gow1, gob1 = self._views(gout)
+        if outer_factors:
+            base = self.t * self.kg
+            U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
+        else:
+            base, U, V, R = 0, 0, 0, 0
+        nat.call("lds_engine_bwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.d_o),
+                 nat.ptr(sl.y0), nat.ptr(sl.dh2), nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h,
+                 nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2),
+                 U, V, self.ldk, R, base + HID, self.cw, st)
+        nat.call("lds_engine_bwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.dy0),
+                 nat.ptr(sl.dh0), nat.ptr(sl.y0), nat.ptr(sl.h0), U, V, self.ldk, R, base, st)
+        # gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
+        nat.call("lds_engine_colreduce", n, c, nat.ptr(sl.dh2), nat.ptr(sl.h1d), 0, 0, nat.ptr(sl.dh0),
+                 nat.ptr(sl.dh2), nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), nat.ptr(self.partials), self.nblocks,
+                 nat.ptr(gow1), nat.ptr(gob0), HID, nat.ptr(gob1), c, nat.ptr(metrics_row), 0, st)
+        nat.call("lds_engine_xt_linear", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self.xtval), self.fin,
+                 nat.ptr(sl.dh0), nat.ptr(go0t), 0, 0.0, 0, self.seed, self.tag_x, nat.ptr(self.scalars),
+                 fwd_off, train, self.keep, self.scale, st)
+
+    # ----------------------------------------------------------------- steps
+    def inner_step(self):
+        """One InnerProblemTrainer.train_step (sample + forward + backward +
+        differentiable Adam), recorded on the tape.  Metrics stay on device
+        (`metrics[t]` = [Σ NLL over train rows, #correct])."""
+        t = self.t
+        if t >= len(self.slots):
+            self._grow(t + 1)
+            self.tau = t + 1
+            self._alloc_factors()
+            self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=self.dev)
+        sl = self.slots[t]
+        self._sample(sl.g)
+        fwd_off = self.pending_fwd
+        self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off)
+        self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False)
+        if self.train_flag:
+            self.pending_fwd += 1
+        nat.call("lds_engine_adam", self.np, nat.ptr(self.w[t]), nat.ptr(self.g), nat.ptr(self.m[t]),
+                 nat.ptr(self.v[t]), nat.ptr(self.w[t + 1]), nat.ptr(self.m[t + 1]), nat.ptr(self.v[t + 1]),
+                 nat.ptr(self.gp[t]), self.hyper_np.ctypes.data, nat.ptr(self.betas_dev), self.n_wd,
+                 nat.ptr(self.scalars), t, self._stream())
+        self.t = t + 1
+        return self.metrics[t]
+
+    def hyper_step(self, grad_reducer=None):
+        """OuterProblemTrainer.train_step + both detaches.  Returns the device
+        metrics row [Σ NLL over opt rows, #correct]."""
+        st, n, c = self._stream(), self.n, self.c
+        T = self.t
+        if T * self.kg + HID + self.cw > self.ldk:
+            self._alloc_factors()
+        out = self.outer
+        self._sample(out.g)
+        fwd_off = self.pending_fwd
+        self.R.zero_()
+        self._forward(out, self.w[T], self.opt_mask, self.inv_opt, self.train_flag, fwd_off)
+        self._backward(out, self.w[T], self.wbar, self.train_flag, fwd_off, self.metrics[self.tau], True)
+        if self.train_flag:
+            self.pending_fwd += 1
+        self.mbar.zero_()
+        self.vbar.zero_()
+        for t in range(T - 1, -1, -1):
+            self._reverse_step(t)
+        k = T * self.kg + HID + self.cw
+        nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k, nat.ptr(self.R), 1, 1,
+                 nat.ptr(self.theta), n, nat.ptr(self.grad), 0, st)
+        if grad_reducer is not None:
+            grad_reducer(self.grad)
+        nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
+                 nat.ptr(self.scalars), st)
+        # detach: the window restarts from the latest weights / Adam state
+        self._flush(hypers=1)
+        if T:
+            self.w[0].copy_(self.w[T])
+            self.m[0].copy_(self.m[T])
+            self.v[0].copy_(self.v[T])
+        self.t = 0
+        return self.metrics[self.tau]
+
+    def _reverse_step(self, t: int):
+        st, n, c = self._stream(), self.n, self.c
+        sl, g = self.slots[t], self.slots[t].g
+        fwd_off = t if self.train_flag else 0  # forward counter of inner step t within the window
+        nat.call("lds_engine_adam_reverse", self.np, nat.ptr(self.wbar), nat.ptr(self.mbar), nat.ptr(self.vbar),
+                 nat.ptr(self.m[t + 1]), nat.ptr(self.v[t + 1]), nat.ptr(self.gp[t]), nat.ptr(self.gbar),
+                 self.hyper_np.ctypes.data, nat.ptr(self.betas_dev), self.n_wd, nat.ptr(self.scalars), t, st)
+        gw0t, gb0, gw1, gb1 = self._views(self.gbar)
+        _, _, w1, _ = self._views(self.w[t])
+        ww0t, wb0, ww1, wb1 = self._views(self.wbar)
+        base = t * self.kg
+        rp, cl, s = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s)
+        U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
+        tr = self.train_flag
+        nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
+                 nat.ptr(gw0t), nat.ptr(gb0), nat.ptr(self.dh0bar), self.seed, self.tag_x, nat.ptr(self.scalars),
+                 fwd_off, tr, self.keep, self.scale, st)
+        nat.call("lds_engine_rev_a", rp, cl, s, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
+                 nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
+                 nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
+                 nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldk, R,
+                 base + HID + 2 * self.cw, st)
+        nat.call("lds_engine_rev_b", rp, cl, s, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
+                 nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldk,
+                 R, base + HID + self.cw, self.cw, st)
+        nat.call("lds_engine_rev_c", rp, cl, s, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
+                 nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
+                 self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
+                 self.ldk, R, base + HID, self.cw, st)
+        nat.call("lds_engine_rev_d", rp, cl, s, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
+                 nat.ptr(self.h0bar), U, V, self.ldk, R, base, st)
+        nat.call("lds_engine_xt_linear", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self.xtval), self.fin,
+                 nat.ptr(self.h0bar), nat.ptr(ww0t), 0, 0.0, 1, self.seed, self.tag_x, nat.ptr(self.scalars),
+                 fwd_off, tr, self.keep, self.scale, st)
+        # W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
+        nat.call("lds_engine_colreduce", n, c, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar), nat.ptr(self.h2bar),
+                 nat.ptr(sl.h1d), nat.ptr(self.h0bar), nat.ptr(self.h2bar), 0, 0, nat.ptr(self.partials),
+                 self.nblocks, nat.ptr(ww1), nat.ptr(wb0), HID, nat.ptr(wb1), c, 0, 1, st)
+
+    # ------------------------------------------------------------- graphs
+    def run_window(self, tau: int):
+        """τ inner steps followed by the hyper step (eager)."""
+        for _ in range(tau):
+            self.inner_step()
+        return self.hyper_step()
+
+    def capture_window(self, tau: int):
+        """Record run_window(tau) as one HIP graph (state must be at a window
+        start).  Replays advance RNG counters, Adam step and lr on device."""
+        assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
+        if tau > len(self.slots):
+            self._grow(tau)
+            self.tau = tau
+            self._alloc_factors()
+            self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=self.dev)
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                self.run_window(tau)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        self._graph_capture = (graph, tau)
+        return graph
+
+    def replay(self, windows: int = 1):
+        graph, _ = self._graph_capture
+        for _ in range(windows):
+            graph.replay()
+
+    # ------------------------------------------------------------ metrics
+    def inner_metrics(self, t: int):
+        """(loss, acc) of inner step t of the last window (host sync)."""
+        row = self.metrics[t].cpu()
+        return float(row[0]) * self.inv_train, float(row[1]) * self.inv_train
+
+    def outer_metrics(self):
+        row = self.metrics[self.tau].cpu()
+        return float(row[0]) * self.inv_opt, float(row[1]) * self.inv_opt
+
+    def scalars_host(self):
+        i = self._i32.cpu().tolist()
+        f = self._f64.cpu().tolist()
+        return dict(graph_ctr=i[0], fwd_ctr=i[1], adam_step=i[2], hyper_steps=i[3], outer_lr=f[0], lr_decay=f[1])
+
+    @staticmethod
+    def window_columns(tau: int, c: int) -> int:
+        cw = (c + 3) & ~3
+        return tau * (2 * HID + 2 * cw) + HID + cw
+
+    def flops_theta_grad(self, tau: int) -> float:
+        return 4.0 * self.window_columns(tau, self.c) * (self.n * (self.n + 1) // 2)
+
+
+def _unused(*_):  # pragma: no cover
+    return math.nan

@@ -85,3 +85,44 @@ def run_product_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5
         theta_changed=float((theta_o - O.get_triu_values(prob["adj"])).abs().max()),
         losses=p_losses, outer=p_outer,
     )
+
+
+def run_engine_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5, seed=0, p_edge=0.05,
+                          hidden=16):
+    """Fused engine (ldsgnn.engine) vs the oracle on the same problem: per-step
+    inner losses, final GCN params, every θ-gradient and the final θ."""
+    import ldsgnn
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.models.gcn import MetaDenseGCN
+    prob = synthetic_problem(n, f_in, classes, seed, p_edge)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(f_in, hidden, classes, dropout=dropout)
+    params = OrderedDict((k, v.detach()) for k, v in gcn.named_parameters())
+    dev = "cuda"
+    theta = O.get_triu_values(prob["adj"]).to(dev).contiguous()
+    eng = LdsEngine(prob["x"].to(dev), prob["y"].to(dev), prob["train"].to(dev), prob["opt"].to(dev), theta,
+                    classes, dropout=dropout, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99, tau=tau,
+                    generator=ldsgnn.rng.Generator(seed, 0), params=OrderedDict((k, v.to(dev)) for k, v in params.items()))
+    oracle = O.LdsProblem(prob["x"], prob["y"], prob["train"], prob["val"], prob["test"], prob["opt"],
+                          O.get_triu_values(prob["adj"]), hidden=hidden, dropout_p=dropout, gcn_lr=0.01,
+                          gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99, rnd=O.Randomness(seed, 0), params=params)
+    e_losses, o_losses, gerr, grel = [], [], [], []
+    for step in range(steps):
+        t = eng.t
+        eng.inner_step()
+        e_losses.append(eng.inner_metrics(t)[0])
+        o_losses.append(oracle.inner_step(oracle.sample())[0])
+        if tau == 0 or step % tau == 0:
+            eng.hyper_step()
+            og = oracle.hyper_step()[2]
+            eg = eng.grad.detach().cpu()
+            gerr.append(float((eg - og).abs().max()))
+            grel.append(float((eg - og).abs().max() / og.abs().max().clamp(min=1e-30)))
+    eparams = eng.get_params()
+    perr = max(float((eparams[k].cpu() - oracle.params[k].detach()).abs().max()) for k in eparams)
+    return dict(max_loss_err=float(np.max(np.abs(np.array(e_losses) - np.array(o_losses)))),
+                max_param_err=perr, max_grad_err=max(gerr) if gerr else 0.0,
+                max_grad_rel=max(grel) if grel else 0.0,
+                max_theta_err=float((eng.theta.cpu() - oracle.theta.detach()).abs().max()),
+                theta_changed=float((oracle.theta.detach() - O.get_triu_values(prob["adj"])).abs().max()),
+                engine=eng, oracle=oracle)
