@@ -64,6 +64,30 @@ def build(args, rank, device):
     return data, BilevelProblemRunner(inner, outer, data), opt_mask
 
 
+def make_engine(runner, tau, world):
+    import ldsgnn
+    from ldsgnn.fused import engine_from_trainers
+    eng = engine_from_trainers(runner.inner_trainer, runner.outer_trainer, tau=tau,
+                               generator=ldsgnn.rng.default_generator)
+    reducer = None
+    if world > 1:
+        def reducer(grad):
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM)
+            grad.div_(world)
+    return eng, reducer
+
+
+def run_engine_windows(eng, reducer, windows, tau, use_graph):
+    """`windows` τ-windows (τ inner steps + hyper step each)."""
+    if use_graph:
+        eng.replay(windows)
+        return
+    for _ in range(windows):
+        for _ in range(tau):
+            eng.inner_step()
+        eng.hyper_step(grad_reducer=reducer)
+
+
 def run_steps(runner, start: int, count: int, tau: int) -> int:
     step = start
     for _ in range(count):
@@ -106,6 +130,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=11)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", default="lds_theta_grad", help="kernel for the roofline leg")
+    ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
+                    help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,10 +154,25 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    step = run_steps(runner, 0, args.warmup, args.tau)
+    use_engine = args.path == "engine"
+    if use_engine:
+        assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
+        eng, reducer = make_engine(runner, args.tau, world)
+        # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
+        eng.inner_step()
+        eng.hyper_step(grad_reducer=reducer)
+        use_graph = world == 1
+        if use_graph:
+            eng.capture_window(args.tau)
+        run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)
+    else:
+        step = run_steps(runner, 0, args.warmup, args.tau)
     barrier_sync()
     t0 = time.perf_counter()
-    step = run_steps(runner, step, args.steps, args.tau)
+    if use_engine:
+        run_engine_windows(eng, reducer, args.steps // args.tau, args.tau, use_graph)
+    else:
+        step = run_steps(runner, step, args.steps, args.tau)
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -142,11 +183,17 @@ def main():
 
     # roofline leg: the same K steps again with HIP events around the kernel
     nat.timer.enable(args.kernel)
-    step = run_steps(runner, step, args.steps, args.tau)
+    if use_engine:
+        run_engine_windows(eng, reducer, args.steps // args.tau, args.tau, False)
+    else:
+        step = run_steps(runner, step, args.steps, args.tau)
     ksum = nat.timer.summary()[args.kernel]
     nat.timer.disable()
-    g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
-    nnz = g.nnz()
+    if use_engine:
+        nnz = int(eng.outer.g.row_ptr[n].item())
+    else:
+        g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
+        nnz = g.nnz()
     tri = n * (n + 1) // 2
     if args.kernel == "lds_spmm_norm":
         f = 16
@@ -160,8 +207,12 @@ def main():
         achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
-    else:  # lds_theta_grad: rank-2k update of the packed triangle (k = 48 at C=7)
-        k = 16 + 8 + 8 + 16
+    else:  # lds_theta_grad: rank-2k update of the packed triangle
+        if use_engine:  # one launch per window: k = tau*(32 + 2*8) + 24 columns at C=7
+            from ldsgnn.engine import LdsEngine
+            k = LdsEngine.window_columns(args.tau, data.num_classes)
+        else:  # one launch per graph: 4 uses (16 + 8 + 8 + 16 columns)
+            k = 16 + 8 + 8 + 16
         flops = 4.0 * k * tri
         achieved = flops / (ksum["avg_us"] * 1e-6) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -180,7 +231,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": f"synthetic {args.dataset}-shaped (N={n}, F_in={data.num_features}, "
                     f"C={data.num_classes}), kNN-initialised theta",
-            "config": {"workload": f"{args.dataset}-lds-knn-init-S1-tau{args.tau}", "nodes": n,
+            "config": {"workload": f"{args.dataset}-lds-knn-init-S1-tau{args.tau}", "path": args.path, "nodes": n,
                        "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": 1, "parallelism": f"replicas{world}",
                        "sampled_nnz": nnz},
