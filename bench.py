@@ -129,7 +129,8 @@ def main():
     ap.add_argument("--seed", type=int, default=597905255 % (2 ** 31))
     ap.add_argument("--cpu-steps", type=int, default=11)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel", default="lds_theta_grad", help="kernel for the roofline leg")
+    ap.add_argument("--kernel", default="auto", help="entry point for the roofline leg (auto: the θ-grad "
+                    "assembly the path uses)")
     ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
                     help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
@@ -155,6 +156,8 @@ def main():
         torch.cuda.synchronize()
 
     use_engine = args.path == "engine"
+    if args.kernel == "auto":
+        args.kernel = "lds_theta_grad_sgd" if (use_engine and world == 1) else "lds_theta_grad"
     if use_engine:
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
         eng, reducer = make_engine(runner, args.tau, world)
@@ -207,7 +210,7 @@ def main():
         achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
-    else:  # lds_theta_grad: rank-2k update of the packed triangle
+    else:  # lds_theta_grad[_sgd]: rank-2k update of the packed triangle
         if use_engine:  # one launch per window: k = tau*(32 + 2*8) + 24 columns at C=7
             from ldsgnn.engine import LdsEngine
             k = LdsEngine.window_columns(args.tau, data.num_classes)

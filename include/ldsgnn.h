@@ -138,6 +138,21 @@ int lds_theta_grad(const float* u, const float* v, int ld, int k,
                    const float* r, int ldr, int nr, const float* theta, int n,
                    float* grad, int accumulate, void* stream);
 
+/* The same update on the fp32 VALU (the MFMA form above is the default);
+ * kept for A/B timing. */
+int lds_theta_grad_valu(const float* u, const float* v, int ld, int k,
+                        const float* r, int ldr, int nr, const float* theta, int n,
+                        float* grad, int accumulate, void* stream);
+
+/* lds_theta_grad fused with the outer update (single replica):
+ *   θ_ij = clamp(θ_ij - lr·g_ij, 0, 1),  lr = the engine scalars' outer_lr
+ * (`scalars`: EngineScalars, see "Fused engine" below); grad = g when
+ * grad != NULL.  Replaces loss.backward → SGD.step → clamp_
+ * (src/trainers/outer.py:77-83) for one hyper step. */
+int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
+                       const float* r, int ldr, int nr, float* theta, int n,
+                       float* grad, const void* scalars, void* stream);
+
 /* Slot factors for lds_theta_grad from one aggregation Y = ÂZ and its
  * cotangent G (dZ = ÂG):  U = s⊙G, V = s⊙Z, r = -½ s² (G·Y + Z·dZ) rowwise.
  * Columns [f, fpad) of U and V are zero-filled. */

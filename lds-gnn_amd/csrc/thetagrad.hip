@@ -115,6 +115,125 @@ __global__ __launch_bounds__(256) void theta_grad_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// MFMA form: C_IJ = U_I V_Jᵀ + V_I U_Jᵀ on fp32-in v_mfma_f32_32x32x2_f32
+// (exact f32 FMA chains, 64 FLOP/clk/SIMD = the fp32 peak with one VGPR per
+// operand).  One 256-thread block per 64×64 tile of the upper triangle, each
+// wave a 32×32 sub-tile; k staged through LDS in chunks of 16, transposed to
+// [k][row] with a +1 row pad (conflict-free transposed writes and b32 reads).
+// Epilogue per mode: 0 grad = g, 1 grad += g, 2 θ = clamp(θ - lr·g, 0, 1)
+// with lr read from device memory (and grad = g when grad != NULL).
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kLdsRow = kTile + 1;
+
+__global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4) {
+    __shared__ float Ui[kKC][kLdsRow];
+    __shared__ float Vi[kKC][kLdsRow];
+    __shared__ float Uj[kKC][kLdsRow];
+    __shared__ float Vj[kKC][kLdsRow];
+    __shared__ float Ri[kTile], Rj[kTile];
+
+    int a, b;
+    tri_tile(blockIdx.x, a, b);
+    const int bi = b, bj = a;
+    const int i0 = bi * kTile, j0 = bj * kTile;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 1, wc = wave & 1;  // 32×32 sub-tile of this wave
+
+    if (t < 2 * kTile) {
+        const int rr = t & (kTile - 1);
+        const int row = (t < kTile ? i0 : j0) + rr;
+        float acc = 0.f;
+        if (row < n)
+            for (int c = 0; c < nr; ++c) acc += r[(int64_t)row * ldr + c];
+        (t < kTile ? Ri : Rj)[rr] = acc;
+    }
+
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+
+    // fill mapping: thread -> (row fr, k quad fq)
+    const int fr = t >> 2, fq = (t & 3) * 4;
+    const int gi = i0 + fr, gj = j0 + fr;
+    for (int k0 = 0; k0 < k; k0 += kKC) {
+        __syncthreads();
+        const int gk = k0 + fq;
+        float4 ui = {0.f, 0.f, 0.f, 0.f}, vi = ui, uj = ui, vj = ui;
+        if (vec4 && gk + 3 < k) {
+            if (gi < n) {
+                ui = *reinterpret_cast<const float4*>(u + (int64_t)gi * ld + gk);
+                vi = *reinterpret_cast<const float4*>(v + (int64_t)gi * ld + gk);
+            }
+            if (gj < n) {
+                uj = *reinterpret_cast<const float4*>(u + (int64_t)gj * ld + gk);
+                vj = *reinterpret_cast<const float4*>(v + (int64_t)gj * ld + gk);
+            }
+        } else {
+            float* pui = &ui.x;
+            float* pvi = &vi.x;
+            float* puj = &uj.x;
+            float* pvj = &vj.x;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (gk + e < k) {
+                    if (gi < n) {
+                        pui[e] = u[(int64_t)gi * ld + gk + e];
+                        pvi[e] = v[(int64_t)gi * ld + gk + e];
+                    }
+                    if (gj < n) {
+                        puj[e] = u[(int64_t)gj * ld + gk + e];
+                        pvj[e] = v[(int64_t)gj * ld + gk + e];
+                    }
+                }
+            }
+        }
+        Ui[fq + 0][fr] = ui.x; Ui[fq + 1][fr] = ui.y; Ui[fq + 2][fr] = ui.z; Ui[fq + 3][fr] = ui.w;
+        Vi[fq + 0][fr] = vi.x; Vi[fq + 1][fr] = vi.y; Vi[fq + 2][fr] = vi.z; Vi[fq + 3][fr] = vi.w;
+        Uj[fq + 0][fr] = uj.x; Uj[fq + 1][fr] = uj.y; Uj[fq + 2][fr] = uj.z; Uj[fq + 3][fr] = uj.w;
+        Vj[fq + 0][fr] = vj.x; Vj[fq + 1][fr] = vj.y; Vj[fq + 2][fr] = vj.z; Vj[fq + 3][fr] = vj.w;
+        __syncthreads();
+        const int ar = wr * 32 + (lane & 31), bc = wc * 32 + (lane & 31), kh = lane >> 5;
+#pragma unroll
+        for (int kk = 0; kk < kKC; kk += 2) {
+            // A[i][k] (lane: i = lane&31, k = lane>>5), B[k][j] (k = lane>>5, j = lane&31)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ui[kk + kh][ar], Vj[kk + kh][bc], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Vi[kk + kh][ar], Uj[kk + kh][bc], acc, 0, 0, 0);
+        }
+    }
+
+    const float lr = mode == 2 ? (float)(*lr_dev) : 0.f;
+    const int64_t nn = n;
+    const int lj = wc * 32 + (lane & 31);
+    const int j = j0 + lj;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int li = wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int i = i0 + li;
+        if (i >= n || j >= n || j < i) continue;
+        const int64_t idx = tri_index(i, i, nn) + (j - i);
+        float g = 0.f;
+        const float th = theta != nullptr ? theta[idx] : 0.f;
+        if (j > i) {
+            g = acc[e] + Ri[li] + Rj[lj];
+            if (theta != nullptr && !(th >= 0.f && th <= 1.f)) g = 0.f;  // clamp backward
+        }
+        if (mode == 2) {
+            if (grad != nullptr) grad[idx] = g;
+            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th), 0.f), 1.f);
+        } else if (mode == 1) {
+            grad[idx] += g;
+        } else {
+            grad[idx] = g;
+        }
+    }
+}
+
 // Slot factors: G lanes per row (fpad <= G), one feature per lane.
 template <int G>
 __global__ __launch_bounds__(256) void slot_factors_kernel(
@@ -194,8 +313,40 @@ extern "C" int lds_theta_grad(const float* u, const float* v, int ld, int k, con
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
     const int nb = (n + kTile - 1) / kTile;
     const int ntiles = nb * (nb + 1) / 2;
+    const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
+    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
+                       v, ld, k, r, ldr, nr, const_cast<float*>(theta), n, grad, accumulate ? 1 : 0,
+                       (const double*)nullptr, vec4);
+    LDS_RETURN_LAST_ERROR();
+}
+
+// VALU reference form of lds_theta_grad (kept for A/B timing and testing).
+extern "C" int lds_theta_grad_valu(const float* u, const float* v, int ld, int k, const float* r,
+                                   int ldr, int nr, const float* theta, int n, float* grad,
+                                   int accumulate, void* stream) {
+    LDS_CHECK_ARG(grad != nullptr && n > 0 && k >= 0 && nr >= 0);
+    LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
+    const int nb = (n + kTile - 1) / kTile;
+    const int ntiles = nb * (nb + 1) / 2;
     hipLaunchKernelGGL(theta_grad_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u, v,
                        ld, k, r, ldr, nr, theta, n, grad, accumulate);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k, const float* r,
+                                  int ldr, int nr, float* theta, int n, float* grad,
+                                  const void* scalars, void* stream) {
+    LDS_CHECK_ARG(theta != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
+    LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
+    const int nb = (n + kTile - 1) / kTile;
+    const int ntiles = nb * (nb + 1) / 2;
+    const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
+    // EngineScalars: f64 outer_lr at byte offset 16
+    const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
+    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
+                       v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4);
     LDS_RETURN_LAST_ERROR();
 }
 

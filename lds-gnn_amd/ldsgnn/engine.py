@@ -157,6 +157,7 @@ class LdsEngine:
         self.partials = torch.zeros((self.nblocks, _RED_LEN), dtype=torch.float32, device=dev)
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
+        self.keep_grad = True  # write dθ (θ.grad) even when it is fused with the update
         self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=dev)
         self.eval_metrics = torch.zeros((64, 4), dtype=torch.float32, device=dev)
         self._graph_capture = None
@@ -337,12 +338,16 @@ class LdsEngine:
         for t in range(T - 1, -1, -1):
             self._reverse_step(t)
         k = T * self.kg + HID + self.cw
-        nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k, nat.ptr(self.R), 1, 1,
-                 nat.ptr(self.theta), n, nat.ptr(self.grad), 0, st)
-        if grad_reducer is not None:
+        if grad_reducer is None:  # one launch: dθ assembly fused with SGD + clamp
+            nat.call("lds_theta_grad_sgd", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k, nat.ptr(self.R), 1,
+                     1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
+                     nat.ptr(self.scalars), st)
+        else:  # replicas: dθ, all-reduce (mean), then the identical update everywhere
+            nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k, nat.ptr(self.R), 1, 1,
+                     nat.ptr(self.theta), n, nat.ptr(self.grad), 0, st)
             grad_reducer(self.grad)
-        nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
-                 nat.ptr(self.scalars), st)
+            nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
+                     nat.ptr(self.scalars), st)
         # detach: the window restarts from the latest weights / Adam state
         self._flush(hypers=1)
         if T:

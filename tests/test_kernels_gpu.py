@@ -190,3 +190,26 @@ def test_degree_scale_is_correctly_rounded(device):
     want = np.float32(1.0) / np.sqrt(deg.numpy().astype(np.float32))
     assert np.array_equal(d.cpu().numpy(), deg.numpy())
     assert np.array_equal(s.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_theta_grad_mfma_matches_valu_and_sgd_mode(device):
+    """MFMA and VALU forms agree; the fused SGD mode equals grad-then-update."""
+    n, k = 200, 40
+    g = torch.Generator().manual_seed(1)
+    u = torch.randn(n, k, generator=g).to(device)
+    v = torch.randn(n, k, generator=g).to(device)
+    r = torch.randn(n, 2, generator=g).to(device)
+    theta = torch.rand(n * (n + 1) // 2, generator=g).to(device)
+    a = ops.theta_grad(u, v, r, n, theta=theta)
+    b = torch.empty_like(a)
+    nat.call("lds_theta_grad_valu", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 2, 2, nat.ptr(theta), n, nat.ptr(b),
+             0, nat.stream_of(u.device))
+    assert torch.allclose(a, b, rtol=1e-5, atol=1e-5)
+    sc = torch.zeros(32, dtype=torch.uint8, device=device)
+    sc[16:24].view(torch.float64).fill_(0.3)
+    th2 = theta.clone()
+    gout = torch.empty_like(theta)
+    nat.call("lds_theta_grad_sgd", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 2, 2, nat.ptr(th2), n, nat.ptr(gout),
+             nat.ptr(sc), nat.stream_of(u.device))
+    assert torch.equal(gout, a)
+    assert torch.allclose(th2, (theta - 0.3 * a).clamp(0, 1), atol=1e-6)
