@@ -116,12 +116,13 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
             x = xval[p];
             if (train) x = u_at(keys, keys.tag_x, ctr, row, f) < keep ? x * scale : 0.f;
         }
-        const int cnt = min(HID, end - p0);
-        for (int k = 0; k < cnt; ++k) {
-            const int fk = __shfl(f, k, HID);
-            const float xk = __shfl(x, k, HID);
-            acc = fmaf(xk, wt[fk * HID + lane], acc);
-        }
+        // fixed trip count, fully unrolled: the 16 gathers are independent and all
+        // in flight at once (entries past `end` carry x = 0 and a valid index 0)
+        float wk[HID];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) wk[k] = wt[__shfl(f, k, HID) * HID + lane];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(x, k, HID), wk[k], acc);
     }
     out[row * HID + lane] = acc;
 }
@@ -147,12 +148,11 @@ __global__ __launch_bounds__(256) void xt_linear_kernel(
             x = xval[p];
             if (train) x = u_at(keys, keys.tag_x, ctr, i, f) < keep ? x * scale : 0.f;
         }
-        const int cnt = min(HID, end - p0);
-        for (int k = 0; k < cnt; ++k) {
-            const int ik = __shfl(i, k, HID);
-            const float xk = __shfl(x, k, HID);
-            acc = fmaf(xk, d[ik * HID + lane], acc);
-        }
+        float dk[HID];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) dk[k] = d[__shfl(i, k, HID) * HID + lane];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(x, k, HID), dk[k], acc);
     }
     float* o = out + f * HID + lane;
     if (w != nullptr) acc = acc + wd * w[f * HID + lane];
@@ -284,6 +284,7 @@ __global__ __launch_bounds__(256) void bwd_layer1_kernel(
 // Layout of a partial: [A (16×16) | v1 (16) | v2 (16) | l0 | l1 | pad to 304].
 // ---------------------------------------------------------------------------
 constexpr int kRedLen = 16 * 16 + 16 + 16 + 16;  // 304 floats per partial
+constexpr int kRedBlocks = 64;                      // max first-stage blocks
 
 __global__ __launch_bounds__(256) void colreduce_kernel(
     int n, int c_n, const float* __restrict__ a1, const float* __restrict__ b1,
@@ -344,8 +345,15 @@ __global__ __launch_bounds__(320) void colreduce_final_kernel(
     float* __restrict__ dst_l, int accumulate) {
     const int e = threadIdx.x;
     if (e >= kRedLen) return;
-    float t = 0.f;
-    for (int b = 0; b < nblocks; ++b) t += partials[(int64_t)b * kRedLen + e];
+    // all partial loads issued at once, then a fixed-shape tree sum (deterministic)
+    float v[kRedBlocks];
+#pragma unroll
+    for (int b = 0; b < kRedBlocks; ++b) v[b] = b < nblocks ? partials[(int64_t)b * kRedLen + e] : 0.f;
+#pragma unroll
+    for (int w = kRedBlocks / 2; w > 0; w >>= 1)
+#pragma unroll
+        for (int b = 0; b < w; ++b) v[b] += v[b + w];
+    const float t = v[0];
     float* dst = nullptr;
     if (e < 256) {
         const int k = e / 16;
@@ -646,7 +654,7 @@ extern "C" int lds_engine_colreduce(int n, int c_n, const float* a1, const float
                                     const float* q, float* partials, int nblocks, float* dst_a,
                                     float* dst_v1, int v1_width, float* dst_v2, int v2_width,
                                     float* dst_l, int accumulate, void* stream) {
-    LDS_CHECK_ARG(partials && n > 0 && nblocks > 0 && c_n >= 0 && c_n <= HID);
+    LDS_CHECK_ARG(partials && n > 0 && nblocks > 0 && nblocks <= kRedBlocks && c_n >= 0 && c_n <= HID);
     const int rpb = (n + nblocks - 1) / nblocks;
     hipLaunchKernelGGL(colreduce_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, n, c_n, a1,
                        b1, a2, b2, x1, x2, l, q, partials, rpb);

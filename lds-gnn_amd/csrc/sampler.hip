@@ -14,31 +14,42 @@
 
 namespace lds {
 
-// One wave per 64×64 tile (bi <= bj) of the upper triangle.  Lane l owns
-// column j = 64*bj + l; the wave walks the tile's 64 rows four at a time (one
-// Philox call yields the four rows' uniforms for that column).  Row words come
-// out of __ballot, the transposed (lower-triangle) words accumulate one bit
-// per row in each lane: every word of `bits` has exactly one writer, so the
-// kernel needs neither atomics nor a memset.
+// One 4-wave block per 64×64 tile (bi <= bj) of the upper triangle.  Lane l
+// owns column j = 64*bj + l; wave w owns the tile's rows 16w .. 16w+15 and
+// issues all 16 of its θ loads (each a coalesced 256-B row segment) before any
+// compute, then draws four Philox quads (one call = four rows' uniforms of a
+// column).  Row words come out of __ballot; the transposed (lower-triangle)
+// words collect one bit per row in each lane and are OR-combined across the
+// four waves in LDS.  Every word of `bits` has exactly one writer: no atomics,
+// no memset.
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
     uint64_t* __restrict__ bits, int words, int ntiles) {
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= ntiles) return;  // wave-uniform
+    __shared__ uint64_t colpart[4][64];
+    __shared__ uint64_t rowword[64];
+    const int tile = blockIdx.x;
     if (counter_base != nullptr) counter += *counter_base;  // device-resident draw counter
     const int lane = wave_lane();
+    const int wave = threadIdx.x >> 6;
     int a, b;
     tri_tile(tile, a, b);
     const int bi = b, bj = a;  // bi <= bj
     const int j = bj * 64 + lane;
     const bool diag_tile = (bi == bj);
     const int64_t nn = n;
+    const int r0 = bi * 64 + wave * 16;  // first row of this wave
 
-    uint64_t colword = 0, myrow = 0;
-    for (int q = 0; q < 16; ++q) {
-        const int i0 = bi * 64 + 4 * q;
-        if (i0 >= n) break;  // wave-uniform
+    float th[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = r0 + r;
+        th[r] = (i < j && j < n) ? theta[tri_index(i, j, nn)] : -1.0f;  // i < n follows
+    }
+    uint64_t colword = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int i0 = r0 + 4 * q;
         float u[4];
         if (u_inj != nullptr) {
 #pragma unroll
@@ -52,26 +63,26 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = i0 + r;
-            bool e = false;
-            if (i < j && j < n) {  // i < n follows from i < j < n
-                float t = theta[tri_index(i, j, nn)];
-                t = fminf(fmaxf(t, 0.0f), 1.0f);  // clamp(0, 1), src/utils/graph.py:180
-                e = u[r] < t;
-            }
+            const float t = th[4 * q + r];
+            // clamp(0, 1) as triu_values_to_symmetric_matrix (src/utils/graph.py:180);
+            // t = -1 marks pairs outside the strict upper triangle
+            const bool e = t >= 0.0f && u[r] < fminf(t, 1.0f);
             const uint64_t w = __ballot(e);
             if (i < n) {
                 if (!diag_tile) {
                     if (lane == 0) bits[(int64_t)i * words + bj] = w;
-                } else if (lane == i - bi * 64) {
-                    myrow = w;
+                } else if (lane == 0) {
+                    rowword[i - bi * 64] = w;
                 }
             }
             if (e) colword |= 1ull << (i - bi * 64);
         }
     }
-    if (j < n) {
-        uint64_t out = colword;
-        if (diag_tile) out |= myrow | (1ull << lane);  // self-loop: diagonal set to 1
+    colpart[wave][lane] = colword;
+    __syncthreads();
+    if (wave == 0 && j < n) {
+        uint64_t out = colpart[0][lane] | colpart[1][lane] | colpart[2][lane] | colpart[3][lane];
+        if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
         bits[(int64_t)j * words + bi] = out;
     }
 }
@@ -204,7 +215,7 @@ extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint
     LDS_CHECK_ARG(words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
-    hipLaunchKernelGGL(sample_tiles_kernel, dim3((ntiles + 3) / 4), dim3(256), 0,
+    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                        counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles);
     LDS_RETURN_LAST_ERROR();
@@ -217,7 +228,7 @@ extern "C" int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, 
     LDS_CHECK_ARG(n > 0 && n <= (1 << 20) && words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
-    hipLaunchKernelGGL(sample_tiles_kernel, dim3((ntiles + 3) / 4), dim3(256), 0,
+    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                        counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles);
     LDS_RETURN_LAST_ERROR();

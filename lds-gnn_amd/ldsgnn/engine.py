@@ -153,7 +153,7 @@ class LdsEngine:
         self.obar, self.h2bar, self.y0bar, self.h0bar = z(), z(), z(), z()
         zp = lambda: torch.zeros(self.np, dtype=torch.float32, device=dev)  # noqa: E731
         self.wbar, self.mbar, self.vbar, self.gbar, self.g = zp(), zp(), zp(), zp(), zp()
-        self.nblocks = max(1, min(64, (n + 15) // 16))
+        self.nblocks = max(1, min(64, (n + 15) // 16))  # colreduce first-stage blocks (<= 64)
         self.partials = torch.zeros((self.nblocks, _RED_LEN), dtype=torch.float32, device=dev)
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
