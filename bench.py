@@ -83,9 +83,7 @@ def run_engine_windows(eng, reducer, windows, tau, use_graph):
         eng.replay(windows)
         return
     for _ in range(windows):
-        for _ in range(tau):
-            eng.inner_step()
-        eng.hyper_step(grad_reducer=reducer)
+        eng.run_window(tau, grad_reducer=reducer)
 
 
 def run_steps(runner, start: int, count: int, tau: int) -> int:

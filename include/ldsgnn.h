@@ -99,6 +99,15 @@ int lds_bitmask_fill_csr(const uint64_t* bits, int n, int words,
 int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* s,
                          void* stream);
 
+/* Batched form for a window of graphs drawn from the same θ: graph g
+ * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
+ * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
+ * col + g·col_stride, s + g·n.  Four launches for all `count` graphs. */
+int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
+                      const uint32_t* counter_base, uint32_t counter_offset, int count,
+                      uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
+                      int64_t col_stride, float* s, void* stream);
+
 /* The four launches above in order: sample -> degree/s -> scan -> fill.
  * deg_ws: n ints of workspace. */
 int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32_t tag,

@@ -29,6 +29,9 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     __shared__ uint64_t colpart[4][64];
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
+    // batched launches: graph blockIdx.y draws counter + blockIdx.y into its own bit matrix
+    counter += blockIdx.y;
+    bits += (int64_t)blockIdx.y * n * words;
     if (counter_base != nullptr) counter += *counter_base;  // device-resident draw counter
     const int lane = wave_lane();
     const int wave = threadIdx.x >> 6;
@@ -93,6 +96,9 @@ __global__ __launch_bounds__(256) void degree_kernel(const uint64_t* __restrict_
                                                       float* __restrict__ s) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
+    bits += (int64_t)blockIdx.y * n * words;  // batched: graph blockIdx.y
+    deg += (int64_t)blockIdx.y * n;
+    s += (int64_t)blockIdx.y * n;
     const int lane = wave_lane();
     const int nbw = (n + 63) / 64;
     const uint64_t* rb = bits + (int64_t)row * words;
@@ -109,6 +115,8 @@ __global__ __launch_bounds__(256) void degree_kernel(const uint64_t* __restrict_
 __global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ deg, int n,
                                                      int* __restrict__ row_ptr) {
     __shared__ int partial[1024];
+    deg += (int64_t)blockIdx.y * n;  // batched: graph blockIdx.y
+    row_ptr += (int64_t)blockIdx.y * (n + 1);
     const int t = threadIdx.x;
     const int per = (n + 1023) / 1024;
     const int beg = min(n, t * per), end = min(n, beg + per);
@@ -138,6 +146,9 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
                                                         int* __restrict__ overflow) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
+    bits += (int64_t)blockIdx.y * n * words;  // batched: graph blockIdx.y, col stride = capacity
+    row_ptr += (int64_t)blockIdx.y * (n + 1);
+    col += (int64_t)blockIdx.y * capacity;
     const int lane = wave_lane();
     const int nbw = (n + 63) / 64;
     const uint64_t* rb = bits + (int64_t)row * words;
@@ -264,6 +275,26 @@ extern "C" int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* 
     LDS_CHECK_ARG(row_ptr != nullptr && s != nullptr && n > 0);
     hipLaunchKernelGGL(csr_degree_scale_kernel, dim3((n + 255) / 256), dim3(256), 0,
                        (hipStream_t)stream, row_ptr, n, deg, s);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
+                                 const uint32_t* counter_base, uint32_t counter_offset, int count,
+                                 uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
+                                 int64_t col_stride, float* s, void* stream) {
+    LDS_CHECK_ARG(theta && bits && deg_ws && row_ptr && col && s && n > 0 && n <= (1 << 20));
+    LDS_CHECK_ARG(count > 0 && count <= 65535 && words >= (n + 63) / 64 && col_stride > 0);
+    const int nb = (n + 63) / 64;
+    const int ntiles = nb * (nb + 1) / 2;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles, count), dim3(256), 0, st, theta, n,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
+                       (const float*)nullptr, bits, words, ntiles);
+    hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, count), dim3(256), 0, st, bits, n, words,
+                       deg_ws, s);
+    hipLaunchKernelGGL(scan_kernel, dim3(1, count), dim3(1024), 0, st, deg_ws, n, row_ptr);
+    hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4, count), dim3(256), 0, st, bits, n, words,
+                       row_ptr, col, col_stride, (int*)nullptr);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -30,6 +30,7 @@ SIGNATURES = {
     "lds_exclusive_scan": [P, c_int, P, P],
     "lds_bitmask_fill_csr": [P, c_int, c_int, P, P, c_int64, P, P],
     "lds_csr_degree_scale": [P, c_int, P, P, P],
+    "lds_sample_graphs": [P, c_int, c_uint64, c_uint32, P, c_uint32, c_int, P, c_int, P, P, P, c_int64, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],
     "lds_spmm_norm": [P, P, P, c_int, P, c_int, c_int, P, c_int, c_int, P],

@@ -45,17 +45,34 @@ _ACT = ("h0", "y0", "h1d", "h2", "o", "p", "d_o", "dh2", "dy0", "dh0")
 class _Graph:
     """Device buffers of one sampled graph (CSR with self-loops + s)."""
 
-    def __init__(self, n: int, cap: int, dev):
+    def __init__(self, n: int, cap: int, dev, views=None):
+        if views is not None:
+            self.row_ptr, self.col, self.s = views
+            return
         self.row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
         self.col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
         self.s = torch.empty(n, dtype=torch.float32, device=dev)
 
 
+class _GraphBatch:
+    """Contiguous storage for the τ+1 graphs of a window, so that one batched
+    lds_sample_graphs launch set draws them all (θ is fixed within a window)."""
+
+    def __init__(self, count: int, n: int, words: int, cap: int, dev):
+        self.count, self.cap = count, cap
+        self.bits = torch.empty((count, n, words), dtype=torch.int64, device=dev)
+        self.deg = torch.empty((count, n), dtype=torch.int32, device=dev)
+        self.row_ptr = torch.empty((count, n + 1), dtype=torch.int32, device=dev)
+        self.col = torch.empty((count, cap), dtype=torch.int32, device=dev)
+        self.s = torch.empty((count, n), dtype=torch.float32, device=dev)
+        self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g])) for g in range(count)]
+
+
 class _Slot:
     """Tape of one inner step (or the outer step): graph + activations."""
 
-    def __init__(self, n: int, cap: int, dev):
-        self.g = _Graph(n, cap, dev)
+    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None):
+        self.g = graph if graph is not None else _Graph(n, cap, dev)
         for a in _ACT:
             setattr(self, a, torch.zeros((n, HID), dtype=torch.float32, device=dev))
         self.lossrow = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -141,8 +158,9 @@ class LdsEngine:
         self.m: List[torch.Tensor] = []
         self.v: List[torch.Tensor] = []
         self.gp: List[torch.Tensor] = []
+        self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev)
         self._grow(self.tau)
-        self.outer = _Slot(n, self.cap, dev)
+        self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau])
         self.t = 0  # inner steps in the current window
         self.pending_graph = 0
         self.pending_fwd = 0
@@ -175,7 +193,9 @@ class LdsEngine:
 
     def _grow(self, slots: int):
         while len(self.slots) < slots:
-            self.slots.append(_Slot(self.n, self.cap, self.dev))
+            t = len(self.slots)
+            g = self.gbatch.graphs[t] if t < self.gbatch.count - 1 else None
+            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g))
         while len(self.w) < slots + 1:
             for lst in (self.w, self.m, self.v):
                 lst.append(torch.zeros(self.np, dtype=torch.float32, device=self.dev))
@@ -294,7 +314,16 @@ class LdsEngine:
                  fwd_off, train, self.keep, self.scale, st)
 
     # ----------------------------------------------------------------- steps
-    def inner_step(self):
+    def _sample_batch(self, count: int):
+        """Draw the window's `count` graphs in one batched launch set; graph g
+        takes draw counter (pending + g), exactly the counter the step-by-step
+        path would give it."""
+        gb = self.gbatch
+        nat.call("lds_sample_graphs", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, nat.ptr(self.scalars),
+                 self.pending_graph, count, nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), nat.ptr(gb.row_ptr),
+                 nat.ptr(gb.col), self.cap, nat.ptr(gb.s), self._stream())
+
+    def inner_step(self, presampled: bool = False):
         """One InnerProblemTrainer.train_step (sample + forward + backward +
         differentiable Adam), recorded on the tape.  Metrics stay on device
         (`metrics[t]` = [Σ NLL over train rows, #correct])."""
@@ -305,7 +334,10 @@ class LdsEngine:
             self._alloc_factors()
             self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=self.dev)
         sl = self.slots[t]
-        self._sample(sl.g)
+        if presampled:
+            self.pending_graph += 1
+        else:
+            self._sample(sl.g)
         fwd_off = self.pending_fwd
         self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off)
         self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False)
@@ -318,7 +350,7 @@ class LdsEngine:
         self.t = t + 1
         return self.metrics[t]
 
-    def hyper_step(self, grad_reducer=None):
+    def hyper_step(self, grad_reducer=None, presampled: bool = False):
         """OuterProblemTrainer.train_step + both detaches.  Returns the device
         metrics row [Σ NLL over opt rows, #correct]."""
         st, n, c = self._stream(), self.n, self.c
@@ -326,7 +358,10 @@ class LdsEngine:
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
         out = self.outer
-        self._sample(out.g)
+        if presampled:
+            self.pending_graph += 1
+        else:
+            self._sample(out.g)
         fwd_off = self.pending_fwd
         self.R.zero_()
         self._forward(out, self.w[T], self.opt_mask, self.inv_opt, self.train_flag, fwd_off)
@@ -397,21 +432,22 @@ class LdsEngine:
                  self.nblocks, nat.ptr(ww1), nat.ptr(wb0), HID, nat.ptr(wb1), c, 0, 1, st)
 
     # ------------------------------------------------------------- graphs
-    def run_window(self, tau: int):
-        """τ inner steps followed by the hyper step (eager)."""
+    def run_window(self, tau: int, grad_reducer=None):
+        """τ inner steps followed by the hyper step.  A full window from a
+        window start draws its τ+1 graphs in one batched launch set."""
+        batch = self.t == 0 and tau == self.tau and self.gbatch.count == tau + 1
+        if batch:
+            self._sample_batch(tau + 1)
         for _ in range(tau):
-            self.inner_step()
-        return self.hyper_step()
+            self.inner_step(presampled=batch)
+        return self.hyper_step(grad_reducer=grad_reducer, presampled=batch)
 
     def capture_window(self, tau: int):
         """Record run_window(tau) as one HIP graph (state must be at a window
         start).  Replays advance RNG counters, Adam step and lr on device."""
         assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
-        if tau > len(self.slots):
-            self._grow(tau)
-            self.tau = tau
-            self._alloc_factors()
-            self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=self.dev)
+        if tau != self.tau:
+            raise ValueError(f"engine was built for tau={self.tau}; capture that window length")
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         graph = torch.cuda.CUDAGraph()

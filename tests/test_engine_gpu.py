@@ -43,3 +43,19 @@ def test_graph_replay_equals_eager():
     for k, v in a.get_params().items():
         assert torch.equal(v, b.get_params()[k]), k
     assert a.scalars_host() == b.scalars_host()
+
+
+def test_batched_window_sampling_equals_stepwise():
+    """run_window draws the window's graphs in one batched launch set: same
+    draws (counters), same results as sampling step by step."""
+    a = run_engine_and_oracle(n=140, f_in=30, classes=6, steps=1, tau=5, dropout=0.5, seed=21)["engine"]
+    b = run_engine_and_oracle(n=140, f_in=30, classes=6, steps=1, tau=5, dropout=0.5, seed=21)["engine"]
+    for _ in range(2):
+        a.run_window(5)  # batched sampling
+        for _ in range(5):  # step by step
+            b.inner_step()
+        b.hyper_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
