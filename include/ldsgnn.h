@@ -215,23 +215,30 @@ int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, uint32_t ta
                            const uint32_t* counter_base, uint32_t counter_offset,
                            uint64_t* bits, int words, void* stream);
 
-/* H0 = dropout(X) W0ᵀ + b0 (X in CSR; wt = W0ᵀ as [fin][16]). */
+/* H0 = dropout(X) W0ᵀ + b0 (X in CSR; wt = W0ᵀ as [fin][16]).  When
+ * xd_csr != NULL the dropped values are also stored in CSR order, and when
+ * xd_csc != NULL scattered to CSC order via csr2csc (position of each CSR entry
+ * in the CSC arrays) — later products of the same step read them with
+ * train = 0 instead of redrawing the mask. */
 int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int n,
                         const float* wt, const float* bias, float* out, uint64_t seed,
                         uint32_t tag_x, const void* scalars, int fwd_off, int train,
-                        float keep, float scale, void* stream);
+                        float keep, float scale, float* xd_csr, float* xd_csc,
+                        const int* csr2csc, void* stream);
 /* out[f][:] (+)= Σ_i dropout(X)[i][f] · d[i][:]  (+ wd · w)   (X in CSC). */
 int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int fin,
                          const float* d, float* out, const float* w, float wd,
                          int accumulate, uint64_t seed, uint32_t tag_x,
                          const void* scalars, int fwd_off, int train, float keep,
                          float scale, void* stream);
-/* Y0 = ÂH0; H1d = dropout(relu(Y0)); H2 = H1d W1ᵀ + b1. */
+/* Y0 = ÂH0; H1d = dropout(relu(Y0)); H2 = H1d W1ᵀ + b1.  dmask (may be
+ * NULL) receives D1 ⊙ [Y0 > 0] / keep, the Jacobian mask of relu + dropout,
+ * which lds_engine_bwd_layer2 / rev_a / rev_c read instead of y0 + RNG. */
 int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, int n,
                           const float* h0, float* y0, float* h1d, float* h2,
                           const float* w1, const float* b1, int c, uint64_t seed,
                           uint32_t tag_h, const void* scalars, int fwd_off, int train,
-                          float keep, float scale, void* stream);
+                          float keep, float scale, float* dmask, void* stream);
 /* O = ÂH2; P = softmax(O); dO = (P - onehot) ⊙ mask · inv_count; per-row
  * NLL and correctness where mask. */
 int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, int n,
@@ -239,14 +246,15 @@ int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, int n,
                           const int* label, const uint8_t* mask, float inv_count,
                           float* lossrow, float* corrrow, int c, void* stream);
 /* dH2 = ÂdO; dY0 = (dH2 W1) ⊙ dropout' ⊙ relu'.  U != NULL: emit the outer
- * graph's factor (dO, H2) at columns [foff, foff + fwidth). */
+ * graph's factor (dO, H2) at columns [foff, foff + fwidth); r_assign != 0
+ * writes R (first emitter of a window) instead of accumulating into it. */
 int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, int n,
                           const float* d_o, const float* y0, float* dh2, float* dy0,
                           const float* w1, int c, uint64_t seed, uint32_t tag_h,
                           const void* scalars, int fwd_off, int train, float keep,
                           float scale, const float* o, const float* h2, float* U,
                           float* V, int ldk, float* R, int foff, int fwidth,
-                          void* stream);
+                          int r_assign, const float* dmask, void* stream);
 /* dH0 = ÂdY0.  U != NULL: emit the outer graph's factor (dY0, H0). */
 int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, int n,
                           const float* dy0, float* dh0, const float* y0,
@@ -279,7 +287,8 @@ int lds_engine_rev_a(const int* rp, const int* col, const float* s, int n,
                      const float* gw1bar, const float* gb1bar, int c, float* dh1dbar,
                      float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
-                     float* U, float* V, int ldk, float* R, int foff, void* stream);
+                     float* U, float* V, int ldk, float* R, int foff, const float* dmask,
+                     void* stream);
 int lds_engine_rev_b(const int* rp, const int* col, const float* s, int n,
                      const float* dh2bar, const float* d_o, const float* dh2,
                      const float* p, const uint8_t* mask, float inv_count, int c,
@@ -291,7 +300,7 @@ int lds_engine_rev_c(const int* rp, const int* col, const float* s, int n,
                      float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, int cw,
-                     void* stream);
+                     const float* dmask, void* stream);
 int lds_engine_rev_d(const int* rp, const int* col, const float* s, int n,
                      const float* y0bar, const float* h0, const float* y0,
                      float* h0bar, float* U, float* V, int ldk, float* R, int foff,
@@ -303,6 +312,74 @@ int lds_engine_sgd_clamp(float* theta, const float* grad, int64_t count,
  * adam_steps, and `hypers` times {hyper_steps += 1; outer_lr *= lr_decay}. */
 int lds_engine_advance(void* scalars, int graphs, int forwards, int adam_steps,
                        int hypers, void* stream);
+
+/* ----- fused engine forms (fewer launches per τ-window) -----
+ * Replaces, per inner step, the reference's loss.backward(create_graph=True)
+ * + DifferentiableAdam.step (src/trainers/inner.py:64-72) and, per reversed
+ * step, the corresponding part of the outer loss.backward through the unrolled
+ * window (src/trainers/outer.py:70-80).
+ *
+ * Adam arguments common to lds_engine_final / lds_engine_xt_adam
+ * (adam_mode 0 none, 1 forward, 2 reverse; pointers are whole flat parameter
+ * vectors):
+ *   mode 1: w0, m0, v0 -> w1, m1, v1 and g' (= g + wd·w) into gp;
+ *   mode 2: reverse of the step with post-state m1, v1 and g' gp: the
+ *           completed entry is the adjoint of w1; writes gbar, mbar, vbar
+ *           (read as 0 when `first`), wbar (+ wd·ḡ in the decayed group).
+ * The step's bias-corrected constants come from the Adam table (adam_tab,
+ * 2 floats per step offset: {lr/(1-β1^k), sqrt(1-β2^k)}, k = adam_step + 1 +
+ * step_off), written by lds_engine_adam_table / lds_engine_end_window;
+ * step_off < 256. */
+
+/* dH0 = ÂdY0 (+ outer factor (dY0, H0) when U != NULL) fused with the first
+ * stage of {gW1 = dH2ᵀH1d, gb0 = ΣdH0, gb1 = ΣdH2, Σloss, Σcorrect}:
+ * ceil(n/64) partials of 304 floats. */
+int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, int n,
+                           const float* dy0, float* dh0, const float* y0, const float* h0,
+                           float* U, float* V, int ldk, float* R, int foff,
+                           const float* dh2, const float* h1d, const float* lossrow,
+                           const float* corrrow, int c, float* partials, void* stream);
+/* H0bar = ÂY0bar (+ factor use 1) fused with the first stage of
+ * {W̄1 += dH2ᵀdH1dbar + H2barᵀH1d, b̄0 += ΣH0bar, b̄1 += ΣH2bar}. */
+int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, int n,
+                            const float* y0bar, const float* h0, const float* y0,
+                            float* h0bar, float* U, float* V, int ldk, float* R, int foff,
+                            const float* dh2, const float* dh1dbar, const float* h2bar,
+                            const float* h1d, int c, float* partials, void* stream);
+/* Final stage: partials -> dst (flat parameter layout; = or +=), metrics[0..1]
+ * (may be NULL), then Adam (mode) on b0 / W1 / b1. */
+int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int off_b0,
+                     int off_w1, int off_b1, int accumulate, float* metrics, int adam_mode,
+                     int first, const float* w0, const float* m0, const float* v0, float* w1,
+                     float* m1, float* v1, float* gp, float* wbar, float* mbar, float* vbar,
+                     float* gbar, const double* hyper, const float* adam_tab, int n_wd,
+                     const void* scalars, int step_off, void* stream);
+/* out: flat parameter-shaped buffer.  Its W0ᵀ part (= or +=) Xdᵀ d (the W0
+ * gradient / adjoint), then Adam (mode) on it.  With partials != NULL the same
+ * launch also runs the final stage of the fused reduction (as lds_engine_final
+ * with dst = out), so one launch completes every parameter. */
+int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int fin,
+                       const float* d, float* out, int accumulate, uint64_t seed,
+                       uint32_t tag_x, const void* scalars, int fwd_off, int train, float keep,
+                       float scale, const float* partials, int nblocks, int c, int off_b0,
+                       int off_w1, int off_b1, float* metrics, int adam_mode, int first,
+                       const float* w0, const float* m0, const float* v0, float* w1, float* m1,
+                       float* v1, float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
+                       const double* hyper, const float* adam_tab, int n_wd, int step_off,
+                       void* stream);
+/* Window end (both trainers' detach, src/trainers/bilevel.py:109-114): copy
+ * w/m/v of slot T to slot 0 (skipped when wT == NULL), advance the scalars
+ * as lds_engine_advance and (adam_tab != NULL) refresh the first tab_count
+ * entries of the Adam table for the new adam_step. */
+int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT,
+                          float* w0, float* m0, float* v0, void* scalars, int graphs,
+                          int forwards, int adam_steps, int hypers, const double* betas_dev,
+                          float* adam_tab, int tab_count, void* stream);
+/* Adam table for the current scalars->adam_step (betas_dev = {β1, β2, lr}
+ * doubles): entry k = {lr/(1-β1^(s+1+k)), sqrt(1-β2^(s+1+k))}, k < tab_count
+ * <= 256; the constants of torch/higher's Adam, computed in double. */
+int lds_engine_adam_table(const void* scalars, const double* betas_dev, float* adam_tab,
+                          int tab_count, void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,21 +59,22 @@ __device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr,
 __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* __restrict__ col,
                                          const float* __restrict__ s, const float* __restrict__ z,
                                          int row, int lane) {
+    // Chunks of 16 neighbours: one coalesced load of their column indices, each
+    // lane fetches s of its own neighbour, then all 16 row gathers are in
+    // flight at once (3 dependent loads per chunk instead of 2 per 4 entries).
+    // Past the row's end: index = row, weight 0 (fmaf(0, z, acc) == acc), so
+    // the sum is the same sequential order as the plain loop.
     const int beg = rp[row], end = rp[row + 1];
     float acc = 0.f;
-    int p = beg;
-    for (; p + 4 <= end; p += 4) {
-        const int j0 = col[p], j1 = col[p + 1], j2 = col[p + 2], j3 = col[p + 3];
-        const float z0 = z[j0 * HID + lane], z1 = z[j1 * HID + lane];
-        const float z2 = z[j2 * HID + lane], z3 = z[j3 * HID + lane];
-        acc = fmaf(s[j0], z0, acc);
-        acc = fmaf(s[j1], z1, acc);
-        acc = fmaf(s[j2], z2, acc);
-        acc = fmaf(s[j3], z3, acc);
-    }
-    for (; p < end; ++p) {
-        const int j = col[p];
-        acc = fmaf(s[j], z[j * HID + lane], acc);
+    for (int p0 = beg; p0 < end; p0 += HID) {
+        const int p = p0 + lane;
+        const int jl = p < end ? col[p] : row;
+        const float sl = p < end ? s[jl] : 0.f;
+        float zk[HID];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, k, HID) * HID + lane];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, k, HID), zk[k], acc);
     }
     return s[row] * acc;
 }
@@ -82,49 +83,80 @@ __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* 
 // window's factor matrices and add r = -½ s² (G·Y + Z·ÂG) into R[row].
 __device__ __forceinline__ void emit_factor(float* __restrict__ U, float* __restrict__ V, int ldk,
                                             float* __restrict__ R, int off, int width, int row,
-                                            int lane, float si, float g, float z, float y, float ag) {
+                                            int lane, float si, float g, float z, float y, float ag,
+                                            bool assign = false) {
     const float d = gsum16(g * y + z * ag);
     if (lane < width) {
         U[(int64_t)row * ldk + off + lane] = si * g;
         V[(int64_t)row * ldk + off + lane] = si * z;
     }
-    if (lane == 0) R[row] += -0.5f * si * si * d;
+    if (lane == 0) {
+        const float r = -0.5f * si * si * d;
+        R[row] = assign ? r : R[row] + r;
+    }
 }
 
 // ---------------------------------------------------------------------------
 // X-side products (X is CSR / CSC, dropout keyed per (node, feature))
 // ---------------------------------------------------------------------------
 
+// One wave per X row (CSR) or X column (CSC): its entries are split over the
+// wave's four 16-lane groups in chunks of 16 (group q takes chunks q, q+4, ...);
+// per chunk one coalesced index/value load, dropout keyed per (node, feature)
+// (optionally stored: xd_out in this order, xd_perm_out[perm[p]] in the other),
+// then 16 independent row gathers of `src`; the groups' partials are combined
+// by two xor-shuffles (fixed order).  Returns the full sum in every lane.
+template <bool kCsc>
+__device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const int* __restrict__ idx,
+                                            const float* __restrict__ val, int r,
+                                            const float* __restrict__ src, const Keys& keys,
+                                            uint32_t ctr, int train, float keep, float scale,
+                                            float* __restrict__ xd_out = nullptr,
+                                            float* __restrict__ xd_perm_out = nullptr,
+                                            const int* __restrict__ perm = nullptr) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int q = (threadIdx.x >> 4) & 3;
+    const int beg = ptr[r], end = ptr[r + 1];
+    float acc = 0.f;
+    for (int p0 = beg + q * HID; p0 < end; p0 += 4 * HID) {
+        const int p = p0 + lane;
+        int j = 0;
+        float x = 0.f;
+        if (p < end) {
+            j = idx[p];
+            x = val[p];
+            if (train) {
+                const int node = kCsc ? j : r, feat = kCsc ? r : j;
+                x = u_at(keys, keys.tag_x, ctr, node, feat) < keep ? x * scale : 0.f;
+            }
+            // keep Xd for the later products of this step (no redraw there)
+            if (xd_out != nullptr) xd_out[p] = x;
+            if (xd_perm_out != nullptr) xd_perm_out[perm[p]] = x;
+        }
+        float sk[HID];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) sk[k] = src[__shfl(j, k, HID) * HID + lane];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(x, k, HID), sk[k], acc);
+    }
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 32);
+    return acc;
+}
+
 // out[i][h] = bias[h] + Σ_f Xd[i][f] · Wt[f][h]      (H0 = Xd W0ᵀ + b0)
 // Xd = dropout(X) with key (tag_x, fwd counter) when `train`, else X.
 __global__ __launch_bounds__(256) void x_linear_kernel(
     const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
-    const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale) {
-    const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
+    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc) {
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
     if (row >= n) return;
-    const uint32_t ctr = sc->fwd_ctr + fwd_off;
-    float acc = bias != nullptr ? bias[lane] : 0.f;
-    const int beg = xrp[row], end = xrp[row + 1];
-    for (int p0 = beg; p0 < end; p0 += HID) {
-        const int p = p0 + lane;
-        int f = 0;
-        float x = 0.f;
-        if (p < end) {
-            f = xcol[p];
-            x = xval[p];
-            if (train) x = u_at(keys, keys.tag_x, ctr, row, f) < keep ? x * scale : 0.f;
-        }
-        // fixed trip count, fully unrolled: the 16 gathers are independent and all
-        // in flight at once (entries past `end` carry x = 0 and a valid index 0)
-        float wk[HID];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) wk[k] = wt[__shfl(f, k, HID) * HID + lane];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(x, k, HID), wk[k], acc);
-    }
-    out[row * HID + lane] = acc;
+    const int lane = threadIdx.x & 63;
+    const float acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, sc->fwd_ctr + fwd_off, train, keep,
+                                        scale, xd_csr, xd_csc, csr2csc);
+    if (lane < HID) out[row * HID + lane] = bias != nullptr ? bias[lane] + acc : acc;
 }
 
 // out[f][h] (= or +=) Σ_i Xd[i][f] · D[i][h]  (+ wd · w[f][h])   via CSC of X.
@@ -175,15 +207,21 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
-    float scale) {
+    float scale, float* __restrict__ dmask) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    // the dropout draw does not depend on the aggregation: issue it first
+    const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
+                           : 1.f;
     const float y = agg_row(rp, col, s, h0, row, lane);
     float hd = fmaxf(y, 0.f);
-    if (train) hd = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? hd * scale : 0.f;
+    if (train) hd = dk != 0.f ? hd * scale : 0.f;
     y0[row * HID + lane] = y;
     h1d[row * HID + lane] = hd;
+    // D1 ⊙ [Y0 > 0] (× 1/keep): the mask every later product with this layer's
+    // ReLU + dropout Jacobian reads instead of redrawing it
+    if (dmask != nullptr) dmask[row * HID + lane] = y > 0.f ? dk : 0.f;
     float out = 0.f;
     for (int k = 0; k < c; ++k) {
         const float t = gsum16(hd * w.w1[k * HID + lane]);
@@ -244,7 +282,8 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const float* __restrict__ d_o, const float* __restrict__ y0, float* __restrict__ dh2,
     float* __restrict__ dy0, GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off,
     int train, float keep, float scale, const float* __restrict__ o_in, const float* __restrict__ h2,
-    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth) {
+    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth,
+    int r_assign, const float* __restrict__ dmask) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
@@ -252,12 +291,17 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
     for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
-    float mask = y0[row * HID + lane] > 0.f ? 1.f : 0.f;
-    if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    float mask;
+    if (dmask != nullptr) {
+        mask = dmask[row * HID + lane];
+    } else {
+        mask = y0[row * HID + lane] > 0.f ? 1.f : 0.f;
+        if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    }
     dy0[row * HID + lane] = dh1d * mask;
     if (U != nullptr)  // outer graph, use 2: G = dO, Z = H2, Y = O, ÂG = dH2
         emit_factor(U, V, ldk, R, foff, fwidth, row, lane, s[row], d_o[row * HID + lane],
-                    h2[row * HID + lane], o_in[row * HID + lane], g2);
+                    h2[row * HID + lane], o_in[row * HID + lane], g2, r_assign != 0);
 }
 
 // dH0 = Â dY0.  Outer mode: emit factor (dY0, H0).
@@ -459,15 +503,21 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     GcnW w, const float* __restrict__ gw1bar, const float* __restrict__ gb1bar, int c,
     float* __restrict__ dh1dbar, float* __restrict__ dh2bar, float* __restrict__ h1dbar,
     Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
-    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff) {
+    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff,
+    const float* __restrict__ dmask) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, dh0bar, row, lane);  // dY0bar
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
-    float mask = y0[ix] > 0.f ? 1.f : 0.f;
-    if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    float mask;
+    if (dmask != nullptr) {
+        mask = dmask[ix];
+    } else {
+        mask = y0[ix] > 0.f ? 1.f : 0.f;
+        if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    }
     const float a = ag * mask;  // dH1dbar
     dh1dbar[ix] = a;
     const float hd = h1d[ix];
@@ -512,7 +562,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     const float* __restrict__ h1dbar_part, const float* __restrict__ y0, GcnW w, int c,
     float* __restrict__ h2bar, float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc,
     int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
-    int ldk, float* __restrict__ R, int foff, int cw) {
+    int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
@@ -522,8 +572,13 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     h2bar[ix] = ag;
     float hb = h1dbar_part[ix];
     for (int k = 0; k < c; ++k) hb = fmaf(bcast16(ag, k), w.w1[k * HID + lane], hb);
-    float mask = y0[ix] > 0.f ? 1.f : 0.f;
-    if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    float mask;
+    if (dmask != nullptr) {
+        mask = dmask[ix];
+    } else {
+        mask = y0[ix] > 0.f ? 1.f : 0.f;
+        if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    }
     y0bar[ix] = hb * mask;
 }
 
@@ -540,6 +595,370 @@ __global__ __launch_bounds__(256) void rev_d_kernel(
     const float ag = agg_row(rp, col, s, y0bar, row, lane);
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
     h0bar[ix] = ag;
+}
+
+// ---------------------------------------------------------------------------
+// Fused forms (fewer launches per window).
+//   * the column reductions run in the epilogue of the aggregation that
+//     produces their last input, one row per 16-lane group in 1024-thread
+//     blocks (64 rows), reduced in-wave by xor-shuffles and across waves in
+//     LDS into one partial per block (fixed order: deterministic);
+//   * the final reduction applies the differentiable-Adam forward (inner
+//     step) or reverse (hyper step) to b0 / W1 / b1, and xt_adam applies it
+//     to W0 right where each W0 gradient / adjoint is completed.
+// ---------------------------------------------------------------------------
+struct AdamArgs {
+    // mode 1 (forward): w0, m0, v0 -> w1, m1, v1, gp
+    // mode 2 (reverse of the step whose post-state is m1, v1 and whose g' is
+    //         gp): wbar (in: complete adjoint of w1; out: + wd·ḡ), mbar, vbar
+    //         (in/out; read as 0 when `first`), gbar (out)
+    const float* w0;
+    const float* m0;
+    const float* v0;
+    float* w1;
+    float* m1;
+    float* v1;
+    float* gp;
+    float* wbar;
+    float* mbar;
+    float* vbar;
+    float* gbar;
+    AdamHyper hp;
+    const float* tab;  // Adam step table (refresh_adam_table): {step_size, c2} per step offset
+    int step_off;
+    int mode;
+    int first;
+};
+
+// Operands of one parameter's Adam step, loaded ahead of the value they wait
+// for (so their latency overlaps the reduction / product that completes it).
+struct AdamOps {
+    float p0, p1, p2, p3, p4;
+};
+
+__device__ __forceinline__ AdamOps adam_load(const AdamArgs& a, int idx) {
+    AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
+    if (a.mode == 1) {
+        o.p0 = a.w0[idx];
+        o.p1 = a.m0[idx];
+        o.p2 = a.v0[idx];
+    } else if (a.mode == 2) {
+        o.p0 = a.m1[idx];
+        o.p1 = a.v1[idx];
+        o.p2 = a.gp[idx];
+        if (!a.first) {
+            o.p3 = a.mbar[idx];
+            o.p4 = a.vbar[idx];
+        }
+    }
+    return o;
+}
+
+// x: mode 1 the data gradient g; mode 2 the complete adjoint of w1.
+__device__ __forceinline__ void adam_apply(const AdamArgs& a, int idx, float x, const AdamOps& o,
+                                           float step_size, float c2) {
+    if (a.mode == 1) {
+        const float w = o.p0;
+        float gp = x;
+        if (idx < a.hp.n_wd && a.hp.wd != 0.f) gp = gp + a.hp.wd * w;
+        const float m = o.p1 * a.hp.beta1 + a.hp.omb1 * gp;
+        const float v = o.p2 * a.hp.beta2 + (a.hp.omb2 * gp) * gp;
+        const float denom = sqrtf(v) / c2 + a.hp.eps;
+        a.w1[idx] = w + ((-step_size) * m) / denom;
+        a.m1[idx] = m;
+        a.v1[idx] = v;
+        a.gp[idx] = gp;
+    } else if (a.mode == 2) {
+        const float wb = x;
+        const float m = o.p0, v = o.p1, g = o.p2;
+        const float sq = sqrtf(v);
+        const float denom = sq / c2 + a.hp.eps;
+        const float alpha = -step_size;
+        const float mb = o.p3 + wb * alpha / denom;
+        const float db = -wb * alpha * m / (denom * denom);
+        float vb = o.p4 + (db / c2) / (2.f * sq);
+        if (v == 0.f) vb = 0.f;  // higher's _maybe_mask hook on exp_avg_sq
+        const float gb = a.hp.omb1 * mb + 2.f * (a.hp.omb2 * g) * vb;
+        a.gbar[idx] = gb;
+        a.mbar[idx] = a.hp.beta1 * mb;
+        a.vbar[idx] = a.hp.beta2 * vb;
+        a.wbar[idx] = (idx < a.hp.n_wd && a.hp.wd != 0.f) ? wb + a.hp.wd * gb : wb;
+    }
+}
+
+__device__ __forceinline__ void adam_step_consts(const AdamArgs& a, const EngineScalars* __restrict__ sc,
+                                                 float& step_size, float& c2) {
+    (void)sc;
+    step_size = 0.f;
+    c2 = 1.f;
+    if (a.mode) {
+        step_size = a.tab[2 * a.step_off];
+        c2 = a.tab[2 * a.step_off + 1];
+    }
+}
+
+// {step_size, c2} of the Adam steps adam_step + 1 + k, k < count (one thread
+// each): the fp64 pow of the bias corrections runs once per window here
+// instead of in every wave of every Adam-fused kernel.
+__device__ __forceinline__ void refresh_adam_table(int adam_step, const double* __restrict__ betas,
+                                                   float* __restrict__ tab, int count, int k) {
+    if (k < count) {
+        const int step = adam_step + k + 1;
+        const double bc1 = 1.0 - pow(betas[0], (double)step);
+        const double bc2 = 1.0 - pow(betas[1], (double)step);
+        tab[2 * k] = (float)(betas[2] / bc1);
+        tab[2 * k + 1] = (float)sqrt(bc2);
+    }
+}
+
+constexpr int RG1K = 1024 / HID;  // row groups (rows) per 1024-thread block
+constexpr int kAdamTabMax = 256;  // step offsets covered by one Adam table
+
+// One row per 16-lane group (`valid` false past n); per-row terms as
+// colreduce_kernel; writes the block's partial (kRedLen floats).
+__device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1, float bh1, float av2,
+                                                  float bh2, float x1, float x2, float l, float q,
+                                                  float* __restrict__ partials) {
+    __shared__ float red[16][kRedLen];
+    const int lane = threadIdx.x & (HID - 1);
+    const int gw = (threadIdx.x >> 4) & 3;
+    const int wave = threadIdx.x >> 6;
+    if (!valid) av1 = bh1 = av2 = bh2 = x1 = x2 = l = q = 0.f;
+    float acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const float p1 = bcast16(av1, k), p2 = bcast16(av2, k);
+        acc[k] = k < c_n ? fmaf(p2, bh2, p1 * bh1) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        acc[k] += __shfl_xor(acc[k], 16);
+        acc[k] += __shfl_xor(acc[k], 32);
+    }
+    x1 += __shfl_xor(x1, 16);
+    x1 += __shfl_xor(x1, 32);
+    x2 += __shfl_xor(x2, 16);
+    x2 += __shfl_xor(x2, 32);
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    q += __shfl_xor(q, 16);
+    q += __shfl_xor(q, 32);
+    if (gw == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) red[wave][k * 16 + lane] = acc[k];
+        red[wave][256 + lane] = x1;
+        red[wave][272 + lane] = x2;
+        red[wave][288 + lane] = lane == 0 ? l : (lane == 1 ? q : 0.f);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kRedLen; e += 1024) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) t += red[w][e];
+        partials[(int64_t)blockIdx.x * kRedLen + e] = t;
+    }
+}
+
+// dH0 = Â dY0 (+ outer factor (dY0, H0)); block partials of
+// {gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, Σ loss, Σ correct}.
+__global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ dy0, float* __restrict__ dh0, const float* __restrict__ y0,
+    const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
+    float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ h1d,
+    const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
+    const bool valid = row < n;
+    float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
+    if (valid) {
+        const int ix = row * HID + lane;
+        g = agg_row(rp, col, s, dy0, row, lane);
+        dh0[ix] = g;
+        a1 = dh2[ix];
+        b1 = h1d[ix];
+        lr = lossrow[row];
+        qr = corrrow[row];
+    }
+    if (U != nullptr && valid)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
+        emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dy0[row * HID + lane],
+                    h0[row * HID + lane], y0[row * HID + lane], g);
+    block_reduce_1024(c, valid, a1, b1, 0.f, 0.f, g, a1, lr, qr, partials);
+}
+
+// H0bar = Â Y0bar (+ factor use 1); block partials of
+// {W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d, b̄0 += Σ H0bar, b̄1 += Σ H2bar}.
+__global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ y0bar, const float* __restrict__ h0, const float* __restrict__ y0,
+    float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
+    float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ dh1dbar,
+    const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
+    const bool valid = row < n;
+    float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
+    if (valid) {
+        const int ix = row * HID + lane;
+        ag = agg_row(rp, col, s, y0bar, row, lane);
+        emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
+        h0bar[ix] = ag;
+        a1 = dh2[ix];
+        b1 = dh1dbar[ix];
+        a2 = h2bar[ix];
+        b2 = h1d[ix];
+    }
+    block_reduce_1024(c, valid, a1, b1, a2, b2, ag, a2, 0.f, 0.f, partials);
+}
+
+// Sum the block partials (fixed order) into the flat parameter-shaped buffer
+// `dst` (W1 at off_w1, b0 at off_b0, b1 at off_b1; = or +=), Σ loss / Σ correct
+// into metrics[0..1], then Adam (mode 1 forward / mode 2 reverse) on those
+// parameters.  Element e of a partial (layout of colreduce_kernel).
+struct FinalArgs {
+    const float* partials;
+    int nblocks, c, off_b0, off_w1, off_b1, accumulate;
+    float* dst;
+    float* metrics;
+};
+
+// Parameter index of partial element e (-1: none; -2 / -3: Σ loss / Σ correct).
+__device__ __forceinline__ int final_index(const FinalArgs& f, int e) {
+    if (e < 256) return (e >> 4) < f.c ? f.off_w1 + e : -1;
+    if (e < 272) return f.off_b0 + (e - 256);
+    if (e < 288) return e - 272 < f.c ? f.off_b1 + (e - 272) : -1;
+    if (e < 290) return -2 - (e - 288);
+    return -1;
+}
+
+__device__ __forceinline__ float final_sum(const FinalArgs& f, int e) {
+    float t = 0.f;
+    for (int b0 = 0; b0 < f.nblocks; b0 += kRedBlocks) {
+        float v[kRedBlocks];
+#pragma unroll
+        for (int b = 0; b < kRedBlocks; ++b)
+            v[b] = b0 + b < f.nblocks ? f.partials[(int64_t)(b0 + b) * kRedLen + e] : 0.f;
+#pragma unroll
+        for (int w = kRedBlocks / 2; w > 0; w >>= 1)
+#pragma unroll
+            for (int b = 0; b < w; ++b) v[b] += v[b + w];
+        t += v[0];
+    }
+    return t;
+}
+
+// Final stage for up to two partial elements per thread (e1 < 0: none): all
+// loads (Adam operands, dst, partials) are issued before the sums complete.
+__device__ __forceinline__ void final_pair(const FinalArgs& f, int e0, int e1, const AdamArgs& adam,
+                                           const EngineScalars* __restrict__ sc) {
+    const int i0 = final_index(f, e0);
+    const int i1 = e1 >= 0 ? final_index(f, e1) : -1;
+    AdamOps o0{0.f, 0.f, 0.f, 0.f, 0.f}, o1{0.f, 0.f, 0.f, 0.f, 0.f};
+    float d0 = 0.f, d1 = 0.f;
+    if (i0 >= 0) {
+        o0 = adam_load(adam, i0);
+        if (f.accumulate) d0 = f.dst[i0];
+    }
+    if (i1 >= 0) {
+        o1 = adam_load(adam, i1);
+        if (f.accumulate) d1 = f.dst[i1];
+    }
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
+    const float t0 = final_sum(f, e0);
+    const float t1 = e1 >= 0 ? final_sum(f, e1) : 0.f;
+    if (i0 >= 0) {
+        const float val = f.accumulate ? d0 + t0 : t0;
+        f.dst[i0] = val;
+        adam_apply(adam, i0, val, o0, step_size, c2);
+    } else if (i0 <= -2 && f.metrics) {
+        f.metrics[-2 - i0] = t0;
+    }
+    if (i1 >= 0) {
+        const float val = f.accumulate ? d1 + t1 : t1;
+        f.dst[i1] = val;
+        adam_apply(adam, i1, val, o1, step_size, c2);
+    } else if (i1 <= -2 && f.metrics) {
+        f.metrics[-2 - i1] = t1;
+    }
+}
+
+__global__ __launch_bounds__(320) void final_kernel(FinalArgs f, AdamArgs adam,
+                                                    const EngineScalars* __restrict__ sc) {
+    if (threadIdx.x < kRedLen) final_pair(f, threadIdx.x, -1, adam, sc);
+}
+
+// out[W0 part] (= or +=) Xdᵀ d (one wave per feature) + Adam on the W0 entry it
+// completes (param index f·16 + h).  With f.partials != NULL the grid carries
+// one extra block that runs the final reduction of b0 / W1 / b1 (+ their Adam)
+// concurrently: both only need the kernel that produced d and the partials.
+__global__ __launch_bounds__(256) void xt_adam_kernel(
+    const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
+    const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
+    float keep, float scale, FinalArgs fin_args, AdamArgs adam) {
+    if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
+        const int e1 = threadIdx.x + 256;
+        final_pair(fin_args, threadIdx.x, e1 < kRedLen ? e1 : -1, adam, sc);
+        return;
+    }
+    const int f = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (f >= fin) return;
+    const int lane = threadIdx.x & 63;
+    const int idx = f * HID + (lane & (HID - 1));
+    // Adam operands and constants first: they overlap the product's loads
+    AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
+    float prev = 0.f;
+    if (lane < HID) {
+        o = adam_load(adam, idx);
+        if (fin_args.accumulate) prev = fin_args.dst[idx];
+    }
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
+    const float acc = x_wave_dot<true>(xcp, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
+    if (lane < HID) {
+        const float val = fin_args.accumulate ? prev + acc : acc;
+        fin_args.dst[idx] = val;
+        adam_apply(adam, idx, val, o, step_size, c2);
+    }
+}
+
+// End of a window: slot T -> slot 0 for w, m, v, and advance the scalars.
+__global__ __launch_bounds__(256) void end_window_kernel(int np, const float* __restrict__ wT,
+                                                         const float* __restrict__ mT,
+                                                         const float* __restrict__ vT,
+                                                         float* __restrict__ w0, float* __restrict__ m0,
+                                                         float* __restrict__ v0, EngineScalars* sc,
+                                                         int graphs, int forwards, int adam_steps,
+                                                         int hypers, const double* __restrict__ betas,
+                                                         float* __restrict__ tab, int tab_count) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (wT != nullptr && e < np) {
+        w0[e] = wT[e];
+        m0[e] = mT[e];
+        v0[e] = vT[e];
+    }
+    if (blockIdx.x == 0) {
+        __shared__ int new_step;
+        if (threadIdx.x == 0) {
+            sc->graph_ctr += graphs;
+            sc->fwd_ctr += forwards;
+            const int st = sc->adam_step + adam_steps;
+            sc->adam_step = st;
+            new_step = st;
+            for (int h = 0; h < hypers; ++h) {
+                sc->hyper_steps += 1;
+                sc->outer_lr = sc->outer_lr * sc->lr_decay;
+            }
+        }
+        __syncthreads();
+        if (tab != nullptr) refresh_adam_table(new_step, betas, tab, tab_count, threadIdx.x);
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_table_kernel(const EngineScalars* __restrict__ sc,
+                                                         const double* __restrict__ betas,
+                                                         float* __restrict__ tab, int count) {
+    refresh_adam_table(sc->adam_step, betas, tab, count, threadIdx.x);
 }
 
 // θ <- clamp(θ - lr·g, 0, 1) with lr from the scalars, then StepLR: lr *= γ.
@@ -580,11 +999,13 @@ static inline Keys mk_keys(uint64_t seed, uint32_t tag_x, uint32_t tag_h) {
 extern "C" int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int n,
                                    const float* wt, const float* bias, float* out, uint64_t seed,
                                    uint32_t tag_x, const void* scalars, int fwd_off, int train,
-                                   float keep, float scale, void* stream) {
+                                   float keep, float scale, float* xd_csr, float* xd_csc,
+                                   const int* csr2csc, void* stream) {
     LDS_CHECK_ARG(xrp && xcol && xval && wt && out && scalars && n > 0);
-    hipLaunchKernelGGL(x_linear_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, xrp,
+    LDS_CHECK_ARG(xd_csc == nullptr || (xd_csr && csr2csc));
+    hipLaunchKernelGGL(x_linear_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, xrp,
                        xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale);
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -603,13 +1024,13 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
                                      const float* h0, float* y0, float* h1d, float* h2,
                                      const float* w1, const float* b1, int c, uint64_t seed,
                                      uint32_t tag_h, const void* scalars, int fwd_off, int train,
-                                     float keep, float scale, void* stream) {
+                                     float keep, float scale, float* dmask, void* stream) {
     LDS_CHECK_ARG(rp && col && s && h0 && y0 && h1d && h2 && w1 && b1 && scalars && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID);
     GcnW w{nullptr, nullptr, w1, b1};
     hipLaunchKernelGGL(fwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale);
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -628,14 +1049,15 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
                                      const float* w1, int c, uint64_t seed, uint32_t tag_h,
                                      const void* scalars, int fwd_off, int train, float keep,
                                      float scale, const float* o, const float* h2, float* U, float* V,
-                                     int ldk, float* R, int foff, int fwidth, void* stream) {
+                                     int ldk, float* R, int foff, int fwidth, int r_assign,
+                                     const float* dmask, void* stream) {
     LDS_CHECK_ARG(rp && col && s && d_o && y0 && dh2 && dy0 && w1 && scalars && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && o && h2 && fwidth <= HID)));
     GcnW w{nullptr, nullptr, w1, nullptr};
     hipLaunchKernelGGL(bwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
-                       foff, fwidth);
+                       foff, fwidth, r_assign, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -699,14 +1121,15 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, i
                                 const float* gw1bar, const float* gb1bar, int c, float* dh1dbar,
                                 float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
                                 const void* scalars, int fwd_off, int train, float keep, float scale,
-                                float* U, float* V, int ldk, float* R, int foff, void* stream) {
+                                float* U, float* V, int ldk, float* R, int foff, const float* dmask,
+                                void* stream) {
     LDS_CHECK_ARG(rp && col && s && dh0bar && dy0 && dh0 && y0 && h1d && dh2 && w1 && gw1bar && gb1bar);
     LDS_CHECK_ARG(dh1dbar && dh2bar && h1dbar && scalars && U && V && R && n > 0 && c > 0 && c <= HID);
     GcnW w{nullptr, nullptr, w1, nullptr};
     hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar, h1dbar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
-                       scale, U, V, ldk, R, foff);
+                       scale, U, V, ldk, R, foff, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -726,14 +1149,15 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, i
                                 const float* h1dbar_part, const float* y0, const float* w1, int c,
                                 float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                                 const void* scalars, int fwd_off, int train, float keep, float scale,
-                                float* U, float* V, int ldk, float* R, int foff, int cw, void* stream) {
+                                float* U, float* V, int ldk, float* R, int foff, int cw,
+                                const float* dmask, void* stream) {
     LDS_CHECK_ARG(rp && col && s && obar && h2 && o && h1dbar_part && y0 && w1 && h2bar && y0bar);
     LDS_CHECK_ARG(scalars && U && V && R && n > 0 && c > 0 && c <= HID && cw >= c && cw <= HID);
     GcnW w{nullptr, nullptr, w1, nullptr};
     hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff,
-                       cw);
+                       cw, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -765,3 +1189,113 @@ extern "C" int lds_engine_advance(void* scalars, int graphs, int forwards, int a
 }
 
 extern "C" int lds_engine_scalars_size(void) { return (int)sizeof(EngineScalars); }
+
+// ----- fused entry points -----
+static AdamArgs mk_adam_args(int mode, int first, const float* w0, const float* m0, const float* v0,
+                             float* w1, float* m1, float* v1, float* gp, float* wbar, float* mbar,
+                             float* vbar, float* gbar, const double* hyper, const float* tab,
+                             int n_wd, int step_off) {
+    AdamArgs a;
+    a.w0 = w0; a.m0 = m0; a.v0 = v0; a.w1 = w1; a.m1 = m1; a.v1 = v1; a.gp = gp;
+    a.wbar = wbar; a.mbar = mbar; a.vbar = vbar; a.gbar = gbar;
+    a.hp = hyper ? mk_adam(hyper, n_wd) : AdamHyper{};
+    a.tab = tab; a.step_off = step_off; a.mode = mode; a.first = first;
+    return a;
+}
+
+static bool adam_ok(int mode, const float* w0, const float* m0, const float* v0, const float* w1,
+                    const float* m1, const float* v1, const float* gp, const float* wbar,
+                    const float* mbar, const float* vbar, const float* gbar, const double* hyper,
+                    const float* tab, int step_off) {
+    if (mode == 0) return true;
+    if (!hyper || !tab || step_off < 0 || step_off >= kAdamTabMax) return false;
+    if (mode == 1) return w0 && m0 && v0 && w1 && m1 && v1 && gp;
+    if (mode == 2) return m1 && v1 && gp && wbar && mbar && vbar && gbar;
+    return false;
+}
+
+extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, int n,
+                                      const float* dy0, float* dh0, const float* y0, const float* h0,
+                                      float* U, float* V, int ldk, float* R, int foff, const float* dh2,
+                                      const float* h1d, const float* lossrow, const float* corrrow, int c,
+                                      float* partials, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && dh2 && h1d && lossrow && corrrow && partials && n > 0);
+    LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)));
+    hipLaunchKernelGGL(bwd1_reduce_kernel, dim3((n + RG1K - 1) / RG1K), dim3(1024), 0, (hipStream_t)stream,
+                       rp, col, s, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow, corrrow, c,
+                       partials);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, int n,
+                                       const float* y0bar, const float* h0, const float* y0, float* h0bar,
+                                       float* U, float* V, int ldk, float* R, int foff, const float* dh2,
+                                       const float* dh1dbar, const float* h2bar, const float* h1d, int c,
+                                       float* partials, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && dh2 && dh1dbar && h2bar);
+    LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID);
+    hipLaunchKernelGGL(rev_d_reduce_kernel, dim3((n + RG1K - 1) / RG1K), dim3(1024), 0,
+                       (hipStream_t)stream, rp, col, s, n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff, dh2,
+                       dh1dbar, h2bar, h1d, c, partials);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int off_b0,
+                                int off_w1, int off_b1, int accumulate, float* metrics, int adam_mode,
+                                int first, const float* w0, const float* m0, const float* v0, float* w1,
+                                float* m1, float* v1, float* gp, float* wbar, float* mbar, float* vbar,
+                                float* gbar, const double* hyper, const float* adam_tab, int n_wd,
+                                const void* scalars, int step_off, void* stream) {
+    LDS_CHECK_ARG(partials && dst && scalars && nblocks > 0 && c > 0 && c <= HID);
+    LDS_CHECK_ARG(adam_ok(adam_mode, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper, adam_tab,
+                          step_off));
+    AdamArgs a = mk_adam_args(adam_mode, first, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper,
+                              adam_tab, n_wd, step_off);
+    FinalArgs f{partials, nblocks, c, off_b0, off_w1, off_b1, accumulate, dst, metrics};
+    hipLaunchKernelGGL(final_kernel, dim3(1), dim3(320), 0, (hipStream_t)stream, f, a,
+                       (const EngineScalars*)scalars);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int fin,
+                                  const float* d, float* out, int accumulate, uint64_t seed, uint32_t tag_x,
+                                  const void* scalars, int fwd_off, int train, float keep, float scale,
+                                  const float* partials, int nblocks, int c, int off_b0, int off_w1,
+                                  int off_b1, float* metrics, int adam_mode, int first, const float* w0,
+                                  const float* m0, const float* v0, float* w1, float* m1, float* v1,
+                                  float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
+                                  const double* hyper, const float* adam_tab, int n_wd, int step_off,
+                                  void* stream) {
+    LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && fin > 0);
+    LDS_CHECK_ARG(partials == nullptr || (nblocks > 0 && c > 0 && c <= HID));
+    LDS_CHECK_ARG(adam_ok(adam_mode, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper, adam_tab,
+                          step_off));
+    AdamArgs a = mk_adam_args(adam_mode, first, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper,
+                              adam_tab, n_wd, step_off);
+    FinalArgs f{partials, nblocks, c, off_b0, off_w1, off_b1, accumulate, out, metrics};
+    const int blocks = (fin + 3) / 4 + (partials != nullptr ? 1 : 0);
+    hipLaunchKernelGGL(xt_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin, d,
+                       mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
+                       a);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT, float* w0,
+                                     float* m0, float* v0, void* scalars, int graphs, int forwards,
+                                     int adam_steps, int hypers, const double* betas_dev, float* adam_tab,
+                                     int tab_count, void* stream) {
+    LDS_CHECK_ARG(scalars && np > 0 && (wT == nullptr || (mT && vT && w0 && m0 && v0)));
+    LDS_CHECK_ARG(adam_tab == nullptr || (betas_dev && tab_count > 0 && tab_count <= kAdamTabMax));
+    hipLaunchKernelGGL(end_window_kernel, dim3((np + 255) / 256), dim3(256), 0, (hipStream_t)stream, np, wT,
+                       mT, vT, w0, m0, v0, (EngineScalars*)scalars, graphs, forwards, adam_steps, hypers,
+                       betas_dev, adam_tab, tab_count);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_adam_table(const void* scalars, const double* betas_dev, float* adam_tab,
+                                     int tab_count, void* stream) {
+    LDS_CHECK_ARG(scalars && betas_dev && adam_tab && tab_count > 0 && tab_count <= kAdamTabMax);
+    hipLaunchKernelGGL(adam_table_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream,
+                       (const EngineScalars*)scalars, betas_dev, adam_tab, tab_count);
+    LDS_RETURN_LAST_ERROR();
+}

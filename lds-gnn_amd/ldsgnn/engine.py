@@ -39,6 +39,7 @@ from .rng import TAG_DROP_H, TAG_DROP_X, TAG_GRAPH, Generator, tag_for
 
 HID = 16
 _RED_LEN = 304
+_TAB_MAX = 256  # Adam table entries (kAdamTabMax in engine.hip)
 _ACT = ("h0", "y0", "h1d", "h2", "o", "p", "d_o", "dh2", "dy0", "dh0")
 
 
@@ -69,12 +70,16 @@ class _GraphBatch:
 
 
 class _Slot:
-    """Tape of one inner step (or the outer step): graph + activations."""
+    """Tape of one inner step (or the outer step): graph + activations, the
+    relu/dropout mask of layer 1 and (training with dropout) the dropped X
+    values in CSR and CSC order."""
 
-    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None):
+    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None, x_nnz: int = 0):
         self.g = graph if graph is not None else _Graph(n, cap, dev)
-        for a in _ACT:
+        for a in _ACT + ("dmask",):
             setattr(self, a, torch.zeros((n, HID), dtype=torch.float32, device=dev))
+        self.xd_csr = torch.zeros(x_nnz, dtype=torch.float32, device=dev) if x_nnz else None
+        self.xd_csc = torch.zeros(x_nnz, dtype=torch.float32, device=dev) if x_nnz else None
         self.lossrow = torch.zeros(n, dtype=torch.float32, device=dev)
         self.corrrow = torch.zeros(n, dtype=torch.float32, device=dev)
 
@@ -110,6 +115,8 @@ class LdsEngine:
         self.train_flag = 1 if self.dropout > 0.0 else 0
         self.hyper_np = np.array([gcn_lr, betas[0], betas[1], eps, gcn_wd], dtype=np.float64)
         self.betas_dev = torch.tensor([betas[0], betas[1], gcn_lr], dtype=torch.float64, device=dev)
+        # Adam table: {lr/bc1, sqrt(bc2)} for steps adam_step+1+k (refreshed on device)
+        self.adam_tab = torch.zeros(2 * _TAB_MAX, dtype=torch.float32, device=dev)
         self.gen = generator or Generator(0, 0)
         rep = self.gen.replica
         self.seed = self.gen.seed
@@ -120,6 +127,13 @@ class LdsEngine:
         # data
         self.xrp, self.xcol, self.xval = _csr_of(x.float())
         self.xcp, self.xrow, self.xtval = _csr_of(x.float().t().contiguous())
+        # position of each CSR entry of X in the CSC arrays (X is fixed)
+        nnz = int(self.xcol.numel())
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), (self.xrp[1:] - self.xrp[:-1]).long())
+        order = torch.argsort(self.xcol.long() * n + rows)
+        self.csr2csc = torch.empty(nnz, dtype=torch.int32, device=dev)
+        self.csr2csc[order] = torch.arange(nnz, dtype=torch.int32, device=dev)
+        self.x_nnz = nnz if self.train_flag else 0
         self.label = y.to(device=dev, dtype=torch.int32).contiguous()
         self.train_mask = train_mask.to(device=dev, dtype=torch.uint8).contiguous()
         self.opt_mask = opt_mask.to(device=dev, dtype=torch.uint8).contiguous()
@@ -160,7 +174,7 @@ class LdsEngine:
         self.gp: List[torch.Tensor] = []
         self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev)
         self._grow(self.tau)
-        self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau])
+        self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau], x_nnz=self.x_nnz)
         self.t = 0  # inner steps in the current window
         self.pending_graph = 0
         self.pending_fwd = 0
@@ -171,8 +185,8 @@ class LdsEngine:
         self.obar, self.h2bar, self.y0bar, self.h0bar = z(), z(), z(), z()
         zp = lambda: torch.zeros(self.np, dtype=torch.float32, device=dev)  # noqa: E731
         self.wbar, self.mbar, self.vbar, self.gbar, self.g = zp(), zp(), zp(), zp(), zp()
-        self.nblocks = max(1, min(64, (n + 15) // 16))  # colreduce first-stage blocks (<= 64)
-        self.partials = torch.zeros((self.nblocks, _RED_LEN), dtype=torch.float32, device=dev)
+        self.nred = (n + 63) // 64  # first-stage partials of the fused reductions (64 rows per block)
+        self.partials = torch.zeros((self.nred, _RED_LEN), dtype=torch.float32, device=dev)
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
         self.keep_grad = True  # write dθ (θ.grad) even when it is fused with the update
@@ -192,10 +206,12 @@ class LdsEngine:
         self.R = torch.zeros(self.n, dtype=torch.float32, device=self.dev)
 
     def _grow(self, slots: int):
+        if slots > _TAB_MAX:
+            raise NotImplementedError(f"LdsEngine: at most {_TAB_MAX} inner steps per hyper step")
         while len(self.slots) < slots:
             t = len(self.slots)
             g = self.gbatch.graphs[t] if t < self.gbatch.count - 1 else None
-            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g))
+            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g, x_nnz=self.x_nnz))
         while len(self.w) < slots + 1:
             for lst in (self.w, self.m, self.v):
                 lst.append(torch.zeros(self.np, dtype=torch.float32, device=self.dev))
@@ -239,13 +255,23 @@ class LdsEngine:
         self.m[0].zero_()
         self.v[0].zero_()
         self._i32[2:3].zero_()
+        self._refresh_adam_table()
         self.t = 0
+
+    def _tab_count(self) -> int:
+        return max(1, len(self.slots))
+
+    def _refresh_adam_table(self):
+        nat.call("lds_engine_adam_table", nat.ptr(self.scalars), nat.ptr(self.betas_dev), nat.ptr(self.adam_tab),
+                 self._tab_count(), self._stream())
 
     def _flush(self, hypers: int = 0):
         """Apply pending counter offsets to the device scalars."""
         if self.pending_graph or self.pending_fwd or self.t or hypers:
             nat.call("lds_engine_advance", nat.ptr(self.scalars), self.pending_graph, self.pending_fwd, self.t,
                      hypers, self._stream())
+            if self.t:
+                self._refresh_adam_table()
         self.pending_graph = 0
         self.pending_fwd = 0
 
@@ -277,41 +303,69 @@ class LdsEngine:
         st, n, c = self._stream(), self.n, self.c
         w0t, b0, w1, b1 = self._views(w)
         g = sl.g
+        # training forwards keep Xd (CSR + CSC order) and the relu/dropout mask
+        # on the tape: the step's later products read them instead of redrawing
+        keep_xd = train and sl.xd_csr is not None
+        xd = (nat.ptr(sl.xd_csr), nat.ptr(sl.xd_csc), nat.ptr(self.csr2csc)) if keep_xd else (0, 0, 0)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
                  nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, train, self.keep, self.scale, st)
+                 fwd_off, train, self.keep, self.scale, *xd, st)
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
-                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, st)
+                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask), st)
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
                  nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, st)
 
+    def _adam_args(self, mode: int, t: int, first: int = 0):
+        """Trailing Adam arguments of lds_engine_final / lds_engine_xt_adam.
+        mode 1: forward of inner step t; mode 2: reverse of inner step t."""
+        P = nat.ptr
+        if mode == 0:
+            return (0, 0) + (0,) * 11 + (0, 0, self.n_wd)
+        if mode == 1:
+            ws = (P(self.w[t]), P(self.m[t]), P(self.v[t]), P(self.w[t + 1]), P(self.m[t + 1]), P(self.v[t + 1]),
+                  P(self.gp[t]), 0, 0, 0, 0)
+        else:
+            ws = (0, 0, 0, 0, P(self.m[t + 1]), P(self.v[t + 1]), P(self.gp[t]), P(self.wbar), P(self.mbar),
+                  P(self.vbar), P(self.gbar))
+        return (mode, first) + ws + (self.hyper_np.ctypes.data, P(self.adam_tab), self.n_wd)
+
+    def _xvals(self, sl: _Slot):
+        """(CSR, CSC) values of X as the slot's training forward used them."""
+        if self.train_flag:
+            return sl.xd_csr, sl.xd_csc
+        return self.xval, self.xtval
+
     def _backward(self, sl: _Slot, w: torch.Tensor, gout: torch.Tensor, train: int, fwd_off: int,
-                  metrics_row: torch.Tensor, outer_factors: bool):
-        """First-order backward into `gout` (data gradient, no weight decay)."""
+                  metrics_row: torch.Tensor, outer_factors: bool, adam_mode: int, adam_t: int):
+        """First-order backward into `gout` (data gradient, no weight decay),
+        fused with the Adam forward of inner step adam_t (adam_mode 1) or the
+        Adam reverse of inner step adam_t (adam_mode 2, hyper step)."""
         st, n, c = self._stream(), self.n, self.c
         _, _, w1, _ = self._views(w)
         g = sl.g
-        go0t, gob0, gow1, gob1 = self._views(gout)
         if outer_factors:
             base = self.t * self.kg
             U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
         else:
             base, U, V, R = 0, 0, 0, 0
-        nat.call("lds_engine_bwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.d_o),
-                 nat.ptr(sl.y0), nat.ptr(sl.dh2), nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h,
-                 nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2),
-                 U, V, self.ldk, R, base + HID, self.cw, st)
-        nat.call("lds_engine_bwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.dy0),
-                 nat.ptr(sl.dh0), nat.ptr(sl.y0), nat.ptr(sl.h0), U, V, self.ldk, R, base, st)
-        # gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
-        nat.call("lds_engine_colreduce", n, c, nat.ptr(sl.dh2), nat.ptr(sl.h1d), 0, 0, nat.ptr(sl.dh0),
-                 nat.ptr(sl.dh2), nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), nat.ptr(self.partials), self.nblocks,
-                 nat.ptr(gow1), nat.ptr(gob0), HID, nat.ptr(gob1), c, nat.ptr(metrics_row), 0, st)
-        nat.call("lds_engine_xt_linear", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self.xtval), self.fin,
-                 nat.ptr(sl.dh0), nat.ptr(go0t), 0, 0.0, 0, self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, train, self.keep, self.scale, st)
+        rp, cl, s = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s)
+        nat.call("lds_engine_bwd_layer2", rp, cl, s, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
+                 nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
+                 self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldk, R, base + HID, self.cw,
+                 1, nat.ptr(sl.dmask), st)
+        # dH0 + first stage of gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
+        nat.call("lds_engine_bwd1_reduce", rp, cl, s, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
+                 nat.ptr(sl.h0), U, V, self.ldk, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
+                 nat.ptr(sl.corrrow), c, nat.ptr(self.partials), st)
+        first = 1 if adam_mode == 2 else 0
+        adam = self._adam_args(adam_mode, adam_t, first)
+        # W0 part (Xdᵀ dH0) and the final stage of the reduction, one launch
+        nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self._xvals(sl)[1]),
+                 self.fin, nat.ptr(sl.dh0), nat.ptr(gout), 0, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
+                 0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
+                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, st)
 
     # ----------------------------------------------------------------- steps
     def _sample_batch(self, count: int):
@@ -333,6 +387,7 @@ class LdsEngine:
             self.tau = t + 1
             self._alloc_factors()
             self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=self.dev)
+            self._refresh_adam_table()  # entries for the new step offsets
         sl = self.slots[t]
         if presampled:
             self.pending_graph += 1
@@ -340,13 +395,9 @@ class LdsEngine:
             self._sample(sl.g)
         fwd_off = self.pending_fwd
         self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off)
-        self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False)
+        self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False, 1, t)
         if self.train_flag:
             self.pending_fwd += 1
-        nat.call("lds_engine_adam", self.np, nat.ptr(self.w[t]), nat.ptr(self.g), nat.ptr(self.m[t]),
-                 nat.ptr(self.v[t]), nat.ptr(self.w[t + 1]), nat.ptr(self.m[t + 1]), nat.ptr(self.v[t + 1]),
-                 nat.ptr(self.gp[t]), self.hyper_np.ctypes.data, nat.ptr(self.betas_dev), self.n_wd,
-                 nat.ptr(self.scalars), t, self._stream())
         self.t = t + 1
         return self.metrics[t]
 
@@ -363,13 +414,13 @@ class LdsEngine:
         else:
             self._sample(out.g)
         fwd_off = self.pending_fwd
-        self.R.zero_()
         self._forward(out, self.w[T], self.opt_mask, self.inv_opt, self.train_flag, fwd_off)
-        self._backward(out, self.w[T], self.wbar, self.train_flag, fwd_off, self.metrics[self.tau], True)
+        # R is assigned by the outer layer-2 backward (first emitter); the
+        # Adam reverse of step T-1 starts from zero m̄ / v̄ (`first`)
+        self._backward(out, self.w[T], self.wbar, self.train_flag, fwd_off, self.metrics[self.tau], True,
+                       2 if T else 0, T - 1 if T else 0)
         if self.train_flag:
             self.pending_fwd += 1
-        self.mbar.zero_()
-        self.vbar.zero_()
         for t in range(T - 1, -1, -1):
             self._reverse_step(t)
         k = T * self.kg + HID + self.cw
@@ -384,52 +435,54 @@ class LdsEngine:
             nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
                      nat.ptr(self.scalars), st)
         # detach: the window restarts from the latest weights / Adam state
-        self._flush(hypers=1)
-        if T:
-            self.w[0].copy_(self.w[T])
-            self.m[0].copy_(self.m[T])
-            self.v[0].copy_(self.v[T])
+        P = nat.ptr
+        wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
+        nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
+                 P(self.scalars), self.pending_graph, self.pending_fwd, T, 1, P(self.betas_dev), P(self.adam_tab),
+                 self._tab_count(), st)
+        self.pending_graph = 0
+        self.pending_fwd = 0
         self.t = 0
         return self.metrics[self.tau]
 
     def _reverse_step(self, t: int):
+        """Reverse of inner step t; gbar already holds ḡ of step t (from the
+        Adam reverse fused into the previous stage).  Ends with the Adam
+        reverse of step t-1 fused into the W̄ completion."""
         st, n, c = self._stream(), self.n, self.c
         sl, g = self.slots[t], self.slots[t].g
         fwd_off = t if self.train_flag else 0  # forward counter of inner step t within the window
-        nat.call("lds_engine_adam_reverse", self.np, nat.ptr(self.wbar), nat.ptr(self.mbar), nat.ptr(self.vbar),
-                 nat.ptr(self.m[t + 1]), nat.ptr(self.v[t + 1]), nat.ptr(self.gp[t]), nat.ptr(self.gbar),
-                 self.hyper_np.ctypes.data, nat.ptr(self.betas_dev), self.n_wd, nat.ptr(self.scalars), t, st)
         gw0t, gb0, gw1, gb1 = self._views(self.gbar)
         _, _, w1, _ = self._views(self.w[t])
-        ww0t, wb0, ww1, wb1 = self._views(self.wbar)
         base = t * self.kg
         rp, cl, s = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s)
         U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
         tr = self.train_flag
-        nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
+        xcsr, xcsc = self._xvals(sl)  # Xd of step t (no redraw: train = 0 below)
+        nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(xcsr), n,
                  nat.ptr(gw0t), nat.ptr(gb0), nat.ptr(self.dh0bar), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, tr, self.keep, self.scale, st)
+                 fwd_off, 0, self.keep, self.scale, 0, 0, 0, st)
         nat.call("lds_engine_rev_a", rp, cl, s, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
                  nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldk, R,
-                 base + HID + 2 * self.cw, st)
+                 base + HID + 2 * self.cw, nat.ptr(sl.dmask), st)
         nat.call("lds_engine_rev_b", rp, cl, s, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
                  nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldk,
                  R, base + HID + self.cw, self.cw, st)
         nat.call("lds_engine_rev_c", rp, cl, s, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
                  nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
                  self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
-                 self.ldk, R, base + HID, self.cw, st)
-        nat.call("lds_engine_rev_d", rp, cl, s, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
-                 nat.ptr(self.h0bar), U, V, self.ldk, R, base, st)
-        nat.call("lds_engine_xt_linear", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self.xtval), self.fin,
-                 nat.ptr(self.h0bar), nat.ptr(ww0t), 0, 0.0, 1, self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, tr, self.keep, self.scale, st)
-        # W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
-        nat.call("lds_engine_colreduce", n, c, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar), nat.ptr(self.h2bar),
-                 nat.ptr(sl.h1d), nat.ptr(self.h0bar), nat.ptr(self.h2bar), 0, 0, nat.ptr(self.partials),
-                 self.nblocks, nat.ptr(ww1), nat.ptr(wb0), HID, nat.ptr(wb1), c, 0, 1, st)
+                 self.ldk, R, base + HID, self.cw, nat.ptr(sl.dmask), st)
+        # H0bar + first stage of W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
+        nat.call("lds_engine_rev_d_reduce", rp, cl, s, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
+                 nat.ptr(self.h0bar), U, V, self.ldk, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
+                 nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), st)
+        adam = self._adam_args(2 if t else 0, t - 1 if t else 0)
+        nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
+                 nat.ptr(self.h0bar), nat.ptr(self.wbar), 1, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
+                 0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
+                 self.off_b1, 0, *adam, t - 1, st)
 
     # ------------------------------------------------------------- graphs
     def run_window(self, tau: int, grad_reducer=None):
