@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel", default="auto", help="entry point for the roofline leg (auto: the θ-grad "
                     "assembly the path uses)")
+    ap.add_argument("--split", action="store_true", help="engine: per-graph dθ chunks on a side stream beside "
+                    "the reverse pass instead of one assembly launch per window (measured slower on MI355X)")
     ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
                     help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
@@ -155,10 +157,14 @@ def main():
 
     use_engine = args.path == "engine"
     if args.kernel == "auto":
-        args.kernel = "lds_theta_grad_sgd" if (use_engine and world == 1) else "lds_theta_grad"
+        if use_engine and world == 1:
+            args.kernel = "lds_theta_grad_sgd_accum" if args.split else "lds_theta_grad_sgd"
+        else:
+            args.kernel = "lds_theta_grad"
     if use_engine:
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
         eng, reducer = make_engine(runner, args.tau, world)
+        eng.split_theta_grad = args.split
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
@@ -209,9 +215,11 @@ def main():
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
     else:  # lds_theta_grad[_sgd]: rank-2k update of the packed triangle
-        if use_engine:  # one launch per window: k = tau*(32 + 2*8) + 24 columns at C=7
-            from ldsgnn.engine import LdsEngine
+        from ldsgnn.engine import LdsEngine
+        if use_engine and args.kernel == "lds_theta_grad_sgd":  # one launch per window: all columns
             k = LdsEngine.window_columns(args.tau, data.num_classes)
+        elif use_engine:  # split assembly: the timed launch is one graph's chunk (+ R, SGD)
+            k = LdsEngine.window_columns(1, data.num_classes) - LdsEngine.window_columns(0, data.num_classes)
         else:  # one launch per graph: 4 uses (16 + 8 + 8 + 16 columns)
             k = 16 + 8 + 8 + 16
         flops = 4.0 * k * tri

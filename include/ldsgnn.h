@@ -99,14 +99,23 @@ int lds_bitmask_fill_csr(const uint64_t* bits, int n, int words,
 int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* s,
                          void* stream);
 
+/* ELL head of a graph (the engine's aggregation layout): for every row its
+ * first 16 CSR entries as {j, bits of s_j} int pairs (n × 16 × 2 ints),
+ * padded with {row, 0}.  lds_bitmask_fill_csr plus the ELL head (s from
+ * lds_bitmask_degree). */
+int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
+                             const int* row_ptr, int* col, int64_t col_capacity,
+                             int* overflow, const float* s, int* ell, void* stream);
+
 /* Batched form for a window of graphs drawn from the same θ: graph g
  * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
  * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
- * col + g·col_stride, s + g·n.  Four launches for all `count` graphs. */
+ * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·32.  Four launches
+ * for all `count` graphs. */
 int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
                       const uint32_t* counter_base, uint32_t counter_offset, int count,
                       uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
-                      int64_t col_stride, float* s, void* stream);
+                      int64_t col_stride, float* s, int* ell, void* stream);
 
 /* The four launches above in order: sample -> degree/s -> scan -> fill.
  * deg_ws: n ints of workspace. */
@@ -162,6 +171,14 @@ int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
                        const float* r, int ldr, int nr, float* theta, int n,
                        float* grad, const void* scalars, void* stream);
 
+/* lds_theta_grad_sgd for the last column chunk of a split assembly: grad
+ * holds the sum of the earlier chunks (lds_theta_grad with accumulate, no R,
+ * theta NULL); g = grad + this chunk + R_i + R_j (clamp mask on θ), grad = g,
+ * θ = clamp(θ - lr·g, 0, 1).  Lets the chunks of finished graphs run on a side
+ * stream while the reverse pass continues. */
+int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k,
+                             const float* r, int ldr, int nr, float* theta, int n,
+                             float* grad, const void* scalars, void* stream);
 /* Slot factors for lds_theta_grad from one aggregation Y = ÂZ and its
  * cotangent G (dZ = ÂG):  U = s⊙G, V = s⊙Z, r = -½ s² (G·Y + Z·dZ) rowwise.
  * Columns [f, fpad) of U and V are zero-filled. */
@@ -234,21 +251,21 @@ int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int
 /* Y0 = ÂH0; H1d = dropout(relu(Y0)); H2 = H1d W1ᵀ + b1.  dmask (may be
  * NULL) receives D1 ⊙ [Y0 > 0] / keep, the Jacobian mask of relu + dropout,
  * which lds_engine_bwd_layer2 / rev_a / rev_c read instead of y0 + RNG. */
-int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, int n,
+int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* h0, float* y0, float* h1d, float* h2,
                           const float* w1, const float* b1, int c, uint64_t seed,
                           uint32_t tag_h, const void* scalars, int fwd_off, int train,
                           float keep, float scale, float* dmask, void* stream);
 /* O = ÂH2; P = softmax(O); dO = (P - onehot) ⊙ mask · inv_count; per-row
  * NLL and correctness where mask. */
-int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, int n,
+int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* h2, float* o, float* p, float* d_o,
                           const int* label, const uint8_t* mask, float inv_count,
                           float* lossrow, float* corrrow, int c, void* stream);
 /* dH2 = ÂdO; dY0 = (dH2 W1) ⊙ dropout' ⊙ relu'.  U != NULL: emit the outer
  * graph's factor (dO, H2) at columns [foff, foff + fwidth); r_assign != 0
  * writes R (first emitter of a window) instead of accumulating into it. */
-int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, int n,
+int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* d_o, const float* y0, float* dh2, float* dy0,
                           const float* w1, int c, uint64_t seed, uint32_t tag_h,
                           const void* scalars, int fwd_off, int train, float keep,
@@ -256,7 +273,7 @@ int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, int n,
                           float* V, int ldk, float* R, int foff, int fwidth,
                           int r_assign, const float* dmask, void* stream);
 /* dH0 = ÂdY0.  U != NULL: emit the outer graph's factor (dY0, H0). */
-int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, int n,
+int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* dy0, float* dh0, const float* y0,
                           const float* h0, float* U, float* V, int ldk, float* R,
                           int foff, void* stream);
@@ -281,7 +298,7 @@ int lds_engine_adam_reverse(int np, float* wbar, float* mbar, float* vbar,
 /* Reverse of the inner backward (Hessian-vector part): aggregation kernels
  * a (dY0bar = ÂdH0bar), b (dObar = ÂdH2bar), c (H2bar = ÂObar),
  * d (H0bar = ÂY0bar), each emitting its use's factor pair. */
-int lds_engine_rev_a(const int* rp, const int* col, const float* s, int n,
+int lds_engine_rev_a(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* dh0bar, const float* dy0, const float* dh0,
                      const float* y0, const float* h1d, const float* dh2, const float* w1,
                      const float* gw1bar, const float* gb1bar, int c, float* dh1dbar,
@@ -289,19 +306,19 @@ int lds_engine_rev_a(const int* rp, const int* col, const float* s, int n,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, const float* dmask,
                      void* stream);
-int lds_engine_rev_b(const int* rp, const int* col, const float* s, int n,
+int lds_engine_rev_b(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* dh2bar, const float* d_o, const float* dh2,
                      const float* p, const uint8_t* mask, float inv_count, int c,
                      float* obar, float* U, float* V, int ldk, float* R, int foff,
                      int cw, void* stream);
-int lds_engine_rev_c(const int* rp, const int* col, const float* s, int n,
+int lds_engine_rev_c(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* obar, const float* h2, const float* o,
                      const float* h1dbar_part, const float* y0, const float* w1, int c,
                      float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, int cw,
                      const float* dmask, void* stream);
-int lds_engine_rev_d(const int* rp, const int* col, const float* s, int n,
+int lds_engine_rev_d(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* y0bar, const float* h0, const float* y0,
                      float* h0bar, float* U, float* V, int ldk, float* R, int foff,
                      void* stream);
@@ -334,14 +351,14 @@ int lds_engine_advance(void* scalars, int graphs, int forwards, int adam_steps,
 /* dH0 = ÂdY0 (+ outer factor (dY0, H0) when U != NULL) fused with the first
  * stage of {gW1 = dH2ᵀH1d, gb0 = ΣdH0, gb1 = ΣdH2, Σloss, Σcorrect}:
  * ceil(n/64) partials of 304 floats. */
-int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, int n,
+int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, const int* ell, int n,
                            const float* dy0, float* dh0, const float* y0, const float* h0,
                            float* U, float* V, int ldk, float* R, int foff,
                            const float* dh2, const float* h1d, const float* lossrow,
                            const float* corrrow, int c, float* partials, void* stream);
 /* H0bar = ÂY0bar (+ factor use 1) fused with the first stage of
  * {W̄1 += dH2ᵀdH1dbar + H2barᵀH1d, b̄0 += ΣH0bar, b̄1 += ΣH2bar}. */
-int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, int n,
+int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, const int* ell, int n,
                             const float* y0bar, const float* h0, const float* y0,
                             float* h0bar, float* U, float* V, int ldk, float* R, int foff,
                             const float* dh2, const float* dh1dbar, const float* h2bar,

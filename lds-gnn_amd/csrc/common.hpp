@@ -14,6 +14,7 @@
 namespace lds {
 
 constexpr int kWave = 64;
+constexpr int kEllWidth = 16;  // neighbours per row in a graph's ELL head ({j, s_j} pairs)
 
 // Packed upper-triangle index of (i, j), i <= j, of an n×n matrix in
 // torch.triu_indices(n, n) row-major order (src/utils/graph.py:41-45).
@@ -40,6 +41,8 @@ struct U32x4 {
 __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+        // (a v_mad_u64_u32 form was 1.31x faster in isolation,
+        // tools/microbench/philox_rate.hip, but slower inside the sampler)
         const uint32_t lo0 = 0xD2511F53u * c.x;
         const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
         const uint32_t lo1 = 0xCD9E8D57u * c.z;

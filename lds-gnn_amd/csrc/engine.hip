@@ -56,17 +56,32 @@ __device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr,
 }
 
 // Normalised aggregation of one 16-wide row: s_i Σ_j s_j Z[j][lane].
+// Chunks of 16 neighbours: one coalesced load of their column indices, each
+// lane fetches s of its own neighbour, then all 16 row gathers are in flight at
+// once.  With `ell` (the graph's first 16 neighbours per row as {j, s_j} pairs,
+// padding {row, 0}: lds_bitmask_fill_csr) the first chunk needs no row_ptr /
+// col / s round trip: ell, row_ptr and s[row] load together and the gathers
+// follow directly.  Past the row's end the weight is 0 (fmaf(0, z, acc) ==
+// acc), so the sum keeps the plain loop's sequential order either way.
 __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* __restrict__ col,
-                                         const float* __restrict__ s, const float* __restrict__ z,
-                                         int row, int lane) {
-    // Chunks of 16 neighbours: one coalesced load of their column indices, each
-    // lane fetches s of its own neighbour, then all 16 row gathers are in
-    // flight at once (3 dependent loads per chunk instead of 2 per 4 entries).
-    // Past the row's end: index = row, weight 0 (fmaf(0, z, acc) == acc), so
-    // the sum is the same sequential order as the plain loop.
-    const int beg = rp[row], end = rp[row + 1];
+                                         const float* __restrict__ s, const int2* __restrict__ ell,
+                                         const float* __restrict__ z, int row, int lane) {
     float acc = 0.f;
-    for (int p0 = beg; p0 < end; p0 += HID) {
+    int p0;
+    const int end = rp[row + 1];
+    if (ell != nullptr) {
+        const int2 e = ell[row * HID + lane];
+        const float sl = __int_as_float(e.y);
+        float zk[HID];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(e.x, k, HID) * HID + lane];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, k, HID), zk[k], acc);
+        p0 = rp[row] + HID;
+    } else {
+        p0 = rp[row];
+    }
+    for (; p0 < end; p0 += HID) {
         const int p = p0 + lane;
         const int jl = p < end ? col[p] : row;
         const float sl = p < end ? s[jl] : 0.f;
@@ -204,7 +219,8 @@ struct GcnW {  // pointers into a flat parameter vector (layout in engine.py)
 
 // Y0 = Â H0;  H1d = relu(Y0) ⊙ D1;  H2 = H1d W1ᵀ + b1  (16-padded, zeros past C)
 __global__ __launch_bounds__(256) void fwd_layer1_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ dmask) {
@@ -214,7 +230,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     // the dropout draw does not depend on the aggregation: issue it first
     const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
                            : 1.f;
-    const float y = agg_row(rp, col, s, h0, row, lane);
+    const float y = agg_row(rp, col, s, ell, h0, row, lane);
     float hd = fmaxf(y, 0.f);
     if (train) hd = dk != 0.f ? hd * scale : 0.f;
     y0[row * HID + lane] = y;
@@ -233,14 +249,15 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
 // O = Â H2; P = softmax(O) (over c classes); dO = (P - onehot(y)) ⊙ m / |m|;
 // per-row loss -log P[y] and correctness (argmax == y) where m.
 __global__ __launch_bounds__(256) void fwd_layer2_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ h2, float* __restrict__ o_out, float* __restrict__ p_out,
     float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
     float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    const float o = agg_row(rp, col, s, h2, row, lane);
+    const float o = agg_row(rp, col, s, ell, h2, row, lane);
     const bool act = lane < c;
     const float m = gmax16(act ? o : -INFINITY);
     const float e = act ? expf(o - m) : 0.f;
@@ -278,7 +295,8 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
 
 // dH2 = Â dO;  dY0 = (dH2 W1) ⊙ D1 ⊙ [Y0 > 0].  Outer mode: emit factor (dO, H2).
 __global__ __launch_bounds__(256) void bwd_layer2_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ d_o, const float* __restrict__ y0, float* __restrict__ dh2,
     float* __restrict__ dy0, GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off,
     int train, float keep, float scale, const float* __restrict__ o_in, const float* __restrict__ h2,
@@ -287,7 +305,7 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    const float g2 = agg_row(rp, col, s, d_o, row, lane);  // zero past c (dO is)
+    const float g2 = agg_row(rp, col, s, ell, d_o, row, lane);  // zero past c (dO is)
     dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
     for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
@@ -306,14 +324,15 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
 
 // dH0 = Â dY0.  Outer mode: emit factor (dY0, H0).
 __global__ __launch_bounds__(256) void bwd_layer1_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ dy0, float* __restrict__ dh0, const float* __restrict__ y0,
     const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    const float g = agg_row(rp, col, s, dy0, row, lane);
+    const float g = agg_row(rp, col, s, ell, dy0, row, lane);
     dh0[row * HID + lane] = g;
     if (U != nullptr)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dy0[row * HID + lane],
@@ -497,7 +516,8 @@ __global__ __launch_bounds__(256) void adam_rev_kernel(
 // dH2bar  = dH1dbar W1ᵀ + H1d ḡW1ᵀ + ḡb1
 // H1dbar_part = dH2 ḡW1
 __global__ __launch_bounds__(256) void rev_a_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ dh0bar, const float* __restrict__ dy0, const float* __restrict__ dh0,
     const float* __restrict__ y0, const float* __restrict__ h1d, const float* __restrict__ dh2,
     GcnW w, const float* __restrict__ gw1bar, const float* __restrict__ gb1bar, int c,
@@ -509,7 +529,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, dh0bar, row, lane);  // dY0bar
+    const float ag = agg_row(rp, col, s, ell, dh0bar, row, lane);  // dY0bar
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
     float mask;
     if (dmask != nullptr) {
@@ -536,7 +556,8 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
 // dObar = Â dH2bar.  Factor use 3 (G = dH2bar, Z = dO, Y = dH2, ÂG = dObar).
 // Obar = P ⊙ (ū - P·ū), ū = dObar ⊙ m / |m|   (softmax Jacobian of dO = (P - E) m/|m|)
 __global__ __launch_bounds__(256) void rev_b_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ dh2bar, const float* __restrict__ d_o, const float* __restrict__ dh2,
     const float* __restrict__ p, const uint8_t* __restrict__ mask, float inv_count, int c,
     float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
@@ -545,7 +566,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, dh2bar, row, lane);  // dObar
+    const float ag = agg_row(rp, col, s, ell, dh2bar, row, lane);  // dObar
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
     const bool sel = mask[row] != 0;
     const float ub = (sel && lane < c) ? ag * inv_count : 0.f;
@@ -557,7 +578,8 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
 // H2bar = Â Obar.  Factor use 2 (G = Obar, Z = H2, Y = O, ÂG = H2bar).
 // H1dbar = H1dbar_part + H2bar W1;  Y0bar = H1dbar ⊙ D1 ⊙ [Y0 > 0]
 __global__ __launch_bounds__(256) void rev_c_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ obar, const float* __restrict__ h2, const float* __restrict__ o,
     const float* __restrict__ h1dbar_part, const float* __restrict__ y0, GcnW w, int c,
     float* __restrict__ h2bar, float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc,
@@ -567,7 +589,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, obar, row, lane);  // H2bar (zero past c)
+    const float ag = agg_row(rp, col, s, ell, obar, row, lane);  // H2bar (zero past c)
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
     h2bar[ix] = ag;
     float hb = h1dbar_part[ix];
@@ -584,7 +606,8 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
 
 // H0bar = Â Y0bar.  Factor use 1 (G = Y0bar, Z = H0, Y = Y0, ÂG = H0bar).
 __global__ __launch_bounds__(256) void rev_d_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ y0bar, const float* __restrict__ h0, const float* __restrict__ y0,
     float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff) {
@@ -592,7 +615,7 @@ __global__ __launch_bounds__(256) void rev_d_kernel(
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, y0bar, row, lane);
+    const float ag = agg_row(rp, col, s, ell, y0bar, row, lane);
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
     h0bar[ix] = ag;
 }
@@ -762,7 +785,8 @@ __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1
 // dH0 = Â dY0 (+ outer factor (dY0, H0)); block partials of
 // {gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, Σ loss, Σ correct}.
 __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ dy0, float* __restrict__ dh0, const float* __restrict__ y0,
     const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ h1d,
@@ -773,7 +797,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        g = agg_row(rp, col, s, dy0, row, lane);
+        g = agg_row(rp, col, s, ell, dy0, row, lane);
         dh0[ix] = g;
         a1 = dh2[ix];
         b1 = h1d[ix];
@@ -789,7 +813,8 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
 // H0bar = Â Y0bar (+ factor use 1); block partials of
 // {W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d, b̄0 += Σ H0bar, b̄1 += Σ H2bar}.
 __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
-    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n,
     const float* __restrict__ y0bar, const float* __restrict__ h0, const float* __restrict__ y0,
     float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ dh1dbar,
@@ -800,7 +825,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        ag = agg_row(rp, col, s, y0bar, row, lane);
+        ag = agg_row(rp, col, s, ell, y0bar, row, lane);
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
         h0bar[ix] = ag;
         a1 = dh2[ix];
@@ -1020,7 +1045,7 @@ extern "C" int lds_engine_xt_linear(const int* xcp, const int* xrow, const float
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, const int* ell, int n,
                                      const float* h0, float* y0, float* h1d, float* h2,
                                      const float* w1, const float* b1, int c, uint64_t seed,
                                      uint32_t tag_h, const void* scalars, int fwd_off, int train,
@@ -1029,22 +1054,22 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     LDS_CHECK_ARG(c > 0 && c <= HID);
     GcnW w{nullptr, nullptr, w1, b1};
     hipLaunchKernelGGL(fwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
-                       col, s, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
+                       col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                                      const float* h2, float* o, float* p, float* d_o,
                                      const int* label, const uint8_t* mask, float inv_count,
                                      float* lossrow, float* corrrow, int c, void* stream) {
     LDS_CHECK_ARG(rp && col && s && h2 && label && lossrow && corrrow && n > 0 && c > 0 && c <= HID);
     hipLaunchKernelGGL(fwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
-                       col, s, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c);
+                       col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                                      const float* d_o, const float* y0, float* dh2, float* dy0,
                                      const float* w1, int c, uint64_t seed, uint32_t tag_h,
                                      const void* scalars, int fwd_off, int train, float keep,
@@ -1055,19 +1080,19 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && o && h2 && fwidth <= HID)));
     GcnW w{nullptr, nullptr, w1, nullptr};
     hipLaunchKernelGGL(bwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
-                       col, s, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
+                       col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
                        foff, fwidth, r_assign, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, const int* ell, int n,
                                      const float* dy0, float* dh0, const float* y0, const float* h0,
                                      float* U, float* V, int ldk, float* R, int foff, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && n > 0);
     LDS_CHECK_ARG(U == nullptr || (V && R && y0 && h0));
     hipLaunchKernelGGL(bwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
-                       col, s, n, dy0, dh0, y0, h0, U, V, ldk, R, foff);
+                       col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1115,7 +1140,7 @@ extern "C" int lds_engine_adam_reverse(int np, float* wbar, float* mbar, float* 
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, const int* ell, int n,
                                 const float* dh0bar, const float* dy0, const float* dh0,
                                 const float* y0, const float* h1d, const float* dh2, const float* w1,
                                 const float* gw1bar, const float* gb1bar, int c, float* dh1dbar,
@@ -1126,25 +1151,25 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, i
     LDS_CHECK_ARG(rp && col && s && dh0bar && dy0 && dh0 && y0 && h1d && dh2 && w1 && gw1bar && gb1bar);
     LDS_CHECK_ARG(dh1dbar && dh2bar && h1dbar && scalars && U && V && R && n > 0 && c > 0 && c <= HID);
     GcnW w{nullptr, nullptr, w1, nullptr};
-    hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
                        n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar, h1dbar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
                        scale, U, V, ldk, R, foff, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, const int* ell, int n,
                                 const float* dh2bar, const float* d_o, const float* dh2, const float* p,
                                 const uint8_t* mask, float inv_count, int c, float* obar, float* U,
                                 float* V, int ldk, float* R, int foff, int cw, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dh2bar && d_o && dh2 && p && mask && obar && U && V && R && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID);
-    hipLaunchKernelGGL(rev_b_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    hipLaunchKernelGGL(rev_b_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
                        n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, const int* ell, int n,
                                 const float* obar, const float* h2, const float* o,
                                 const float* h1dbar_part, const float* y0, const float* w1, int c,
                                 float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
@@ -1154,18 +1179,18 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, i
     LDS_CHECK_ARG(rp && col && s && obar && h2 && o && h1dbar_part && y0 && w1 && h2bar && y0bar);
     LDS_CHECK_ARG(scalars && U && V && R && n > 0 && c > 0 && c <= HID && cw >= c && cw <= HID);
     GcnW w{nullptr, nullptr, w1, nullptr};
-    hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
                        n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff,
                        cw, dmask);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_rev_d(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_rev_d(const int* rp, const int* col, const float* s, const int* ell, int n,
                                 const float* y0bar, const float* h0, const float* y0, float* h0bar,
                                 float* U, float* V, int ldk, float* R, int foff, void* stream) {
     LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && n > 0);
-    hipLaunchKernelGGL(rev_d_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    hipLaunchKernelGGL(rev_d_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
                        n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff);
     LDS_RETURN_LAST_ERROR();
 }
@@ -1214,7 +1239,7 @@ static bool adam_ok(int mode, const float* w0, const float* m0, const float* v0,
     return false;
 }
 
-extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, const int* ell, int n,
                                       const float* dy0, float* dh0, const float* y0, const float* h0,
                                       float* U, float* V, int ldk, float* R, int foff, const float* dh2,
                                       const float* h1d, const float* lossrow, const float* corrrow, int c,
@@ -1222,12 +1247,12 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
     LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && dh2 && h1d && lossrow && corrrow && partials && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)));
     hipLaunchKernelGGL(bwd1_reduce_kernel, dim3((n + RG1K - 1) / RG1K), dim3(1024), 0, (hipStream_t)stream,
-                       rp, col, s, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow, corrrow, c,
+                       rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow, corrrow, c,
                        partials);
     LDS_RETURN_LAST_ERROR();
 }
 
-extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, int n,
+extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, const int* ell, int n,
                                        const float* y0bar, const float* h0, const float* y0, float* h0bar,
                                        float* U, float* V, int ldk, float* R, int foff, const float* dh2,
                                        const float* dh1dbar, const float* h2bar, const float* h1d, int c,
@@ -1235,7 +1260,7 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
     LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && dh2 && dh1dbar && h2bar);
     LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID);
     hipLaunchKernelGGL(rev_d_reduce_kernel, dim3((n + RG1K - 1) / RG1K), dim3(1024), 0,
-                       (hipStream_t)stream, rp, col, s, n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff, dh2,
+                       (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff, dh2,
                        dh1dbar, h2bar, h1d, c, partials);
     LDS_RETURN_LAST_ERROR();
 }

@@ -122,63 +122,41 @@ __global__ __launch_bounds__(256) void theta_grad_kernel(
 // wave a 32×32 sub-tile; k staged through LDS in chunks of 16, transposed to
 // [k][row] with a +1 row pad (conflict-free transposed writes and b32 reads).
 // Epilogue per mode: 0 grad = g, 1 grad += g, 2 θ = clamp(θ - lr·g, 0, 1)
-// with lr read from device memory (and grad = g when grad != NULL).
+// with lr read from device memory (and grad = g when grad != NULL), 3 as 2
+// with g += grad (the partial sum of earlier column chunks) and grad = g.
 // ---------------------------------------------------------------------------
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kLdsRow = kTile + 1;
+constexpr int kMC = 32;  // k-chunk of the MFMA form
 
-__global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
-    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
-    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
-    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4) {
-    __shared__ float Ui[kKC][kLdsRow];
-    __shared__ float Vi[kKC][kLdsRow];
-    __shared__ float Uj[kKC][kLdsRow];
-    __shared__ float Vj[kKC][kLdsRow];
-    __shared__ float Ri[kTile], Rj[kTile];
+// Global -> register stage of one k-chunk: thread t holds rows (t >> 2) of the
+// i- and j-blocks, k quads (t & 3)·4 and 16 + (t & 3)·4, of U and V.
+struct ChunkRegs {
+    float4 ui[2], vi[2], uj[2], vj[2];
+};
 
-    int a, b;
-    tri_tile(blockIdx.x, a, b);
-    const int bi = b, bj = a;
-    const int i0 = bi * kTile, j0 = bj * kTile;
-    const int t = threadIdx.x;
-    const int lane = t & 63, wave = t >> 6;
-    const int wr = wave >> 1, wc = wave & 1;  // 32×32 sub-tile of this wave
-
-    if (t < 2 * kTile) {
-        const int rr = t & (kTile - 1);
-        const int row = (t < kTile ? i0 : j0) + rr;
-        float acc = 0.f;
-        if (row < n)
-            for (int c = 0; c < nr; ++c) acc += r[(int64_t)row * ldr + c];
-        (t < kTile ? Ri : Rj)[rr] = acc;
-    }
-
-    f32x16 acc;
+__device__ __forceinline__ void load_chunk(const float* __restrict__ u, const float* __restrict__ v, int ld,
+                                           int k, int n, int gi, int gj, int k0, int fq, int vec4,
+                                           ChunkRegs& c) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-
-    // fill mapping: thread -> (row fr, k quad fq)
-    const int fr = t >> 2, fq = (t & 3) * 4;
-    const int gi = i0 + fr, gj = j0 + fr;
-    for (int k0 = 0; k0 < k; k0 += kKC) {
-        __syncthreads();
-        const int gk = k0 + fq;
-        float4 ui = {0.f, 0.f, 0.f, 0.f}, vi = ui, uj = ui, vj = ui;
+    for (int h = 0; h < 2; ++h) {
+        const int gk = k0 + fq + 16 * h;
+        float4 z = {0.f, 0.f, 0.f, 0.f};
+        c.ui[h] = z; c.vi[h] = z; c.uj[h] = z; c.vj[h] = z;
         if (vec4 && gk + 3 < k) {
             if (gi < n) {
-                ui = *reinterpret_cast<const float4*>(u + (int64_t)gi * ld + gk);
-                vi = *reinterpret_cast<const float4*>(v + (int64_t)gi * ld + gk);
+                c.ui[h] = *reinterpret_cast<const float4*>(u + (int64_t)gi * ld + gk);
+                c.vi[h] = *reinterpret_cast<const float4*>(v + (int64_t)gi * ld + gk);
             }
             if (gj < n) {
-                uj = *reinterpret_cast<const float4*>(u + (int64_t)gj * ld + gk);
-                vj = *reinterpret_cast<const float4*>(v + (int64_t)gj * ld + gk);
+                c.uj[h] = *reinterpret_cast<const float4*>(u + (int64_t)gj * ld + gk);
+                c.vj[h] = *reinterpret_cast<const float4*>(v + (int64_t)gj * ld + gk);
             }
         } else {
-            float* pui = &ui.x;
-            float* pvi = &vi.x;
-            float* puj = &uj.x;
-            float* pvj = &vj.x;
+            float* pui = &c.ui[h].x;
+            float* pvi = &c.vi[h].x;
+            float* puj = &c.uj[h].x;
+            float* pvj = &c.vj[h].x;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (gk + e < k) {
@@ -193,24 +171,104 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
                 }
             }
         }
-        Ui[fq + 0][fr] = ui.x; Ui[fq + 1][fr] = ui.y; Ui[fq + 2][fr] = ui.z; Ui[fq + 3][fr] = ui.w;
-        Vi[fq + 0][fr] = vi.x; Vi[fq + 1][fr] = vi.y; Vi[fq + 2][fr] = vi.z; Vi[fq + 3][fr] = vi.w;
-        Uj[fq + 0][fr] = uj.x; Uj[fq + 1][fr] = uj.y; Uj[fq + 2][fr] = uj.z; Uj[fq + 3][fr] = uj.w;
-        Vj[fq + 0][fr] = vj.x; Vj[fq + 1][fr] = vj.y; Vj[fq + 2][fr] = vj.z; Vj[fq + 3][fr] = vj.w;
-        __syncthreads();
-        const int ar = wr * 32 + (lane & 31), bc = wc * 32 + (lane & 31), kh = lane >> 5;
-#pragma unroll
-        for (int kk = 0; kk < kKC; kk += 2) {
-            // A[i][k] (lane: i = lane&31, k = lane>>5), B[k][j] (k = lane>>5, j = lane&31)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ui[kk + kh][ar], Vj[kk + kh][bc], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Vi[kk + kh][ar], Uj[kk + kh][bc], acc, 0, 0, 0);
-        }
     }
+}
 
-    const float lr = mode == 2 ? (float)(*lr_dev) : 0.f;
+__device__ __forceinline__ void store4(float (*dst)[kLdsRow], int kq, int row, const float4& x) {
+    dst[kq + 0][row] = x.x;
+    dst[kq + 1][row] = x.y;
+    dst[kq + 2][row] = x.z;
+    dst[kq + 3][row] = x.w;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA form: C_IJ = U_I V_Jᵀ + V_I U_Jᵀ on fp32-in v_mfma_f32_32x32x2_f32
+// (exact f32 FMA chains, 64 FLOP/clk/SIMD = the fp32 peak with one VGPR per
+// operand).  One 256-thread block per 64×64 tile of the upper triangle, each
+// wave a 32×32 sub-tile; k staged through LDS in chunks of 32, transposed to
+// [k][row] with a +1 row pad (conflict-free transposed writes and b32 reads).
+// Software-pipelined: chunk c+1's global loads are in flight during chunk c's
+// MFMAs, and the tile's θ values are loaded before the k loop.
+// Epilogue per mode: 0 grad = g, 1 grad += g, 2 θ = clamp(θ - lr·g, 0, 1)
+// with lr read from device memory (and grad = g when grad != NULL), 3 as 2
+// with g += grad (the partial sum of earlier column chunks) and grad = g.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4) {
+    __shared__ float Ui[kMC][kLdsRow];
+    __shared__ float Vi[kMC][kLdsRow];
+    __shared__ float Uj[kMC][kLdsRow];
+    __shared__ float Vj[kMC][kLdsRow];
+    __shared__ float Ri[kTile], Rj[kTile];
+
+    int a, b;
+    tri_tile(blockIdx.x, a, b);
+    const int bi = b, bj = a;
+    const int i0 = bi * kTile, j0 = bj * kTile;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 1, wc = wave & 1;  // 32×32 sub-tile of this wave
     const int64_t nn = n;
     const int lj = wc * 32 + (lane & 31);
     const int j = j0 + lj;
+
+    // fill mapping: thread -> (row fr, k quads fq and fq + 16)
+    const int fr = t >> 2, fq = (t & 3) * 4;
+    const int gi = i0 + fr, gj = j0 + fr;
+    ChunkRegs cr;
+    if (k > 0) load_chunk(u, v, ld, k, n, gi, gj, 0, fq, vec4, cr);
+
+    // the epilogue's θ / partial-grad operands: issued now, used after the k loop
+    float th[16], part[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int i = i0 + wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const bool in = i < n && j < n && j >= i;
+        const int64_t idx = in ? tri_index(i, i, nn) + (j - i) : 0;
+        th[e] = (in && theta != nullptr) ? theta[idx] : 0.f;
+        part[e] = (in && (mode == 1 || mode == 3)) ? grad[idx] : 0.f;
+    }
+
+    if (t < 2 * kTile) {
+        const int rr = t & (kTile - 1);
+        const int row = (t < kTile ? i0 : j0) + rr;
+        float acc = 0.f;
+        if (row < n)
+            for (int c = 0; c < nr; ++c) acc += r[(int64_t)row * ldr + c];
+        (t < kTile ? Ri : Rj)[rr] = acc;
+    }
+
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+
+    const int ar = wr * 32 + (lane & 31), bc = wc * 32 + (lane & 31), kh = lane >> 5;
+    for (int k0 = 0; k0 < k; k0 += kMC) {
+        __syncthreads();  // previous chunk's MFMAs are done with the LDS stage
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            store4(Ui, fq + 16 * h, fr, cr.ui[h]);
+            store4(Vi, fq + 16 * h, fr, cr.vi[h]);
+            store4(Uj, fq + 16 * h, fr, cr.uj[h]);
+            store4(Vj, fq + 16 * h, fr, cr.vj[h]);
+        }
+        __syncthreads();
+        if (k0 + kMC < k) load_chunk(u, v, ld, k, n, gi, gj, k0 + kMC, fq, vec4, cr);
+        const int kc = min(kMC, k - k0);  // trailing chunk: zero-filled past k, skip whole pairs
+#pragma unroll
+        for (int kk = 0; kk < kMC; kk += 2) {
+            if (kk < kc) {
+                // A[i][k] (lane: i = lane&31, k = lane>>5), B[k][j] (k = lane>>5, j = lane&31)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ui[kk + kh][ar], Vj[kk + kh][bc], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Vi[kk + kh][ar], Uj[kk + kh][bc], acc, 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // Ri / Rj written by other waves
+
+    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int li = wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
@@ -218,16 +276,18 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
         if (i >= n || j >= n || j < i) continue;
         const int64_t idx = tri_index(i, i, nn) + (j - i);
         float g = 0.f;
-        const float th = theta != nullptr ? theta[idx] : 0.f;
         if (j > i) {
-            g = acc[e] + Ri[li] + Rj[lj];
-            if (theta != nullptr && !(th >= 0.f && th <= 1.f)) g = 0.f;  // clamp backward
+            g = mode == 3 ? part[e] + acc[e] + Ri[li] + Rj[lj] : acc[e] + Ri[li] + Rj[lj];
+            if (theta != nullptr && !(th[e] >= 0.f && th[e] <= 1.f)) g = 0.f;  // clamp backward
         }
-        if (mode == 2) {
+        if (mode == 3) {
+            grad[idx] = g;
+            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
+        } else if (mode == 2) {
             if (grad != nullptr) grad[idx] = g;
-            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th), 0.f), 1.f);
+            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
         } else if (mode == 1) {
-            grad[idx] += g;
+            grad[idx] = part[e] + g;
         } else {
             grad[idx] = g;
         }
@@ -347,6 +407,21 @@ extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
     hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
                        v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k, const float* r,
+                                        int ldr, int nr, float* theta, int n, float* grad,
+                                        const void* scalars, void* stream) {
+    LDS_CHECK_ARG(theta != nullptr && grad != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
+    LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
+    const int nb = (n + kTile - 1) / kTile;
+    const int ntiles = nb * (nb + 1) / 2;
+    const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
+    const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
+    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
+                       v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -30,13 +30,16 @@ SIGNATURES = {
     "lds_exclusive_scan": [P, c_int, P, P],
     "lds_bitmask_fill_csr": [P, c_int, c_int, P, P, c_int64, P, P],
     "lds_csr_degree_scale": [P, c_int, P, P, P],
-    "lds_sample_graphs": [P, c_int, c_uint64, c_uint32, P, c_uint32, c_int, P, c_int, P, P, P, c_int64, P, P],
+    "lds_sample_graphs": [P, c_int, c_uint64, c_uint32, P, c_uint32, c_int, P, c_int, P, P, P, c_int64, P, P,
+                          P],
+    "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],
     "lds_spmm_norm": [P, P, P, c_int, P, c_int, c_int, P, c_int, c_int, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
+    "lds_theta_grad_sgd_accum": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
     "lds_slot_factors": [P, c_int, P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, P, c_int, P,
                          c_int, P, c_int, P],
     "lds_sgd_clamp": [P, P, c_float, c_int64, P],
@@ -49,27 +52,27 @@ SIGNATURES = {
                             P, P, P, P],
     "lds_engine_xt_linear": [P, P, P, c_int, P, P, P, c_float, c_int, c_uint64, c_uint32, P, c_int, c_int,
                              c_float, c_float, P],
-    "lds_engine_fwd_layer1": [P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
+    "lds_engine_fwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
                               c_float, c_float, P, P],
-    "lds_engine_fwd_layer2": [P, P, P, c_int, P, P, P, P, P, P, c_float, P, P, c_int, P],
-    "lds_engine_bwd_layer2": [P, P, P, c_int, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
+    "lds_engine_fwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, P, c_float, P, P, c_int, P],
+    "lds_engine_bwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
                               c_float, c_float, P, P, P, P, c_int, P, c_int, c_int, c_int, P, P],
-    "lds_engine_bwd_layer1": [P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
+    "lds_engine_bwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_colreduce": [c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, c_int, P, c_int, P, c_int,
                              P],
     "lds_engine_adam": [c_int, P, P, P, P, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_adam_reverse": [c_int, P, P, P, P, P, P, P, P, P, c_int, P, c_int, P],
-    "lds_engine_rev_a": [P, P, P, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, c_uint64, c_uint32, P,
+    "lds_engine_rev_a": [P, P, P, P, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, c_uint64, c_uint32, P,
                          c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, P, P],
-    "lds_engine_rev_b": [P, P, P, c_int, P, P, P, P, P, c_float, c_int, P, P, P, c_int, P, c_int, c_int, P],
-    "lds_engine_rev_c": [P, P, P, c_int, P, P, P, P, P, P, c_int, P, P, c_uint64, c_uint32, P, c_int, c_int,
+    "lds_engine_rev_b": [P, P, P, P, c_int, P, P, P, P, P, c_float, c_int, P, P, P, c_int, P, c_int, c_int, P],
+    "lds_engine_rev_c": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, P, c_uint64, c_uint32, P, c_int, c_int,
                          c_float, c_float, P, P, c_int, P, c_int, c_int, P, P],
-    "lds_engine_rev_d": [P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
+    "lds_engine_rev_d": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_sgd_clamp": [P, P, c_int64, P, P],
     "lds_engine_advance": [P, c_int, c_int, c_int, c_int, P],
     # fused forms
-    "lds_engine_bwd1_reduce": [P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P],
-    "lds_engine_rev_d_reduce": [P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P],
+    "lds_engine_bwd1_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P],
+    "lds_engine_rev_d_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P],
     "lds_engine_final": [P, c_int, c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P, P, P, P, P,
                          P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_xt_adam": [P, P, P, c_int, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,

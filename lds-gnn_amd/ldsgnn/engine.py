@@ -48,11 +48,12 @@ class _Graph:
 
     def __init__(self, n: int, cap: int, dev, views=None):
         if views is not None:
-            self.row_ptr, self.col, self.s = views
+            self.row_ptr, self.col, self.s, self.ell = views
             return
         self.row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
         self.col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
         self.s = torch.empty(n, dtype=torch.float32, device=dev)
+        self.ell = torch.empty(n * 2 * HID, dtype=torch.int32, device=dev)  # ELL head {j, s_j}
 
 
 class _GraphBatch:
@@ -66,7 +67,9 @@ class _GraphBatch:
         self.row_ptr = torch.empty((count, n + 1), dtype=torch.int32, device=dev)
         self.col = torch.empty((count, cap), dtype=torch.int32, device=dev)
         self.s = torch.empty((count, n), dtype=torch.float32, device=dev)
-        self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g])) for g in range(count)]
+        self.ell = torch.empty((count, n * 2 * HID), dtype=torch.int32, device=dev)
+        self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g], self.ell[g]))
+                       for g in range(count)]
 
 
 class _Slot:
@@ -190,6 +193,12 @@ class LdsEngine:
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
         self.keep_grad = True  # write dθ (θ.grad) even when it is fused with the update
+        # dθ assembly split per graph: chunks of finished graphs run on a side
+        # stream beside the (latency-bound) reverse pass.  Off by default: on
+        # MI355X the replayed graph did not overlap the branches and the
+        # chunks' read-modify-write of dθ cost 2.3x the single launch (r01).
+        self.split_theta_grad = False
+        self.side = torch.cuda.Stream(dev)
         self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=dev)
         self.eval_metrics = torch.zeros((64, 4), dtype=torch.float32, device=dev)
         self._graph_capture = None
@@ -295,8 +304,8 @@ class LdsEngine:
                  nat.ptr(self.scalars), self.pending_graph, nat.ptr(self.bits), self.words, st)
         nat.call("lds_bitmask_degree", nat.ptr(self.bits), self.n, self.words, nat.ptr(self.deg), nat.ptr(g.s), st)
         nat.call("lds_exclusive_scan", nat.ptr(self.deg), self.n, nat.ptr(g.row_ptr), st)
-        nat.call("lds_bitmask_fill_csr", nat.ptr(self.bits), self.n, self.words, nat.ptr(g.row_ptr),
-                 nat.ptr(g.col), self.cap, 0, st)
+        nat.call("lds_bitmask_fill_csr_ell", nat.ptr(self.bits), self.n, self.words, nat.ptr(g.row_ptr),
+                 nat.ptr(g.col), self.cap, 0, nat.ptr(g.s), nat.ptr(g.ell), st)
         self.pending_graph += 1
 
     def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int):
@@ -310,10 +319,10 @@ class LdsEngine:
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
                  nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
                  fwd_off, train, self.keep, self.scale, *xd, st)
-        nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.h0),
+        nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
                  self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask), st)
-        nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), n, nat.ptr(sl.h2),
+        nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
                  nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, st)
 
@@ -350,13 +359,13 @@ class LdsEngine:
             U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
         else:
             base, U, V, R = 0, 0, 0, 0
-        rp, cl, s = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s)
-        nat.call("lds_engine_bwd_layer2", rp, cl, s, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
+        rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
+        nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
                  nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
                  self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldk, R, base + HID, self.cw,
                  1, nat.ptr(sl.dmask), st)
         # dH0 + first stage of gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
-        nat.call("lds_engine_bwd1_reduce", rp, cl, s, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
+        nat.call("lds_engine_bwd1_reduce", rp, cl, s, el, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
                  nat.ptr(sl.h0), U, V, self.ldk, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
                  nat.ptr(sl.corrrow), c, nat.ptr(self.partials), st)
         first = 1 if adam_mode == 2 else 0
@@ -375,7 +384,7 @@ class LdsEngine:
         gb = self.gbatch
         nat.call("lds_sample_graphs", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, nat.ptr(self.scalars),
                  self.pending_graph, count, nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), nat.ptr(gb.row_ptr),
-                 nat.ptr(gb.col), self.cap, nat.ptr(gb.s), self._stream())
+                 nat.ptr(gb.col), self.cap, nat.ptr(gb.s), nat.ptr(gb.ell), self._stream())
 
     def inner_step(self, presampled: bool = False):
         """One InnerProblemTrainer.train_step (sample + forward + backward +
@@ -421,16 +430,29 @@ class LdsEngine:
                        2 if T else 0, T - 1 if T else 0)
         if self.train_flag:
             self.pending_fwd += 1
+        split = self.split_theta_grad and T > 0
+        if split:  # outer graph's columns: first chunk of dθ, beside reverse step T-1
+            self._theta_chunk(T * self.kg, HID + self.cw, accumulate=0)
         for t in range(T - 1, -1, -1):
             self._reverse_step(t)
-        k = T * self.kg + HID + self.cw
-        if grad_reducer is None:  # one launch: dθ assembly fused with SGD + clamp
-            nat.call("lds_theta_grad_sgd", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k, nat.ptr(self.R), 1,
-                     1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
-                     nat.ptr(self.scalars), st)
+            if split and t > 0:  # graph t's columns are final: its chunk runs beside step t-1
+                self._theta_chunk(t * self.kg, self.kg, accumulate=1)
+        if split:
+            torch.cuda.current_stream(self.dev).wait_stream(self.side)
+            k0 = self.kg  # the last chunk (graph 0) + R on the main stream
+        else:
+            k0 = T * self.kg + HID + self.cw
+        if grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
+            if split:
+                nat.call("lds_theta_grad_sgd_accum", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0,
+                         nat.ptr(self.R), 1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad), nat.ptr(self.scalars), st)
+            else:
+                nat.call("lds_theta_grad_sgd", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1,
+                         1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
+                         nat.ptr(self.scalars), st)
         else:  # replicas: dθ, all-reduce (mean), then the identical update everywhere
-            nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k, nat.ptr(self.R), 1, 1,
-                     nat.ptr(self.theta), n, nat.ptr(self.grad), 0, st)
+            nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
+                     nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, st)
             grad_reducer(self.grad)
             nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
                      nat.ptr(self.scalars), st)
@@ -445,6 +467,16 @@ class LdsEngine:
         self.t = 0
         return self.metrics[self.tau]
 
+    def _theta_chunk(self, col0: int, k: int, accumulate: int):
+        """grad (=|+=) U[:, col0:col0+k] V[...]ᵀ + V U ᵀ on the side stream, after
+        everything queued so far on the main stream (no R, no clamp mask:
+        the last chunk adds them)."""
+        side = self.side
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        off = 4 * col0
+        nat.call("lds_theta_grad", nat.ptr(self.U) + off, nat.ptr(self.V) + off, self.ldk, k, 0, 0, 0, 0, self.n,
+                 nat.ptr(self.grad), accumulate, side.cuda_stream)
+
     def _reverse_step(self, t: int):
         """Reverse of inner step t; gbar already holds ḡ of step t (from the
         Adam reverse fused into the previous stage).  Ends with the Adam
@@ -455,27 +487,27 @@ class LdsEngine:
         gw0t, gb0, gw1, gb1 = self._views(self.gbar)
         _, _, w1, _ = self._views(self.w[t])
         base = t * self.kg
-        rp, cl, s = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s)
+        rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
         U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
         tr = self.train_flag
         xcsr, xcsc = self._xvals(sl)  # Xd of step t (no redraw: train = 0 below)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(xcsr), n,
                  nat.ptr(gw0t), nat.ptr(gb0), nat.ptr(self.dh0bar), self.seed, self.tag_x, nat.ptr(self.scalars),
                  fwd_off, 0, self.keep, self.scale, 0, 0, 0, st)
-        nat.call("lds_engine_rev_a", rp, cl, s, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
+        nat.call("lds_engine_rev_a", rp, cl, s, el, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
                  nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldk, R,
                  base + HID + 2 * self.cw, nat.ptr(sl.dmask), st)
-        nat.call("lds_engine_rev_b", rp, cl, s, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
+        nat.call("lds_engine_rev_b", rp, cl, s, el, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
                  nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldk,
                  R, base + HID + self.cw, self.cw, st)
-        nat.call("lds_engine_rev_c", rp, cl, s, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
+        nat.call("lds_engine_rev_c", rp, cl, s, el, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
                  nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
                  self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
                  self.ldk, R, base + HID, self.cw, nat.ptr(sl.dmask), st)
         # H0bar + first stage of W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
-        nat.call("lds_engine_rev_d_reduce", rp, cl, s, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
+        nat.call("lds_engine_rev_d_reduce", rp, cl, s, el, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
                  nat.ptr(self.h0bar), U, V, self.ldk, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
                  nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), st)
         adam = self._adam_args(2 if t else 0, t - 1 if t else 0)
