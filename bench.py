@@ -96,6 +96,27 @@ def run_steps(runner, start: int, count: int, tau: int) -> int:
     return step
 
 
+# entry point -> HIP kernel symbol (for the PMC traffic record)
+KERNEL_SYMBOL = {"lds_theta_grad_sgd": "lds::theta_grad_mfma_kernel", "lds_theta_grad": "lds::theta_grad_mfma_kernel",
+                 "lds_theta_grad_sgd_accum": "lds::theta_grad_mfma_kernel", "lds_spmm_norm": "lds::spmm_norm_group_kernel",
+                 "lds_sample_bitmask": "lds::sample_tiles_kernel"}
+PMC_RECORD = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel, use_engine, world):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    PMC record (tools/gpu_pmc.sh + tools/pmc_summary.py: 2 x FETCH_SIZE +
+    WRITE_SIZE, separate passes, gfx950 read correction), measured on this
+    default workload; None for any other configuration."""
+    if not (use_engine and world == 1 and kernel == "lds_theta_grad_sgd") or not os.path.exists(PMC_RECORD):
+        return None, None
+    with open(PMC_RECORD) as f:
+        rec = json.load(f).get(KERNEL_SYMBOL[kernel])
+    if rec is None:
+        return None, None
+    return rec["traffic_bytes"], os.path.relpath(PMC_RECORD, ROOT)
+
+
 def cpu_baseline(args, data, opt_mask):
     """The oracle (dense CPU restatement of the reference) on a bounded sample:
     `cpu_steps` inner steps incl. their τ-hyper steps, host threads."""
@@ -227,6 +248,7 @@ def main():
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None}
     roof.update(kernel=args.kernel, avg_us=ksum["avg_us"], launches=ksum["launches"])
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.kernel, use_engine, world)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
