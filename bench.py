@@ -152,6 +152,9 @@ def main():
                     "assembly the path uses)")
     ap.add_argument("--split", action="store_true", help="engine: per-graph dθ chunks on a side stream beside "
                     "the reverse pass instead of one assembly launch per window (measured slower on MI355X)")
+    ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
+    ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
+                    "for rehearsing several ranks on one device)")
     ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
                     help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
@@ -159,10 +162,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
 
     import ldsgnn
     from ldsgnn import _native as nat
@@ -189,9 +196,9 @@ def main():
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
-        use_graph = world == 1
-        if use_graph:
-            eng.capture_window(args.tau)
+        use_graph = not args.eager
+        if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
+            eng.capture_window(args.tau, grad_reducer=reducer)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)
     else:
         step = run_steps(runner, 0, args.warmup, args.tau)
@@ -208,6 +215,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * args.steps / elapsed
+    in_sync = None
+    if world > 1:  # replicas must hold bit-identical θ after every update
+        th = eng.theta if use_engine else runner.outer_trainer.model.probs.data
+        mine = torch.tensor([th.double().sum().item(), th.double().square().sum().item()], dtype=torch.float64)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine.to(device) if args.backend == "nccl" else mine)
+        in_sync = all(torch.equal(v.cpu(), allv[0].cpu()) for v in allv)
 
     # roofline leg: the same K steps again with HIP events around the kernel
     nat.timer.enable(args.kernel)
@@ -265,7 +279,7 @@ def main():
             "config": {"workload": f"{args.dataset}-lds-knn-init-S1-tau{args.tau}", "path": args.path, "nodes": n,
                        "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": 1, "parallelism": f"replicas{world}",
-                       "sampled_nnz": nnz},
+                       "sampled_nnz": nnz, "replicas_in_sync": in_sync},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -527,26 +527,56 @@ class LdsEngine:
             self.inner_step(presampled=batch)
         return self.hyper_step(grad_reducer=grad_reducer, presampled=batch)
 
-    def capture_window(self, tau: int):
-        """Record run_window(tau) as one HIP graph (state must be at a window
-        start).  Replays advance RNG counters, Adam step and lr on device."""
+    def capture_window(self, tau: int, grad_reducer=None):
+        """Record run_window(tau) as HIP graphs (state must be at a window
+        start).  Replays advance RNG counters, Adam step and lr on device.
+
+        Without a reducer the window is ONE graph (dθ assembly fused with the
+        SGD step).  With a reducer (replicas over RCCL) the window is split at
+        the exchange: graph A runs up to dθ, `grad_reducer(grad)` runs eagerly
+        between the replays (the collective stays outside the captured work),
+        graph B applies SGD + clamp and the detach."""
         assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
         if tau != self.tau:
             raise ValueError(f"engine was built for tau={self.tau}; capture that window length")
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        graph = torch.cuda.CUDAGraph()
+        if grad_reducer is None:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(graph, stream=s):
+                    self.run_window(tau)
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            self._graph_capture = ((graph,), tau, None)
+            return graph
+        head, tail = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        pool = torch.cuda.graph_pool_handle()
+
+        def switch(_grad):  # the exchange point: close graph A, open graph B
+            head.capture_end()
+            tail.capture_begin(pool=pool)
+
         with torch.cuda.stream(s):
-            with torch.cuda.graph(graph, stream=s):
-                self.run_window(tau)
+            head.capture_begin(pool=pool)
+            try:
+                self.run_window(tau, grad_reducer=switch)
+            finally:
+                tail.capture_end()
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        self._graph_capture = (graph, tau)
-        return graph
+        self._graph_capture = ((head, tail), tau, grad_reducer)
+        return head, tail
 
     def replay(self, windows: int = 1):
-        graph, _ = self._graph_capture
+        graphs, _, reducer = self._graph_capture
+        if reducer is None:
+            for _ in range(windows):
+                graphs[0].replay()
+            return
+        head, tail = graphs
         for _ in range(windows):
-            graph.replay()
+            head.replay()
+            reducer(self.grad)
+            tail.replay()
 
     # ------------------------------------------------------------ metrics
     def inner_metrics(self, t: int):

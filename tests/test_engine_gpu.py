@@ -59,3 +59,32 @@ def test_batched_window_sampling_equals_stepwise():
     assert torch.equal(a.theta, b.theta)
     for k, v in a.get_params().items():
         assert torch.equal(v, b.get_params()[k]), k
+
+
+def test_split_graph_replay_with_reducer_equals_eager():
+    """N>1 capture: the window is split at the θ-grad exchange (graph A, the
+    reducer run eagerly, graph B).  Replays must equal eager windows that call
+    the same reducer, and the reducer must really act between the graphs."""
+    calls = []
+
+    def halve(grad):  # stands in for all_reduce(SUM)/world
+        calls.append(1)
+        grad.mul_(0.5)
+
+    a = run_engine_and_oracle(n=130, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    b = run_engine_and_oracle(n=130, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    c = run_engine_and_oracle(n=130, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    a.capture_window(5, grad_reducer=halve)
+    calls.clear()
+    a.replay(3)
+    assert len(calls) == 3
+    for _ in range(3):
+        b.run_window(5, grad_reducer=halve)
+        c.run_window(5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    assert torch.equal(a.grad, b.grad)
+    assert not torch.equal(a.theta, c.theta)  # the halved gradient moved θ differently
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+    assert a.scalars_host() == b.scalars_host()
