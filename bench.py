@@ -54,7 +54,7 @@ def build(args, rank, device):
     data.val_mask, opt_mask = split_mask(data.val_mask, 0.5, shuffle=True)
     data = data.to(device)
     opt_mask = opt_mask.to(device)
-    ldsgnn.rng.manual_seed(args.seed, replica=rank)
+    ldsgnn.rng.manual_seed(args.seed, replica=rank * args.samples)  # rank r: replicas r·S .. r·S+S-1
     torch.manual_seed(args.seed)
     gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(device)
     inner = InnerProblemTrainer(gcn, data, lr=0.01, weight_decay=5e-4)
@@ -64,11 +64,11 @@ def build(args, rank, device):
     return data, BilevelProblemRunner(inner, outer, data), opt_mask
 
 
-def make_engine(runner, tau, world):
+def make_engine(runner, tau, world, samples=1):
     import ldsgnn
     from ldsgnn.fused import engine_from_trainers
     eng = engine_from_trainers(runner.inner_trainer, runner.outer_trainer, tau=tau,
-                               generator=ldsgnn.rng.default_generator)
+                               generator=ldsgnn.rng.default_generator, samples=samples)
     reducer = None
     if world > 1:
         def reducer(grad):
@@ -97,7 +97,7 @@ def run_steps(runner, start: int, count: int, tau: int) -> int:
 
 
 # entry point -> HIP kernel symbol (for the PMC traffic record)
-KERNEL_SYMBOL = {"lds_theta_grad_sgd": "lds::theta_grad_mfma_kernel", "lds_theta_grad": "lds::theta_grad_mfma_kernel",
+KERNEL_SYMBOL = {"lds_theta_grad_ex": "lds::theta_grad_mfma_kernel", "lds_theta_grad_sgd": "lds::theta_grad_mfma_kernel", "lds_theta_grad": "lds::theta_grad_mfma_kernel",
                  "lds_theta_grad_sgd_accum": "lds::theta_grad_mfma_kernel", "lds_spmm_norm": "lds::spmm_norm_group_kernel",
                  "lds_sample_bitmask": "lds::sample_tiles_kernel"}
 PMC_RECORD = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
@@ -152,6 +152,8 @@ def main():
                     "assembly the path uses)")
     ap.add_argument("--split", action="store_true", help="engine: per-graph dθ chunks on a side stream beside "
                     "the reverse pass instead of one assembly launch per window (measured slower on MI355X)")
+    ap.add_argument("--samples", type=int, default=1, help="Monte-Carlo replica samples per GPU, batched in "
+                    "every launch (BASELINE configs 3/4); value is then sample-steps/s")
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
                     "for rehearsing several ranks on one device)")
@@ -185,13 +187,15 @@ def main():
 
     use_engine = args.path == "engine"
     if args.kernel == "auto":
-        if use_engine and world == 1:
+        if use_engine and args.samples > 1:
+            args.kernel = "lds_theta_grad_ex"
+        elif use_engine and world == 1:
             args.kernel = "lds_theta_grad_sgd_accum" if args.split else "lds_theta_grad_sgd"
         else:
             args.kernel = "lds_theta_grad"
     if use_engine:
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
-        eng, reducer = make_engine(runner, args.tau, world)
+        eng, reducer = make_engine(runner, args.tau, world, args.samples)
         eng.split_theta_grad = args.split
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
@@ -214,7 +218,7 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    value = world * args.steps / elapsed
+    value = world * args.samples * args.steps / elapsed
     in_sync = None
     if world > 1:  # replicas must hold bit-identical θ after every update
         th = eng.theta if use_engine else runner.outer_trainer.model.probs.data
@@ -232,7 +236,7 @@ def main():
     ksum = nat.timer.summary()[args.kernel]
     nat.timer.disable()
     if use_engine:
-        nnz = int(eng.outer.g.row_ptr[n].item())
+        nnz = int(eng.outer.g.row_ptr[0, n].item())
     else:
         g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
         nnz = g.nnz()
@@ -251,7 +255,9 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
     else:  # lds_theta_grad[_sgd]: rank-2k update of the packed triangle
         from ldsgnn.engine import LdsEngine
-        if use_engine and args.kernel == "lds_theta_grad_sgd":  # one launch per window: all columns
+        if use_engine and args.kernel == "lds_theta_grad_ex":  # S factor blocks of ldk columns
+            k = eng.S * eng.ldk
+        elif use_engine and args.kernel in ("lds_theta_grad_sgd", "lds_theta_grad"):  # one launch per window
             k = LdsEngine.window_columns(args.tau, data.num_classes)
         elif use_engine:  # split assembly: the timed launch is one graph's chunk (+ R, SGD)
             k = LdsEngine.window_columns(1, data.num_classes) - LdsEngine.window_columns(0, data.num_classes)
@@ -271,14 +277,15 @@ def main():
     if rank == 0:
         out = {
             "metric": "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X",
-            "value": value, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+            "value": value, "unit": "steps/s" if args.samples == 1 else "sample-steps/s", "n_gpus": world,
+            "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": f"synthetic {args.dataset}-shaped (N={n}, F_in={data.num_features}, "
                     f"C={data.num_classes}), kNN-initialised theta",
-            "config": {"workload": f"{args.dataset}-lds-knn-init-S1-tau{args.tau}", "path": args.path, "nodes": n,
+            "config": {"workload": f"{args.dataset}-lds-knn-init-S{args.samples}-tau{args.tau}", "path": args.path, "nodes": n,
                        "features": data.num_features, "classes": data.num_classes, "hidden": 16,
-                       "tau": args.tau, "samples_per_rank": 1, "parallelism": f"replicas{world}",
+                       "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
                        "sampled_nnz": nnz, "replicas_in_sync": in_sync},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 1
+#define LDS_ABI_VERSION 2
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -112,6 +112,14 @@ int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
  * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
  * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·32.  Four launches
  * for all `count` graphs. */
+/* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
+ * b < samples, is draw counter *counter_base + counter_offset + g with tag
+ * tag + b·tag_step, stored as graph g·samples + b of the batch arrays. */
+int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
+                            uint32_t tag_step, const uint32_t* counter_base,
+                            uint32_t counter_offset, int count, int samples, uint64_t* bits,
+                            int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
+                            float* s, int* ell, void* stream);
 int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
                       const uint32_t* counter_base, uint32_t counter_offset, int count,
                       uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
@@ -179,6 +187,18 @@ int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
 int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k,
                              const float* r, int ldr, int nr, float* theta, int n,
                              float* grad, const void* scalars, void* stream);
+
+/* General form of the assembly, for S replica samples per GPU (their factor
+ * blocks side by side in U, V: k = S·ldk columns):
+ *   g_ij = gscale · (Σ_c U_ic V_jc + V_ic U_jc + R_i + R_j),  i < j,
+ *   R_i  = Σ_{c<nr} r[i·ldr_row + c·ldr_col]   (ldr_col = n: S stacked rows)
+ * gscale = 1/S makes g the mean of the S replica hypergradients (the mean
+ * OuterProblemTrainer.train_step's loss over S samples would give).
+ * mode 0 grad = g; 1 grad += g; 2 θ = clamp(θ - lr·g, 0, 1) (+ grad = g when
+ * grad != NULL); 3 as 2 with g += grad first.  lr from `scalars` (modes 2, 3). */
+int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
+                      int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
+                      int mode, const void* scalars, float gscale, void* stream);
 /* Slot factors for lds_theta_grad from one aggregation Y = ÂZ and its
  * cotangent G (dZ = ÂG):  U = s⊙G, V = s⊙Z, r = -½ s² (G·Y + Z·dZ) rowwise.
  * Columns [f, fpad) of U and V are zero-filled. */
@@ -226,6 +246,28 @@ int lds_dropout(const float* x, int ldx, float* y, int ldy, int rows, int cols,
  * ------------------------------------------------------------------------- */
 int lds_engine_scalars_size(void);
 
+/* Replica-sample batching (config "S Monte-Carlo samples per GPU"): the
+ * engine entries taking `const LdsBatch* batch` run `samples` independent
+ * replicas in one launch (grid.y = sample).  Sample b reads / writes every
+ * per-sample array at base + b·stride (strides in elements of the array's
+ * type; 0 = shared by all samples) and draws its dropout masks with the
+ * replica tags tag_x / tag_h + b·tag_step.  Shared: X, labels, masks, θ, the
+ * scalars (every replica advances them identically) and the Adam table.
+ * batch == NULL (or samples == 1) is the single-replica launch.
+ *   act : n×16 activation / adjoint arrays      row : n-vectors (s, R, loss rows)
+ *   rp  : row_ptr (n+1)   col : CSR capacity     ell : ELL head (n·32 int32)
+ *   par : flat parameter vectors (w, m, v, g', adjoints)
+ *   xval: the X-values argument (0 when it is the shared X, else the Xd stride)
+ *   xd  : stored Xd arrays (CSR / CSC order)
+ *   uv  : factor COLUMN offset per sample (U, V are n × (samples·ldk); the
+ *         ldk argument is then the row stride samples·ldk)
+ *   part: reduction partials   met: metrics rows (2 floats) */
+typedef struct LdsBatch {
+    int32_t samples;
+    uint32_t tag_step;
+    int64_t act, row, rp, col, ell, par, xval, xd, uv, part, met;
+} LdsBatch;
+
 /* lds_sample_bitmask with the draw counter read from device memory:
  * counter = *counter_base + counter_offset. */
 int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, uint32_t tag,
@@ -241,7 +283,7 @@ int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int 
                         const float* wt, const float* bias, float* out, uint64_t seed,
                         uint32_t tag_x, const void* scalars, int fwd_off, int train,
                         float keep, float scale, float* xd_csr, float* xd_csc,
-                        const int* csr2csc, void* stream);
+                        const int* csr2csc, const LdsBatch* batch, void* stream);
 /* out[f][:] (+)= Σ_i dropout(X)[i][f] · d[i][:]  (+ wd · w)   (X in CSC). */
 int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int fin,
                          const float* d, float* out, const float* w, float wd,
@@ -255,13 +297,13 @@ int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, const i
                           const float* h0, float* y0, float* h1d, float* h2,
                           const float* w1, const float* b1, int c, uint64_t seed,
                           uint32_t tag_h, const void* scalars, int fwd_off, int train,
-                          float keep, float scale, float* dmask, void* stream);
+                          float keep, float scale, float* dmask, const LdsBatch* batch, void* stream);
 /* O = ÂH2; P = softmax(O); dO = (P - onehot) ⊙ mask · inv_count; per-row
  * NLL and correctness where mask. */
 int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* h2, float* o, float* p, float* d_o,
                           const int* label, const uint8_t* mask, float inv_count,
-                          float* lossrow, float* corrrow, int c, void* stream);
+                          float* lossrow, float* corrrow, int c, const LdsBatch* batch, void* stream);
 /* dH2 = ÂdO; dY0 = (dH2 W1) ⊙ dropout' ⊙ relu'.  U != NULL: emit the outer
  * graph's factor (dO, H2) at columns [foff, foff + fwidth); r_assign != 0
  * writes R (first emitter of a window) instead of accumulating into it. */
@@ -271,7 +313,7 @@ int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, const i
                           const void* scalars, int fwd_off, int train, float keep,
                           float scale, const float* o, const float* h2, float* U,
                           float* V, int ldk, float* R, int foff, int fwidth,
-                          int r_assign, const float* dmask, void* stream);
+                          int r_assign, const float* dmask, const LdsBatch* batch, void* stream);
 /* dH0 = ÂdY0.  U != NULL: emit the outer graph's factor (dY0, H0). */
 int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* dy0, float* dh0, const float* y0,
@@ -305,19 +347,19 @@ int lds_engine_rev_a(const int* rp, const int* col, const float* s, const int* e
                      float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, const float* dmask,
-                     void* stream);
+                     const LdsBatch* batch, void* stream);
 int lds_engine_rev_b(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* dh2bar, const float* d_o, const float* dh2,
                      const float* p, const uint8_t* mask, float inv_count, int c,
                      float* obar, float* U, float* V, int ldk, float* R, int foff,
-                     int cw, void* stream);
+                     int cw, const LdsBatch* batch, void* stream);
 int lds_engine_rev_c(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* obar, const float* h2, const float* o,
                      const float* h1dbar_part, const float* y0, const float* w1, int c,
                      float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, int cw,
-                     const float* dmask, void* stream);
+                     const float* dmask, const LdsBatch* batch, void* stream);
 int lds_engine_rev_d(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* y0bar, const float* h0, const float* y0,
                      float* h0bar, float* U, float* V, int ldk, float* R, int foff,
@@ -355,14 +397,14 @@ int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, const 
                            const float* dy0, float* dh0, const float* y0, const float* h0,
                            float* U, float* V, int ldk, float* R, int foff,
                            const float* dh2, const float* h1d, const float* lossrow,
-                           const float* corrrow, int c, float* partials, void* stream);
+                           const float* corrrow, int c, float* partials, const LdsBatch* batch, void* stream);
 /* H0bar = ÂY0bar (+ factor use 1) fused with the first stage of
  * {W̄1 += dH2ᵀdH1dbar + H2barᵀH1d, b̄0 += ΣH0bar, b̄1 += ΣH2bar}. */
 int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, const int* ell, int n,
                             const float* y0bar, const float* h0, const float* y0,
                             float* h0bar, float* U, float* V, int ldk, float* R, int foff,
                             const float* dh2, const float* dh1dbar, const float* h2bar,
-                            const float* h1d, int c, float* partials, void* stream);
+                            const float* h1d, int c, float* partials, const LdsBatch* batch, void* stream);
 /* Final stage: partials -> dst (flat parameter layout; = or +=), metrics[0..1]
  * (may be NULL), then Adam (mode) on b0 / W1 / b1. */
 int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int off_b0,
@@ -383,7 +425,7 @@ int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int f
                        const float* w0, const float* m0, const float* v0, float* w1, float* m1,
                        float* v1, float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                        const double* hyper, const float* adam_tab, int n_wd, int step_off,
-                       void* stream);
+                       const LdsBatch* batch, void* stream);
 /* Window end (both trainers' detach, src/trainers/bilevel.py:109-114): copy
  * w/m/v of slot T to slot 0 (skipped when wT == NULL), advance the scalars
  * as lds_engine_advance and (adam_tab != NULL) refresh the first tab_count
@@ -391,7 +433,7 @@ int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int f
 int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT,
                           float* w0, float* m0, float* v0, void* scalars, int graphs,
                           int forwards, int adam_steps, int hypers, const double* betas_dev,
-                          float* adam_tab, int tab_count, void* stream);
+                          float* adam_tab, int tab_count, const LdsBatch* batch, void* stream);
 /* Adam table for the current scalars->adam_step (betas_dev = {β1, β2, lr}
  * doubles): entry k = {lr/(1-β1^(s+1+k)), sqrt(1-β2^(s+1+k))}, k < tab_count
  * <= 256; the constants of torch/higher's Adam, computed in double. */

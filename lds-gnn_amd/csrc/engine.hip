@@ -49,6 +49,24 @@ struct Keys {
     uint32_t k0, k1, tag_x, tag_h;
 };
 
+// Per-sample element strides of a batched launch (include/ldsgnn.h LdsBatch):
+// sample = blockIdx.y owns every per-sample array at base + sample·stride, its
+// replica tags at tag + sample·tag.  A single-sample launch passes all zeros.
+struct Batch {
+    int64_t act, row, rp, col, ell2, par, xval, xd, uv, part, met;
+    uint32_t tag;
+};
+
+template <typename T>
+__device__ __forceinline__ T* boff(T* p, int64_t stride) {
+    return p == nullptr ? p : p + (int64_t)blockIdx.y * stride;
+}
+
+__device__ __forceinline__ void bkeys(Keys& k, const Batch& bt) {
+    k.tag_x += blockIdx.y * bt.tag;
+    k.tag_h += blockIdx.y * bt.tag;
+}
+
 __device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr, int row, int col) {
     const U32x4 o = philox4x32_10(U32x4{(uint32_t)col, (uint32_t)(row >> 2), tag, ctr}, k.k0, k.k1);
     const uint32_t w = (row & 3) == 0 ? o.x : (row & 3) == 1 ? o.y : (row & 3) == 2 ? o.z : o.w;
@@ -165,9 +183,16 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
     const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
-    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc) {
+    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc, Batch bt) {
     const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
     if (row >= n) return;
+    xval = boff(xval, bt.xval);
+    wt = boff(wt, bt.par);
+    bias = boff(bias, bt.par);
+    out = boff(out, bt.act);
+    xd_csr = boff(xd_csr, bt.xd);
+    xd_csc = boff(xd_csc, bt.xd);
+    bkeys(keys, bt);
     const int lane = threadIdx.x & 63;
     const float acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, sc->fwd_ctr + fwd_off, train, keep,
                                         scale, xd_csr, xd_csc, csr2csc);
@@ -223,10 +248,22 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int2* __restrict__ ell, int n,
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
-    float scale, float* __restrict__ dmask) {
+    float scale, float* __restrict__ dmask, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    h0 = boff(h0, bt.act);
+    y0 = boff(y0, bt.act);
+    h1d = boff(h1d, bt.act);
+    h2 = boff(h2, bt.act);
+    dmask = boff(dmask, bt.act);
+    w.w1 = boff(w.w1, bt.par);
+    w.b1 = boff(w.b1, bt.par);
+    bkeys(keys, bt);
     // the dropout draw does not depend on the aggregation: issue it first
     const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
                            : 1.f;
@@ -253,10 +290,20 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const int2* __restrict__ ell, int n,
     const float* __restrict__ h2, float* __restrict__ o_out, float* __restrict__ p_out,
     float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
-    float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c) {
+    float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    h2 = boff(h2, bt.act);
+    o_out = boff(o_out, bt.act);
+    p_out = boff(p_out, bt.act);
+    d_o = boff(d_o, bt.act);
+    lossrow = boff(lossrow, bt.row);
+    corrrow = boff(corrrow, bt.row);
     const float o = agg_row(rp, col, s, ell, h2, row, lane);
     const bool act = lane < c;
     const float m = gmax16(act ? o : -INFINITY);
@@ -301,10 +348,26 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     float* __restrict__ dy0, GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off,
     int train, float keep, float scale, const float* __restrict__ o_in, const float* __restrict__ h2,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth,
-    int r_assign, const float* __restrict__ dmask) {
+    int r_assign, const float* __restrict__ dmask, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    d_o = boff(d_o, bt.act);
+    y0 = boff(y0, bt.act);
+    dh2 = boff(dh2, bt.act);
+    dy0 = boff(dy0, bt.act);
+    o_in = boff(o_in, bt.act);
+    h2 = boff(h2, bt.act);
+    dmask = boff(dmask, bt.act);
+    U = boff(U, bt.uv);
+    V = boff(V, bt.uv);
+    R = boff(R, bt.row);
+    w.w1 = boff(w.w1, bt.par);
+    bkeys(keys, bt);
     const float g2 = agg_row(rp, col, s, ell, d_o, row, lane);  // zero past c (dO is)
     dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
@@ -524,10 +587,31 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     float* __restrict__ dh1dbar, float* __restrict__ dh2bar, float* __restrict__ h1dbar,
     Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff,
-    const float* __restrict__ dmask) {
+    const float* __restrict__ dmask, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    dh0bar = boff(dh0bar, bt.act);
+    dy0 = boff(dy0, bt.act);
+    dh0 = boff(dh0, bt.act);
+    y0 = boff(y0, bt.act);
+    h1d = boff(h1d, bt.act);
+    dh2 = boff(dh2, bt.act);
+    dh1dbar = boff(dh1dbar, bt.act);
+    dh2bar = boff(dh2bar, bt.act);
+    h1dbar = boff(h1dbar, bt.act);
+    dmask = boff(dmask, bt.act);
+    w.w1 = boff(w.w1, bt.par);
+    gw1bar = boff(gw1bar, bt.par);
+    gb1bar = boff(gb1bar, bt.par);
+    U = boff(U, bt.uv);
+    V = boff(V, bt.uv);
+    R = boff(R, bt.row);
+    bkeys(keys, bt);
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, dh0bar, row, lane);  // dY0bar
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
@@ -561,10 +645,22 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     const float* __restrict__ dh2bar, const float* __restrict__ d_o, const float* __restrict__ dh2,
     const float* __restrict__ p, const uint8_t* __restrict__ mask, float inv_count, int c,
     float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
-    float* __restrict__ R, int foff, int cw) {
+    float* __restrict__ R, int foff, int cw, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    dh2bar = boff(dh2bar, bt.act);
+    d_o = boff(d_o, bt.act);
+    dh2 = boff(dh2, bt.act);
+    p = boff(p, bt.act);
+    obar = boff(obar, bt.act);
+    U = boff(U, bt.uv);
+    V = boff(V, bt.uv);
+    R = boff(R, bt.row);
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, dh2bar, row, lane);  // dObar
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
@@ -584,10 +680,27 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     const float* __restrict__ h1dbar_part, const float* __restrict__ y0, GcnW w, int c,
     float* __restrict__ h2bar, float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc,
     int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
-    int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask) {
+    int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    obar = boff(obar, bt.act);
+    h2 = boff(h2, bt.act);
+    o = boff(o, bt.act);
+    h1dbar_part = boff(h1dbar_part, bt.act);
+    y0 = boff(y0, bt.act);
+    h2bar = boff(h2bar, bt.act);
+    y0bar = boff(y0bar, bt.act);
+    dmask = boff(dmask, bt.act);
+    w.w1 = boff(w.w1, bt.par);
+    U = boff(U, bt.uv);
+    V = boff(V, bt.uv);
+    R = boff(R, bt.row);
+    bkeys(keys, bt);
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, obar, row, lane);  // H2bar (zero past c)
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
@@ -790,10 +903,27 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const float* __restrict__ dy0, float* __restrict__ dh0, const float* __restrict__ y0,
     const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ h1d,
-    const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials) {
+    const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials,
+    Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    dy0 = boff(dy0, bt.act);
+    dh0 = boff(dh0, bt.act);
+    y0 = boff(y0, bt.act);
+    h0 = boff(h0, bt.act);
+    dh2 = boff(dh2, bt.act);
+    h1d = boff(h1d, bt.act);
+    lossrow = boff(lossrow, bt.row);
+    corrrow = boff(corrrow, bt.row);
+    partials = boff(partials, bt.part);
+    U = boff(U, bt.uv);
+    V = boff(V, bt.uv);
+    R = boff(R, bt.row);
     float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
@@ -818,10 +948,27 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const float* __restrict__ y0bar, const float* __restrict__ h0, const float* __restrict__ y0,
     float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ dh1dbar,
-    const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials) {
+    const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials,
+    Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
+    rp = boff(rp, bt.rp);
+    col = boff(col, bt.col);
+    s = boff(s, bt.row);
+    ell = boff(ell, bt.ell2);
+    y0bar = boff(y0bar, bt.act);
+    h0 = boff(h0, bt.act);
+    y0 = boff(y0, bt.act);
+    h0bar = boff(h0bar, bt.act);
+    dh2 = boff(dh2, bt.act);
+    dh1dbar = boff(dh1dbar, bt.act);
+    h2bar = boff(h2bar, bt.act);
+    h1d = boff(h1d, bt.act);
+    partials = boff(partials, bt.part);
+    U = boff(U, bt.uv);
+    V = boff(V, bt.uv);
+    R = boff(R, bt.row);
     float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
@@ -920,7 +1067,24 @@ __global__ __launch_bounds__(320) void final_kernel(FinalArgs f, AdamArgs adam,
 __global__ __launch_bounds__(256) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
     const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
-    float keep, float scale, FinalArgs fin_args, AdamArgs adam) {
+    float keep, float scale, FinalArgs fin_args, AdamArgs adam, Batch bt) {
+    fin_args.partials = boff(fin_args.partials, bt.part);
+    fin_args.dst = boff(fin_args.dst, bt.par);
+    fin_args.metrics = boff(fin_args.metrics, bt.met);
+    adam.w0 = boff(adam.w0, bt.par);
+    adam.m0 = boff(adam.m0, bt.par);
+    adam.v0 = boff(adam.v0, bt.par);
+    adam.w1 = boff(adam.w1, bt.par);
+    adam.m1 = boff(adam.m1, bt.par);
+    adam.v1 = boff(adam.v1, bt.par);
+    adam.gp = boff(adam.gp, bt.par);
+    adam.wbar = boff(adam.wbar, bt.par);
+    adam.mbar = boff(adam.mbar, bt.par);
+    adam.vbar = boff(adam.vbar, bt.par);
+    adam.gbar = boff(adam.gbar, bt.par);
+    xval = boff(xval, bt.xval);
+    d = boff(d, bt.act);
+    bkeys(keys, bt);
     if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
         const int e1 = threadIdx.x + 256;
         final_pair(fin_args, threadIdx.x, e1 < kRedLen ? e1 : -1, adam, sc);
@@ -955,14 +1119,15 @@ __global__ __launch_bounds__(256) void end_window_kernel(int np, const float* __
                                                          float* __restrict__ v0, EngineScalars* sc,
                                                          int graphs, int forwards, int adam_steps,
                                                          int hypers, const double* __restrict__ betas,
-                                                         float* __restrict__ tab, int tab_count) {
+                                                         float* __restrict__ tab, int tab_count, int64_t par) {
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (wT != nullptr && e < np) {
-        w0[e] = wT[e];
-        m0[e] = mT[e];
-        v0[e] = vT[e];
+        const int64_t o = (int64_t)blockIdx.y * par;
+        w0[o + e] = wT[o + e];
+        m0[o + e] = mT[o + e];
+        v0[o + e] = vT[o + e];
     }
-    if (blockIdx.x == 0) {
+    if (blockIdx.x == 0 && blockIdx.y == 0) {  // the scalars are shared by all samples
         __shared__ int new_step;
         if (threadIdx.x == 0) {
             sc->graph_ctr += graphs;
@@ -1017,6 +1182,18 @@ using namespace lds;
 // C-ABI (see include/ldsgnn.h, "Fused engine")
 // ---------------------------------------------------------------------------
 static inline int rows_blocks(int n) { return (n + RG - 1) / RG; }
+
+// Kernel-side strides of a host LdsBatch (NULL: one sample); returns grid.y.
+static inline int mk_batch(const LdsBatch* b, Batch& bt) {
+    bt = Batch{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0u};
+    if (b == nullptr || b->samples <= 1) return 1;
+    bt = Batch{b->act, b->row, b->rp, b->col, b->ell / 2, b->par, b->xval, b->xd, b->uv, b->part, b->met,
+               b->tag_step};
+    return b->samples;
+}
+static inline bool batch_ok(const LdsBatch* b) {
+    return b == nullptr || (b->samples >= 1 && b->samples <= 65535 && (b->ell & 1) == 0);
+}
 static inline Keys mk_keys(uint64_t seed, uint32_t tag_x, uint32_t tag_h) {
     return Keys{(uint32_t)seed, (uint32_t)(seed >> 32), tag_x, tag_h};
 }
@@ -1025,12 +1202,14 @@ extern "C" int lds_engine_x_linear(const int* xrp, const int* xcol, const float*
                                    const float* wt, const float* bias, float* out, uint64_t seed,
                                    uint32_t tag_x, const void* scalars, int fwd_off, int train,
                                    float keep, float scale, float* xd_csr, float* xd_csc,
-                                   const int* csr2csc, void* stream) {
-    LDS_CHECK_ARG(xrp && xcol && xval && wt && out && scalars && n > 0);
+                                   const int* csr2csc, const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(xrp && xcol && xval && wt && out && scalars && n > 0 && batch_ok(batch));
     LDS_CHECK_ARG(xd_csc == nullptr || (xd_csr && csr2csc));
-    hipLaunchKernelGGL(x_linear_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, xrp,
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(x_linear_kernel, dim3((n + 3) / 4, ns), dim3(256), 0, (hipStream_t)stream, xrp,
                        xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc);
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1049,23 +1228,31 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
                                      const float* h0, float* y0, float* h1d, float* h2,
                                      const float* w1, const float* b1, int c, uint64_t seed,
                                      uint32_t tag_h, const void* scalars, int fwd_off, int train,
-                                     float keep, float scale, float* dmask, void* stream) {
+                                     float keep, float scale, float* dmask, const LdsBatch* batch,
+                                     void* stream) {
     LDS_CHECK_ARG(rp && col && s && h0 && y0 && h1d && h2 && w1 && b1 && scalars && n > 0);
-    LDS_CHECK_ARG(c > 0 && c <= HID);
+    LDS_CHECK_ARG(c > 0 && c <= HID && batch_ok(batch));
     GcnW w{nullptr, nullptr, w1, b1};
-    hipLaunchKernelGGL(fwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(fwd_layer1_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask);
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                                      const float* h2, float* o, float* p, float* d_o,
                                      const int* label, const uint8_t* mask, float inv_count,
-                                     float* lossrow, float* corrrow, int c, void* stream) {
+                                     float* lossrow, float* corrrow, int c, const LdsBatch* batch,
+                                     void* stream) {
     LDS_CHECK_ARG(rp && col && s && h2 && label && lossrow && corrrow && n > 0 && c > 0 && c <= HID);
-    hipLaunchKernelGGL(fwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
-                       col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c);
+    LDS_CHECK_ARG(batch_ok(batch));
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(fwd_layer2_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+                       col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c,
+                       bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1075,14 +1262,16 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
                                      const void* scalars, int fwd_off, int train, float keep,
                                      float scale, const float* o, const float* h2, float* U, float* V,
                                      int ldk, float* R, int foff, int fwidth, int r_assign,
-                                     const float* dmask, void* stream) {
-    LDS_CHECK_ARG(rp && col && s && d_o && y0 && dh2 && dy0 && w1 && scalars && n > 0);
+                                     const float* dmask, const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && d_o && y0 && dh2 && dy0 && w1 && scalars && n > 0 && batch_ok(batch));
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && o && h2 && fwidth <= HID)));
     GcnW w{nullptr, nullptr, w1, nullptr};
-    hipLaunchKernelGGL(bwd_layer2_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(bwd_layer2_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
-                       foff, fwidth, r_assign, dmask);
+                       foff, fwidth, r_assign, dmask, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1147,25 +1336,32 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
                                 float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
                                 const void* scalars, int fwd_off, int train, float keep, float scale,
                                 float* U, float* V, int ldk, float* R, int foff, const float* dmask,
-                                void* stream) {
+                                const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dh0bar && dy0 && dh0 && y0 && h1d && dh2 && w1 && gw1bar && gb1bar);
     LDS_CHECK_ARG(dh1dbar && dh2bar && h1dbar && scalars && U && V && R && n > 0 && c > 0 && c <= HID);
+    LDS_CHECK_ARG(batch_ok(batch));
     GcnW w{nullptr, nullptr, w1, nullptr};
-    hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
-                       n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar, h1dbar,
-                       mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
-                       scale, U, V, ldk, R, foff, dmask);
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       (const int2*)ell, n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar,
+                       h1dbar, mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
+                       scale, U, V, ldk, R, foff, dmask, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, const int* ell, int n,
                                 const float* dh2bar, const float* d_o, const float* dh2, const float* p,
                                 const uint8_t* mask, float inv_count, int c, float* obar, float* U,
-                                float* V, int ldk, float* R, int foff, int cw, void* stream) {
+                                float* V, int ldk, float* R, int foff, int cw, const LdsBatch* batch,
+                                void* stream) {
     LDS_CHECK_ARG(rp && col && s && dh2bar && d_o && dh2 && p && mask && obar && U && V && R && n > 0);
-    LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID);
-    hipLaunchKernelGGL(rev_b_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
-                       n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw);
+    LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(rev_b_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       (const int2*)ell, n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw,
+                       bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1175,14 +1371,17 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
                                 float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                                 const void* scalars, int fwd_off, int train, float keep, float scale,
                                 float* U, float* V, int ldk, float* R, int foff, int cw,
-                                const float* dmask, void* stream) {
+                                const float* dmask, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && obar && h2 && o && h1dbar_part && y0 && w1 && h2bar && y0bar);
     LDS_CHECK_ARG(scalars && U && V && R && n > 0 && c > 0 && c <= HID && cw >= c && cw <= HID);
+    LDS_CHECK_ARG(batch_ok(batch));
     GcnW w{nullptr, nullptr, w1, nullptr};
-    hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
-                       n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar, mk_keys(seed, 0, tag_h),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff,
-                       cw, dmask);
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+                       (const int2*)ell, n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar,
+                       mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V,
+                       ldk, R, foff, cw, dmask, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1243,12 +1442,14 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
                                       const float* dy0, float* dh0, const float* y0, const float* h0,
                                       float* U, float* V, int ldk, float* R, int foff, const float* dh2,
                                       const float* h1d, const float* lossrow, const float* corrrow, int c,
-                                      float* partials, void* stream) {
+                                      float* partials, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && dh2 && h1d && lossrow && corrrow && partials && n > 0);
-    LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)));
-    hipLaunchKernelGGL(bwd1_reduce_kernel, dim3((n + RG1K - 1) / RG1K), dim3(1024), 0, (hipStream_t)stream,
-                       rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow, corrrow, c,
-                       partials);
+    LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)) && batch_ok(batch));
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(bwd1_reduce_kernel, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
+                       rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow,
+                       corrrow, c, partials, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1256,12 +1457,14 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
                                        const float* y0bar, const float* h0, const float* y0, float* h0bar,
                                        float* U, float* V, int ldk, float* R, int foff, const float* dh2,
                                        const float* dh1dbar, const float* h2bar, const float* h1d, int c,
-                                       float* partials, void* stream) {
+                                       float* partials, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && dh2 && dh1dbar && h2bar);
-    LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID);
-    hipLaunchKernelGGL(rev_d_reduce_kernel, dim3((n + RG1K - 1) / RG1K), dim3(1024), 0,
-                       (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff, dh2,
-                       dh1dbar, h2bar, h1d, c, partials);
+    LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID && batch_ok(batch));
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(rev_d_reduce_kernel, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
+                       (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R,
+                       foff, dh2, dh1dbar, h2bar, h1d, c, partials, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1290,8 +1493,8 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                                   const float* m0, const float* v0, float* w1, float* m1, float* v1,
                                   float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                                   const double* hyper, const float* adam_tab, int n_wd, int step_off,
-                                  void* stream) {
-    LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && fin > 0);
+                                  const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && fin > 0 && batch_ok(batch));
     LDS_CHECK_ARG(partials == nullptr || (nblocks > 0 && c > 0 && c <= HID));
     LDS_CHECK_ARG(adam_ok(adam_mode, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper, adam_tab,
                           step_off));
@@ -1299,21 +1502,25 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                               adam_tab, n_wd, step_off);
     FinalArgs f{partials, nblocks, c, off_b0, off_w1, off_b1, accumulate, out, metrics};
     const int blocks = (fin + 3) / 4 + (partials != nullptr ? 1 : 0);
-    hipLaunchKernelGGL(xt_adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin, d,
-                       mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
-                       a);
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(xt_adam_kernel, dim3(blocks, ns), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
+                       d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
+                       a, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT, float* w0,
                                      float* m0, float* v0, void* scalars, int graphs, int forwards,
                                      int adam_steps, int hypers, const double* betas_dev, float* adam_tab,
-                                     int tab_count, void* stream) {
-    LDS_CHECK_ARG(scalars && np > 0 && (wT == nullptr || (mT && vT && w0 && m0 && v0)));
+                                     int tab_count, const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(scalars && np > 0 && (wT == nullptr || (mT && vT && w0 && m0 && v0)) && batch_ok(batch));
     LDS_CHECK_ARG(adam_tab == nullptr || (betas_dev && tab_count > 0 && tab_count <= kAdamTabMax));
-    hipLaunchKernelGGL(end_window_kernel, dim3((np + 255) / 256), dim3(256), 0, (hipStream_t)stream, np, wT,
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    hipLaunchKernelGGL(end_window_kernel, dim3((np + 255) / 256, ns), dim3(256), 0, (hipStream_t)stream, np, wT,
                        mT, vT, w0, m0, v0, (EngineScalars*)scalars, graphs, forwards, adam_steps, hypers,
-                       betas_dev, adam_tab, tab_count);
+                       betas_dev, adam_tab, tab_count, bt.par);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -22,7 +22,8 @@ namespace lds {
 // words collect one bit per row in each lane and are OR-combined across the
 // four waves in LDS.  Every word of `bits` has exactly one writer: no atomics,
 // no memset.
-// Batched launches: grid.y = graph (counter + y, bits + y·n·words).  Measured
+// Batched launches: grid.y = graph (counter + y), grid.z = replica sample (tag +
+// z·tag_step); bit matrix (y·samples + z) of the batch.  Measured
 // on MI355X (r01, 6 Cora graphs per window): drawing all graphs of a window
 // from one θ load inside the block (a loop over graphs) took 41-53 µs against
 // 35 µs here — the loop raised the kernel to 157 VGPRs (occupancy 3 vs 8), and
@@ -30,13 +31,14 @@ namespace lds {
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
-    uint64_t* __restrict__ bits, int words, int ntiles) {
+    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step) {
     __shared__ uint64_t colpart[4][64];
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
     // batched launches: graph blockIdx.y draws counter + blockIdx.y into its own bit matrix
     counter += blockIdx.y;
-    bits += (int64_t)blockIdx.y * n * words;
+    tag += blockIdx.z * tag_step;
+    bits += ((int64_t)blockIdx.y * gridDim.z + blockIdx.z) * n * words;
     if (counter_base != nullptr) counter += *counter_base;  // device-resident draw counter
     const int lane = wave_lane();
     const int wave = threadIdx.x >> 6;
@@ -246,7 +248,7 @@ extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint
     const int ntiles = nb * (nb + 1) / 2;
     hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles);
+                       counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -259,7 +261,7 @@ extern "C" int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, 
     const int ntiles = nb * (nb + 1) / 2;
     hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles);
+                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -307,24 +309,35 @@ extern "C" int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* 
     LDS_RETURN_LAST_ERROR();
 }
 
+extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
+                                       uint32_t tag_step, const uint32_t* counter_base,
+                                       uint32_t counter_offset, int count, int samples, uint64_t* bits,
+                                       int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
+                                       float* s, int* ell, void* stream) {
+    LDS_CHECK_ARG(theta && bits && deg_ws && row_ptr && col && s && n > 0 && n <= (1 << 20));
+    LDS_CHECK_ARG(count > 0 && samples > 0 && samples <= 65535 && (int64_t)count * samples <= 65535);
+    LDS_CHECK_ARG(words >= (n + 63) / 64 && col_stride > 0);
+    const int nb = (n + 63) / 64;
+    const int ntiles = nb * (nb + 1) / 2;
+    const int graphs = count * samples;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles, count, samples), dim3(256), 0, st, theta, n,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
+                       (const float*)nullptr, bits, words, ntiles, tag_step);
+    hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
+                       deg_ws, s);
+    hipLaunchKernelGGL(scan_kernel, dim3(1, graphs), dim3(1024), 0, st, deg_ws, n, row_ptr);
+    hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
+                       row_ptr, col, col_stride, (int*)nullptr, (const float*)s, (int2*)ell);
+    LDS_RETURN_LAST_ERROR();
+}
+
 extern "C" int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
                                  const uint32_t* counter_base, uint32_t counter_offset, int count,
                                  uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
                                  int64_t col_stride, float* s, int* ell, void* stream) {
-    LDS_CHECK_ARG(theta && bits && deg_ws && row_ptr && col && s && n > 0 && n <= (1 << 20));
-    LDS_CHECK_ARG(count > 0 && count <= 65535 && words >= (n + 63) / 64 && col_stride > 0);
-    const int nb = (n + 63) / 64;
-    const int ntiles = nb * (nb + 1) / 2;
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles, count), dim3(256), 0, st, theta, n,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
-                       (const float*)nullptr, bits, words, ntiles);
-    hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, count), dim3(256), 0, st, bits, n, words,
-                       deg_ws, s);
-    hipLaunchKernelGGL(scan_kernel, dim3(1, count), dim3(1024), 0, st, deg_ws, n, row_ptr);
-    hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4, count), dim3(256), 0, st, bits, n, words,
-                       row_ptr, col, col_stride, (int*)nullptr, (const float*)s, (int2*)ell);
-    LDS_RETURN_LAST_ERROR();
+    return lds_sample_graphs_multi(theta, n, seed, tag, 0u, counter_base, counter_offset, count, 1, bits,
+                                   words, deg_ws, row_ptr, col, col_stride, s, ell, stream);
 }
 
 extern "C" int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32_t tag,

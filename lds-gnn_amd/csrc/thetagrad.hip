@@ -196,7 +196,8 @@ __device__ __forceinline__ void store4(float (*dst)[kLdsRow], int kq, int row, c
 __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
-    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4) {
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
+    float gscale) {
     __shared__ float Ui[kMC][kLdsRow];
     __shared__ float Vi[kMC][kLdsRow];
     __shared__ float Uj[kMC][kLdsRow];
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
         const int row = (t < kTile ? i0 : j0) + rr;
         float acc = 0.f;
         if (row < n)
-            for (int c = 0; c < nr; ++c) acc += r[(int64_t)row * ldr + c];
+            for (int c = 0; c < nr; ++c) acc += r[(int64_t)row * ldr + (int64_t)c * ldrc];
         (t < kTile ? Ri : Rj)[rr] = acc;
     }
 
@@ -277,7 +278,9 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
         const int64_t idx = tri_index(i, i, nn) + (j - i);
         float g = 0.f;
         if (j > i) {
-            g = mode == 3 ? part[e] + acc[e] + Ri[li] + Rj[lj] : acc[e] + Ri[li] + Rj[lj];
+            // gscale: 1/S for the mean over S replica samples (exactly 1 otherwise)
+            const float gs = gscale * (acc[e] + Ri[li] + Rj[lj]);
+            g = mode == 3 ? part[e] + gs : gs;
             if (theta != nullptr && !(th[e] >= 0.f && th[e] <= 1.f)) g = 0.f;  // clamp backward
         }
         if (mode == 3) {
@@ -376,7 +379,7 @@ extern "C" int lds_theta_grad(const float* u, const float* v, int ld, int k, con
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
                        v, ld, k, r, ldr, nr, const_cast<float*>(theta), n, grad, accumulate ? 1 : 0,
-                       (const double*)nullptr, vec4);
+                       (const double*)nullptr, vec4, 1, 1.0f);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -406,7 +409,7 @@ extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
     // EngineScalars: f64 outer_lr at byte offset 16
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
     hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
-                       v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4);
+                       v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4, 1, 1.0f);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -421,7 +424,24 @@ extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, 
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
     hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
-                       v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4);
+                       v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4, 1, 1.0f);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
+                                 int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
+                                 int mode, const void* scalars, float gscale, void* stream) {
+    LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
+    LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
+    LDS_CHECK_ARG(mode < 2 ? grad != nullptr : (theta != nullptr && scalars != nullptr));
+    LDS_CHECK_ARG(mode != 3 || grad != nullptr);
+    const int nb = (n + kTile - 1) / kTile;
+    const int ntiles = nb * (nb + 1) / 2;
+    const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
+    const double* lr = mode >= 2 ? reinterpret_cast<const double*>((const char*)scalars + 16) : nullptr;
+    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u, v, ld, k, r,
+                       ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -32,6 +32,9 @@ SIGNATURES = {
     "lds_csr_degree_scale": [P, c_int, P, P, P],
     "lds_sample_graphs": [P, c_int, c_uint64, c_uint32, P, c_uint32, c_int, P, c_int, P, P, P, c_int64, P, P,
                           P],
+    "lds_sample_graphs_multi": [P, c_int, c_uint64, c_uint32, c_uint32, P, c_uint32, c_int, c_int, P, c_int, P,
+                                P, P, c_int64, P, P, P],
+    "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
     "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],
@@ -49,36 +52,36 @@ SIGNATURES = {
     "lds_engine_scalars_size": [],
     "lds_sample_bitmask_dev": [P, c_int, c_uint64, c_uint32, P, c_uint32, P, c_int, P],
     "lds_engine_x_linear": [P, P, P, c_int, P, P, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
-                            P, P, P, P],
+                            P, P, P, P, P],
     "lds_engine_xt_linear": [P, P, P, c_int, P, P, P, c_float, c_int, c_uint64, c_uint32, P, c_int, c_int,
                              c_float, c_float, P],
     "lds_engine_fwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
-                              c_float, c_float, P, P],
-    "lds_engine_fwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, P, c_float, P, P, c_int, P],
+                              c_float, c_float, P, P, P],
+    "lds_engine_fwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, P, c_float, P, P, c_int, P, P],
     "lds_engine_bwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
-                              c_float, c_float, P, P, P, P, c_int, P, c_int, c_int, c_int, P, P],
+                              c_float, c_float, P, P, P, P, c_int, P, c_int, c_int, c_int, P, P, P],
     "lds_engine_bwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_colreduce": [c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, c_int, P, c_int, P, c_int,
                              P],
     "lds_engine_adam": [c_int, P, P, P, P, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_adam_reverse": [c_int, P, P, P, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_rev_a": [P, P, P, P, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, c_uint64, c_uint32, P,
-                         c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, P, P],
-    "lds_engine_rev_b": [P, P, P, P, c_int, P, P, P, P, P, c_float, c_int, P, P, P, c_int, P, c_int, c_int, P],
+                         c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, P, P, P],
+    "lds_engine_rev_b": [P, P, P, P, c_int, P, P, P, P, P, c_float, c_int, P, P, P, c_int, P, c_int, c_int, P, P],
     "lds_engine_rev_c": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, P, c_uint64, c_uint32, P, c_int, c_int,
-                         c_float, c_float, P, P, c_int, P, c_int, c_int, P, P],
+                         c_float, c_float, P, P, c_int, P, c_int, c_int, P, P, P],
     "lds_engine_rev_d": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_sgd_clamp": [P, P, c_int64, P, P],
     "lds_engine_advance": [P, c_int, c_int, c_int, c_int, P],
     # fused forms
-    "lds_engine_bwd1_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P],
-    "lds_engine_rev_d_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P],
+    "lds_engine_bwd1_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P, P],
+    "lds_engine_rev_d_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P, P],
     "lds_engine_final": [P, c_int, c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P, P, P, P, P,
                          P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_xt_adam": [P, P, P, c_int, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
                            P, c_int, c_int, c_int, c_int, c_int, P,
-                           c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P],
-    "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P],
+                           c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, P],
+    "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
     "lds_engine_adam_table": [P, P, P, c_int, P],
 }
 
@@ -154,6 +157,18 @@ def call(name: str, *args) -> None:
         check(err, name)
         return
     check(getattr(lib, name)(*args), name)
+
+
+class LdsBatch(ctypes.Structure):
+    """include/ldsgnn.h LdsBatch: per-sample element strides of a batched
+    engine launch (S replica samples in one launch, grid.y = sample)."""
+    _fields_ = [("samples", ctypes.c_int32), ("tag_step", ctypes.c_uint32)] + [
+        (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")]
+
+
+def batch_ptr(b) -> int:
+    """Address of an LdsBatch (None -> NULL = one sample)."""
+    return 0 if b is None else ctypes.addressof(b)
 
 
 def ptr(t) -> int:

@@ -24,6 +24,14 @@ advancing state.
 
 Layout: per-node arrays are n × 16 fp32 (hidden 16; classes padded to 16);
 parameters are one flat vector [W0ᵀ (fin×16) | b0 (16) | W1 (C×16) | b1 (C)].
+
+Replica samples (`samples=S`, SURVEY §8(e), BASELINE configs 3/4): S independent
+Monte-Carlo chains — own graphs, dropout masks (replica tags replica0 + b), GCN
+weights and Adam state — share θ, X and the scalars, and run in the SAME
+launches (grid.y = sample; include/ldsgnn.h LdsBatch).  Every per-sample array
+carries a leading S dimension.  The hyper step assembles the mean of the S
+hypergradients in one rank-(S·K) update (lds_theta_grad_ex, gscale = 1/S);
+S = 1 is the reference's single chain.
 """
 from __future__ import annotations
 
@@ -44,30 +52,33 @@ _ACT = ("h0", "y0", "h1d", "h2", "o", "p", "d_o", "dh2", "dy0", "dh0")
 
 
 class _Graph:
-    """Device buffers of one sampled graph (CSR with self-loops + s)."""
+    """Device buffers of one sampled graph per replica sample (CSR with
+    self-loops + s): arrays [S, ...]."""
 
-    def __init__(self, n: int, cap: int, dev, views=None):
+    def __init__(self, n: int, cap: int, dev, views=None, samples: int = 1):
         if views is not None:
             self.row_ptr, self.col, self.s, self.ell = views
             return
-        self.row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        self.col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
-        self.s = torch.empty(n, dtype=torch.float32, device=dev)
-        self.ell = torch.empty(n * 2 * HID, dtype=torch.int32, device=dev)  # ELL head {j, s_j}
+        S = samples
+        self.row_ptr = torch.empty((S, n + 1), dtype=torch.int32, device=dev)
+        self.col = torch.empty((S, max(cap, 1)), dtype=torch.int32, device=dev)
+        self.s = torch.empty((S, n), dtype=torch.float32, device=dev)
+        self.ell = torch.empty((S, n * 2 * HID), dtype=torch.int32, device=dev)  # ELL head {j, s_j}
 
 
 class _GraphBatch:
     """Contiguous storage for the τ+1 graphs of a window, so that one batched
     lds_sample_graphs launch set draws them all (θ is fixed within a window)."""
 
-    def __init__(self, count: int, n: int, words: int, cap: int, dev):
+    def __init__(self, count: int, n: int, words: int, cap: int, dev, samples: int = 1):
         self.count, self.cap = count, cap
-        self.bits = torch.empty((count, n, words), dtype=torch.int64, device=dev)
-        self.deg = torch.empty((count, n), dtype=torch.int32, device=dev)
-        self.row_ptr = torch.empty((count, n + 1), dtype=torch.int32, device=dev)
-        self.col = torch.empty((count, cap), dtype=torch.int32, device=dev)
-        self.s = torch.empty((count, n), dtype=torch.float32, device=dev)
-        self.ell = torch.empty((count, n * 2 * HID), dtype=torch.int32, device=dev)
+        S = samples
+        self.bits = torch.empty((count, S, n, words), dtype=torch.int64, device=dev)
+        self.deg = torch.empty((count, S, n), dtype=torch.int32, device=dev)
+        self.row_ptr = torch.empty((count, S, n + 1), dtype=torch.int32, device=dev)
+        self.col = torch.empty((count, S, cap), dtype=torch.int32, device=dev)
+        self.s = torch.empty((count, S, n), dtype=torch.float32, device=dev)
+        self.ell = torch.empty((count, S, n * 2 * HID), dtype=torch.int32, device=dev)
         self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g], self.ell[g]))
                        for g in range(count)]
 
@@ -77,14 +88,15 @@ class _Slot:
     relu/dropout mask of layer 1 and (training with dropout) the dropped X
     values in CSR and CSC order."""
 
-    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None, x_nnz: int = 0):
-        self.g = graph if graph is not None else _Graph(n, cap, dev)
+    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None, x_nnz: int = 0, samples: int = 1):
+        S = samples
+        self.g = graph if graph is not None else _Graph(n, cap, dev, samples=S)
         for a in _ACT + ("dmask",):
-            setattr(self, a, torch.zeros((n, HID), dtype=torch.float32, device=dev))
-        self.xd_csr = torch.zeros(x_nnz, dtype=torch.float32, device=dev) if x_nnz else None
-        self.xd_csc = torch.zeros(x_nnz, dtype=torch.float32, device=dev) if x_nnz else None
-        self.lossrow = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.corrrow = torch.zeros(n, dtype=torch.float32, device=dev)
+            setattr(self, a, torch.zeros((S, n, HID), dtype=torch.float32, device=dev))
+        self.xd_csr = torch.zeros((S, x_nnz), dtype=torch.float32, device=dev) if x_nnz else None
+        self.xd_csc = torch.zeros((S, x_nnz), dtype=torch.float32, device=dev) if x_nnz else None
+        self.lossrow = torch.zeros((S, n), dtype=torch.float32, device=dev)
+        self.corrrow = torch.zeros((S, n), dtype=torch.float32, device=dev)
 
 
 def _csr_of(dense: torch.Tensor):
@@ -100,10 +112,13 @@ class LdsEngine:
                  theta: torch.Tensor, num_classes: int, dropout: float = 0.5, gcn_lr: float = 0.01,
                  gcn_wd: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8, outer_lr: float = 1.0,
                  lr_decay: Optional[float] = None, tau: int = 5, generator: Optional[Generator] = None,
-                 params: Optional["OrderedDict[str, torch.Tensor]"] = None):
+                 params: Optional["OrderedDict[str, torch.Tensor]"] = None, samples: int = 1):
         nat.require_device(x, "LdsEngine")
         dev = x.device
         self.dev = dev
+        self.S = int(samples)
+        if not (1 <= self.S <= 4096):
+            raise ValueError("samples must be in 1..4096")
         self.n, self.fin = int(x.shape[0]), int(x.shape[1])
         self.c = int(num_classes)
         if not (0 < self.c <= HID):
@@ -121,7 +136,9 @@ class LdsEngine:
         # Adam table: {lr/bc1, sqrt(bc2)} for steps adam_step+1+k (refreshed on device)
         self.adam_tab = torch.zeros(2 * _TAB_MAX, dtype=torch.float32, device=dev)
         self.gen = generator or Generator(0, 0)
-        rep = self.gen.replica
+        rep = self.gen.replica  # sample b is replica rep + b (tags + b)
+        if rep + self.S > 0xFFFFFF:
+            raise ValueError("replica tags exceed 24 bits")
         self.seed = self.gen.seed
         self.tag_graph = tag_for(TAG_GRAPH, rep)
         self.tag_x = tag_for(TAG_DROP_X, rep)
@@ -163,8 +180,9 @@ class LdsEngine:
         if self.cap is None:
             raise NotImplementedError("LdsEngine at n > 11585 needs exact CSR sizing (not yet)")
         self.words = nat.lib.lds_bitmask_words(n)
-        self.bits = torch.empty((n, self.words), dtype=torch.int64, device=dev)
-        self.deg = torch.empty(n, dtype=torch.int32, device=dev)
+        S = self.S
+        self.bits = torch.empty((S, n, self.words), dtype=torch.int64, device=dev)
+        self.deg = torch.empty((S, n), dtype=torch.int32, device=dev)
 
         # tape
         self.tau = max(1, int(tau))
@@ -175,21 +193,21 @@ class LdsEngine:
         self.m: List[torch.Tensor] = []
         self.v: List[torch.Tensor] = []
         self.gp: List[torch.Tensor] = []
-        self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev)
+        self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev, samples=S)
         self._grow(self.tau)
-        self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau], x_nnz=self.x_nnz)
+        self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau], x_nnz=self.x_nnz, samples=S)
         self.t = 0  # inner steps in the current window
         self.pending_graph = 0
         self.pending_fwd = 0
 
         # reverse-pass buffers
-        z = lambda: torch.zeros((n, HID), dtype=torch.float32, device=dev)  # noqa: E731
+        z = lambda: torch.zeros((S, n, HID), dtype=torch.float32, device=dev)  # noqa: E731
         self.dh0bar, self.dh1dbar, self.dh2bar, self.h1dbar = z(), z(), z(), z()
         self.obar, self.h2bar, self.y0bar, self.h0bar = z(), z(), z(), z()
-        zp = lambda: torch.zeros(self.np, dtype=torch.float32, device=dev)  # noqa: E731
+        zp = lambda: torch.zeros((S, self.np), dtype=torch.float32, device=dev)  # noqa: E731
         self.wbar, self.mbar, self.vbar, self.gbar, self.g = zp(), zp(), zp(), zp(), zp()
         self.nred = (n + 63) // 64  # first-stage partials of the fused reductions (64 rows per block)
-        self.partials = torch.zeros((self.nred, _RED_LEN), dtype=torch.float32, device=dev)
+        self.partials = torch.zeros((S, self.nred, _RED_LEN), dtype=torch.float32, device=dev)
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
         self.keep_grad = True  # write dθ (θ.grad) even when it is fused with the update
@@ -199,8 +217,7 @@ class LdsEngine:
         # chunks' read-modify-write of dθ cost 2.3x the single launch (r01).
         self.split_theta_grad = False
         self.side = torch.cuda.Stream(dev)
-        self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=dev)
-        self.eval_metrics = torch.zeros((64, 4), dtype=torch.float32, device=dev)
+        self.metrics = torch.zeros((self.tau + 1, S, 2), dtype=torch.float32, device=dev)
         self._graph_capture = None
         if params is not None:
             self.set_params(params)
@@ -208,11 +225,27 @@ class LdsEngine:
 
     # ------------------------------------------------------------------ setup
     def _alloc_factors(self):
+        """U, V: n × (S·ldk), sample b in columns [b·ldk, (b+1)·ldk); R: [S, n]."""
         self.ktot = self.tau * self.kg + HID + self.cw
         self.ldk = (self.ktot + 3) & ~3
-        self.U = torch.zeros((self.n, self.ldk), dtype=torch.float32, device=self.dev)
+        self.ldu = self.S * self.ldk  # row stride of U / V (the kernels' `ldk` argument)
+        self.U = torch.zeros((self.n, self.ldu), dtype=torch.float32, device=self.dev)
         self.V = torch.zeros_like(self.U)
-        self.R = torch.zeros(self.n, dtype=torch.float32, device=self.dev)
+        self.R = torch.zeros((self.S, self.n), dtype=torch.float32, device=self.dev)
+        self._make_batches()
+
+    def _make_batches(self):
+        """LdsBatch strides for this engine's layout (kept alive on self)."""
+        n, S = self.n, self.S
+
+        def mk(xval_stride):
+            return nat.LdsBatch(samples=S, tag_step=1, act=n * HID, row=n, rp=n + 1, col=self.cap,
+                                ell=n * 2 * HID, par=self.np, xval=xval_stride, xd=self.x_nnz, uv=self.ldk,
+                                part=self.nred * _RED_LEN, met=2)
+        self._bt = mk(0)  # X values argument = the shared X
+        self._btx = mk(self.x_nnz if self.train_flag else 0)  # X values argument = the slot's stored Xd
+        self.bt = nat.batch_ptr(self._bt)
+        self.btx = nat.batch_ptr(self._btx)
 
     def _grow(self, slots: int):
         if slots > _TAB_MAX:
@@ -220,34 +253,37 @@ class LdsEngine:
         while len(self.slots) < slots:
             t = len(self.slots)
             g = self.gbatch.graphs[t] if t < self.gbatch.count - 1 else None
-            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g, x_nnz=self.x_nnz))
+            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g, x_nnz=self.x_nnz, samples=self.S))
         while len(self.w) < slots + 1:
             for lst in (self.w, self.m, self.v):
-                lst.append(torch.zeros(self.np, dtype=torch.float32, device=self.dev))
+                lst.append(torch.zeros((self.S, self.np), dtype=torch.float32, device=self.dev))
         while len(self.gp) < slots:
-            self.gp.append(torch.zeros(self.np, dtype=torch.float32, device=self.dev))
+            self.gp.append(torch.zeros((self.S, self.np), dtype=torch.float32, device=self.dev))
 
     def _stream(self) -> int:
         return nat.stream_of(self.dev)
 
     def _views(self, flat: torch.Tensor):
+        """(W0ᵀ, b0, W1, b1) slices of a flat [.., np] parameter vector; their
+        data pointers address sample 0 (kernels add b·np)."""
         c = self.c
-        return (flat[: self.off_b0], flat[self.off_b0:self.off_w1], flat[self.off_w1:self.off_b1],
-                flat[self.off_b1:self.off_b1 + c])
+        return (flat[..., : self.off_b0], flat[..., self.off_b0:self.off_w1], flat[..., self.off_w1:self.off_b1],
+                flat[..., self.off_b1:self.off_b1 + c])
 
     def set_params(self, params):
-        """Load reference-layout params (layer_in.fc.weight [16, fin], ...)."""
-        w = self.w[0]
-        w0t, b0, w1, b1 = self._views(w)
-        with torch.no_grad():
-            w0t.view(self.fin, HID).copy_(params["layer_in.fc.weight"].detach().t())
-            b0.copy_(params["layer_in.fc.bias"].detach())
-            w1.view(self.c, HID).copy_(params["layer_out.fc.weight"].detach())
-            b1.copy_(params["layer_out.fc.bias"].detach())
+        """Load reference-layout params (layer_in.fc.weight [16, fin], ...)
+        into every replica sample (all chains start from the same GCN)."""
+        for b in range(self.S):
+            w0t, b0, w1, b1 = self._views(self.w[0][b])
+            with torch.no_grad():
+                w0t.view(self.fin, HID).copy_(params["layer_in.fc.weight"].detach().t())
+                b0.copy_(params["layer_in.fc.bias"].detach())
+                w1.view(self.c, HID).copy_(params["layer_out.fc.weight"].detach())
+                b1.copy_(params["layer_out.fc.bias"].detach())
         self.t = 0
 
-    def get_params(self) -> "OrderedDict[str, torch.Tensor]":
-        w0t, b0, w1, b1 = self._views(self.w[self.t])
+    def get_params(self, sample: int = 0) -> "OrderedDict[str, torch.Tensor]":
+        w0t, b0, w1, b1 = self._views(self.w[self.t][sample])
         return OrderedDict([
             ("layer_in.fc.weight", w0t.view(self.fin, HID).t().contiguous()),
             ("layer_in.fc.bias", b0.clone()),
@@ -299,13 +335,11 @@ class LdsEngine:
 
     # --------------------------------------------------------------- pieces
     def _sample(self, g: _Graph):
-        st = self._stream()
-        nat.call("lds_sample_bitmask_dev", nat.ptr(self.theta), self.n, self.seed, self.tag_graph,
-                 nat.ptr(self.scalars), self.pending_graph, nat.ptr(self.bits), self.words, st)
-        nat.call("lds_bitmask_degree", nat.ptr(self.bits), self.n, self.words, nat.ptr(self.deg), nat.ptr(g.s), st)
-        nat.call("lds_exclusive_scan", nat.ptr(self.deg), self.n, nat.ptr(g.row_ptr), st)
-        nat.call("lds_bitmask_fill_csr_ell", nat.ptr(self.bits), self.n, self.words, nat.ptr(g.row_ptr),
-                 nat.ptr(g.col), self.cap, 0, nat.ptr(g.s), nat.ptr(g.ell), st)
+        """Draw the next graph of every replica sample into `g`."""
+        nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
+                 nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(self.bits), self.words,
+                 nat.ptr(self.deg), nat.ptr(g.row_ptr), nat.ptr(g.col), self.cap, nat.ptr(g.s), nat.ptr(g.ell),
+                 self._stream())
         self.pending_graph += 1
 
     def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int):
@@ -318,13 +352,14 @@ class LdsEngine:
         xd = (nat.ptr(sl.xd_csr), nat.ptr(sl.xd_csc), nat.ptr(self.csr2csc)) if keep_xd else (0, 0, 0)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
                  nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, train, self.keep, self.scale, *xd, st)
+                 fwd_off, train, self.keep, self.scale, *xd, self.bt, st)
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
-                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask), st)
+                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask), self.bt,
+                 st)
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
-                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, st)
+                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self.bt, st)
 
     def _adam_args(self, mode: int, t: int, first: int = 0):
         """Trailing Adam arguments of lds_engine_final / lds_engine_xt_adam.
@@ -362,19 +397,19 @@ class LdsEngine:
         rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
         nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
                  nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
-                 self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldk, R, base + HID, self.cw,
-                 1, nat.ptr(sl.dmask), st)
+                 self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldu, R, base + HID, self.cw,
+                 1, nat.ptr(sl.dmask), self.bt, st)
         # dH0 + first stage of gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
         nat.call("lds_engine_bwd1_reduce", rp, cl, s, el, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
-                 nat.ptr(sl.h0), U, V, self.ldk, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
-                 nat.ptr(sl.corrrow), c, nat.ptr(self.partials), st)
+                 nat.ptr(sl.h0), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
+                 nat.ptr(sl.corrrow), c, nat.ptr(self.partials), self.bt, st)
         first = 1 if adam_mode == 2 else 0
         adam = self._adam_args(adam_mode, adam_t, first)
         # W0 part (Xdᵀ dH0) and the final stage of the reduction, one launch
         nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self._xvals(sl)[1]),
                  self.fin, nat.ptr(sl.dh0), nat.ptr(gout), 0, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
-                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, st)
+                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, self.btx, st)
 
     # ----------------------------------------------------------------- steps
     def _sample_batch(self, count: int):
@@ -382,9 +417,10 @@ class LdsEngine:
         takes draw counter (pending + g), exactly the counter the step-by-step
         path would give it."""
         gb = self.gbatch
-        nat.call("lds_sample_graphs", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, nat.ptr(self.scalars),
-                 self.pending_graph, count, nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), nat.ptr(gb.row_ptr),
-                 nat.ptr(gb.col), self.cap, nat.ptr(gb.s), nat.ptr(gb.ell), self._stream())
+        nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
+                 nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
+                 nat.ptr(gb.deg), nat.ptr(gb.row_ptr), nat.ptr(gb.col), self.cap, nat.ptr(gb.s), nat.ptr(gb.ell),
+                 self._stream())
 
     def inner_step(self, presampled: bool = False):
         """One InnerProblemTrainer.train_step (sample + forward + backward +
@@ -395,7 +431,7 @@ class LdsEngine:
             self._grow(t + 1)
             self.tau = t + 1
             self._alloc_factors()
-            self.metrics = torch.zeros((self.tau + 1, 2), dtype=torch.float32, device=self.dev)
+            self.metrics = torch.zeros((self.tau + 1, self.S, 2), dtype=torch.float32, device=self.dev)
             self._refresh_adam_table()  # entries for the new step offsets
         sl = self.slots[t]
         if presampled:
@@ -431,6 +467,8 @@ class LdsEngine:
         if self.train_flag:
             self.pending_fwd += 1
         split = self.split_theta_grad and T > 0
+        if split and self.S > 1:
+            raise NotImplementedError("split θ-grad assembly is single-sample only")
         if split:  # outer graph's columns: first chunk of dθ, beside reverse step T-1
             self._theta_chunk(T * self.kg, HID + self.cw, accumulate=0)
         for t in range(T - 1, -1, -1):
@@ -442,7 +480,9 @@ class LdsEngine:
             k0 = self.kg  # the last chunk (graph 0) + R on the main stream
         else:
             k0 = T * self.kg + HID + self.cw
-        if grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
+        if self.S > 1:
+            self._assemble_samples(k0, grad_reducer)
+        elif grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
             if split:
                 nat.call("lds_theta_grad_sgd_accum", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0,
                          nat.ptr(self.R), 1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad), nat.ptr(self.scalars), st)
@@ -461,11 +501,31 @@ class LdsEngine:
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
         nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
                  P(self.scalars), self.pending_graph, self.pending_fwd, T, 1, P(self.betas_dev), P(self.adam_tab),
-                 self._tab_count(), st)
+                 self._tab_count(), self.bt, st)
         self.pending_graph = 0
         self.pending_fwd = 0
         self.t = 0
         return self.metrics[self.tau]
+
+    def _assemble_samples(self, k0: int, grad_reducer):
+        """Mean hypergradient of the S replica samples: one rank-(S·ldk)
+        update over the side-by-side factor blocks (columns past k0 of each
+        block zeroed first), R summed over the S stacked rows, gscale = 1/S;
+        fused with SGD + clamp, or (replicas over ranks) dθ → reducer → SGD."""
+        st, n, S = self._stream(), self.n, self.S
+        if k0 < self.ldk:  # stale columns of a longer earlier window
+            self.U.view(n, S, self.ldk)[:, :, k0:].zero_()
+            self.V.view(n, S, self.ldk)[:, :, k0:].zero_()
+        P = nat.ptr
+        gs = float(np.float32(1.0) / np.float32(S))
+        if grad_reducer is None:
+            nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
+                     P(self.theta), n, P(self.grad) if self.keep_grad else 0, 2, P(self.scalars), gs, st)
+        else:
+            nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
+                     P(self.theta), n, P(self.grad), 0, 0, gs, st)
+            grad_reducer(self.grad)
+            nat.call("lds_engine_sgd_clamp", P(self.theta), P(self.grad), self.theta.numel(), P(self.scalars), st)
 
     def _theta_chunk(self, col0: int, k: int, accumulate: int):
         """grad (=|+=) U[:, col0:col0+k] V[...]ᵀ + V U ᵀ on the side stream, after
@@ -493,28 +553,28 @@ class LdsEngine:
         xcsr, xcsc = self._xvals(sl)  # Xd of step t (no redraw: train = 0 below)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(xcsr), n,
                  nat.ptr(gw0t), nat.ptr(gb0), nat.ptr(self.dh0bar), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, 0, self.keep, self.scale, 0, 0, 0, st)
+                 fwd_off, 0, self.keep, self.scale, 0, 0, 0, self.btx, st)
         nat.call("lds_engine_rev_a", rp, cl, s, el, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
-                 nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldk, R,
-                 base + HID + 2 * self.cw, nat.ptr(sl.dmask), st)
+                 nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldu, R,
+                 base + HID + 2 * self.cw, nat.ptr(sl.dmask), self.bt, st)
         nat.call("lds_engine_rev_b", rp, cl, s, el, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
-                 nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldk,
-                 R, base + HID + self.cw, self.cw, st)
+                 nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldu,
+                 R, base + HID + self.cw, self.cw, self.bt, st)
         nat.call("lds_engine_rev_c", rp, cl, s, el, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
                  nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
                  self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
-                 self.ldk, R, base + HID, self.cw, nat.ptr(sl.dmask), st)
+                 self.ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self.bt, st)
         # H0bar + first stage of W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
         nat.call("lds_engine_rev_d_reduce", rp, cl, s, el, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
-                 nat.ptr(self.h0bar), U, V, self.ldk, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
-                 nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), st)
+                 nat.ptr(self.h0bar), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
+                 nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), self.bt, st)
         adam = self._adam_args(2 if t else 0, t - 1 if t else 0)
         nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
                  nat.ptr(self.h0bar), nat.ptr(self.wbar), 1, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
-                 self.off_b1, 0, *adam, t - 1, st)
+                 self.off_b1, 0, *adam, t - 1, self.btx, st)
 
     # ------------------------------------------------------------- graphs
     def run_window(self, tau: int, grad_reducer=None):
@@ -580,12 +640,13 @@ class LdsEngine:
 
     # ------------------------------------------------------------ metrics
     def inner_metrics(self, t: int):
-        """(loss, acc) of inner step t of the last window (host sync)."""
-        row = self.metrics[t].cpu()
+        """(loss, acc) of inner step t of the last window, averaged over the
+        replica samples (host sync)."""
+        row = self.metrics[t].double().mean(0).cpu()
         return float(row[0]) * self.inv_train, float(row[1]) * self.inv_train
 
     def outer_metrics(self):
-        row = self.metrics[self.tau].cpu()
+        row = self.metrics[self.tau].double().mean(0).cpu()
         return float(row[0]) * self.inv_opt, float(row[1]) * self.inv_opt
 
     def scalars_host(self):
@@ -599,7 +660,10 @@ class LdsEngine:
         return tau * (2 * HID + 2 * cw) + HID + cw
 
     def flops_theta_grad(self, tau: int) -> float:
-        return 4.0 * self.window_columns(tau, self.c) * (self.n * (self.n + 1) // 2)
+        """Algorithmic flops of one window's assembly (S blocks of ldk columns
+        when S > 1: the padded columns are multiplied too)."""
+        k = self.window_columns(tau, self.c) if self.S == 1 else self.S * self.ldk
+        return 4.0 * k * (self.n * (self.n + 1) // 2)
 
 
 def _unused(*_):  # pragma: no cover

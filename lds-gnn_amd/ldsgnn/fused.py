@@ -11,7 +11,10 @@ from . import rng as _rng
 from .engine import LdsEngine
 
 
-def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator" = None) -> LdsEngine:
+def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator" = None,
+                         samples: int = 1) -> LdsEngine:
+    """samples > 1: S replica chains (replicas generator.replica + b) batched
+    in one engine; θ moves by their mean hypergradient."""
     from .models.graph import BernoulliGraphModel
     gm = outer.model
     if not isinstance(gm, BernoulliGraphModel) or gm.directed:
@@ -30,4 +33,4 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
     return LdsEngine(data.x, data.y, data.train_mask, outer.opt_mask, gm.probs.data, data.num_classes,
                      dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=grp["lr"],
                      lr_decay=outer.lr_decay, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
-                     params=inner.model_params)
+                     params=inner.model_params, samples=samples)

@@ -375,6 +375,13 @@ class LdsProblem:
 
     # --- outer (src/trainers/outer.py:57-87) ---
     def hyper_step(self) -> Tuple[float, float, torch.Tensor]:
+        """src/trainers/outer.py:57-87 + the detaches of bilevel.py:109-114."""
+        loss, acc, grad = self.hyper_grad()
+        self.apply_hyper_update(grad)
+        return loss, acc, grad
+
+    def hyper_grad(self) -> Tuple[float, float, torch.Tensor]:
+        """The outer loss.backward of a hyper step: (loss, acc, dθ); θ unchanged."""
         if self.theta.grad is not None:
             self.theta.grad = None
         graph = self.sample()
@@ -383,14 +390,16 @@ class LdsProblem:
         loss = F.nll_loss(pred[m], self.y[m])
         acc = accuracy(pred[m], self.y[m])
         loss.backward(retain_graph=True)
-        grad = self.theta.grad.detach().clone()
+        return loss.item(), acc, self.theta.grad.detach().clone()
+
+    def apply_hyper_update(self, grad: torch.Tensor) -> None:
+        """SGD (no momentum) → StepLR → clamp (project_parameters), then detach."""
         with torch.no_grad():
-            self.theta.add_(self.theta.grad, alpha=-self.outer_lr)   # SGD, no momentum
+            self.theta.add_(grad, alpha=-self.outer_lr)                # SGD, no momentum
             if self.lr_decay is not None:
                 self.outer_lr = self.outer_lr * self.lr_decay          # StepLR(step_size=1)
             self.theta.clamp_(0.0, 1.0)                                # project_parameters
         self.detach()
-        return loss.item(), acc, grad
 
     def empirical_mean_loss(self, n_samples: int, params=None):
         """src/utils/evaluation.py:51-84"""
@@ -453,3 +462,20 @@ class LdsProblem:
             if hyper_gradient_interval == 0 or step % hyper_gradient_interval == 0:
                 self.hyper_step()
         return out
+
+
+def replica_hyper_step(problems: List["LdsProblem"]) -> Tuple[List[Tuple[float, float]], torch.Tensor]:
+    """One hyper step of S Monte-Carlo replicas (not in the
+    reference, which runs S = 1): every replica — its own graph / dropout
+    stream (Randomness replica b), GCN weights and Adam state, the same θ —
+    computes its hypergradient; the mean over replicas (what an all-reduce
+    SUM / S gives) updates every replica's θ identically.  S = 1 is exactly
+    LdsProblem.hyper_step."""
+    res = [p.hyper_grad() for p in problems]
+    g = res[0][2].clone()
+    for r in res[1:]:
+        g += r[2]
+    g /= len(problems)
+    for p in problems:
+        p.apply_hyper_update(g)
+    return [(r[0], r[1]) for r in res], g

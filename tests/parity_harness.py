@@ -126,3 +126,52 @@ def run_engine_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5,
                 max_theta_err=float((eng.theta.cpu() - oracle.theta.detach()).abs().max()),
                 theta_changed=float((oracle.theta.detach() - O.get_triu_values(prob["adj"])).abs().max()),
                 engine=eng, oracle=oracle)
+
+
+def run_engine_samples_and_oracle(samples=3, n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5, seed=0,
+                                  p_edge=0.05, hidden=16, replica0=0):
+    """Batched engine (S replica samples in one launch set) vs S oracle
+    replicas (Randomness replica replica0 + b) sharing θ and updated by the
+    mean hypergradient (oracle.replica_hyper_step)."""
+    import ldsgnn
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.models.gcn import MetaDenseGCN
+    prob = synthetic_problem(n, f_in, classes, seed, p_edge)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(f_in, hidden, classes, dropout=dropout)
+    params = OrderedDict((k, v.detach()) for k, v in gcn.named_parameters())
+    dev = "cuda"
+    theta = O.get_triu_values(prob["adj"]).to(dev).contiguous()
+    eng = LdsEngine(prob["x"].to(dev), prob["y"].to(dev), prob["train"].to(dev), prob["opt"].to(dev), theta,
+                    classes, dropout=dropout, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99, tau=tau,
+                    generator=ldsgnn.rng.Generator(seed, replica0),
+                    params=OrderedDict((k, v.to(dev)) for k, v in params.items()), samples=samples)
+    oracles = [O.LdsProblem(prob["x"], prob["y"], prob["train"], prob["val"], prob["test"], prob["opt"],
+                            O.get_triu_values(prob["adj"]), hidden=hidden, dropout_p=dropout, gcn_lr=0.01,
+                            gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99, rnd=O.Randomness(seed, replica0 + b),
+                            params=params) for b in range(samples)]
+    lerr, grel = [], []
+    for step in range(steps):
+        t = eng.t
+        eng.inner_step()
+        e_rows = eng.metrics[t].cpu().numpy()  # [S, 2] Σ loss, #correct
+        for b, orc in enumerate(oracles):
+            ol = orc.inner_step(orc.sample())[0]
+            lerr.append(abs(float(e_rows[b, 0]) * eng.inv_train - ol))
+        if tau == 0 or step % tau == 0:
+            eng.hyper_step()
+            outs, og = O.replica_hyper_step(oracles)
+            e_rows = eng.metrics[eng.tau].cpu().numpy()
+            for b, (ol, _) in enumerate(outs):
+                lerr.append(abs(float(e_rows[b, 0]) * eng.inv_opt - ol))
+            eg = eng.grad.detach().cpu()
+            grel.append(float((eg - og).abs().max() / og.abs().max().clamp(min=1e-30)))
+    perr = 0.0
+    for b, orc in enumerate(oracles):
+        ep = eng.get_params(b)
+        perr = max(perr, max(float((ep[k].cpu() - orc.params[k].detach()).abs().max()) for k in ep))
+    terr = max(float((eng.theta.cpu() - orc.theta.detach()).abs().max()) for orc in oracles)
+    return dict(max_loss_err=float(max(lerr)), max_param_err=perr, max_grad_rel=max(grel) if grel else 0.0,
+                max_theta_err=terr,
+                theta_changed=float((oracles[0].theta.detach() - O.get_triu_values(prob["adj"])).abs().max()),
+                engine=eng, oracles=oracles)

@@ -88,3 +88,73 @@ def test_split_graph_replay_with_reducer_equals_eager():
     for k, v in a.get_params().items():
         assert torch.equal(v, b.get_params()[k]), k
     assert a.scalars_host() == b.scalars_host()
+
+
+@pytest.mark.parametrize("samples,tau,dropout,replica0", [(2, 5, 0.5, 2), (3, 5, 0.5, 5), (4, 1, 0.0, 2),
+                                                          (2, 5, 0.0, 2)])
+def test_engine_replica_samples_match_oracle(samples, tau, dropout, replica0):
+    """S replica samples batched in one launch set (grid.y = sample) against S
+    oracle replicas sharing θ, updated by the mean hypergradient.
+    θ.grad tolerance: with dropout, single chains of this problem (S = 1,
+    e.g. replica 4) hit the reference's conditioning spikes and
+    hold 5e-4 relative there; a mean over replicas inherits the worst chain.
+    The batched engine reproduces each chain bit for bit
+    (test_engine_batched_sample_equals_single_chain), and losses, weights and
+    θ hold 1e-5."""
+    from tests.parity_harness import run_engine_samples_and_oracle
+    res = run_engine_samples_and_oracle(samples=samples, n=110, f_in=26, classes=5, steps=11, tau=tau,
+                                        dropout=dropout, seed=7, replica0=replica0)
+    assert res["theta_changed"] > 0
+    assert res["max_loss_err"] < TOL, res
+    assert res["max_param_err"] < TOL, res
+    assert res["max_grad_rel"] < (1e-3 if dropout > 0 else 1e-4), res
+    assert res["max_theta_err"] < TOL, res
+
+
+def test_engine_batched_sample_equals_single_chain():
+    """Sample b of a batched engine is exactly the single-chain engine of
+    replica replica0 + b: same draws, bit-identical weights (θ kept fixed by a
+    zero outer learning rate, so the chains do not couple through the mean)."""
+    from collections import OrderedDict
+
+    import ldsgnn
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from oracle import lds_oracle as O
+    from tests.parity_harness import synthetic_problem
+    prob = synthetic_problem(120, 28, 5, 13, 0.06)
+    theta0 = O.get_triu_values(prob["adj"]).cuda().contiguous()
+
+    def mk(samples, replica):
+        torch.manual_seed(0)
+        gcn = MetaDenseGCN(28, 16, 5, dropout=0.5)
+        params = OrderedDict((k, v.detach().cuda()) for k, v in gcn.named_parameters())
+        return LdsEngine(prob["x"].cuda(), prob["y"].cuda(), prob["train"].cuda(), prob["opt"].cuda(),
+                         theta0.clone(), 5, outer_lr=0.0, tau=5, generator=ldsgnn.rng.Generator(5, replica),
+                         params=params, samples=samples)
+    big = mk(3, 4)
+    singles = [mk(1, 4 + b) for b in range(3)]
+    for e in [big] + singles:
+        for _ in range(2):
+            e.run_window(5)
+    torch.cuda.synchronize()
+    for b, e in enumerate(singles):
+        for k, v in e.get_params().items():
+            assert torch.equal(v, big.get_params(b)[k]), (b, k)
+
+
+def test_batched_graph_replay_equals_eager():
+    """A batched (S = 4) window captured as a HIP graph replays exactly like
+    eager batched windows."""
+    from tests.parity_harness import run_engine_samples_and_oracle
+    a = run_engine_samples_and_oracle(samples=4, n=100, f_in=20, classes=4, steps=1, tau=5, seed=3)["engine"]
+    b = run_engine_samples_and_oracle(samples=4, n=100, f_in=20, classes=4, steps=1, tau=5, seed=3)["engine"]
+    a.capture_window(5)
+    a.replay(3)
+    for _ in range(3):
+        b.run_window(5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for s in range(4):
+        for k, v in a.get_params(s).items():
+            assert torch.equal(v, b.get_params(s)[k]), (s, k)
