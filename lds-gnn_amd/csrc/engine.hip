@@ -57,14 +57,19 @@ struct Batch {
     uint32_t tag;
 };
 
-template <typename T>
+// kB = false (single-sample launch): no offset code at all.
+template <bool kB, typename T>
 __device__ __forceinline__ T* boff(T* p, int64_t stride) {
+    if constexpr (!kB) return p;
     return p == nullptr ? p : p + (int64_t)blockIdx.y * stride;
 }
 
+template <bool kB>
 __device__ __forceinline__ void bkeys(Keys& k, const Batch& bt) {
-    k.tag_x += blockIdx.y * bt.tag;
-    k.tag_h += blockIdx.y * bt.tag;
+    if constexpr (kB) {
+        k.tag_x += blockIdx.y * bt.tag;
+        k.tag_h += blockIdx.y * bt.tag;
+    }
 }
 
 __device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr, int row, int col) {
@@ -179,6 +184,7 @@ __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const i
 
 // out[i][h] = bias[h] + Σ_f Xd[i][f] · Wt[f][h]      (H0 = Xd W0ᵀ + b0)
 // Xd = dropout(X) with key (tag_x, fwd counter) when `train`, else X.
+template <bool kB>
 __global__ __launch_bounds__(256) void x_linear_kernel(
     const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
@@ -186,13 +192,13 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
     float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc, Batch bt) {
     const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
     if (row >= n) return;
-    xval = boff(xval, bt.xval);
-    wt = boff(wt, bt.par);
-    bias = boff(bias, bt.par);
-    out = boff(out, bt.act);
-    xd_csr = boff(xd_csr, bt.xd);
-    xd_csc = boff(xd_csc, bt.xd);
-    bkeys(keys, bt);
+    xval = boff<kB>(xval, bt.xval);
+    wt = boff<kB>(wt, bt.par);
+    bias = boff<kB>(bias, bt.par);
+    out = boff<kB>(out, bt.act);
+    xd_csr = boff<kB>(xd_csr, bt.xd);
+    xd_csc = boff<kB>(xd_csc, bt.xd);
+    bkeys<kB>(keys, bt);
     const int lane = threadIdx.x & 63;
     const float acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, sc->fwd_ctr + fwd_off, train, keep,
                                         scale, xd_csr, xd_csc, csr2csc);
@@ -243,6 +249,7 @@ struct GcnW {  // pointers into a flat parameter vector (layout in engine.py)
 };
 
 // Y0 = Â H0;  H1d = relu(Y0) ⊙ D1;  H2 = H1d W1ᵀ + b1  (16-padded, zeros past C)
+template <bool kB>
 __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -252,18 +259,18 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    h0 = boff(h0, bt.act);
-    y0 = boff(y0, bt.act);
-    h1d = boff(h1d, bt.act);
-    h2 = boff(h2, bt.act);
-    dmask = boff(dmask, bt.act);
-    w.w1 = boff(w.w1, bt.par);
-    w.b1 = boff(w.b1, bt.par);
-    bkeys(keys, bt);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    h0 = boff<kB>(h0, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    h1d = boff<kB>(h1d, bt.act);
+    h2 = boff<kB>(h2, bt.act);
+    dmask = boff<kB>(dmask, bt.act);
+    w.w1 = boff<kB>(w.w1, bt.par);
+    w.b1 = boff<kB>(w.b1, bt.par);
+    bkeys<kB>(keys, bt);
     // the dropout draw does not depend on the aggregation: issue it first
     const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
                            : 1.f;
@@ -285,6 +292,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
 
 // O = Â H2; P = softmax(O) (over c classes); dO = (P - onehot(y)) ⊙ m / |m|;
 // per-row loss -log P[y] and correctness (argmax == y) where m.
+template <bool kB>
 __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -294,16 +302,16 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    h2 = boff(h2, bt.act);
-    o_out = boff(o_out, bt.act);
-    p_out = boff(p_out, bt.act);
-    d_o = boff(d_o, bt.act);
-    lossrow = boff(lossrow, bt.row);
-    corrrow = boff(corrrow, bt.row);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    h2 = boff<kB>(h2, bt.act);
+    o_out = boff<kB>(o_out, bt.act);
+    p_out = boff<kB>(p_out, bt.act);
+    d_o = boff<kB>(d_o, bt.act);
+    lossrow = boff<kB>(lossrow, bt.row);
+    corrrow = boff<kB>(corrrow, bt.row);
     const float o = agg_row(rp, col, s, ell, h2, row, lane);
     const bool act = lane < c;
     const float m = gmax16(act ? o : -INFINITY);
@@ -341,6 +349,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
 // ---------------------------------------------------------------------------
 
 // dH2 = Â dO;  dY0 = (dH2 W1) ⊙ D1 ⊙ [Y0 > 0].  Outer mode: emit factor (dO, H2).
+template <bool kB>
 __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -352,22 +361,22 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    d_o = boff(d_o, bt.act);
-    y0 = boff(y0, bt.act);
-    dh2 = boff(dh2, bt.act);
-    dy0 = boff(dy0, bt.act);
-    o_in = boff(o_in, bt.act);
-    h2 = boff(h2, bt.act);
-    dmask = boff(dmask, bt.act);
-    U = boff(U, bt.uv);
-    V = boff(V, bt.uv);
-    R = boff(R, bt.row);
-    w.w1 = boff(w.w1, bt.par);
-    bkeys(keys, bt);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    d_o = boff<kB>(d_o, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    dy0 = boff<kB>(dy0, bt.act);
+    o_in = boff<kB>(o_in, bt.act);
+    h2 = boff<kB>(h2, bt.act);
+    dmask = boff<kB>(dmask, bt.act);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
+    w.w1 = boff<kB>(w.w1, bt.par);
+    bkeys<kB>(keys, bt);
     const float g2 = agg_row(rp, col, s, ell, d_o, row, lane);  // zero past c (dO is)
     dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
@@ -578,6 +587,7 @@ __global__ __launch_bounds__(256) void adam_rev_kernel(
 // dH1dbar = dY0bar ⊙ D1 ⊙ [Y0 > 0]
 // dH2bar  = dH1dbar W1ᵀ + H1d ḡW1ᵀ + ḡb1
 // H1dbar_part = dH2 ḡW1
+template <bool kB>
 __global__ __launch_bounds__(256) void rev_a_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -591,27 +601,27 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    dh0bar = boff(dh0bar, bt.act);
-    dy0 = boff(dy0, bt.act);
-    dh0 = boff(dh0, bt.act);
-    y0 = boff(y0, bt.act);
-    h1d = boff(h1d, bt.act);
-    dh2 = boff(dh2, bt.act);
-    dh1dbar = boff(dh1dbar, bt.act);
-    dh2bar = boff(dh2bar, bt.act);
-    h1dbar = boff(h1dbar, bt.act);
-    dmask = boff(dmask, bt.act);
-    w.w1 = boff(w.w1, bt.par);
-    gw1bar = boff(gw1bar, bt.par);
-    gb1bar = boff(gb1bar, bt.par);
-    U = boff(U, bt.uv);
-    V = boff(V, bt.uv);
-    R = boff(R, bt.row);
-    bkeys(keys, bt);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    dh0bar = boff<kB>(dh0bar, bt.act);
+    dy0 = boff<kB>(dy0, bt.act);
+    dh0 = boff<kB>(dh0, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    h1d = boff<kB>(h1d, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    dh1dbar = boff<kB>(dh1dbar, bt.act);
+    dh2bar = boff<kB>(dh2bar, bt.act);
+    h1dbar = boff<kB>(h1dbar, bt.act);
+    dmask = boff<kB>(dmask, bt.act);
+    w.w1 = boff<kB>(w.w1, bt.par);
+    gw1bar = boff<kB>(gw1bar, bt.par);
+    gb1bar = boff<kB>(gb1bar, bt.par);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
+    bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, dh0bar, row, lane);  // dY0bar
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
@@ -639,6 +649,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
 
 // dObar = Â dH2bar.  Factor use 3 (G = dH2bar, Z = dO, Y = dH2, ÂG = dObar).
 // Obar = P ⊙ (ū - P·ū), ū = dObar ⊙ m / |m|   (softmax Jacobian of dO = (P - E) m/|m|)
+template <bool kB>
 __global__ __launch_bounds__(256) void rev_b_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -649,18 +660,18 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    dh2bar = boff(dh2bar, bt.act);
-    d_o = boff(d_o, bt.act);
-    dh2 = boff(dh2, bt.act);
-    p = boff(p, bt.act);
-    obar = boff(obar, bt.act);
-    U = boff(U, bt.uv);
-    V = boff(V, bt.uv);
-    R = boff(R, bt.row);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    dh2bar = boff<kB>(dh2bar, bt.act);
+    d_o = boff<kB>(d_o, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    p = boff<kB>(p, bt.act);
+    obar = boff<kB>(obar, bt.act);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, dh2bar, row, lane);  // dObar
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
@@ -673,6 +684,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
 
 // H2bar = Â Obar.  Factor use 2 (G = Obar, Z = H2, Y = O, ÂG = H2bar).
 // H1dbar = H1dbar_part + H2bar W1;  Y0bar = H1dbar ⊙ D1 ⊙ [Y0 > 0]
+template <bool kB>
 __global__ __launch_bounds__(256) void rev_c_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -684,23 +696,23 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    obar = boff(obar, bt.act);
-    h2 = boff(h2, bt.act);
-    o = boff(o, bt.act);
-    h1dbar_part = boff(h1dbar_part, bt.act);
-    y0 = boff(y0, bt.act);
-    h2bar = boff(h2bar, bt.act);
-    y0bar = boff(y0bar, bt.act);
-    dmask = boff(dmask, bt.act);
-    w.w1 = boff(w.w1, bt.par);
-    U = boff(U, bt.uv);
-    V = boff(V, bt.uv);
-    R = boff(R, bt.row);
-    bkeys(keys, bt);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    obar = boff<kB>(obar, bt.act);
+    h2 = boff<kB>(h2, bt.act);
+    o = boff<kB>(o, bt.act);
+    h1dbar_part = boff<kB>(h1dbar_part, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    h2bar = boff<kB>(h2bar, bt.act);
+    y0bar = boff<kB>(y0bar, bt.act);
+    dmask = boff<kB>(dmask, bt.act);
+    w.w1 = boff<kB>(w.w1, bt.par);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
+    bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, obar, row, lane);  // H2bar (zero past c)
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
@@ -897,6 +909,7 @@ __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1
 
 // dH0 = Â dY0 (+ outer factor (dY0, H0)); block partials of
 // {gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, Σ loss, Σ correct}.
+template <bool kB>
 __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -908,22 +921,22 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    dy0 = boff(dy0, bt.act);
-    dh0 = boff(dh0, bt.act);
-    y0 = boff(y0, bt.act);
-    h0 = boff(h0, bt.act);
-    dh2 = boff(dh2, bt.act);
-    h1d = boff(h1d, bt.act);
-    lossrow = boff(lossrow, bt.row);
-    corrrow = boff(corrrow, bt.row);
-    partials = boff(partials, bt.part);
-    U = boff(U, bt.uv);
-    V = boff(V, bt.uv);
-    R = boff(R, bt.row);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    dy0 = boff<kB>(dy0, bt.act);
+    dh0 = boff<kB>(dh0, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    h0 = boff<kB>(h0, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    h1d = boff<kB>(h1d, bt.act);
+    lossrow = boff<kB>(lossrow, bt.row);
+    corrrow = boff<kB>(corrrow, bt.row);
+    partials = boff<kB>(partials, bt.part);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
     float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
@@ -942,6 +955,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
 
 // H0bar = Â Y0bar (+ factor use 1); block partials of
 // {W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d, b̄0 += Σ H0bar, b̄1 += Σ H2bar}.
+template <bool kB>
 __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -953,22 +967,22 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
-    rp = boff(rp, bt.rp);
-    col = boff(col, bt.col);
-    s = boff(s, bt.row);
-    ell = boff(ell, bt.ell2);
-    y0bar = boff(y0bar, bt.act);
-    h0 = boff(h0, bt.act);
-    y0 = boff(y0, bt.act);
-    h0bar = boff(h0bar, bt.act);
-    dh2 = boff(dh2, bt.act);
-    dh1dbar = boff(dh1dbar, bt.act);
-    h2bar = boff(h2bar, bt.act);
-    h1d = boff(h1d, bt.act);
-    partials = boff(partials, bt.part);
-    U = boff(U, bt.uv);
-    V = boff(V, bt.uv);
-    R = boff(R, bt.row);
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    y0bar = boff<kB>(y0bar, bt.act);
+    h0 = boff<kB>(h0, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    h0bar = boff<kB>(h0bar, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    dh1dbar = boff<kB>(dh1dbar, bt.act);
+    h2bar = boff<kB>(h2bar, bt.act);
+    h1d = boff<kB>(h1d, bt.act);
+    partials = boff<kB>(partials, bt.part);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
     float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
@@ -1064,27 +1078,28 @@ __global__ __launch_bounds__(320) void final_kernel(FinalArgs f, AdamArgs adam,
 // completes (param index f·16 + h).  With f.partials != NULL the grid carries
 // one extra block that runs the final reduction of b0 / W1 / b1 (+ their Adam)
 // concurrently: both only need the kernel that produced d and the partials.
+template <bool kB>
 __global__ __launch_bounds__(256) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
     const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
     float keep, float scale, FinalArgs fin_args, AdamArgs adam, Batch bt) {
-    fin_args.partials = boff(fin_args.partials, bt.part);
-    fin_args.dst = boff(fin_args.dst, bt.par);
-    fin_args.metrics = boff(fin_args.metrics, bt.met);
-    adam.w0 = boff(adam.w0, bt.par);
-    adam.m0 = boff(adam.m0, bt.par);
-    adam.v0 = boff(adam.v0, bt.par);
-    adam.w1 = boff(adam.w1, bt.par);
-    adam.m1 = boff(adam.m1, bt.par);
-    adam.v1 = boff(adam.v1, bt.par);
-    adam.gp = boff(adam.gp, bt.par);
-    adam.wbar = boff(adam.wbar, bt.par);
-    adam.mbar = boff(adam.mbar, bt.par);
-    adam.vbar = boff(adam.vbar, bt.par);
-    adam.gbar = boff(adam.gbar, bt.par);
-    xval = boff(xval, bt.xval);
-    d = boff(d, bt.act);
-    bkeys(keys, bt);
+    fin_args.partials = boff<kB>(fin_args.partials, bt.part);
+    fin_args.dst = boff<kB>(fin_args.dst, bt.par);
+    fin_args.metrics = boff<kB>(fin_args.metrics, bt.met);
+    adam.w0 = boff<kB>(adam.w0, bt.par);
+    adam.m0 = boff<kB>(adam.m0, bt.par);
+    adam.v0 = boff<kB>(adam.v0, bt.par);
+    adam.w1 = boff<kB>(adam.w1, bt.par);
+    adam.m1 = boff<kB>(adam.m1, bt.par);
+    adam.v1 = boff<kB>(adam.v1, bt.par);
+    adam.gp = boff<kB>(adam.gp, bt.par);
+    adam.wbar = boff<kB>(adam.wbar, bt.par);
+    adam.mbar = boff<kB>(adam.mbar, bt.par);
+    adam.vbar = boff<kB>(adam.vbar, bt.par);
+    adam.gbar = boff<kB>(adam.gbar, bt.par);
+    xval = boff<kB>(xval, bt.xval);
+    d = boff<kB>(d, bt.act);
+    bkeys<kB>(keys, bt);
     if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
         const int e1 = threadIdx.x + 256;
         final_pair(fin_args, threadIdx.x, e1 < kRedLen ? e1 : -1, adam, sc);
@@ -1191,6 +1206,13 @@ static inline int mk_batch(const LdsBatch* b, Batch& bt) {
                b->tag_step};
     return b->samples;
 }
+// Launch the batched (kB = true) instantiation only for more than one sample.
+#define LDS_LAUNCH_B(kern, ns, ...)                          \
+    do {                                                      \
+        if ((ns) > 1) hipLaunchKernelGGL(kern<true>, __VA_ARGS__);  \
+        else hipLaunchKernelGGL(kern<false>, __VA_ARGS__);          \
+    } while (0)
+
 static inline bool batch_ok(const LdsBatch* b) {
     return b == nullptr || (b->samples >= 1 && b->samples <= 65535 && (b->ell & 1) == 0);
 }
@@ -1207,7 +1229,7 @@ extern "C" int lds_engine_x_linear(const int* xrp, const int* xcol, const float*
     LDS_CHECK_ARG(xd_csc == nullptr || (xd_csr && csr2csc));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(x_linear_kernel, dim3((n + 3) / 4, ns), dim3(256), 0, (hipStream_t)stream, xrp,
+    LDS_LAUNCH_B(x_linear_kernel, ns, dim3((n + 3) / 4, ns), dim3(256), 0, (hipStream_t)stream, xrp,
                        xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1235,7 +1257,7 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, b1};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(fwd_layer1_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_B(fwd_layer1_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1250,7 +1272,7 @@ extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float*
     LDS_CHECK_ARG(batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(fwd_layer2_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_B(fwd_layer2_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c,
                        bt);
     LDS_RETURN_LAST_ERROR();
@@ -1268,7 +1290,7 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(bwd_layer2_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_B(bwd_layer2_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
                        foff, fwidth, r_assign, dmask, bt);
@@ -1343,7 +1365,7 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(rev_a_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_B(rev_a_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar,
                        h1dbar, mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
                        scale, U, V, ldk, R, foff, dmask, bt);
@@ -1359,7 +1381,7 @@ extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, c
     LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(rev_b_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_B(rev_b_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw,
                        bt);
     LDS_RETURN_LAST_ERROR();
@@ -1378,7 +1400,7 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(rev_c_kernel, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_B(rev_c_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V,
                        ldk, R, foff, cw, dmask, bt);
@@ -1447,7 +1469,7 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)) && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(bwd1_reduce_kernel, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
+    LDS_LAUNCH_B(bwd1_reduce_kernel, ns, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
                        rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow,
                        corrrow, c, partials, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1462,7 +1484,7 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
     LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(rev_d_reduce_kernel, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
+    LDS_LAUNCH_B(rev_d_reduce_kernel, ns, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
                        (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R,
                        foff, dh2, dh1dbar, h2bar, h1d, c, partials, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1504,7 +1526,7 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
     const int blocks = (fin + 3) / 4 + (partials != nullptr ? 1 : 0);
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    hipLaunchKernelGGL(xt_adam_kernel, dim3(blocks, ns), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
+    LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
                        a, bt);
     LDS_RETURN_LAST_ERROR();

@@ -28,18 +28,21 @@ namespace lds {
 // from one θ load inside the block (a loop over graphs) took 41-53 µs against
 // 35 µs here — the loop raised the kernel to 157 VGPRs (occupancy 3 vs 8), and
 // the θ re-read per graph is cheap (MALL-resident).
+template <bool kInj, bool kLoop>
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
-    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step) {
+    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples) {
     __shared__ uint64_t colpart[4][64];
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
-    // batched launches: graph blockIdx.y draws counter + blockIdx.y into its own bit matrix
+    // batched launches: graph blockIdx.y draws counter + blockIdx.y; replica
+    // samples either come from grid.z (one per block) or, with `samples` > 1,
+    // from the loop below over ONE θ tile load (the θ re-read per sample was
+    // the sampler's dominant traffic at 16 samples per GPU)
     counter += blockIdx.y;
-    tag += blockIdx.z * tag_step;
-    bits += ((int64_t)blockIdx.y * gridDim.z + blockIdx.z) * n * words;
     if (counter_base != nullptr) counter += *counter_base;  // device-resident draw counter
+    const int nsamp = kLoop ? samples : (int)gridDim.z;
     const int lane = wave_lane();
     const int wave = threadIdx.x >> 6;
     int a, b;
@@ -56,44 +59,52 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
         const int i = r0 + r;
         th[r] = (i < j && j < n) ? theta[tri_index(i, j, nn)] : -1.0f;  // i < n follows
     }
-    uint64_t colword = 0;
+    const int z0 = kLoop ? 0 : (int)blockIdx.z;
+    const int z1 = kLoop ? samples : z0 + 1;
+#pragma unroll 1
+    for (int z = z0; z < z1; ++z) {
+        const uint32_t tg = tag + (uint32_t)z * tag_step;
+        uint64_t* __restrict__ gb = bits + ((int64_t)blockIdx.y * nsamp + z) * n * words;
+        uint64_t colword = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i0 = r0 + 4 * q;
-        float u[4];
-        if (u_inj != nullptr) {
+        for (int q = 0; q < 4; ++q) {
+            const int i0 = r0 + 4 * q;
+            float u[4];
+            if constexpr (kInj) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = i0 + r;
+                    u[r] = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
+                }
+            } else {
+                philox_quad(k0, k1, tg, counter, (uint32_t)j, (uint32_t)(i0 >> 2), u);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = i0 + r;
-                u[r] = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
-            }
-        } else {
-            philox_quad(k0, k1, tag, counter, (uint32_t)j, (uint32_t)(i0 >> 2), u);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = i0 + r;
-            const float t = th[4 * q + r];
-            // clamp(0, 1) as triu_values_to_symmetric_matrix (src/utils/graph.py:180);
-            // t = -1 marks pairs outside the strict upper triangle
-            const bool e = t >= 0.0f && u[r] < fminf(t, 1.0f);
-            const uint64_t w = __ballot(e);
-            if (i < n) {
-                if (!diag_tile) {
-                    if (lane == 0) bits[(int64_t)i * words + bj] = w;
-                } else if (lane == 0) {
-                    rowword[i - bi * 64] = w;
+                const float t = th[4 * q + r];
+                // clamp(0, 1) as triu_values_to_symmetric_matrix (src/utils/graph.py:180);
+                // t = -1 marks pairs outside the strict upper triangle
+                const bool e = t >= 0.0f && u[r] < fminf(t, 1.0f);
+                const uint64_t w = __ballot(e);
+                if (i < n) {
+                    if (!diag_tile) {
+                        if (lane == 0) gb[(int64_t)i * words + bj] = w;
+                    } else if (lane == 0) {
+                        rowword[i - bi * 64] = w;
+                    }
                 }
+                if (e) colword |= 1ull << (i - bi * 64);
             }
-            if (e) colword |= 1ull << (i - bi * 64);
         }
-    }
-    colpart[wave][lane] = colword;
-    __syncthreads();
-    if (wave == 0 && j < n) {
-        uint64_t out = colpart[0][lane] | colpart[1][lane] | colpart[2][lane] | colpart[3][lane];
-        if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
-        bits[(int64_t)j * words + bi] = out;
+        colpart[wave][lane] = colword;
+        __syncthreads();
+        if (wave == 0 && j < n) {
+            uint64_t out = colpart[0][lane] | colpart[1][lane] | colpart[2][lane] | colpart[3][lane];
+            if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
+            gb[(int64_t)j * words + bi] = out;
+        }
+        if (z + 1 < z1) __syncthreads();  // colpart / rowword are reused by the next sample
     }
 }
 
@@ -246,9 +257,14 @@ extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint
     LDS_CHECK_ARG(words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
-    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles), dim3(256), 0,
-                       (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u);
+    if (u_inject != nullptr)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<true, false>), dim3(ntiles), dim3(256), 0,
+                           (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles), dim3(256), 0,
+                           (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -259,9 +275,9 @@ extern "C" int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, 
     LDS_CHECK_ARG(n > 0 && n <= (1 << 20) && words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
-    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles), dim3(256), 0,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u);
+                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u, 1);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -321,9 +337,15 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
     const int ntiles = nb * (nb + 1) / 2;
     const int graphs = count * samples;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(sample_tiles_kernel, dim3(ntiles, count, samples), dim3(256), 0, st, theta, n,
-                       (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
-                       (const float*)nullptr, bits, words, ntiles, tag_step);
+    // replica samples loop inside the block over one θ tile load
+    if (samples > 1)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true>), dim3(ntiles, count, 1), dim3(256), 0, st, theta, n,
+                           (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
+                           (const float*)nullptr, bits, words, ntiles, tag_step, samples);
+    else
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles, count, 1), dim3(256), 0, st, theta,
+                           n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
+                           (const float*)nullptr, bits, words, ntiles, tag_step, 1);
     hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
                        deg_ws, s);
     hipLaunchKernelGGL(scan_kernel, dim3(1, graphs), dim3(1024), 0, st, deg_ws, n, row_ptr);
