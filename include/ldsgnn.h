@@ -146,6 +146,20 @@ int lds_spmm_norm(const int* row_ptr, const int* col, const float* s, int n,
                   const float* z, int f, int ldz, float* y, int ldy, int beta,
                   void* stream);
 
+/* Long-row form of lds_spmm_norm (dense sampled graphs, ~10^4 neighbours per
+ * row: BASELINE config 5), F = 16 only.  The columns are cut into
+ * lds_spmm_block_count(n) blocks of 1024; a workgroup stages one block of
+ * s⊙Z in LDS and aggregates its rows' segments in that block; the partials
+ * (part_ws: block_count × n × 16 floats, 16-B aligned) are summed in block
+ * order and scaled by s_i.  bptr: n × (block_count + 1) segment starts from
+ * lds_csr_block_ptr (a property of the graph: compute once per sample).
+ * fp32 parity with lds_spmm_norm (different summation order). */
+int lds_spmm_block_count(int n);
+int lds_csr_block_ptr(const int* row_ptr, const int* col, int n, int* bptr, void* stream);
+int lds_spmm_norm_blocked(const int* bptr, const int* col, const float* s, int n,
+                          const float* z, int ldz, float* y, int ldy, int beta,
+                          float* part_ws, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Hypergradient assembly.  Replaces the autograd of
  *   normalize_adjacency_matrix -> straight_through_estimator ->

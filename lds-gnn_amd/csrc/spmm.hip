@@ -65,6 +65,200 @@ static void launch_group(const int* row_ptr, const int* col, const float* s, int
                        col, s, n, z, f, ldz, y, ldy, beta);
 }
 
+// ---------------------------------------------------------------------------
+// Long rows (dense sampled graphs, BASELINE config 5: N = 20 000, θ ~ U(0,1),
+// ~10^4 neighbours per row, 2·10^8 CSR entries = 0.8 GB of column indices per
+// call).  The column-index stream is the only HBM traffic that scales with
+// nnz; the neighbour rows of Z (64 B each at F = 16) are re-read nnz times and
+// must come from on-chip memory.  Z (1.3 MB) fits an XCD's L2 but not one CU's
+// LDS, so the columns are cut into blocks of kBlk rows of s⊙Z (64 KB of LDS):
+//   grid (row tiles, column blocks); a workgroup stages its block once, then
+//   every wave walks its rows' segments inside the block (bptr: segment starts
+//   per (row, block), lds_csr_block_ptr), one neighbour per 4-lane group and
+//   one float4 of the neighbour's row per lane (ds_read_b128), 16 neighbours
+//   per wave-instruction; four xor-shuffle rounds reduce the groups and the
+//   row's block partial (16 floats) goes to P[block][row].
+// lds_spmm_norm_blocked then sums the partials in block order (deterministic)
+// and scales by s_i.  Accumulation order differs from the CSR-order kernel
+// above (blocks, then groups): parity is at fp32 tolerance, not bit-exact.
+// ---------------------------------------------------------------------------
+constexpr int kBlk = 512;       // columns (Z rows) per LDS block: 512 × 80 B = 40 KB (4 workgroups per CU)
+constexpr int kRowsPerWg = 128;  // rows per workgroup tile (16 per wave; measured best of 64/128/256)
+
+__global__ __launch_bounds__(256) void csr_block_ptr_kernel(const int* __restrict__ row_ptr,
+                                                            const int* __restrict__ col, int n, int nb,
+                                                            int blk, int* __restrict__ bptr) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)n * (nb + 1)) return;
+    const int row = (int)(t / (nb + 1)), b = (int)(t % (nb + 1));
+    int lo = row_ptr[row], hi = row_ptr[row + 1];
+    if (b < nb) {  // first position with col >= b·blk (cols ascending)
+        const int key = b * blk;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (col[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+    } else {
+        lo = hi;
+    }
+    bptr[t] = lo;
+}
+
+// Row of the staged block: 16 floats + 4 pad (80 B): consecutive rows start 20
+// banks apart, so the 16 lanes of a ds_read_b128 cycle reading rows j..j+15
+// (a dense segment) hit 64 distinct banks.
+constexpr int kZsStride = 20;
+
+// Cross-lane exchanges without LDS (the ds_bpermute form of __shfl_xor cost as
+// many LDS instructions as the gathers): v_permlane32_swap / v_permlane16_swap
+// (gfx950) pair lanes L and L^32 / L^16; DPP row_mirror pairs i and 15-i,
+// row_half_mirror i and 7-i (both flip the bit that matters: 3, resp. 2);
+// quad_perm does ^1 and ^2.
+__device__ __forceinline__ float xchg32(float v, bool hi) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(hi ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xchg16(float v, bool hi) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(hi ? r[0] : r[1]);
+}
+#define LDS_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xF, 0xF, true))
+
+// 16 per-lane partial sums (features 0..15) -> every lane holds the wave total
+// of feature 8·b5 + 4·b4 + 2·b3 + b2 (b = lane bits): reduce-scatter over lane
+// bits 5..2, then a sum over bits 1..0.  Each step pairs every lane with one
+// lane of the opposite bit (same higher bits), so the partner sets span all
+// 64 lanes; fixed order: deterministic.
+__device__ __forceinline__ float wave_reduce16(float (&a)[16], int lane) {
+    float v8[8], v4[4], v2[2];
+    const bool h32 = lane & 32, h16 = lane & 16, h8 = lane & 8, h4 = lane & 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // lanes < 32 keep features 0-7, the others 8-15
+        const float send = h32 ? a[i] : a[i + 8];
+        const float keep = h32 ? a[i + 8] : a[i];
+        v8[i] = keep + xchg32(send, h32);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float send = h16 ? v8[i] : v8[i + 4];
+        const float keep = h16 ? v8[i + 4] : v8[i];
+        v4[i] = keep + xchg16(send, h16);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const float send = h8 ? v4[i] : v4[i + 2];
+        const float keep = h8 ? v4[i + 2] : v4[i];
+        v2[i] = keep + LDS_DPP(send, 0x140);  // row_mirror: i <-> 15-i
+    }
+    const float send = h4 ? v2[0] : v2[1];
+    float v = (h4 ? v2[1] : v2[0]) + LDS_DPP(send, 0x141);  // row_half_mirror: i <-> 7-i
+    v += LDS_DPP(v, 0x4E);  // quad_perm [2,3,0,1]
+    v += LDS_DPP(v, 0xB1);  // quad_perm [1,0,3,2]
+    return v;
+}
+
+constexpr int kSpmmThreads = 512;  // 8 waves share one staged block
+constexpr int kUnroll = 6;         // index loads per lane per chunk (384 positions: one row segment at config 5)
+
+template <int RPW>
+__global__ __launch_bounds__(kSpmmThreads) void spmm_blocked_kernel(
+    const int* __restrict__ bptr, int nb, const int* __restrict__ col, const float* __restrict__ s, int n,
+    const float* __restrict__ z, int ldz, float* __restrict__ part) {
+    __shared__ float zs[kBlk * kZsStride];  // row j: s_j · Z[c0 + j][0..15], 4 pad floats
+    const int b = blockIdx.y;
+    const int c0 = b * kBlk;
+    const int rows_here = min(kBlk, n - c0);
+    for (int e = threadIdx.x; e < rows_here * 4; e += kSpmmThreads) {
+        const int j = e >> 2, q = e & 3;
+        const float4 v = *reinterpret_cast<const float4*>(z + (int64_t)(c0 + j) * ldz + 4 * q);
+        const float sj = s[c0 + j];
+        *reinterpret_cast<float4*>(zs + j * kZsStride + 4 * q) = make_float4(sj * v.x, sj * v.y, sj * v.z, sj * v.w);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int kWaves = kSpmmThreads / 64;
+    constexpr int kRowsW = (RPW + kWaves - 1) / kWaves;  // rows per wave: row0 + wave + kWaves·k
+    static_assert(kRowsW <= 64, "one bptr pair per lane");
+    const int row0 = blockIdx.x * RPW + wave;
+    // every segment bound of the wave's rows in one load (lane k: row k), so
+    // the index loads of row k+1 never wait on a bptr round trip
+    int rb = 0, re = 0;
+    if (lane < kRowsW) {
+        const int row = row0 + kWaves * lane;
+        if (row < n && lane * kWaves + wave < RPW) {
+            rb = bptr[(int64_t)row * (nb + 1) + b];
+            re = bptr[(int64_t)row * (nb + 1) + b + 1];
+        }
+    }
+    auto load_chunk = [&](int p0, int end, int (&jj)[kUnroll]) {
+#pragma unroll
+        for (int e = 0; e < kUnroll; ++e) {
+            const int p = p0 + lane + 64 * e;
+            jj[e] = p < end ? col[p] - c0 : -1;
+        }
+    };
+    float a[16];
+    auto accumulate = [&](const int (&jj)[kUnroll]) {
+#pragma unroll
+        for (int e = 0; e < kUnroll; ++e) {
+            if (jj[e] >= 0) {
+                const float4* zr = reinterpret_cast<const float4*>(zs + jj[e] * kZsStride);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = zr[q];
+                    a[4 * q] += v.x;
+                    a[4 * q + 1] += v.y;
+                    a[4 * q + 2] += v.z;
+                    a[4 * q + 3] += v.w;
+                }
+            }
+        }
+    };
+    int beg = __builtin_amdgcn_readlane(rb, 0), end = __builtin_amdgcn_readlane(re, 0);
+    int cur[kUnroll];
+    load_chunk(beg, end, cur);
+    for (int k = 0; k < kRowsW; ++k) {
+        const int row = row0 + kWaves * k;
+        if (row >= n || k * kWaves + wave >= RPW) break;
+        // next row's first chunk in flight during this row's LDS reads
+        const int nbeg = k + 1 < kRowsW ? __builtin_amdgcn_readlane(rb, k + 1) : 0;
+        const int nend = k + 1 < kRowsW ? __builtin_amdgcn_readlane(re, k + 1) : 0;
+        int nxt[kUnroll];
+        load_chunk(nbeg, nend, nxt);
+#pragma unroll
+        for (int f = 0; f < 16; ++f) a[f] = 0.f;
+        accumulate(cur);
+        for (int p0 = beg + 64 * kUnroll; p0 < end; p0 += 64 * kUnroll) {  // long segments
+            int jj[kUnroll];
+            load_chunk(p0, end, jj);
+            accumulate(jj);
+        }
+        const float t = wave_reduce16(a, lane);
+        // lane bits 5..2 = (b5, b4, b3, b2) select feature 8·b5 + 4·b4 + 2·b3 + b2
+        const int f = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+        if ((lane & 3) == 0) part[((int64_t)b * n + row) * 16 + f] = t;
+        beg = nbeg;
+        end = nend;
+#pragma unroll
+        for (int e = 0; e < kUnroll; ++e) cur[e] = nxt[e];
+    }
+}
+
+// Y[i] (= or +=) s_i · Σ_b P[b][i]  (16 lanes per row, blocks in order)
+__global__ __launch_bounds__(256) void spmm_blocked_final_kernel(const float* __restrict__ part, int nb,
+                                                                 const float* __restrict__ s, int n,
+                                                                 float* __restrict__ y, int ldy, int beta) {
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int f = threadIdx.x & 15;
+    if (row >= n) return;
+    float acc = 0.f;
+    for (int b = 0; b < nb; ++b) acc += part[((int64_t)b * n + row) * 16 + f];
+    float* out = y + (int64_t)row * ldy + f;
+    const float v = s[row] * acc;
+    *out = beta ? *out + v : v;
+}
+
 }  // namespace lds
 
 using namespace lds;
@@ -81,5 +275,32 @@ extern "C" int lds_spmm_norm(const int* row_ptr, const int* col, const float* s,
     else if (f <= 16) launch_group<16>(row_ptr, col, s, n, z, f, ldz, y, ldy, beta, st);
     else if (f <= 32) launch_group<32>(row_ptr, col, s, n, z, f, ldz, y, ldy, beta, st);
     else launch_group<64>(row_ptr, col, s, n, z, f, ldz, y, ldy, beta, st);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_spmm_block_count(int n) { return (n + kBlk - 1) / kBlk; }
+
+extern "C" int lds_csr_block_ptr(const int* row_ptr, const int* col, int n, int* bptr, void* stream) {
+    LDS_CHECK_ARG(row_ptr != nullptr && col != nullptr && bptr != nullptr && n > 0);
+    const int nb = (n + kBlk - 1) / kBlk;
+    const int64_t total = (int64_t)n * (nb + 1);
+    hipLaunchKernelGGL(csr_block_ptr_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, row_ptr, col, n, nb, kBlk, bptr);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_spmm_norm_blocked(const int* bptr, const int* col, const float* s, int n,
+                                     const float* z, int ldz, float* y, int ldy, int beta, float* part_ws,
+                                     void* stream) {
+    LDS_CHECK_ARG(bptr != nullptr && col != nullptr && s != nullptr && z != nullptr && y != nullptr);
+    LDS_CHECK_ARG(part_ws != nullptr && n > 0 && ldz >= 16 && (ldz & 3) == 0 && ldy >= 16);
+    LDS_CHECK_ARG((((uintptr_t)z) & 15) == 0 && (((uintptr_t)part_ws) & 15) == 0);
+    const int nb = (n + kBlk - 1) / kBlk;
+    LDS_CHECK_ARG(nb <= 65535);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(spmm_blocked_kernel<kRowsPerWg>, dim3((n + kRowsPerWg - 1) / kRowsPerWg, nb),
+                       dim3(kSpmmThreads), 0, st, bptr, nb, col, s, n, z, ldz, part_ws);
+    hipLaunchKernelGGL(spmm_blocked_final_kernel, dim3((n + 15) / 16), dim3(256), 0, st, part_ws, nb, s, n,
+                       y, ldy, beta);
     LDS_RETURN_LAST_ERROR();
 }

@@ -39,6 +39,9 @@ SIGNATURES = {
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],
     "lds_spmm_norm": [P, P, P, c_int, P, c_int, c_int, P, c_int, c_int, P],
+    "lds_spmm_block_count": [c_int],
+    "lds_csr_block_ptr": [P, P, c_int, P, P],
+    "lds_spmm_norm_blocked": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
@@ -147,6 +150,8 @@ timer = KernelTimer()
 
 
 def call(name: str, *args) -> None:
+    if name not in SIGNATURES:  # an untyped ctypes call would truncate pointers to int
+        raise KeyError(f"{name} has no ctypes signature in ldsgnn._native.SIGNATURES")
     if name in timer.names:
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)

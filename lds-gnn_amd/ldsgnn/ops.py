@@ -93,14 +93,43 @@ class CsrGraph:
         """Undirected off-diagonal edges."""
         return (self.nnz() - self.n) // 2
 
-    def spmm(self, z: torch.Tensor, out: Optional[torch.Tensor] = None, beta: int = 0) -> torch.Tensor:
-        """Y = Â·Z (lds_spmm_norm); no autograd."""
+    # mean entries per row from which the column-blocked LDS kernel
+    # (lds_spmm_norm_blocked) replaces the row-group kernel (F = 16 only)
+    LONG_ROW_DEGREE = 256
+
+    def long_rows(self) -> bool:
+        return self.n >= 1024 and self.nnz() >= self.LONG_ROW_DEGREE * self.n
+
+    def _block_ptr(self) -> torch.Tensor:
+        bp = getattr(self, "_bptr", None)
+        if bp is None:
+            nb = nat.lib.lds_spmm_block_count(self.n)
+            bp = torch.empty(self.n * (nb + 1), dtype=torch.int32, device=self.device)
+            nat.call("lds_csr_block_ptr", nat.ptr(self.row_ptr), nat.ptr(self.col), self.n, nat.ptr(bp),
+                     _stream(self.s))
+            self._bptr = bp
+        return bp
+
+    def spmm(self, z: torch.Tensor, out: Optional[torch.Tensor] = None, beta: int = 0,
+             blocked: Optional[bool] = None) -> torch.Tensor:
+        """Y = Â·Z; no autograd.  Row-group kernel (lds_spmm_norm), or for long
+        rows at F = 16 the column-blocked kernel (lds_spmm_norm_blocked;
+        `blocked` forces the choice)."""
         z = _f32c(z, "spmm")
         if z.dim() != 2 or z.size(0) != self.n:
             raise ValueError(f"spmm: Z must be {self.n}×F, got {tuple(z.shape)}")
         f = z.size(1)
         if out is None:
             out = torch.empty((self.n, f), dtype=torch.float32, device=z.device)
+        use_blocked = (f == 16 and self.long_rows()) if blocked is None else blocked
+        if use_blocked:
+            if f != 16 or z.stride(0) % 4 or z.data_ptr() % 16:
+                raise ValueError("blocked spmm: F = 16, 16-byte aligned rows")
+            nb = nat.lib.lds_spmm_block_count(self.n)
+            part = torch.empty((nb, self.n, 16), dtype=torch.float32, device=z.device)
+            nat.call("lds_spmm_norm_blocked", nat.ptr(self._block_ptr()), nat.ptr(self.col), nat.ptr(self.s),
+                     self.n, nat.ptr(z), z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(part), _stream(z))
+            return out
         nat.call("lds_spmm_norm", nat.ptr(self.row_ptr), nat.ptr(self.col), nat.ptr(self.s), self.n,
                  nat.ptr(z), f, z.stride(0), nat.ptr(out), out.stride(0), beta, _stream(z))
         return out

@@ -213,3 +213,24 @@ def test_theta_grad_mfma_matches_valu_and_sgd_mode(device):
              nat.ptr(sc), nat.stream_of(u.device))
     assert torch.equal(gout, a)
     assert torch.allclose(th2, (theta - 0.3 * a).clamp(0, 1), atol=1e-6)
+
+
+@pytest.mark.parametrize("n,high", [(100, 1.0), (1500, 1.0), (2600, 0.5), (3000, 0.02)])
+def test_spmm_blocked_vs_dense(device, n, high):
+    """Column-blocked LDS SpMM (long rows, config 5's kernel) vs the dense fp64
+    product: a graph smaller than one block, a complete graph (segments longer
+    than one index chunk), dense random rows, and sparse rows (mostly empty
+    segments).  Summation order differs from the CSR order: fp32 tolerance."""
+    g = torch.Generator().manual_seed(n)
+    theta = torch.rand(n * (n + 1) // 2, generator=g) * high
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n), track_grad=False)
+    z = torch.randn(n, 16, generator=g).to(device)
+    y_blk = graph.spmm(z, blocked=True).cpu().double()
+    y_row = graph.spmm(z, blocked=False).cpu().double()
+    ref = graph.normalized_dense().cpu().double() @ z.cpu().double()
+    scale = ref.abs().max()
+    assert float((y_blk - ref).abs().max() / scale) < RTOL
+    assert float((y_row - ref).abs().max() / scale) < RTOL
+    out = torch.ones(n, 16, device=device)
+    graph.spmm(z, out=out, beta=1, blocked=True)
+    assert float((out.cpu().double() - ref - 1.0).abs().max() / scale) < RTOL
