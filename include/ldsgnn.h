@@ -240,6 +240,20 @@ int lds_dropout(const float* x, int ldx, float* y, int ldy, int rows, int cols,
                 uint32_t counter, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * θ pre-training (Pretrainer.train_step, src/trainers/pretrainer.py:68-81, used
+ * when OuterProblemTrainer(pretrain=True), src/trainers/outer.py:54-55,107-109):
+ * one epoch of weighted BCE between P = triu_values_to_symmetric_matrix(θ)
+ * and the training adjacency T (train_bits: n × words uint64 bitmask, the
+ * sampler's layout), W = 1 + T·(pos_weight - 1), mean over n², followed by
+ * torch.optim.Adam (lr, betas, eps; no weight decay) on the packed θ, in one
+ * pass.  `step` = the Adam step count after this update (>= 1).
+ * loss_rows[i] receives row i's Σ w·bce terms (loss = Σ_i loss_rows[i] / n²).
+ * ------------------------------------------------------------------------- */
+int lds_pretrain_step(float* theta, int n, const uint64_t* train_bits, int words, float pos_weight,
+                      float* exp_avg, float* exp_avg_sq, int step, double lr, double beta1,
+                      double beta2, double eps, float* loss_rows, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Fused engine (lds-gnn_amd/csrc/engine.hip; orchestrated by
  * lds-gnn_amd/ldsgnn/engine.py).  Replaces, for the LDS configuration, the
  * autograd work of

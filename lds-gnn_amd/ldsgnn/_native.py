@@ -49,6 +49,8 @@ SIGNATURES = {
     "lds_slot_factors": [P, c_int, P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, P, c_int, P,
                          c_int, P, c_int, P],
     "lds_sgd_clamp": [P, P, c_float, c_int64, P],
+    "lds_pretrain_step": [P, c_int, P, c_int, c_float, P, P, c_int, ctypes.c_double, ctypes.c_double,
+                          ctypes.c_double, ctypes.c_double, P, P],
     "lds_dropout": [P, c_int, P, c_int, c_int, c_int, c_float, c_float, c_uint64, c_uint32, c_uint32,
                     P],
     # fused engine (csrc/engine.hip)

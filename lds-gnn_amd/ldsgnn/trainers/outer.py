@@ -5,8 +5,9 @@
 the outer graph and every unrolled inner step since the last detach.  The
 θ-gradient arrives through the sampled graphs' tokens (ldsgnn.ops), assembled
 by the lds_theta_grad HIP kernel; then SGD → StepLR → clamp as the reference.
-Regularisation / refinement / pre-training branches are out of scope
-(defaults off for LDS, src/trainers/outer.py:121-129 — pretrain is "next").
+pretrain=True runs the fused θ pre-training (ldsgnn.trainers.pretrainer) as
+the reference does (src/trainers/outer.py:54-55,107-109); regularisation /
+refinement are out of scope (defaults off for LDS, src/trainers/outer.py:121-129).
 """
 from __future__ import annotations
 
@@ -36,8 +37,6 @@ class OuterProblemTrainer:
                  grad_reducer: Callable = None):
         if regularize:
             raise NotImplementedError("graph regularisation is outside the LDS hot path (default off)")
-        if pretrain:
-            raise NotImplementedError("θ pre-training is not implemented yet (SURVEY §8(f)3)")
         self.lr_decay = lr_decay
         self.lr_decay_step_size = lr_decay_step_size
         self.dataset = data
@@ -55,6 +54,16 @@ class OuterProblemTrainer:
         # backward and before the SGD step — e.g. ldsgnn.replicas.allreduce_mean
         # to average θ.grad over ranks (one RCCL all-reduce per hyper step).
         self.grad_reducer = grad_reducer
+        self.pretrain_results = None
+        if pretrain:
+            self.pretrain_model()
+
+    def pretrain_model(self, **kwargs) -> None:
+        """src/trainers/outer.py:107-109 with the PretrainerFactory defaults
+        (lr 0.01, Adam, patience 20, max 400 epochs)."""
+        from .pretrainer import Pretrainer
+        self.pretrainer = Pretrainer(self.model, self.dataset, **kwargs)
+        self.pretrain_results = self.pretrainer.train()
 
     def train_step(self, gcn_predict_fct: Callable, mask: Tensor = None,
                    retain_graph: bool = True) -> Metrics:

@@ -479,3 +479,18 @@ def replica_hyper_step(problems: List["LdsProblem"]) -> Tuple[List[Tuple[float, 
     for p in problems:
         p.apply_hyper_update(g)
     return [(r[0], r[1]) for r in res], g
+
+
+def pretrain_epoch_dense(theta: torch.Tensor, train_adj: torch.Tensor, optimizer: torch.optim.Optimizer) -> float:
+    """One Pretrainer.train_step (src/trainers/pretrainer.py:68-81) restated
+    densely: P = triu_values_to_symmetric_matrix(θ), weighted BCE against the
+    training adjacency, backward, optimizer.step().  θ: the Parameter the
+    optimizer holds."""
+    optimizer.zero_grad()
+    p = triu_values_to_symmetric_matrix(theta)
+    pos_weight = (train_adj.numel() - train_adj.sum().item()) / train_adj.sum().item()
+    weight = (train_adj * (pos_weight - 1)) + 1.0
+    loss = F.binary_cross_entropy(p, train_adj, weight=weight)
+    loss.backward()
+    optimizer.step()
+    return loss.item()

@@ -234,3 +234,30 @@ def test_spmm_blocked_vs_dense(device, n, high):
     out = torch.ones(n, 16, device=device)
     graph.spmm(z, out=out, beta=1, blocked=True)
     assert float((out.cpu().double() - ref - 1.0).abs().max() / scale) < RTOL
+
+
+def test_pretrain_step_vs_oracle(device):
+    """Fused pre-training epoch (weighted BCE + clamp/symmetrisation backward +
+    Adam on packed θ, one launch) against the reference's dense restatement
+    (oracle.pretrain_epoch_dense with torch.optim.Adam) over 6 epochs."""
+    from oracle import lds_oracle as O
+    from ldsgnn.trainers.pretrainer import edges_to_bits
+    n = 150
+    g = torch.Generator().manual_seed(21)
+    theta0 = torch.rand(n * (n + 1) // 2, generator=g) * 1.2 - 0.1  # some entries outside [0, 1]
+    a = (torch.rand(n, n, generator=g) < 0.05).float().triu(1)
+    t = a + a.t()
+    th_o = torch.nn.Parameter(theta0.clone())
+    opt = torch.optim.Adam([th_o], lr=0.01)
+    th_p = theta0.clone().to(device)
+    m, v = torch.zeros_like(th_p), torch.zeros_like(th_p)
+    bits = edges_to_bits(t.nonzero().t(), n, device)
+    pos_weight = float(np.float32((n * n - t.sum().item()) / t.sum().item()))
+    rows = torch.zeros(n, device=device)
+    for step in range(1, 7):
+        lo = O.pretrain_epoch_dense(th_o, t, opt)
+        nat.call("lds_pretrain_step", nat.ptr(th_p), n, nat.ptr(bits), bits.size(1), pos_weight, nat.ptr(m),
+                 nat.ptr(v), step, 0.01, 0.9, 0.999, 1e-8, nat.ptr(rows), nat.stream_of(th_p.device))
+        lp = float(rows.double().sum().item()) / (n * n)
+        assert abs(lp - lo) <= 1e-5 * abs(lo), (step, lp, lo)
+        assert float((th_p.cpu() - th_o.detach()).abs().max()) < 1e-5, step

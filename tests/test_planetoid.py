@@ -70,3 +70,27 @@ def test_reader_executes_nothing():
         materialize(node)
     with pytest.raises(ValueError):  # opcodes outside the data subset
         read_pickle_data(b"\x80\x04\x95\x05\x00\x00\x00\x00\x00\x00\x00\x8c\x01a\x94.".replace(b"\x8c\x01a\x94", b"\x93"))
+
+
+def test_pretrain_split_and_bitmask():
+    """GAE.split_edges restatement: 5 % / 10 % positives, equal negatives,
+    disjoint, negatives are non-edges; the training adjacency's bitmask uses
+    the sampler's layout (bit j%64 of word j/64)."""
+    from ldsgnn.trainers.pretrainer import edges_to_bits, split_edges
+    d = load_planetoid_npz("cora")
+    sp = split_edges(d.dense_adj, generator=torch.Generator().manual_seed(0))
+    e = 5278
+    assert sp["val_pos"].shape[1] == e * 5 // 100 and sp["test_pos"].shape[1] == e * 10 // 100
+    assert sp["train_pos"].shape[1] == 2 * (e - e * 5 // 100 - e * 10 // 100)
+    assert sp["val_neg"].shape == sp["val_pos"].shape and sp["test_neg"].shape == sp["test_pos"].shape
+    for k in ("val_neg", "test_neg"):
+        assert float(d.dense_adj[sp[k][0], sp[k][1]].sum()) == 0.0
+    held = set(map(tuple, torch.cat([sp["val_pos"], sp["test_pos"]], 1).t().tolist()))
+    train = set(map(tuple, sp["train_pos"].t().tolist()))
+    assert not (held & train)
+    n = 130
+    a = torch.rand(n, n, generator=torch.Generator().manual_seed(1)) < 0.1
+    b = edges_to_bits(a.nonzero().t(), n, "cpu").numpy().view(np.uint64)
+    cols = np.arange(n)
+    dec = ((b[:, cols // 64] >> (cols % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)
+    assert np.array_equal(dec, a.numpy())
