@@ -107,19 +107,20 @@ int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
                              const int* row_ptr, int* col, int64_t col_capacity,
                              int* overflow, const float* s, int* ell, void* stream);
 
-/* Batched form for a window of graphs drawn from the same θ: graph g
- * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
- * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
- * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·32.  Four launches
- * for all `count` graphs. */
 /* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
  * b < samples, is draw counter *counter_base + counter_offset + g with tag
- * tag + b·tag_step, stored as graph g·samples + b of the batch arrays. */
+ * tag + b·tag_step, stored as graph g·samples + b of the batch arrays (one
+ * θ tile load per block serves all samples). */
 int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                             uint32_t tag_step, const uint32_t* counter_base,
                             uint32_t counter_offset, int count, int samples, uint64_t* bits,
                             int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
                             float* s, int* ell, void* stream);
+/* Batched form for a window of graphs drawn from the same θ: graph g
+ * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
+ * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
+ * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·32.  Four launches
+ * for all `count` graphs. */
 int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
                       const uint32_t* counter_base, uint32_t counter_offset, int count,
                       uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,

@@ -38,7 +38,7 @@ PUBLISHED = {("lds", "cora"): (84.2, 0.5), ("lds", "citeseer"): (74.0, 0.5),
              ("gcn", "cora"): (81.2, 0.4), ("gcn", "citeseer"): (70.8, 0.5)}
 
 
-def run_lds(dataset, seed, device, pretrain=True):
+def run_lds(dataset, seed, device, pretrain=True, tau=5):
     torch.manual_seed(seed)
     np.random.seed(seed)
     ldsgnn.rng.manual_seed(seed, 0)
@@ -62,7 +62,7 @@ def run_lds(dataset, seed, device, pretrain=True):
     def progress(name, value, step=None):  # outer-epoch heartbeat (keeps long runs visibly alive)
         if name == "loss.val.empirical":
             print(f"  seed {seed} step {steps['inner']} {name}={value:.4f}", file=sys.stderr, flush=True)
-    runner.train(patience=20, hyper_gradient_interval=5, sacred_runner=progress)
+    runner.train(patience=20, hyper_gradient_interval=tau, sacred_runner=progress)
     res = runner.evaluate()
     res["inner_steps"] = steps["inner"]
     res["pretrain"] = outer.pretrain_results
@@ -104,6 +104,7 @@ def main():
     ap.add_argument("--seeds", type=int, default=5)
     ap.add_argument("--seed0", type=int, default=597905255 % (2 ** 31))
     ap.add_argument("--no-pretrain", action="store_true")
+    ap.add_argument("--tau", type=int, default=5)
     args = ap.parse_args()
     device = torch.device("cuda:0")
     accs = []
@@ -111,7 +112,7 @@ def main():
         seed = args.seed0 + k
         t0 = time.time()
         if args.model == "lds":
-            res = run_lds(args.dataset, seed, device, pretrain=not args.no_pretrain)
+            res = run_lds(args.dataset, seed, device, pretrain=not args.no_pretrain, tau=args.tau)
         else:
             res = run_gcn(args.dataset, seed, device)
         res.update(seed=seed, seconds=time.time() - t0, dataset=args.dataset, model=args.model)
