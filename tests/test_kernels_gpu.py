@@ -261,3 +261,43 @@ def test_pretrain_step_vs_oracle(device):
         lp = float(rows.double().sum().item()) / (n * n)
         assert abs(lp - lo) <= 1e-5 * abs(lo), (step, lp, lo)
         assert float((th_p.cpu() - th_o.detach()).abs().max()) < 1e-5, step
+
+
+@pytest.mark.parametrize("n,k,mode", [(300, 520, 0), (129, 1030, 1), (257, 600, 2), (64, 512, 0)])
+def test_theta_grad_ex_wide_k(device, n, k, mode):
+    """lds_theta_grad_ex at wide k (the 128×128-tile kernel, replica samples):
+    R stacked as S rows of n (ldr_col = n), gscale = 1/S, modes grad =, +=,
+    and the fused SGD + clamp, vs the dense fp64 formula."""
+    S = 3
+    g = torch.Generator().manual_seed(n + k)
+    u = torch.randn(n, k, generator=g)
+    v = torch.randn(n, k, generator=g)
+    r = torch.randn(S, n, generator=g)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    theta[::5] = 1.25
+    gs = float(np.float32(1.0) / np.float32(S))
+    ud, vd, rd = u.double(), v.double(), r.double().sum(0)
+    m = gs * (ud @ vd.t() + vd @ ud.t() + rd[:, None] + rd[None, :])
+    iu = torch.triu_indices(n, n)
+    ref = m[iu[0], iu[1]]
+    ref[iu[0] == iu[1]] = 0.0
+    ref[(theta.double() < 0) | (theta.double() > 1)] = 0.0
+    base = torch.randn(n * (n + 1) // 2, generator=g)
+    grad = base.clone().to(device)
+    th = theta.clone().to(device)
+    lr = 0.05
+    scal = torch.zeros(32, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(lr)
+    ud_, vd_, rd_ = u.to(device), v.to(device), r.to(device)  # keep the device copies alive across the call
+    nat.call("lds_theta_grad_ex", nat.ptr(ud_), nat.ptr(vd_), k, k, nat.ptr(rd_), 1, n, S, nat.ptr(th), n,
+             nat.ptr(grad), mode, nat.ptr(scal), gs, nat.stream_of(th.device))
+    torch.cuda.synchronize()
+    tol = 1e-5 * float(ref.abs().max())
+    if mode == 0:
+        assert float((grad.cpu().double() - ref).abs().max()) < tol
+    elif mode == 1:
+        assert float((grad.cpu().double() - base.double() - ref).abs().max()) < tol
+    else:
+        assert float((grad.cpu().double() - ref).abs().max()) < tol
+        want = (theta.double() - lr * ref).clamp(0, 1)
+        assert float((th.cpu().double() - want).abs().max()) < 1e-5
