@@ -49,7 +49,12 @@ def build(args, rank, device):
     from ldsgnn.trainers.outer import OuterProblemTrainer
     from ldsgnn.utils.graph import split_mask
 
-    data = knn_init(make_dataset(args.dataset, seed=args.seed), k=10)
+    data = make_dataset(args.dataset, seed=args.seed)
+    if args.dataset == "synthetic20k":  # config 5: dense θ_ij ~ U(0, 1) i.i.d. (seed 20000), no kNN graph
+        g = torch.Generator(device=device).manual_seed(20000)
+        data.dense_adj = torch.rand((data.num_nodes, data.num_nodes), generator=g, device=device)
+    else:
+        data = knn_init(data, k=10)
     np.random.seed(args.seed)
     data.val_mask, opt_mask = split_mask(data.val_mask, 0.5, shuffle=True)
     data = data.to(device)
@@ -103,12 +108,14 @@ KERNEL_SYMBOL = {"lds_theta_grad_ex": "lds::theta_grad_mfma_kernel", "lds_theta_
 PMC_RECORD = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 
-def pmc_traffic(kernel, use_engine, world):
+def pmc_traffic(kernel, use_engine, world, args):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
     PMC record (tools/gpu_pmc.sh + tools/pmc_summary.py: 2 x FETCH_SIZE +
     WRITE_SIZE, separate passes, gfx950 read correction), measured on this
-    default workload; None for any other configuration."""
-    if not (use_engine and world == 1 and kernel == "lds_theta_grad_sgd") or not os.path.exists(PMC_RECORD):
+    default workload (Cora-shaped, S = 1, τ = 5); None for any other."""
+    default = args.dataset == "cora" and args.samples == 1 and args.tau == 5
+    if not (default and use_engine and world == 1 and kernel == "lds_theta_grad_sgd") or \
+            not os.path.exists(PMC_RECORD):
         return None, None
     with open(PMC_RECORD) as f:
         rec = json.load(f).get(KERNEL_SYMBOL[kernel])
@@ -241,7 +248,7 @@ def main():
         g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
         nnz = g.nnz()
     tri = n * (n + 1) // 2
-    if args.kernel == "lds_spmm_norm":
+    if args.kernel in ("lds_spmm_norm", "lds_spmm_norm_blocked"):
         f = 16
         algo = 4 * (n + 1) + 4 * nnz + 4 * n + 8 * n * f
         achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
@@ -268,7 +275,7 @@ def main():
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None}
     roof.update(kernel=args.kernel, avg_us=ksum["avg_us"], launches=ksum["launches"])
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.kernel, use_engine, world)
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.kernel, use_engine, world, args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -282,11 +289,15 @@ def main():
             "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": f"synthetic {args.dataset}-shaped (N={n}, F_in={data.num_features}, "
-                    f"C={data.num_classes}), kNN-initialised theta",
-            "config": {"workload": f"{args.dataset}-lds-knn-init-S{args.samples}-tau{args.tau}", "path": args.path, "nodes": n,
+                    f"C={data.num_classes}), " + ("theta ~ U(0,1)" if args.dataset == "synthetic20k"
+                                                  else "kNN-initialised theta"),
+            "config": {"workload": f"{args.dataset}-lds-" + ("uniform" if args.dataset == "synthetic20k" else
+                                                               "knn-init") + f"-S{args.samples}-tau{args.tau}", "path": args.path, "nodes": n,
                        "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
-                       "sampled_nnz": nnz, "replicas_in_sync": in_sync},
+                       "sampled_nnz": nnz, "replicas_in_sync": in_sync,
+                       "aggregation": ("column-blocked LDS SpMM pre-pass" if use_engine and eng.long_rows
+                                       else "in-kernel CSR")},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

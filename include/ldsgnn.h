@@ -283,6 +283,12 @@ int lds_engine_scalars_size(void);
  * replica tags tag_x / tag_h + b·tag_step.  Shared: X, labels, masks, θ, the
  * scalars (every replica advances them identically) and the Adam table.
  * batch == NULL (or samples == 1) is the single-replica launch.
+ *
+ * `agg` (the aggregating entry points: fwd_layer1/2, bwd_layer2, bwd1_reduce,
+ * rev_a..c, rev_d_reduce): NULL = aggregate Â·Z from the CSR inside the
+ * kernel (short rows); non-NULL = read the precomputed Â·Z (n × 16, same
+ * batching as the activations) — long rows (config 5), where
+ * lds_spmm_norm_blocked runs as a pre-pass.
  *   act : n×16 activation / adjoint arrays      row : n-vectors (s, R, loss rows)
  *   rp  : row_ptr (n+1)   col : CSR capacity     ell : ELL head (n·32 int32)
  *   par : flat parameter vectors (w, m, v, g', adjoints)
@@ -326,13 +332,13 @@ int lds_engine_fwd_layer1(const int* rp, const int* col, const float* s, const i
                           const float* h0, float* y0, float* h1d, float* h2,
                           const float* w1, const float* b1, int c, uint64_t seed,
                           uint32_t tag_h, const void* scalars, int fwd_off, int train,
-                          float keep, float scale, float* dmask, const LdsBatch* batch, void* stream);
+                          float keep, float scale, float* dmask, const float* agg, const LdsBatch* batch, void* stream);
 /* O = ÂH2; P = softmax(O); dO = (P - onehot) ⊙ mask · inv_count; per-row
  * NLL and correctness where mask. */
 int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* h2, float* o, float* p, float* d_o,
                           const int* label, const uint8_t* mask, float inv_count,
-                          float* lossrow, float* corrrow, int c, const LdsBatch* batch, void* stream);
+                          float* lossrow, float* corrrow, int c, const float* agg, const LdsBatch* batch, void* stream);
 /* dH2 = ÂdO; dY0 = (dH2 W1) ⊙ dropout' ⊙ relu'.  U != NULL: emit the outer
  * graph's factor (dO, H2) at columns [foff, foff + fwidth); r_assign != 0
  * writes R (first emitter of a window) instead of accumulating into it. */
@@ -342,7 +348,7 @@ int lds_engine_bwd_layer2(const int* rp, const int* col, const float* s, const i
                           const void* scalars, int fwd_off, int train, float keep,
                           float scale, const float* o, const float* h2, float* U,
                           float* V, int ldk, float* R, int foff, int fwidth,
-                          int r_assign, const float* dmask, const LdsBatch* batch, void* stream);
+                          int r_assign, const float* dmask, const float* agg, const LdsBatch* batch, void* stream);
 /* dH0 = ÂdY0.  U != NULL: emit the outer graph's factor (dY0, H0). */
 int lds_engine_bwd_layer1(const int* rp, const int* col, const float* s, const int* ell, int n,
                           const float* dy0, float* dh0, const float* y0,
@@ -376,19 +382,19 @@ int lds_engine_rev_a(const int* rp, const int* col, const float* s, const int* e
                      float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, const float* dmask,
-                     const LdsBatch* batch, void* stream);
+                     const float* agg, const LdsBatch* batch, void* stream);
 int lds_engine_rev_b(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* dh2bar, const float* d_o, const float* dh2,
                      const float* p, const uint8_t* mask, float inv_count, int c,
                      float* obar, float* U, float* V, int ldk, float* R, int foff,
-                     int cw, const LdsBatch* batch, void* stream);
+                     int cw, const float* agg, const LdsBatch* batch, void* stream);
 int lds_engine_rev_c(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* obar, const float* h2, const float* o,
                      const float* h1dbar_part, const float* y0, const float* w1, int c,
                      float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                      const void* scalars, int fwd_off, int train, float keep, float scale,
                      float* U, float* V, int ldk, float* R, int foff, int cw,
-                     const float* dmask, const LdsBatch* batch, void* stream);
+                     const float* dmask, const float* agg, const LdsBatch* batch, void* stream);
 int lds_engine_rev_d(const int* rp, const int* col, const float* s, const int* ell, int n,
                      const float* y0bar, const float* h0, const float* y0,
                      float* h0bar, float* U, float* V, int ldk, float* R, int foff,
@@ -426,14 +432,14 @@ int lds_engine_bwd1_reduce(const int* rp, const int* col, const float* s, const 
                            const float* dy0, float* dh0, const float* y0, const float* h0,
                            float* U, float* V, int ldk, float* R, int foff,
                            const float* dh2, const float* h1d, const float* lossrow,
-                           const float* corrrow, int c, float* partials, const LdsBatch* batch, void* stream);
+                           const float* corrrow, int c, float* partials, const float* agg, const LdsBatch* batch, void* stream);
 /* H0bar = ÂY0bar (+ factor use 1) fused with the first stage of
  * {W̄1 += dH2ᵀdH1dbar + H2barᵀH1d, b̄0 += ΣH0bar, b̄1 += ΣH2bar}. */
 int lds_engine_rev_d_reduce(const int* rp, const int* col, const float* s, const int* ell, int n,
                             const float* y0bar, const float* h0, const float* y0,
                             float* h0bar, float* U, float* V, int ldk, float* R, int foff,
                             const float* dh2, const float* dh1dbar, const float* h2bar,
-                            const float* h1d, int c, float* partials, const LdsBatch* batch, void* stream);
+                            const float* h1d, int c, float* partials, const float* agg, const LdsBatch* batch, void* stream);
 /* Final stage: partials -> dst (flat parameter layout; = or +=), metrics[0..1]
  * (may be NULL), then Adam (mode) on b0 / W1 / b1. */
 int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int off_b0,

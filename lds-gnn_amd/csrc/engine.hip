@@ -255,10 +255,11 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int2* __restrict__ ell, int n,
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
-    float scale, float* __restrict__ dmask, Batch bt) {
+    float scale, float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     // the dropout draw does not depend on the aggregation: issue it first
     const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
                            : 1.f;
-    const float y = agg_row(rp, col, s, ell, h0, row, lane);
+    const float y = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h0, row, lane));
     float hd = fmaxf(y, 0.f);
     if (train) hd = dk != 0.f ? hd * scale : 0.f;
     y0[row * HID + lane] = y;
@@ -298,10 +299,11 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const int2* __restrict__ ell, int n,
     const float* __restrict__ h2, float* __restrict__ o_out, float* __restrict__ p_out,
     float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
-    float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c, Batch bt) {
+    float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     d_o = boff<kB>(d_o, bt.act);
     lossrow = boff<kB>(lossrow, bt.row);
     corrrow = boff<kB>(corrrow, bt.row);
-    const float o = agg_row(rp, col, s, ell, h2, row, lane);
+    const float o = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h2, row, lane));
     const bool act = lane < c;
     const float m = gmax16(act ? o : -INFINITY);
     const float e = act ? expf(o - m) : 0.f;
@@ -357,10 +359,11 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     float* __restrict__ dy0, GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off,
     int train, float keep, float scale, const float* __restrict__ o_in, const float* __restrict__ h2,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth,
-    int r_assign, const float* __restrict__ dmask, Batch bt) {
+    int r_assign, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     R = boff<kB>(R, bt.row);
     w.w1 = boff<kB>(w.w1, bt.par);
     bkeys<kB>(keys, bt);
-    const float g2 = agg_row(rp, col, s, ell, d_o, row, lane);  // zero past c (dO is)
+    const float g2 = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, d_o, row, lane));  // zero past c (dO is)
     dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
     for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
@@ -597,10 +600,11 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     float* __restrict__ dh1dbar, float* __restrict__ dh2bar, float* __restrict__ h1dbar,
     Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff,
-    const float* __restrict__ dmask, Batch bt) {
+    const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -623,7 +627,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, ell, dh0bar, row, lane);  // dY0bar
+    const float ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh0bar, row, lane));  // dY0bar
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
     float mask;
     if (dmask != nullptr) {
@@ -656,10 +660,11 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     const float* __restrict__ dh2bar, const float* __restrict__ d_o, const float* __restrict__ dh2,
     const float* __restrict__ p, const uint8_t* __restrict__ mask, float inv_count, int c,
     float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
-    float* __restrict__ R, int foff, int cw, Batch bt) {
+    float* __restrict__ R, int foff, int cw, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -673,7 +678,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, ell, dh2bar, row, lane);  // dObar
+    const float ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh2bar, row, lane));  // dObar
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
     const bool sel = mask[row] != 0;
     const float ub = (sel && lane < c) ? ag * inv_count : 0.f;
@@ -692,10 +697,11 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     const float* __restrict__ h1dbar_part, const float* __restrict__ y0, GcnW w, int c,
     float* __restrict__ h2bar, float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc,
     int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
-    int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask, Batch bt) {
+    int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -714,7 +720,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
-    const float ag = agg_row(rp, col, s, ell, obar, row, lane);  // H2bar (zero past c)
+    const float ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, obar, row, lane));  // H2bar (zero past c)
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
     h2bar[ix] = ag;
     float hb = h1dbar_part[ix];
@@ -917,10 +923,11 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ h1d,
     const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials,
-    Batch bt) {
+    const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -940,7 +947,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        g = agg_row(rp, col, s, ell, dy0, row, lane);
+        g = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dy0, row, lane));
         dh0[ix] = g;
         a1 = dh2[ix];
         b1 = h1d[ix];
@@ -963,10 +970,11 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ dh1dbar,
     const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials,
-    Batch bt) {
+    const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
+    agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -986,7 +994,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        ag = agg_row(rp, col, s, ell, y0bar, row, lane);
+        ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, y0bar, row, lane));
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
         h0bar[ix] = ag;
         a1 = dh2[ix];
@@ -1250,7 +1258,7 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
                                      const float* h0, float* y0, float* h1d, float* h2,
                                      const float* w1, const float* b1, int c, uint64_t seed,
                                      uint32_t tag_h, const void* scalars, int fwd_off, int train,
-                                     float keep, float scale, float* dmask, const LdsBatch* batch,
+                                     float keep, float scale, float* dmask, const float* agg, const LdsBatch* batch,
                                      void* stream) {
     LDS_CHECK_ARG(rp && col && s && h0 && y0 && h1d && h2 && w1 && b1 && scalars && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID && batch_ok(batch));
@@ -1259,14 +1267,14 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(fwd_layer1_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, bt);
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float* s, const int* ell, int n,
                                      const float* h2, float* o, float* p, float* d_o,
                                      const int* label, const uint8_t* mask, float inv_count,
-                                     float* lossrow, float* corrrow, int c, const LdsBatch* batch,
+                                     float* lossrow, float* corrrow, int c, const float* agg, const LdsBatch* batch,
                                      void* stream) {
     LDS_CHECK_ARG(rp && col && s && h2 && label && lossrow && corrrow && n > 0 && c > 0 && c <= HID);
     LDS_CHECK_ARG(batch_ok(batch));
@@ -1274,7 +1282,7 @@ extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float*
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(fwd_layer2_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c,
-                       bt);
+                       agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1284,7 +1292,7 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
                                      const void* scalars, int fwd_off, int train, float keep,
                                      float scale, const float* o, const float* h2, float* U, float* V,
                                      int ldk, float* R, int foff, int fwidth, int r_assign,
-                                     const float* dmask, const LdsBatch* batch, void* stream) {
+                                     const float* dmask, const float* agg, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && d_o && y0 && dh2 && dy0 && w1 && scalars && n > 0 && batch_ok(batch));
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && o && h2 && fwidth <= HID)));
     GcnW w{nullptr, nullptr, w1, nullptr};
@@ -1293,7 +1301,7 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
     LDS_LAUNCH_B(bwd_layer2_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
-                       foff, fwidth, r_assign, dmask, bt);
+                       foff, fwidth, r_assign, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1358,7 +1366,7 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
                                 float* dh2bar, float* h1dbar, uint64_t seed, uint32_t tag_h,
                                 const void* scalars, int fwd_off, int train, float keep, float scale,
                                 float* U, float* V, int ldk, float* R, int foff, const float* dmask,
-                                const LdsBatch* batch, void* stream) {
+                                const float* agg, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dh0bar && dy0 && dh0 && y0 && h1d && dh2 && w1 && gw1bar && gb1bar);
     LDS_CHECK_ARG(dh1dbar && dh2bar && h1dbar && scalars && U && V && R && n > 0 && c > 0 && c <= HID);
     LDS_CHECK_ARG(batch_ok(batch));
@@ -1368,14 +1376,14 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
     LDS_LAUNCH_B(rev_a_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar,
                        h1dbar, mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
-                       scale, U, V, ldk, R, foff, dmask, bt);
+                       scale, U, V, ldk, R, foff, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, const int* ell, int n,
                                 const float* dh2bar, const float* d_o, const float* dh2, const float* p,
                                 const uint8_t* mask, float inv_count, int c, float* obar, float* U,
-                                float* V, int ldk, float* R, int foff, int cw, const LdsBatch* batch,
+                                float* V, int ldk, float* R, int foff, int cw, const float* agg, const LdsBatch* batch,
                                 void* stream) {
     LDS_CHECK_ARG(rp && col && s && dh2bar && d_o && dh2 && p && mask && obar && U && V && R && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
@@ -1383,7 +1391,7 @@ extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, c
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(rev_b_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw,
-                       bt);
+                       agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1393,7 +1401,7 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
                                 float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
                                 const void* scalars, int fwd_off, int train, float keep, float scale,
                                 float* U, float* V, int ldk, float* R, int foff, int cw,
-                                const float* dmask, const LdsBatch* batch, void* stream) {
+                                const float* dmask, const float* agg, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && obar && h2 && o && h1dbar_part && y0 && w1 && h2bar && y0bar);
     LDS_CHECK_ARG(scalars && U && V && R && n > 0 && c > 0 && c <= HID && cw >= c && cw <= HID);
     LDS_CHECK_ARG(batch_ok(batch));
@@ -1403,7 +1411,7 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
     LDS_LAUNCH_B(rev_c_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V,
-                       ldk, R, foff, cw, dmask, bt);
+                       ldk, R, foff, cw, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1464,14 +1472,14 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
                                       const float* dy0, float* dh0, const float* y0, const float* h0,
                                       float* U, float* V, int ldk, float* R, int foff, const float* dh2,
                                       const float* h1d, const float* lossrow, const float* corrrow, int c,
-                                      float* partials, const LdsBatch* batch, void* stream) {
+                                      float* partials, const float* agg, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && dh2 && h1d && lossrow && corrrow && partials && n > 0);
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)) && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(bwd1_reduce_kernel, ns, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
                        rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow,
-                       corrrow, c, partials, bt);
+                       corrrow, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1479,14 +1487,14 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
                                        const float* y0bar, const float* h0, const float* y0, float* h0bar,
                                        float* U, float* V, int ldk, float* R, int foff, const float* dh2,
                                        const float* dh1dbar, const float* h2bar, const float* h1d, int c,
-                                       float* partials, const LdsBatch* batch, void* stream) {
+                                       float* partials, const float* agg, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && dh2 && dh1dbar && h2bar);
     LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(rev_d_reduce_kernel, ns, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
                        (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R,
-                       foff, dh2, dh1dbar, h2bar, h1d, c, partials, bt);
+                       foff, dh2, dh1dbar, h2bar, h1d, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
 }
 

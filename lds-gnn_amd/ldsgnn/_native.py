@@ -61,26 +61,26 @@ SIGNATURES = {
     "lds_engine_xt_linear": [P, P, P, c_int, P, P, P, c_float, c_int, c_uint64, c_uint32, P, c_int, c_int,
                              c_float, c_float, P],
     "lds_engine_fwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
-                              c_float, c_float, P, P, P],
-    "lds_engine_fwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, P, c_float, P, P, c_int, P, P],
+                              c_float, c_float, P, P, P, P],
+    "lds_engine_fwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, P, c_float, P, P, c_int, P, P, P],
     "lds_engine_bwd_layer2": [P, P, P, P, c_int, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
-                              c_float, c_float, P, P, P, P, c_int, P, c_int, c_int, c_int, P, P, P],
+                              c_float, c_float, P, P, P, P, c_int, P, c_int, c_int, c_int, P, P, P, P],
     "lds_engine_bwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_colreduce": [c_int, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, c_int, P, c_int, P, c_int,
                              P],
     "lds_engine_adam": [c_int, P, P, P, P, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_adam_reverse": [c_int, P, P, P, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_rev_a": [P, P, P, P, c_int, P, P, P, P, P, P, P, P, P, c_int, P, P, P, c_uint64, c_uint32, P,
-                         c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, P, P, P],
-    "lds_engine_rev_b": [P, P, P, P, c_int, P, P, P, P, P, c_float, c_int, P, P, P, c_int, P, c_int, c_int, P, P],
+                         c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, P, P, P, P],
+    "lds_engine_rev_b": [P, P, P, P, c_int, P, P, P, P, P, c_float, c_int, P, P, P, c_int, P, c_int, c_int, P, P, P],
     "lds_engine_rev_c": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, P, c_uint64, c_uint32, P, c_int, c_int,
-                         c_float, c_float, P, P, c_int, P, c_int, c_int, P, P, P],
+                         c_float, c_float, P, P, c_int, P, c_int, c_int, P, P, P, P],
     "lds_engine_rev_d": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_sgd_clamp": [P, P, c_int64, P, P],
     "lds_engine_advance": [P, c_int, c_int, c_int, c_int, P],
     # fused forms
-    "lds_engine_bwd1_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P, P],
-    "lds_engine_rev_d_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P, P],
+    "lds_engine_bwd1_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P, P, P],
+    "lds_engine_rev_d_reduce": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, P, c_int, P, P, P, P, c_int, P, P, P, P],
     "lds_engine_final": [P, c_int, c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, P, P, P, P, P, P, P,
                          P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_xt_adam": [P, P, P, c_int, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,

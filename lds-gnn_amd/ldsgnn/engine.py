@@ -55,22 +55,24 @@ class _Graph:
     """Device buffers of one sampled graph per replica sample (CSR with
     self-loops + s): arrays [S, ...]."""
 
-    def __init__(self, n: int, cap: int, dev, views=None, samples: int = 1):
+    def __init__(self, n: int, cap: int, dev, views=None, samples: int = 1, bptr_len: int = 0):
         if views is not None:
-            self.row_ptr, self.col, self.s, self.ell = views
+            self.row_ptr, self.col, self.s, self.ell, self.bptr = views
             return
         S = samples
         self.row_ptr = torch.empty((S, n + 1), dtype=torch.int32, device=dev)
         self.col = torch.empty((S, max(cap, 1)), dtype=torch.int32, device=dev)
         self.s = torch.empty((S, n), dtype=torch.float32, device=dev)
         self.ell = torch.empty((S, n * 2 * HID), dtype=torch.int32, device=dev)  # ELL head {j, s_j}
+        # long rows: segment starts per (row, column block) for lds_spmm_norm_blocked
+        self.bptr = torch.empty((S, bptr_len), dtype=torch.int32, device=dev) if bptr_len else None
 
 
 class _GraphBatch:
     """Contiguous storage for the τ+1 graphs of a window, so that one batched
     lds_sample_graphs launch set draws them all (θ is fixed within a window)."""
 
-    def __init__(self, count: int, n: int, words: int, cap: int, dev, samples: int = 1):
+    def __init__(self, count: int, n: int, words: int, cap: int, dev, samples: int = 1, bptr_len: int = 0):
         self.count, self.cap = count, cap
         S = samples
         self.bits = torch.empty((count, S, n, words), dtype=torch.int64, device=dev)
@@ -79,7 +81,9 @@ class _GraphBatch:
         self.col = torch.empty((count, S, cap), dtype=torch.int32, device=dev)
         self.s = torch.empty((count, S, n), dtype=torch.float32, device=dev)
         self.ell = torch.empty((count, S, n * 2 * HID), dtype=torch.int32, device=dev)
-        self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g], self.ell[g]))
+        self.bptr = torch.empty((count, S, bptr_len), dtype=torch.int32, device=dev) if bptr_len else None
+        self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g], self.ell[g],
+                                                  self.bptr[g] if bptr_len else None))
                        for g in range(count)]
 
 
@@ -88,9 +92,10 @@ class _Slot:
     relu/dropout mask of layer 1 and (training with dropout) the dropped X
     values in CSR and CSC order."""
 
-    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None, x_nnz: int = 0, samples: int = 1):
+    def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None, x_nnz: int = 0, samples: int = 1,
+                 bptr_len: int = 0):
         S = samples
-        self.g = graph if graph is not None else _Graph(n, cap, dev, samples=S)
+        self.g = graph if graph is not None else _Graph(n, cap, dev, samples=S, bptr_len=bptr_len)
         for a in _ACT + ("dmask",):
             setattr(self, a, torch.zeros((S, n, HID), dtype=torch.float32, device=dev))
         self.xd_csr = torch.zeros((S, x_nnz), dtype=torch.float32, device=dev) if x_nnz else None
@@ -112,7 +117,8 @@ class LdsEngine:
                  theta: torch.Tensor, num_classes: int, dropout: float = 0.5, gcn_lr: float = 0.01,
                  gcn_wd: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8, outer_lr: float = 1.0,
                  lr_decay: Optional[float] = None, tau: int = 5, generator: Optional[Generator] = None,
-                 params: Optional["OrderedDict[str, torch.Tensor]"] = None, samples: int = 1):
+                 params: Optional["OrderedDict[str, torch.Tensor]"] = None, samples: int = 1,
+                 long_rows: Optional[bool] = None):
         nat.require_device(x, "LdsEngine")
         dev = x.device
         self.dev = dev
@@ -175,10 +181,23 @@ class LdsEngine:
         self._i32.copy_(torch.tensor([self.gen.graph_counter, self.gen.forward_counter, 0, 0], dtype=torch.int32))
         self._f64.copy_(torch.tensor([outer_lr, 1.0 if lr_decay is None else lr_decay], dtype=torch.float64))
 
-        # graph buffers
-        self.cap = n * n if n * n <= (1 << 27) else None
-        if self.cap is None:
-            raise NotImplementedError("LdsEngine at n > 11585 needs exact CSR sizing (not yet)")
+        # graph buffers: column capacity n² per graph (int32 CSR positions)
+        if n * n >= (1 << 31):
+            raise NotImplementedError("LdsEngine needs n² < 2^31 (int32 CSR positions)")
+        self.cap = n * n
+        # long rows (dense θ, BASELINE config 5): the aggregations run as a
+        # column-blocked LDS SpMM pre-pass (lds_spmm_norm_blocked) whose Â·Z
+        # the fused kernels read instead of aggregating in-kernel.  Decided once
+        # from θ's expected degree 1 + 2·Σ_{i<j} clamp(θ_ij) / n.
+        if long_rows is None:
+            tsum = float(theta.clamp(0, 1).double().sum().item())
+            diag = float(theta.view(-1)[torch.arange(n, device=dev) * (2 * n + 1 - torch.arange(n, device=dev)) // 2]
+                         .clamp(0, 1).double().sum().item())
+            long_rows = n >= 1024 and 1.0 + 2.0 * (tsum - diag) / n >= 256.0
+        self.long_rows = bool(long_rows)
+        if self.long_rows and self.S > 1:
+            raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
+        self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) if self.long_rows else 0
         self.words = nat.lib.lds_bitmask_words(n)
         S = self.S
         self.bits = torch.empty((S, n, self.words), dtype=torch.int64, device=dev)
@@ -193,7 +212,11 @@ class LdsEngine:
         self.m: List[torch.Tensor] = []
         self.v: List[torch.Tensor] = []
         self.gp: List[torch.Tensor] = []
-        self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev, samples=S)
+        self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev, samples=S, bptr_len=self.bptr_len)
+        if self.long_rows:
+            nb = nat.lib.lds_spmm_block_count(n)
+            self.agg = torch.zeros((S, n, HID), dtype=torch.float32, device=dev)
+            self.spmm_part = torch.zeros((nb, n, HID), dtype=torch.float32, device=dev)
         self._grow(self.tau)
         self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau], x_nnz=self.x_nnz, samples=S)
         self.t = 0  # inner steps in the current window
@@ -253,7 +276,8 @@ class LdsEngine:
         while len(self.slots) < slots:
             t = len(self.slots)
             g = self.gbatch.graphs[t] if t < self.gbatch.count - 1 else None
-            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g, x_nnz=self.x_nnz, samples=self.S))
+            self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g, x_nnz=self.x_nnz, samples=self.S,
+                                    bptr_len=self.bptr_len))
         while len(self.w) < slots + 1:
             for lst in (self.w, self.m, self.v):
                 lst.append(torch.zeros((self.S, self.np), dtype=torch.float32, device=self.dev))
@@ -340,7 +364,23 @@ class LdsEngine:
                  nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(self.bits), self.words,
                  nat.ptr(self.deg), nat.ptr(g.row_ptr), nat.ptr(g.col), self.cap, nat.ptr(g.s), nat.ptr(g.ell),
                  self._stream())
+        self._block_ptrs([g])
         self.pending_graph += 1
+
+    def _block_ptrs(self, graphs):
+        if self.long_rows:
+            for g in graphs:
+                nat.call("lds_csr_block_ptr", nat.ptr(g.row_ptr), nat.ptr(g.col), self.n, nat.ptr(g.bptr),
+                         self._stream())
+
+    def _agg(self, g: _Graph, z: torch.Tensor) -> int:
+        """Long rows: Â·Z by the column-blocked SpMM into self.agg (the fused
+        kernel then reads it); short rows: 0 (aggregate in-kernel)."""
+        if not self.long_rows:
+            return 0
+        nat.call("lds_spmm_norm_blocked", nat.ptr(g.bptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z), HID,
+                 nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
+        return nat.ptr(self.agg)
 
     def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int):
         st, n, c = self._stream(), self.n, self.c
@@ -355,11 +395,11 @@ class LdsEngine:
                  fwd_off, train, self.keep, self.scale, *xd, self.bt, st)
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
-                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask), self.bt,
-                 st)
+                 self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask),
+                 self._agg(g, sl.h0), self.bt, st)
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
-                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self.bt, st)
+                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self._agg(g, sl.h2), self.bt, st)
 
     def _adam_args(self, mode: int, t: int, first: int = 0):
         """Trailing Adam arguments of lds_engine_final / lds_engine_xt_adam.
@@ -398,11 +438,11 @@ class LdsEngine:
         nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
                  nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
                  self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldu, R, base + HID, self.cw,
-                 1, nat.ptr(sl.dmask), self.bt, st)
+                 1, nat.ptr(sl.dmask), self._agg(g, sl.d_o), self.bt, st)
         # dH0 + first stage of gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
         nat.call("lds_engine_bwd1_reduce", rp, cl, s, el, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
                  nat.ptr(sl.h0), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
-                 nat.ptr(sl.corrrow), c, nat.ptr(self.partials), self.bt, st)
+                 nat.ptr(sl.corrrow), c, nat.ptr(self.partials), self._agg(g, sl.dy0), self.bt, st)
         first = 1 if adam_mode == 2 else 0
         adam = self._adam_args(adam_mode, adam_t, first)
         # W0 part (Xdᵀ dH0) and the final stage of the reduction, one launch
@@ -421,6 +461,7 @@ class LdsEngine:
                  nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
                  nat.ptr(gb.deg), nat.ptr(gb.row_ptr), nat.ptr(gb.col), self.cap, nat.ptr(gb.s), nat.ptr(gb.ell),
                  self._stream())
+        self._block_ptrs(gb.graphs[:count])
 
     def inner_step(self, presampled: bool = False):
         """One InnerProblemTrainer.train_step (sample + forward + backward +
@@ -558,18 +599,19 @@ class LdsEngine:
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
                  nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldu, R,
-                 base + HID + 2 * self.cw, nat.ptr(sl.dmask), self.bt, st)
+                 base + HID + 2 * self.cw, nat.ptr(sl.dmask), self._agg(g, self.dh0bar), self.bt, st)
         nat.call("lds_engine_rev_b", rp, cl, s, el, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
                  nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldu,
-                 R, base + HID + self.cw, self.cw, self.bt, st)
+                 R, base + HID + self.cw, self.cw, self._agg(g, self.dh2bar), self.bt, st)
         nat.call("lds_engine_rev_c", rp, cl, s, el, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
                  nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
                  self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
-                 self.ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self.bt, st)
+                 self.ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self._agg(g, self.obar), self.bt, st)
         # H0bar + first stage of W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
         nat.call("lds_engine_rev_d_reduce", rp, cl, s, el, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
                  nat.ptr(self.h0bar), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
-                 nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), self.bt, st)
+                 nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), self._agg(g, self.y0bar), self.bt,
+                 st)
         adam = self._adam_args(2 if t else 0, t - 1 if t else 0)
         nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
                  nat.ptr(self.h0bar), nat.ptr(self.wbar), 1, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,

@@ -88,7 +88,7 @@ def run_product_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5
 
 
 def run_engine_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5, seed=0, p_edge=0.05,
-                          hidden=16):
+                          hidden=16, theta_uniform=None, **engine_kwargs):
     """Fused engine (ldsgnn.engine) vs the oracle on the same problem: per-step
     inner losses, final GCN params, every θ-gradient and the final θ."""
     import ldsgnn
@@ -99,12 +99,16 @@ def run_engine_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5,
     gcn = MetaDenseGCN(f_in, hidden, classes, dropout=dropout)
     params = OrderedDict((k, v.detach()) for k, v in gcn.named_parameters())
     dev = "cuda"
-    theta = O.get_triu_values(prob["adj"]).to(dev).contiguous()
+    theta0 = O.get_triu_values(prob["adj"])
+    if theta_uniform is not None:  # dense θ ~ U(0, theta_uniform) (config 5's kind of graph)
+        theta0 = torch.rand(theta0.numel(), generator=torch.Generator().manual_seed(seed + 1)) * theta_uniform
+    theta = theta0.clone().to(dev).contiguous()
     eng = LdsEngine(prob["x"].to(dev), prob["y"].to(dev), prob["train"].to(dev), prob["opt"].to(dev), theta,
                     classes, dropout=dropout, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99, tau=tau,
-                    generator=ldsgnn.rng.Generator(seed, 0), params=OrderedDict((k, v.to(dev)) for k, v in params.items()))
+                    generator=ldsgnn.rng.Generator(seed, 0), params=OrderedDict((k, v.to(dev)) for k, v in params.items()),
+                    **engine_kwargs)
     oracle = O.LdsProblem(prob["x"], prob["y"], prob["train"], prob["val"], prob["test"], prob["opt"],
-                          O.get_triu_values(prob["adj"]), hidden=hidden, dropout_p=dropout, gcn_lr=0.01,
+                          theta0.clone(), hidden=hidden, dropout_p=dropout, gcn_lr=0.01,
                           gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99, rnd=O.Randomness(seed, 0), params=params)
     e_losses, o_losses, gerr, grel = [], [], [], []
     for step in range(steps):
@@ -124,7 +128,7 @@ def run_engine_and_oracle(n=96, f_in=24, classes=4, steps=6, tau=5, dropout=0.5,
                 max_param_err=perr, max_grad_err=max(gerr) if gerr else 0.0,
                 max_grad_rel=max(grel) if grel else 0.0,
                 max_theta_err=float((eng.theta.cpu() - oracle.theta.detach()).abs().max()),
-                theta_changed=float((oracle.theta.detach() - O.get_triu_values(prob["adj"])).abs().max()),
+                theta_changed=float((oracle.theta.detach() - theta0).abs().max()),
                 engine=eng, oracle=oracle)
 
 

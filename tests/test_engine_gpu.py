@@ -158,3 +158,36 @@ def test_batched_graph_replay_equals_eager():
     for s in range(4):
         for k, v in a.get_params(s).items():
             assert torch.equal(v, b.get_params(s)[k]), (s, k)
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+def test_engine_long_rows_match_oracle(dropout):
+    """Long-row mode (config 5's dense θ): every aggregation is the
+    column-blocked LDS SpMM pre-pass read by the fused kernels.  Dense θ ~
+    U(0, 1) on 300 nodes (≈150 neighbours per row) against the oracle."""
+    res = run_engine_and_oracle(n=300, f_in=32, classes=5, steps=6, tau=5, dropout=dropout, seed=4,
+                                theta_uniform=1.0, long_rows=True)
+    assert res["engine"].long_rows
+    assert res["theta_changed"] > 0
+    assert res["max_loss_err"] < TOL, res
+    assert res["max_param_err"] < TOL, res
+    assert res["max_grad_rel"] < 1e-4, res
+    assert res["max_theta_err"] < TOL, res
+
+
+def test_engine_long_rows_equal_in_kernel_aggregation():
+    """The pre-pass and the in-kernel aggregation give the same window within
+    fp32 tolerance at a size with several column blocks (1300 nodes), and the
+    mode is picked automatically from θ's expected degree."""
+    a = run_engine_and_oracle(n=1300, f_in=20, classes=4, steps=1, tau=5, dropout=0.5, seed=8,
+                              theta_uniform=1.0)["engine"]
+    b = run_engine_and_oracle(n=1300, f_in=20, classes=4, steps=1, tau=5, dropout=0.5, seed=8,
+                              theta_uniform=1.0, long_rows=False)["engine"]
+    assert a.long_rows and not b.long_rows
+    for _ in range(2):
+        a.run_window(5)
+        b.run_window(5)
+    torch.cuda.synchronize()
+    assert float((a.theta - b.theta).abs().max()) < TOL
+    for k, v in a.get_params().items():
+        assert float((v - b.get_params()[k]).abs().max()) < TOL, k
