@@ -249,7 +249,7 @@ struct GcnW {  // pointers into a flat parameter vector (layout in engine.py)
 };
 
 // Y0 = Â H0;  H1d = relu(Y0) ⊙ D1;  H2 = H1d W1ᵀ + b1  (16-padded, zeros past C)
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     // the dropout draw does not depend on the aggregation: issue it first
     const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
                            : 1.f;
-    const float y = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h0, row, lane));
+    const float y = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h0, row, lane));
     float hd = fmaxf(y, 0.f);
     if (train) hd = dk != 0.f ? hd * scale : 0.f;
     y0[row * HID + lane] = y;
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
 
 // O = Â H2; P = softmax(O) (over c classes); dO = (P - onehot(y)) ⊙ m / |m|;
 // per-row loss -log P[y] and correctness (argmax == y) where m.
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     d_o = boff<kB>(d_o, bt.act);
     lossrow = boff<kB>(lossrow, bt.row);
     corrrow = boff<kB>(corrrow, bt.row);
-    const float o = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h2, row, lane));
+    const float o = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h2, row, lane));
     const bool act = lane < c;
     const float m = gmax16(act ? o : -INFINITY);
     const float e = act ? expf(o - m) : 0.f;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
 // ---------------------------------------------------------------------------
 
 // dH2 = Â dO;  dY0 = (dH2 W1) ⊙ D1 ⊙ [Y0 > 0].  Outer mode: emit factor (dO, H2).
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     R = boff<kB>(R, bt.row);
     w.w1 = boff<kB>(w.w1, bt.par);
     bkeys<kB>(keys, bt);
-    const float g2 = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, d_o, row, lane));  // zero past c (dO is)
+    const float g2 = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, d_o, row, lane));  // zero past c (dO is)
     dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
     for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
@@ -590,7 +590,7 @@ __global__ __launch_bounds__(256) void adam_rev_kernel(
 // dH1dbar = dY0bar ⊙ D1 ⊙ [Y0 > 0]
 // dH2bar  = dH1dbar W1ᵀ + H1d ḡW1ᵀ + ḡb1
 // H1dbar_part = dH2 ḡW1
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(256) void rev_a_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
-    const float ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh0bar, row, lane));  // dY0bar
+    const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh0bar, row, lane));  // dY0bar
     emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
     float mask;
     if (dmask != nullptr) {
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
 
 // dObar = Â dH2bar.  Factor use 3 (G = dH2bar, Z = dO, Y = dH2, ÂG = dObar).
 // Obar = P ⊙ (ū - P·ū), ū = dObar ⊙ m / |m|   (softmax Jacobian of dO = (P - E) m/|m|)
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(256) void rev_b_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -678,7 +678,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     const int ix = row * HID + lane;
-    const float ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh2bar, row, lane));  // dObar
+    const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh2bar, row, lane));  // dObar
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
     const bool sel = mask[row] != 0;
     const float ub = (sel && lane < c) ? ag * inv_count : 0.f;
@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
 
 // H2bar = Â Obar.  Factor use 2 (G = Obar, Z = H2, Y = O, ÂG = H2bar).
 // H1dbar = H1dbar_part + H2bar W1;  Y0bar = H1dbar ⊙ D1 ⊙ [Y0 > 0]
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(256) void rev_c_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
     if (row >= n) return;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
-    const float ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, obar, row, lane));  // H2bar (zero past c)
+    const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, obar, row, lane));  // H2bar (zero past c)
     emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
     h2bar[ix] = ag;
     float hb = h1dbar_part[ix];
@@ -915,7 +915,7 @@ __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1
 
 // dH0 = Â dY0 (+ outer factor (dY0, H0)); block partials of
 // {gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, Σ loss, Σ correct}.
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -927,7 +927,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -947,7 +947,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        g = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dy0, row, lane));
+        g = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dy0, row, lane));
         dh0[ix] = g;
         a1 = dh2[ix];
         b1 = h1d[ix];
@@ -962,7 +962,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
 
 // H0bar = Â Y0bar (+ factor use 1); block partials of
 // {W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d, b̄0 += Σ H0bar, b̄1 += Σ H2bar}.
-template <bool kB>
+template <bool kB, bool kAgg>
 __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
     const int2* __restrict__ ell, int n,
@@ -974,7 +974,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const int lane = threadIdx.x & (HID - 1);
     const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
     const bool valid = row < n;
-    agg = boff<kB>(agg, bt.act);
+    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
     s = boff<kB>(s, bt.row);
@@ -994,7 +994,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        ag = (agg != nullptr ? agg[row * HID + lane] : agg_row(rp, col, s, ell, y0bar, row, lane));
+        ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, y0bar, row, lane));
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
         h0bar[ix] = ag;
         a1 = dh2[ix];
@@ -1221,6 +1221,18 @@ static inline int mk_batch(const LdsBatch* b, Batch& bt) {
         else hipLaunchKernelGGL(kern<false>, __VA_ARGS__);          \
     } while (0)
 
+// ... and the precomputed-aggregation (kAgg) instantiation only when agg != NULL.
+#define LDS_LAUNCH_BA(kern, ns, agg, ...)                                                       \
+    do {                                                                                       \
+        if ((agg) != nullptr) {                                                                \
+            if ((ns) > 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(kern<true, true>), __VA_ARGS__);   \
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(kern<false, true>), __VA_ARGS__);           \
+        } else {                                                                               \
+            if ((ns) > 1) hipLaunchKernelGGL(HIP_KERNEL_NAME(kern<true, false>), __VA_ARGS__);  \
+            else hipLaunchKernelGGL(HIP_KERNEL_NAME(kern<false, false>), __VA_ARGS__);          \
+        }                                                                                      \
+    } while (0)
+
 static inline bool batch_ok(const LdsBatch* b) {
     return b == nullptr || (b->samples >= 1 && b->samples <= 65535 && (b->ell & 1) == 0);
 }
@@ -1265,7 +1277,7 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, b1};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(fwd_layer1_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1280,7 +1292,7 @@ extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float*
     LDS_CHECK_ARG(batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(fwd_layer2_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer2_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c,
                        agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1298,7 +1310,7 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(bwd_layer2_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(bwd_layer2_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
                        foff, fwidth, r_assign, dmask, agg, bt);
@@ -1373,7 +1385,7 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(rev_a_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_a_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar,
                        h1dbar, mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
                        scale, U, V, ldk, R, foff, dmask, agg, bt);
@@ -1389,7 +1401,7 @@ extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, c
     LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(rev_b_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_b_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw,
                        agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1408,7 +1420,7 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(rev_c_kernel, ns, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_c_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V,
                        ldk, R, foff, cw, dmask, agg, bt);
@@ -1477,7 +1489,7 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)) && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(bwd1_reduce_kernel, ns, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
+    LDS_LAUNCH_BA(bwd1_reduce_kernel, ns, agg, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
                        rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow,
                        corrrow, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1492,7 +1504,7 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
     LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(rev_d_reduce_kernel, ns, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
+    LDS_LAUNCH_BA(rev_d_reduce_kernel, ns, agg, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
                        (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R,
                        foff, dh2, dh1dbar, h2bar, h1d, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
