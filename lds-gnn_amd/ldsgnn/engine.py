@@ -294,17 +294,66 @@ class LdsEngine:
         return (flat[..., : self.off_b0], flat[..., self.off_b0:self.off_w1], flat[..., self.off_w1:self.off_b1],
                 flat[..., self.off_b1:self.off_b1 + c])
 
+    def _write_params(self, flat: torch.Tensor, params) -> None:
+        w0t, b0, w1, b1 = self._views(flat)
+        with torch.no_grad():
+            w0t.view(self.fin, HID).copy_(params["layer_in.fc.weight"].detach().t())
+            b0.copy_(params["layer_in.fc.bias"].detach())
+            w1.view(self.c, HID).copy_(params["layer_out.fc.weight"].detach())
+            b1.copy_(params["layer_out.fc.bias"].detach())
+
     def set_params(self, params):
         """Load reference-layout params (layer_in.fc.weight [16, fin], ...)
         into every replica sample (all chains start from the same GCN)."""
         for b in range(self.S):
-            w0t, b0, w1, b1 = self._views(self.w[0][b])
-            with torch.no_grad():
-                w0t.view(self.fin, HID).copy_(params["layer_in.fc.weight"].detach().t())
-                b0.copy_(params["layer_in.fc.bias"].detach())
-                w1.view(self.c, HID).copy_(params["layer_out.fc.weight"].detach())
-                b1.copy_(params["layer_out.fc.bias"].detach())
+            self._write_params(self.w[0][b], params)
         self.t = 0
+
+    def flat_params(self, sample: int = 0) -> torch.Tensor:
+        """A copy of the current flat parameter vector of one sample."""
+        return self.w[self.t][sample].clone()
+
+    def params_from_flat(self, flat: torch.Tensor) -> "OrderedDict[str, torch.Tensor]":
+        w0t, b0, w1, b1 = self._views(flat)
+        return OrderedDict([
+            ("layer_in.fc.weight", w0t.reshape(self.fin, HID).t().contiguous()),
+            ("layer_in.fc.bias", b0.clone()),
+            ("layer_out.fc.weight", w1.reshape(self.c, HID).clone()),
+            ("layer_out.fc.bias", b1.clone()),
+        ])
+
+    def empirical_mean(self, flat: torch.Tensor, n_samples: int, val_mask: torch.Tensor,
+                       test_mask: torch.Tensor):
+        """empirical_mean_loss (src/utils/evaluation.py:51-84) with the fused
+        kernels: n_samples graphs drawn from θ (they take graph counters, as
+        the reference's samples take RNG draws), eval-mode forward with the
+        flat parameters, NLL / accuracy on the validation and test masks,
+        averaged over samples; one host sync.  Single-sample engines."""
+        if self.S != 1:
+            raise NotImplementedError("empirical_mean runs on single-sample engines")
+        st, n, c = self._stream(), self.n, self.c
+        if getattr(self, "_eval", None) is None:
+            self._eval = _Slot(n, self.cap, self.dev, x_nnz=0, samples=1, bptr_len=self.bptr_len)
+            self._eval_w = torch.zeros((1, self.np), dtype=torch.float32, device=self.dev)
+            self._eval_rows = torch.zeros((2, n), dtype=torch.float32, device=self.dev)
+        sl, g = self._eval, self._eval.g
+        self._eval_w[0].copy_(flat)
+        vm = val_mask.to(device=self.dev, dtype=torch.uint8).contiguous()
+        tm = test_mask.to(device=self.dev, dtype=torch.uint8).contiguous()
+        inv_v = float(np.float32(1.0) / np.float32(int(val_mask.sum())))
+        inv_t = float(np.float32(1.0) / np.float32(int(test_mask.sum())))
+        sums = []
+        for _ in range(n_samples):
+            self._sample(g)
+            self._forward(sl, self._eval_w, vm, inv_v, 0, 0)  # val rows -> sl.lossrow / corrrow
+            nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n,
+                     nat.ptr(sl.h2), 0, 0, 0, nat.ptr(self.label), nat.ptr(tm), inv_t, nat.ptr(self._eval_rows[0]),
+                     nat.ptr(self._eval_rows[1]), c, self._agg(g, sl.h2), self.bt, st)
+            sums.append(torch.stack([sl.lossrow[0].sum(), sl.corrrow[0].sum(), self._eval_rows[0].sum(),
+                                     self._eval_rows[1].sum()]))
+        host = torch.stack(sums).double().cpu().numpy()
+        return (float(np.mean(host[:, 0] * inv_v)), float(np.mean(host[:, 1] * inv_v)),
+                float(np.mean(host[:, 2] * inv_t)), float(np.mean(host[:, 3] * inv_t)))
 
     def get_params(self, sample: int = 0) -> "OrderedDict[str, torch.Tensor]":
         w0t, b0, w1, b1 = self._views(self.w[self.t][sample])

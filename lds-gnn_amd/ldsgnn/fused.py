@@ -34,3 +34,78 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
                      dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=grp["lr"],
                      lr_decay=outer.lr_decay, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
                      params=inner.model_params, samples=samples)
+
+
+class FusedBilevelRunner:
+    """BilevelProblemRunner.train / evaluate (src/trainers/bilevel.py:34-145)
+    driven by the fused engine: the same loop, counters, early-stopping rules
+    and reset / detach points, with every inner step, hyper step and the
+    16-sample empirical evaluation running as fused HIP kernels.  The trainers
+    supply the initial state and the weight re-initialisation
+    (MetaDenseGCN.reset_weights consumes the torch RNG exactly as there); the
+    per-step train loss is read back for the inner early stopping (one sync per
+    inner step, as the reference's `.item()`), so windows run eagerly rather
+    than as replayed HIP graphs."""
+
+    def __init__(self, inner_trainer, outer_trainer, data, n_samples_empirical_mean: int = 16,
+                 generator: "_rng.Generator" = None):
+        self.inner_trainer = inner_trainer
+        self.outer_trainer = outer_trainer
+        self.data = data
+        self.n_samples_empirical_mean = n_samples_empirical_mean
+        self.generator = generator
+        self.engine = None
+        self.gcn_params = None
+        self.graph_state_dict = None
+        self.inner_steps = 0
+
+    def train(self, patience: int, hyper_gradient_interval: int, inner_loop_max_epochs: int = 400,
+              outer_loop_max_epochs: int = 400, sacred_runner=None):
+        from copy import deepcopy
+
+        from .utils.early_stopping import EarlyStopping
+        tau = hyper_gradient_interval
+        eng = self.engine = engine_from_trainers(self.inner_trainer, self.outer_trainer, tau=max(1, tau),
+                                                 generator=self.generator)
+        log = sacred_runner
+        outer_stop = EarlyStopping(patience=patience, max_epochs=outer_loop_max_epochs)
+        step = 0
+        while not outer_stop.abort:
+            inner_stop = EarlyStopping(patience=patience, max_epochs=inner_loop_max_epochs)
+            self.inner_trainer.reset_weights()       # torch RNG draws as in the reference
+            eng.reset_optimizer()                    # cuts the tape (new leaves), Adam state / step 0
+            eng.set_params(self.inner_trainer.model_params)
+            while not inner_stop.abort:
+                t = eng.t
+                eng.inner_step()
+                loss, acc = eng.inner_metrics(t)
+                inner_stop.update(loss, model_params=eng.flat_params())
+                if log is not None:
+                    log("loss.train", loss, step)
+                    log("acc.train", acc, step)
+                if tau == 0 or step % tau == 0:
+                    eng.hyper_step()
+                    if log is not None:
+                        ol, oa = eng.outer_metrics()
+                        log("loss.outer", ol, step)
+                        log("acc.outer", oa, step)
+                step += 1
+            self.inner_steps = step
+            vl, va, tl, ta = eng.empirical_mean(inner_stop.model_params, self.n_samples_empirical_mean,
+                                                self.data.val_mask, self.data.test_mask)
+            if log is not None:
+                log("loss.val.empirical", vl, None)
+                log("acc.val.empirical", va, None)
+                log("loss.test.empirical", tl, None)
+                log("acc.test.empirical", ta, None)
+            # the reference stores the graph model's state_dict(): views of the
+            # live θ, so evaluate() sees the final θ (kept)
+            outer_stop.update(vl, model_params=[deepcopy(inner_stop.model_params), eng.theta])
+        self.gcn_params, self.graph_state_dict = outer_stop.model_params
+        eng.sync_generator()
+
+    def evaluate(self):
+        assert self.gcn_params is not None, "Models need to be trained before evaluation."
+        vl, va, tl, ta = self.engine.empirical_mean(self.gcn_params, self.n_samples_empirical_mean,
+                                                    self.data.val_mask, self.data.test_mask)
+        return {"loss.val.final": vl, "acc.val.final": va, "loss.test.final": tl, "acc.test.final": ta}

@@ -38,7 +38,7 @@ PUBLISHED = {("lds", "cora"): (84.2, 0.5), ("lds", "citeseer"): (74.0, 0.5),
              ("gcn", "cora"): (81.2, 0.4), ("gcn", "citeseer"): (70.8, 0.5)}
 
 
-def run_lds(dataset, seed, device, pretrain=True, tau=5):
+def run_lds(dataset, seed, device, pretrain=True, tau=5, fused=False):
     torch.manual_seed(seed)
     np.random.seed(seed)
     ldsgnn.rng.manual_seed(seed, 0)
@@ -51,15 +51,21 @@ def run_lds(dataset, seed, device, pretrain=True, tau=5):
     gm = BernoulliGraphModel(data.dense_adj)
     outer = OuterProblemTrainer(torch.optim.SGD(gm.parameters(), lr=0.1), data, opt_mask, gm, lr_decay=0.99,
                                 pretrain=pretrain)
-    runner = BilevelProblemRunner(inner, outer, data, n_samples_empirical_mean=16)
     steps = {"inner": 0}
-    orig = runner.inner_opt_step
+    if fused:  # the fused engine drives the whole loop (ldsgnn.fused.FusedBilevelRunner)
+        from ldsgnn.fused import FusedBilevelRunner
+        runner = FusedBilevelRunner(inner, outer, data, n_samples_empirical_mean=16)
+    else:
+        runner = BilevelProblemRunner(inner, outer, data, n_samples_empirical_mean=16)
+        orig = runner.inner_opt_step
 
-    def counted():
-        steps["inner"] += 1
-        return orig()
-    runner.inner_opt_step = counted
+        def counted():
+            steps["inner"] += 1
+            return orig()
+        runner.inner_opt_step = counted
     def progress(name, value, step=None):  # outer-epoch heartbeat (keeps long runs visibly alive)
+        if fused and name == "loss.train":
+            steps["inner"] += 1
         if name == "loss.val.empirical":
             print(f"  seed {seed} step {steps['inner']} {name}={value:.4f}", file=sys.stderr, flush=True)
     runner.train(patience=20, hyper_gradient_interval=tau, sacred_runner=progress)
@@ -105,6 +111,7 @@ def main():
     ap.add_argument("--seed0", type=int, default=597905255 % (2 ** 31))
     ap.add_argument("--no-pretrain", action="store_true")
     ap.add_argument("--tau", type=int, default=5)
+    ap.add_argument("--fused", action="store_true", help="drive the loop with the fused engine")
     args = ap.parse_args()
     device = torch.device("cuda:0")
     accs = []
@@ -112,7 +119,8 @@ def main():
         seed = args.seed0 + k
         t0 = time.time()
         if args.model == "lds":
-            res = run_lds(args.dataset, seed, device, pretrain=not args.no_pretrain, tau=args.tau)
+            res = run_lds(args.dataset, seed, device, pretrain=not args.no_pretrain, tau=args.tau, fused=args.fused)
+            res["path"] = "fused engine" if args.fused else "drop-in autograd"
         else:
             res = run_gcn(args.dataset, seed, device)
         res.update(seed=seed, seconds=time.time() - t0, dataset=args.dataset, model=args.model)
