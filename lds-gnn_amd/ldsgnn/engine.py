@@ -35,7 +35,6 @@ S = 1 is the reference's single chain.
 """
 from __future__ import annotations
 
-import math
 from collections import OrderedDict
 from typing import List, Optional
 
@@ -756,6 +755,3 @@ class LdsEngine:
         k = self.window_columns(tau, self.c) if self.S == 1 else self.S * self.ldk
         return 4.0 * k * (self.n * (self.n + 1) // 2)
 
-
-def _unused(*_):  # pragma: no cover
-    return math.nan

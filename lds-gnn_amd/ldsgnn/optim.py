@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import math
 from collections import defaultdict
-from typing import List, Optional
+from typing import List
 
 import torch
 

@@ -1,6 +1,5 @@
 """The fused engine (hand-derived reverse pass, csrc/engine.hip) against the
 CPU oracle and the reference goldens; HIP-graph replay against eager."""
-import numpy as np
 import pytest
 import torch
 
