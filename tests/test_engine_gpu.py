@@ -228,3 +228,27 @@ def test_fused_runner_matches_dropin_runner():
             assert abs(va[key] - vb[key]) < 1e-4, (key, va[key], vb[key])
     for k in a:
         assert abs(a[k] - b[k]) < 1e-4, (k, a[k], b[k])
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_runner_control_loop_kats(fused):
+    """The reference's runner KATs (tst/trainers/test_bilevel_runner.py:82-132)
+    on both runners: evaluate() before train() asserts; patience 1, τ = 0,
+    max 1/1 epochs -> 4 inner steps; max 0/0 -> 1 hyper step."""
+    from ldsgnn.fused import FusedBilevelRunner
+    from tests.parity_harness import build_product, synthetic_problem
+    prob = synthetic_problem(64, 12, 3, 2, 0.08)
+
+    def make():
+        r = build_product(prob, dropout=0.5, seed=2)
+        return FusedBilevelRunner(r.inner_trainer, r.outer_trainer, r.data, n_samples_empirical_mean=2) \
+            if fused else r
+
+    with pytest.raises(AssertionError):
+        make().evaluate()
+    for (inner_max, outer_max), want_inner, want_hyper in (((1, 1), 4, 4), ((0, 0), 1, 1)):
+        rec = []
+        make().train(patience=1, hyper_gradient_interval=0, inner_loop_max_epochs=inner_max,
+                     outer_loop_max_epochs=outer_max, sacred_runner=lambda n, v, s=None: rec.append(n))
+        assert rec.count("loss.train") == want_inner
+        assert rec.count("loss.outer") == want_hyper
