@@ -36,6 +36,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
+INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
 
 
 def build(args, rank, device):
@@ -243,7 +244,7 @@ def main():
     ksum = nat.timer.summary()[args.kernel]
     nat.timer.disable()
     if use_engine:
-        nnz = int(eng.outer.g.row_ptr[0, n].item())
+        nnz = eng.sampled_nnz()
     else:
         g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
         nnz = g.nnz()
@@ -254,6 +255,14 @@ def main():
         achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
+    elif args.kernel == "lds_aggregate_bitmask":  # int8 MFMA: 4 limbs x 2 ops per (row, column, feature)
+        rows, cols = -(-n // 256) * 256, -(-n // 512) * 512
+        ops = 2.0 * rows * cols * 16 * 4
+        achieved = ops / (ksum["avg_us"] * 1e-6) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TOP/s",
+                "frac": achieved / INT8_PEAK_TOPS, "traffic": None,
+                "hbm_algorithmic_GBs": (8 * n * nat.lib.lds_bitmask_words(n) + 4 * n + 8 * n * 16)
+                / (ksum["avg_us"] * 1e-6) / 1e9}
     elif args.kernel == "lds_sample_bitmask":
         words = nat.lib.lds_bitmask_words(n)
         algo = 4 * tri + 8 * n * words
@@ -296,8 +305,9 @@ def main():
                        "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
                        "sampled_nnz": nnz, "replicas_in_sync": in_sync,
-                       "aggregation": ("column-blocked LDS SpMM pre-pass" if use_engine and eng.long_rows
-                                       else "in-kernel CSR")},
+                       "aggregation": (("bitmask x fixed-point s*Z on int8 MFMA (pre-pass)" if eng.bitmask_agg
+                                        else "column-blocked LDS SpMM pre-pass")
+                                       if use_engine and eng.long_rows else "in-kernel CSR")},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

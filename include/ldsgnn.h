@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 2
+#define LDS_ABI_VERSION 3
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -110,7 +110,9 @@ int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
 /* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
  * b < samples, is draw counter *counter_base + counter_offset + g with tag
  * tag + b·tag_step, stored as graph g·samples + b of the batch arrays (one
- * θ tile load per block serves all samples). */
+ * θ tile load per block serves all samples).  col == NULL: bitmask, degrees
+ * and s only — no CSR / ELL (dense graphs aggregated by
+ * lds_aggregate_bitmask); row_ptr and ell may then be NULL. */
 int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                             uint32_t tag_step, const uint32_t* counter_base,
                             uint32_t counter_offset, int count, int samples, uint64_t* bits,
@@ -149,7 +151,7 @@ int lds_spmm_norm(const int* row_ptr, const int* col, const float* s, int n,
 
 /* Long-row form of lds_spmm_norm (dense sampled graphs, ~10^4 neighbours per
  * row: BASELINE config 5), F = 16 only.  The columns are cut into
- * lds_spmm_block_count(n) blocks of 1024; a workgroup stages one block of
+ * lds_spmm_block_count(n) blocks of 512; a workgroup stages one block of
  * s⊙Z in LDS and aggregates its rows' segments in that block; the partials
  * (part_ws: block_count × n × 16 floats, 16-B aligned) are summed in block
  * order and scaled by s_i.  bptr: n × (block_count + 1) segment starts from
@@ -160,6 +162,20 @@ int lds_csr_block_ptr(const int* row_ptr, const int* col, int n, int* bptr, void
 int lds_spmm_norm_blocked(const int* bptr, const int* col, const float* s, int n,
                           const float* z, int ldz, float* y, int ldy, int beta,
                           float* part_ws, void* stream);
+
+/* Bitmask aggregation for dense sampled graphs (config 5): the same
+ *   y = diag(s)·Ã·diag(s)·z  (+ y if beta)
+ * as lds_spmm_norm, reading Ã as the sampler's bitmask (bits: n rows ×
+ * `words` uint64, self-loops set, as lds_sample_bitmask writes it) instead of
+ * CSR.  F = 16 features.  s⊙z is quantised per feature column to 32-bit fixed
+ * point against its column maximum (2^-31 relative) and summed exactly on the
+ * int8 matrix cores (csrc/bitagg.hip).  Replaces the same reference code as
+ * lds_spmm_norm (src/models/layers.py:44, src/utils/graph.py:136-153).
+ * ws: lds_bitmask_agg_ws_bytes(n) bytes of device memory. */
+int64_t lds_bitmask_agg_ws_bytes(int n);
+int lds_aggregate_bitmask(const uint64_t* bits, int words, const float* s, int n,
+                          const float* z, int ldz, float* y, int ldy, int beta,
+                          void* ws, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Hypergradient assembly.  Replaces the autograd of
@@ -451,7 +467,9 @@ int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int 
 /* out: flat parameter-shaped buffer.  Its W0ᵀ part (= or +=) Xdᵀ d (the W0
  * gradient / adjoint), then Adam (mode) on it.  With partials != NULL the same
  * launch also runs the final stage of the fused reduction (as lds_engine_final
- * with dst = out), so one launch completes every parameter. */
+ * with dst = out), so one launch completes every parameter.  xt_part != NULL:
+ * Xdᵀ d is read as the xt_splits partials of lds_engine_xt_partials (summed in
+ * range order) instead of one wave per X column running the whole column. */
 int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int fin,
                        const float* d, float* out, int accumulate, uint64_t seed,
                        uint32_t tag_x, const void* scalars, int fwd_off, int train, float keep,
@@ -460,7 +478,14 @@ int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int f
                        const float* w0, const float* m0, const float* v0, float* w1, float* m1,
                        float* v1, float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                        const double* hyper, const float* adam_tab, int n_wd, int step_off,
-                       const LdsBatch* batch, void* stream);
+                       const float* xt_part, int xt_splits, const LdsBatch* batch, void* stream);
+/* Long X columns (dense X, config 5): Xdᵀ d over `splits` entry ranges of every
+ * column, one wave each; part[s][p][f][16] per replica sample s (stride
+ * splits·fin·16).  Feeds lds_engine_xt_adam's xt_part. */
+int lds_engine_xt_partials(const int* xcp, const int* xrow, const float* xval, int fin,
+                           const float* d, uint64_t seed, uint32_t tag_x, const void* scalars,
+                           int fwd_off, int train, float keep, float scale, int splits, float* part,
+                           const LdsBatch* batch, void* stream);
 /* Window end (both trainers' detach, src/trainers/bilevel.py:109-114): copy
  * w/m/v of slot T to slot 0 (skipped when wT == NULL), advance the scalars
  * as lds_engine_advance and (adam_tab != NULL) refresh the first tab_count

@@ -144,17 +144,17 @@ __device__ __forceinline__ void emit_factor(float* __restrict__ U, float* __rest
 // (optionally stored: xd_out in this order, xd_perm_out[perm[p]] in the other),
 // then 16 independent row gathers of `src`; the groups' partials are combined
 // by two xor-shuffles (fixed order).  Returns the full sum in every lane.
+// x_wave_dot_range: the same over the entry range [beg, end) of row / column r.
 template <bool kCsc>
-__device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const int* __restrict__ idx,
-                                            const float* __restrict__ val, int r,
-                                            const float* __restrict__ src, const Keys& keys,
-                                            uint32_t ctr, int train, float keep, float scale,
-                                            float* __restrict__ xd_out = nullptr,
-                                            float* __restrict__ xd_perm_out = nullptr,
-                                            const int* __restrict__ perm = nullptr) {
+__device__ __forceinline__ float x_wave_dot_range(int beg, int end, const int* __restrict__ idx,
+                                                  const float* __restrict__ val, int r,
+                                                  const float* __restrict__ src, const Keys& keys,
+                                                  uint32_t ctr, int train, float keep, float scale,
+                                                  float* __restrict__ xd_out = nullptr,
+                                                  float* __restrict__ xd_perm_out = nullptr,
+                                                  const int* __restrict__ perm = nullptr) {
     const int lane = threadIdx.x & (HID - 1);
     const int q = (threadIdx.x >> 4) & 3;
-    const int beg = ptr[r], end = ptr[r + 1];
     float acc = 0.f;
     for (int p0 = beg + q * HID; p0 < end; p0 += 4 * HID) {
         const int p = p0 + lane;
@@ -180,6 +180,18 @@ __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const i
     acc += __shfl_xor(acc, 16);
     acc += __shfl_xor(acc, 32);
     return acc;
+}
+
+template <bool kCsc>
+__device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const int* __restrict__ idx,
+                                            const float* __restrict__ val, int r,
+                                            const float* __restrict__ src, const Keys& keys,
+                                            uint32_t ctr, int train, float keep, float scale,
+                                            float* __restrict__ xd_out = nullptr,
+                                            float* __restrict__ xd_perm_out = nullptr,
+                                            const int* __restrict__ perm = nullptr) {
+    return x_wave_dot_range<kCsc>(ptr[r], ptr[r + 1], idx, val, r, src, keys, ctr, train, keep, scale, xd_out,
+                                  xd_perm_out, perm);
 }
 
 // out[i][h] = bias[h] + Σ_f Xd[i][f] · Wt[f][h]      (H0 = Xd W0ᵀ + b0)
@@ -1086,11 +1098,36 @@ __global__ __launch_bounds__(320) void final_kernel(FinalArgs f, AdamArgs adam,
 // completes (param index f·16 + h).  With f.partials != NULL the grid carries
 // one extra block that runs the final reduction of b0 / W1 / b1 (+ their Adam)
 // concurrently: both only need the kernel that produced d and the partials.
+// Long X columns (dense X, config 5): Xdᵀ d in `splits` entry ranges per
+// column, one wave per (column, range), partial p of column f in
+// part[(p·fin + f)·16 + h] (per sample: + sample·splits·fin·16); xt_adam then
+// sums the partials in range order instead of running the column dot itself.
+template <bool kB>
+__global__ __launch_bounds__(256) void xt_partials_kernel(
+    const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
+    const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
+    float keep, float scale, int splits, float* __restrict__ part, Batch bt) {
+    xval = boff<kB>(xval, bt.xval);
+    d = boff<kB>(d, bt.act);
+    bkeys<kB>(keys, bt);
+    if (kB) part += (int64_t)blockIdx.y * splits * fin * HID;
+    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;   // f·splits + p
+    if (w >= fin * splits) return;
+    const int f = w / splits, p = w - f * splits;
+    const int beg = xcp[f], end = xcp[f + 1];
+    const int seg = ((end - beg + splits - 1) / splits + 4 * HID - 1) / (4 * HID) * (4 * HID);
+    const int b = min(end, beg + p * seg), e = min(end, b + seg);
+    const float acc = x_wave_dot_range<true>(b, e, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
+    const int lane = threadIdx.x & 63;
+    if (lane < HID) part[((int64_t)p * fin + f) * HID + lane] = acc;
+}
+
 template <bool kB>
 __global__ __launch_bounds__(256) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
     const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
-    float keep, float scale, FinalArgs fin_args, AdamArgs adam, Batch bt) {
+    float keep, float scale, FinalArgs fin_args, AdamArgs adam, const float* __restrict__ xt_part,
+    int xt_splits, Batch bt) {
     fin_args.partials = boff<kB>(fin_args.partials, bt.part);
     fin_args.dst = boff<kB>(fin_args.dst, bt.par);
     fin_args.metrics = boff<kB>(fin_args.metrics, bt.met);
@@ -1126,7 +1163,14 @@ __global__ __launch_bounds__(256) void xt_adam_kernel(
     }
     float step_size, c2;
     adam_step_consts(adam, sc, step_size, c2);
-    const float acc = x_wave_dot<true>(xcp, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
+    float acc = 0.f;
+    if (xt_part != nullptr) {   // partials of xt_partials_kernel, summed in range order
+        if (kB) xt_part += (int64_t)blockIdx.y * xt_splits * fin * HID;
+        if (lane < HID)
+            for (int p = 0; p < xt_splits; ++p) acc += xt_part[((int64_t)p * fin + f) * HID + lane];
+    } else {
+        acc = x_wave_dot<true>(xcp, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
+    }
     if (lane < HID) {
         const float val = fin_args.accumulate ? prev + acc : acc;
         fin_args.dst[idx] = val;
@@ -1535,9 +1579,10 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                                   const float* m0, const float* v0, float* w1, float* m1, float* v1,
                                   float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                                   const double* hyper, const float* adam_tab, int n_wd, int step_off,
-                                  const LdsBatch* batch, void* stream) {
+                                  const float* xt_part, int xt_splits, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && fin > 0 && batch_ok(batch));
     LDS_CHECK_ARG(partials == nullptr || (nblocks > 0 && c > 0 && c <= HID));
+    LDS_CHECK_ARG(xt_part == nullptr || xt_splits > 0);
     LDS_CHECK_ARG(adam_ok(adam_mode, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper, adam_tab,
                           step_off));
     AdamArgs a = mk_adam_args(adam_mode, first, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper,
@@ -1548,7 +1593,22 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
-                       a, bt);
+                       a, xt_part, xt_splits, bt);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_xt_partials(const int* xcp, const int* xrow, const float* xval, int fin,
+                                      const float* d, uint64_t seed, uint32_t tag_x, const void* scalars,
+                                      int fwd_off, int train, float keep, float scale, int splits, float* part,
+                                      const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(xcp && xrow && xval && d && part && scalars && fin > 0 && splits > 0 && batch_ok(batch));
+    LDS_CHECK_ARG((int64_t)fin * splits * 64 <= ((int64_t)1 << 31) - 256);
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    const int blocks = (fin * splits + 3) / 4;
+    LDS_LAUNCH_B(xt_partials_kernel, ns, dim3(blocks, ns), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
+                 d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, splits,
+                 part, bt);
     LDS_RETURN_LAST_ERROR();
 }
 

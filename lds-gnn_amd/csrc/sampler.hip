@@ -27,12 +27,15 @@ namespace lds {
 // on MI355X (r01, 6 Cora graphs per window): drawing all graphs of a window
 // from one θ load inside the block (a loop over graphs) took 41-53 µs against
 // 35 µs here — the loop raised the kernel to 157 VGPRs (occupancy 3 vs 8), and
-// the θ re-read per graph is cheap (MALL-resident).
+// the θ re-read per graph is cheap (MALL-resident).  At config 5 (θ 800 MB,
+// far past the 256 MB MALL) the re-reads are the kernel's HBM traffic, so
+// there the loop runs over every (graph, sample) of the batch (kLoop with
+// `graphs` = count: 1.24 ms -> see DESIGN §4b for 6 graphs at N = 20 000).
 template <bool kInj, bool kLoop>
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
-    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples) {
+    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs) {
     __shared__ uint64_t colpart[4][64];
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
@@ -43,6 +46,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     counter += blockIdx.y;
     if (counter_base != nullptr) counter += *counter_base;  // device-resident draw counter
     const int nsamp = kLoop ? samples : (int)gridDim.z;
+    (void)ntiles;
     const int lane = wave_lane();
     const int wave = threadIdx.x >> 6;
     int a, b;
@@ -59,12 +63,18 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
         const int i = r0 + r;
         th[r] = (i < j && j < n) ? theta[tri_index(i, j, nn)] : -1.0f;  // i < n follows
     }
+    // kLoop: items (graph blockIdx.y + g, sample z), g < graphs, g-major, over
+    // this one θ tile load (graph blockIdx.y + g draws counter + g)
     const int z0 = kLoop ? 0 : (int)blockIdx.z;
-    const int z1 = kLoop ? samples : z0 + 1;
+    const int z1 = kLoop ? samples * graphs : z0 + 1;
 #pragma unroll 1
-    for (int z = z0; z < z1; ++z) {
+    for (int it = z0; it < z1; ++it) {
+        const int gl = kLoop ? it / samples : 0;
+        const int z = kLoop ? it - gl * samples : it;
+        const int gidx = (int)blockIdx.y + gl;
+        const uint32_t ctr = counter + (uint32_t)gl;
         const uint32_t tg = tag + (uint32_t)z * tag_step;
-        uint64_t* __restrict__ gb = bits + ((int64_t)blockIdx.y * nsamp + z) * n * words;
+        uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
         uint64_t colword = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -77,7 +87,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                     u[r] = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
                 }
             } else {
-                philox_quad(k0, k1, tg, counter, (uint32_t)j, (uint32_t)(i0 >> 2), u);
+                philox_quad(k0, k1, tg, ctr, (uint32_t)j, (uint32_t)(i0 >> 2), u);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -104,7 +114,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
             if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
             gb[(int64_t)j * words + bi] = out;
         }
-        if (z + 1 < z1) __syncthreads();  // colpart / rowword are reused by the next sample
+        if (it + 1 < z1) __syncthreads();  // colpart / rowword are reused by the next item
     }
 }
 
@@ -297,11 +307,11 @@ extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint
     if (u_inject != nullptr)
         hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<true, false>), dim3(ntiles), dim3(256), 0,
                            (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1);
+                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1, 1);
     else
         hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles), dim3(256), 0,
                            (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1);
+                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1, 1);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -314,7 +324,7 @@ extern "C" int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, 
     const int ntiles = nb * (nb + 1) / 2;
     hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u, 1);
+                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u, 1, 1);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -367,24 +377,31 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
                                        uint32_t counter_offset, int count, int samples, uint64_t* bits,
                                        int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
                                        float* s, int* ell, void* stream) {
-    LDS_CHECK_ARG(theta && bits && deg_ws && row_ptr && col && s && n > 0 && n <= (1 << 20));
+    // col == NULL: bitmask, degrees and s only (the bitmask aggregation of
+    // dense graphs reads no CSR); row_ptr / ell are then not written
+    LDS_CHECK_ARG(theta && bits && deg_ws && s && n > 0 && n <= (1 << 20));
+    LDS_CHECK_ARG(col == nullptr || (row_ptr != nullptr && col_stride > 0));
     LDS_CHECK_ARG(count > 0 && samples > 0 && samples <= 65535 && (int64_t)count * samples <= 65535);
-    LDS_CHECK_ARG(words >= (n + 63) / 64 && col_stride > 0);
+    LDS_CHECK_ARG(words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
     const int graphs = count * samples;
     hipStream_t st = (hipStream_t)stream;
-    // replica samples loop inside the block over one θ tile load
-    if (samples > 1)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true>), dim3(ntiles, count, 1), dim3(256), 0, st, theta, n,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
-                           (const float*)nullptr, bits, words, ntiles, tag_step, samples);
+    // replica samples loop inside the block over one θ tile load; past the
+    // MALL (θ > ~64 MB) the window's graphs join that loop too
+    const bool big = (int64_t)n * (n + 1) / 2 * 4 > ((int64_t)64 << 20);
+    const int loop_graphs = big ? count : 1;
+    if (samples > 1 || (big && count > 1))
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true>), dim3(ntiles, count / loop_graphs, 1),
+                           dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
+                           counter_base, (const float*)nullptr, bits, words, ntiles, tag_step, samples, loop_graphs);
     else
         hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles, count, 1), dim3(256), 0, st, theta,
                            n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
-                           (const float*)nullptr, bits, words, ntiles, tag_step, 1);
+                           (const float*)nullptr, bits, words, ntiles, tag_step, 1, 1);
     hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
                        deg_ws, s);
+    if (col == nullptr) LDS_RETURN_LAST_ERROR();
     hipLaunchKernelGGL(scan_kernel, dim3(1, graphs), dim3(1024), 0, st, deg_ws, n, row_ptr);
     hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
                        row_ptr, col, col_stride, (int*)nullptr, (const float*)s, (int2*)ell);

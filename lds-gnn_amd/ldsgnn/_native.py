@@ -14,13 +14,14 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
 P = c_void_p  # device pointers travel as integers
 
 # name -> argtypes (restype is always int = hipError_t, except where noted)
+_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes"}  # byte counts
 SIGNATURES = {
     "lds_abi_version": [],
     "lds_bitmask_words": [c_int],
@@ -42,6 +43,8 @@ SIGNATURES = {
     "lds_spmm_block_count": [c_int],
     "lds_csr_block_ptr": [P, P, c_int, P, P],
     "lds_spmm_norm_blocked": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P],
+    "lds_bitmask_agg_ws_bytes": [c_int],
+    "lds_aggregate_bitmask": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
@@ -85,7 +88,9 @@ SIGNATURES = {
                          P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_xt_adam": [P, P, P, c_int, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
                            P, c_int, c_int, c_int, c_int, c_int, P,
-                           c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, P],
+                           c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, c_int, P, P],
+    "lds_engine_xt_partials": [P, P, P, c_int, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float, c_int, P,
+                               P, P],
     "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
     "lds_engine_adam_table": [P, P, P, c_int, P],
 }
@@ -105,7 +110,7 @@ def _load() -> ctypes.CDLL:
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = c_int
+        fn.restype = ctypes.c_int64 if name in _RESTYPE_I64 else c_int
     lib.lds_error_string.argtypes = [c_int]
     lib.lds_error_string.restype = ctypes.c_char_p
     v = lib.lds_abi_version()

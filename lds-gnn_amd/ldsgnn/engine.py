@@ -54,11 +54,12 @@ class _Graph:
     """Device buffers of one sampled graph per replica sample (CSR with
     self-loops + s): arrays [S, ...]."""
 
-    def __init__(self, n: int, cap: int, dev, views=None, samples: int = 1, bptr_len: int = 0):
+    def __init__(self, n: int, cap: int, dev, views=None, samples: int = 1, bptr_len: int = 0, words: int = 0):
         if views is not None:
-            self.row_ptr, self.col, self.s, self.ell, self.bptr = views
+            self.row_ptr, self.col, self.s, self.ell, self.bptr, self.bits = views
             return
         S = samples
+        self.bits = torch.empty((S, n, words), dtype=torch.int64, device=dev)  # the sampled bitmask
         self.row_ptr = torch.empty((S, n + 1), dtype=torch.int32, device=dev)
         self.col = torch.empty((S, max(cap, 1)), dtype=torch.int32, device=dev)
         self.s = torch.empty((S, n), dtype=torch.float32, device=dev)
@@ -77,12 +78,12 @@ class _GraphBatch:
         self.bits = torch.empty((count, S, n, words), dtype=torch.int64, device=dev)
         self.deg = torch.empty((count, S, n), dtype=torch.int32, device=dev)
         self.row_ptr = torch.empty((count, S, n + 1), dtype=torch.int32, device=dev)
-        self.col = torch.empty((count, S, cap), dtype=torch.int32, device=dev)
+        self.col = torch.empty((count, S, max(cap, 1)), dtype=torch.int32, device=dev)
         self.s = torch.empty((count, S, n), dtype=torch.float32, device=dev)
         self.ell = torch.empty((count, S, n * 2 * HID), dtype=torch.int32, device=dev)
         self.bptr = torch.empty((count, S, bptr_len), dtype=torch.int32, device=dev) if bptr_len else None
         self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g], self.ell[g],
-                                                  self.bptr[g] if bptr_len else None))
+                                                  self.bptr[g] if bptr_len else None, self.bits[g]))
                        for g in range(count)]
 
 
@@ -92,9 +93,9 @@ class _Slot:
     values in CSR and CSC order."""
 
     def __init__(self, n: int, cap: int, dev, graph: "_Graph" = None, x_nnz: int = 0, samples: int = 1,
-                 bptr_len: int = 0):
+                 bptr_len: int = 0, words: int = 0):
         S = samples
-        self.g = graph if graph is not None else _Graph(n, cap, dev, samples=S, bptr_len=bptr_len)
+        self.g = graph if graph is not None else _Graph(n, cap, dev, samples=S, bptr_len=bptr_len, words=words)
         for a in _ACT + ("dmask",):
             setattr(self, a, torch.zeros((S, n, HID), dtype=torch.float32, device=dev))
         self.xd_csr = torch.zeros((S, x_nnz), dtype=torch.float32, device=dev) if x_nnz else None
@@ -117,7 +118,8 @@ class LdsEngine:
                  gcn_wd: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8, outer_lr: float = 1.0,
                  lr_decay: Optional[float] = None, tau: int = 5, generator: Optional[Generator] = None,
                  params: Optional["OrderedDict[str, torch.Tensor]"] = None, samples: int = 1,
-                 long_rows: Optional[bool] = None):
+                 long_rows: Optional[bool] = None, long_rows_kernel: str = "bitmask",
+                 xt_splits: Optional[int] = None):
         nat.require_device(x, "LdsEngine")
         dev = x.device
         self.dev = dev
@@ -159,6 +161,12 @@ class LdsEngine:
         self.csr2csc = torch.empty(nnz, dtype=torch.int32, device=dev)
         self.csr2csc[order] = torch.arange(nnz, dtype=torch.int32, device=dev)
         self.x_nnz = nnz if self.train_flag else 0
+        # dense X (config 5: 20 000 entries per column): the W0 products run as
+        # partial ranges of ~512 entries per wave instead of one wave per column
+        col_avg = nnz / max(1, fin)
+        if xt_splits is None:
+            xt_splits = 1 if col_avg < 2048 else min(64, int(np.ceil(col_avg / 512)))
+        self.set_xt_splits(xt_splits)
         self.label = y.to(device=dev, dtype=torch.int32).contiguous()
         self.train_mask = train_mask.to(device=dev, dtype=torch.uint8).contiguous()
         self.opt_mask = opt_mask.to(device=dev, dtype=torch.uint8).contiguous()
@@ -180,14 +188,12 @@ class LdsEngine:
         self._i32.copy_(torch.tensor([self.gen.graph_counter, self.gen.forward_counter, 0, 0], dtype=torch.int32))
         self._f64.copy_(torch.tensor([outer_lr, 1.0 if lr_decay is None else lr_decay], dtype=torch.float64))
 
-        # graph buffers: column capacity n² per graph (int32 CSR positions)
-        if n * n >= (1 << 31):
-            raise NotImplementedError("LdsEngine needs n² < 2^31 (int32 CSR positions)")
-        self.cap = n * n
         # long rows (dense θ, BASELINE config 5): the aggregations run as a
-        # column-blocked LDS SpMM pre-pass (lds_spmm_norm_blocked) whose Â·Z
-        # the fused kernels read instead of aggregating in-kernel.  Decided once
-        # from θ's expected degree 1 + 2·Σ_{i<j} clamp(θ_ij) / n.
+        # pre-pass whose Â·Z the fused kernels read instead of aggregating
+        # in-kernel — the bitmask aggregation on the int8 matrix cores
+        # (lds_aggregate_bitmask, no CSR is built) or the column-blocked LDS
+        # SpMM over CSR (lds_spmm_norm_blocked, long_rows_kernel="blocked").
+        # Decided once from θ's expected degree 1 + 2·Σ_{i<j} clamp(θ_ij) / n.
         if long_rows is None:
             tsum = float(theta.clamp(0, 1).double().sum().item())
             diag = float(theta.view(-1)[torch.arange(n, device=dev) * (2 * n + 1 - torch.arange(n, device=dev)) // 2]
@@ -196,10 +202,17 @@ class LdsEngine:
         self.long_rows = bool(long_rows)
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
-        self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) if self.long_rows else 0
+        if long_rows_kernel not in ("bitmask", "blocked"):
+            raise ValueError("long_rows_kernel: 'bitmask' or 'blocked'")
+        self.bitmask_agg = self.long_rows and long_rows_kernel == "bitmask"
+        # graph buffers: CSR column capacity n² per graph (int32 positions);
+        # none when the bitmask aggregation reads the sampled bits directly
+        if not self.bitmask_agg and n * n >= (1 << 31):
+            raise NotImplementedError("LdsEngine needs n² < 2^31 (int32 CSR positions)")
+        self.cap = 0 if self.bitmask_agg else n * n
+        self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) if self.long_rows and not self.bitmask_agg else 0
         self.words = nat.lib.lds_bitmask_words(n)
         S = self.S
-        self.bits = torch.empty((S, n, self.words), dtype=torch.int64, device=dev)
         self.deg = torch.empty((S, n), dtype=torch.int32, device=dev)
 
         # tape
@@ -213,9 +226,12 @@ class LdsEngine:
         self.gp: List[torch.Tensor] = []
         self.gbatch = _GraphBatch(self.tau + 1, n, self.words, self.cap, dev, samples=S, bptr_len=self.bptr_len)
         if self.long_rows:
-            nb = nat.lib.lds_spmm_block_count(n)
             self.agg = torch.zeros((S, n, HID), dtype=torch.float32, device=dev)
-            self.spmm_part = torch.zeros((nb, n, HID), dtype=torch.float32, device=dev)
+            if self.bitmask_agg:
+                self.agg_ws = torch.empty(int(nat.lib.lds_bitmask_agg_ws_bytes(n)), dtype=torch.uint8, device=dev)
+            else:
+                nb = nat.lib.lds_spmm_block_count(n)
+                self.spmm_part = torch.zeros((nb, n, HID), dtype=torch.float32, device=dev)
         self._grow(self.tau)
         self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau], x_nnz=self.x_nnz, samples=S)
         self.t = 0  # inner steps in the current window
@@ -276,7 +292,7 @@ class LdsEngine:
             t = len(self.slots)
             g = self.gbatch.graphs[t] if t < self.gbatch.count - 1 else None
             self.slots.append(_Slot(self.n, self.cap, self.dev, graph=g, x_nnz=self.x_nnz, samples=self.S,
-                                    bptr_len=self.bptr_len))
+                                    bptr_len=self.bptr_len, words=self.words))
         while len(self.w) < slots + 1:
             for lst in (self.w, self.m, self.v):
                 lst.append(torch.zeros((self.S, self.np), dtype=torch.float32, device=self.dev))
@@ -332,7 +348,7 @@ class LdsEngine:
             raise NotImplementedError("empirical_mean runs on single-sample engines")
         st, n, c = self._stream(), self.n, self.c
         if getattr(self, "_eval", None) is None:
-            self._eval = _Slot(n, self.cap, self.dev, x_nnz=0, samples=1, bptr_len=self.bptr_len)
+            self._eval = _Slot(n, self.cap, self.dev, x_nnz=0, samples=1, bptr_len=self.bptr_len, words=self.words)
             self._eval_w = torch.zeros((1, self.np), dtype=torch.float32, device=self.dev)
             self._eval_rows = torch.zeros((2, n), dtype=torch.float32, device=self.dev)
         sl, g = self._eval, self._eval.g
@@ -409,23 +425,31 @@ class LdsEngine:
     def _sample(self, g: _Graph):
         """Draw the next graph of every replica sample into `g`."""
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
-                 nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(self.bits), self.words,
-                 nat.ptr(self.deg), nat.ptr(g.row_ptr), nat.ptr(g.col), self.cap, nat.ptr(g.s), nat.ptr(g.ell),
-                 self._stream())
+                 nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(g.bits), self.words,
+                 nat.ptr(self.deg), nat.ptr(g.row_ptr), self._col_arg(g.col), self.cap, nat.ptr(g.s),
+                 nat.ptr(g.ell), self._stream())
         self._block_ptrs([g])
         self.pending_graph += 1
 
+    def _col_arg(self, col: torch.Tensor) -> int:
+        return 0 if self.bitmask_agg else nat.ptr(col)  # NULL: no CSR (bitmask aggregation)
+
     def _block_ptrs(self, graphs):
-        if self.long_rows:
+        if self.long_rows and not self.bitmask_agg:
             for g in graphs:
                 nat.call("lds_csr_block_ptr", nat.ptr(g.row_ptr), nat.ptr(g.col), self.n, nat.ptr(g.bptr),
                          self._stream())
 
     def _agg(self, g: _Graph, z: torch.Tensor) -> int:
-        """Long rows: Â·Z by the column-blocked SpMM into self.agg (the fused
-        kernel then reads it); short rows: 0 (aggregate in-kernel)."""
+        """Long rows: Â·Z into self.agg by the bitmask aggregation or the
+        column-blocked SpMM (the fused kernel then reads it); short rows: 0
+        (aggregate in-kernel)."""
         if not self.long_rows:
             return 0
+        if self.bitmask_agg:
+            nat.call("lds_aggregate_bitmask", nat.ptr(g.bits), self.words, nat.ptr(g.s), self.n, nat.ptr(z), HID,
+                     nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), self._stream())
+            return nat.ptr(self.agg)
         nat.call("lds_spmm_norm_blocked", nat.ptr(g.bptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z), HID,
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
         return nat.ptr(self.agg)
@@ -448,6 +472,24 @@ class LdsEngine:
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
                  nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self._agg(g, sl.h2), self.bt, st)
+
+    def set_xt_splits(self, splits: int):
+        """Entry ranges per X column for the W0 products (1: one wave per
+        column; chosen from X's density at construction).  Call between
+        windows, before capture_window."""
+        self.xt_splits = max(1, int(splits))
+        self.xt_part = (torch.zeros((self.S, self.xt_splits, self.fin, HID), dtype=torch.float32, device=self.dev)
+                        if self.xt_splits > 1 else None)
+
+    def _xt_split(self, xcsc: torch.Tensor, d: torch.Tensor, fwd_off: int):
+        """Long X columns: run the column products as xt_splits partial ranges
+        (lds_engine_xt_partials) and return xt_adam's (xt_part, xt_splits)."""
+        if self.xt_splits <= 1:
+            return 0, 0
+        nat.call("lds_engine_xt_partials", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
+                 nat.ptr(d), self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off, 0, self.keep, self.scale,
+                 self.xt_splits, nat.ptr(self.xt_part), self.btx, self._stream())
+        return nat.ptr(self.xt_part), self.xt_splits
 
     def _adam_args(self, mode: int, t: int, first: int = 0):
         """Trailing Adam arguments of lds_engine_final / lds_engine_xt_adam.
@@ -494,10 +536,12 @@ class LdsEngine:
         first = 1 if adam_mode == 2 else 0
         adam = self._adam_args(adam_mode, adam_t, first)
         # W0 part (Xdᵀ dH0) and the final stage of the reduction, one launch
-        nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(self._xvals(sl)[1]),
+        xcsc = self._xvals(sl)[1]
+        nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc),
                  self.fin, nat.ptr(sl.dh0), nat.ptr(gout), 0, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
-                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, self.btx, st)
+                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, *self._xt_split(xcsc, sl.dh0, fwd_off), self.btx,
+                 st)
 
     # ----------------------------------------------------------------- steps
     def _sample_batch(self, count: int):
@@ -507,8 +551,8 @@ class LdsEngine:
         gb = self.gbatch
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
-                 nat.ptr(gb.deg), nat.ptr(gb.row_ptr), nat.ptr(gb.col), self.cap, nat.ptr(gb.s), nat.ptr(gb.ell),
-                 self._stream())
+                 nat.ptr(gb.deg), nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s),
+                 nat.ptr(gb.ell), self._stream())
         self._block_ptrs(gb.graphs[:count])
 
     def inner_step(self, presampled: bool = False):
@@ -664,7 +708,7 @@ class LdsEngine:
         nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
                  nat.ptr(self.h0bar), nat.ptr(self.wbar), 1, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
-                 self.off_b1, 0, *adam, t - 1, self.btx, st)
+                 self.off_b1, 0, *adam, t - 1, *self._xt_split(xcsc, self.h0bar, fwd_off), self.btx, st)
 
     # ------------------------------------------------------------- graphs
     def run_window(self, tau: int, grad_reducer=None):
@@ -743,6 +787,11 @@ class LdsEngine:
         i = self._i32.cpu().tolist()
         f = self._f64.cpu().tolist()
         return dict(graph_ctr=i[0], fwd_ctr=i[1], adam_step=i[2], hyper_steps=i[3], outer_lr=f[0], lr_decay=f[1])
+
+    def sampled_nnz(self) -> int:
+        """Stored entries (self-loops included) of the last window's outer
+        graph, sample 0 (host sync)."""
+        return int(self.gbatch.deg[self.tau, 0].sum().item())
 
     @staticmethod
     def window_columns(tau: int, c: int) -> int:

@@ -134,6 +134,21 @@ class CsrGraph:
                  nat.ptr(z), f, z.stride(0), nat.ptr(out), out.stride(0), beta, _stream(z))
         return out
 
+    def spmm_bitmask(self, z: torch.Tensor, out: Optional[torch.Tensor] = None, beta: int = 0) -> torch.Tensor:
+        """Y = Â·Z from the sampled bitmask on the int8 matrix cores
+        (lds_aggregate_bitmask; F = 16; dense graphs).  Needs `bits`."""
+        if self.bits is None:
+            raise ValueError("spmm_bitmask: this graph carries no bitmask")
+        z = _f32c(z, "spmm_bitmask")
+        if z.dim() != 2 or z.size(0) != self.n or z.size(1) != 16:
+            raise ValueError(f"spmm_bitmask: Z must be {self.n}×16, got {tuple(z.shape)}")
+        if out is None:
+            out = torch.empty((self.n, 16), dtype=torch.float32, device=z.device)
+        ws = torch.empty(int(nat.lib.lds_bitmask_agg_ws_bytes(self.n)), dtype=torch.uint8, device=z.device)
+        nat.call("lds_aggregate_bitmask", nat.ptr(self.bits), self.bits.size(1), nat.ptr(self.s), self.n, nat.ptr(z),
+                 z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(ws), _stream(z))
+        return out
+
     def to_dense(self) -> torch.Tensor:
         """Ã as a dense 0/1 matrix (diagonal = 1).  Inspection only."""
         n = self.n

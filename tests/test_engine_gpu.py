@@ -159,14 +159,16 @@ def test_batched_graph_replay_equals_eager():
             assert torch.equal(v, b.get_params(s)[k]), (s, k)
 
 
+@pytest.mark.parametrize("kernel", ["bitmask", "blocked"])
 @pytest.mark.parametrize("dropout", [0.0, 0.5])
-def test_engine_long_rows_match_oracle(dropout):
-    """Long-row mode (config 5's dense θ): every aggregation is the
-    column-blocked LDS SpMM pre-pass read by the fused kernels.  Dense θ ~
-    U(0, 1) on 300 nodes (≈150 neighbours per row) against the oracle."""
+def test_engine_long_rows_match_oracle(dropout, kernel):
+    """Long-row mode (config 5's dense θ): every aggregation is a pre-pass
+    read by the fused kernels — the bitmask aggregation on the int8 matrix
+    cores (no CSR built) or the column-blocked LDS SpMM.  Dense θ ~ U(0, 1) on
+    300 nodes (≈150 neighbours per row) against the oracle."""
     res = run_engine_and_oracle(n=300, f_in=32, classes=5, steps=6, tau=5, dropout=dropout, seed=4,
-                                theta_uniform=1.0, long_rows=True)
-    assert res["engine"].long_rows
+                                theta_uniform=1.0, long_rows=True, long_rows_kernel=kernel)
+    assert res["engine"].long_rows and res["engine"].bitmask_agg == (kernel == "bitmask")
     assert res["theta_changed"] > 0
     assert res["max_loss_err"] < TOL, res
     assert res["max_param_err"] < TOL, res
@@ -174,12 +176,13 @@ def test_engine_long_rows_match_oracle(dropout):
     assert res["max_theta_err"] < TOL, res
 
 
-def test_engine_long_rows_equal_in_kernel_aggregation():
+@pytest.mark.parametrize("kernel", ["bitmask", "blocked"])
+def test_engine_long_rows_equal_in_kernel_aggregation(kernel):
     """The pre-pass and the in-kernel aggregation give the same window within
-    fp32 tolerance at a size with several column blocks (1300 nodes), and the
-    mode is picked automatically from θ's expected degree."""
+    fp32 tolerance at a size with several column blocks / chunks (1300 nodes),
+    and the mode is picked automatically from θ's expected degree."""
     a = run_engine_and_oracle(n=1300, f_in=20, classes=4, steps=1, tau=5, dropout=0.5, seed=8,
-                              theta_uniform=1.0)["engine"]
+                              theta_uniform=1.0, long_rows_kernel=kernel)["engine"]
     b = run_engine_and_oracle(n=1300, f_in=20, classes=4, steps=1, tau=5, dropout=0.5, seed=8,
                               theta_uniform=1.0, long_rows=False)["engine"]
     assert a.long_rows and not b.long_rows
@@ -190,6 +193,20 @@ def test_engine_long_rows_equal_in_kernel_aggregation():
     assert float((a.theta - b.theta).abs().max()) < TOL
     for k, v in a.get_params().items():
         assert float((v - b.get_params()[k]).abs().max()) < TOL, k
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+def test_engine_split_x_products_match_oracle(dropout):
+    """The W0 products as partial column ranges (lds_engine_xt_partials +
+    xt_adam summing them; config 5's dense-X form, forced here with 3 ranges
+    per column) against the oracle, with and without stored dropout masks."""
+    res = run_engine_and_oracle(n=140, f_in=24, classes=4, steps=6, tau=5, dropout=dropout, seed=11, xt_splits=3)
+    assert res["engine"].xt_splits == 3
+    assert res["theta_changed"] > 0
+    assert res["max_loss_err"] < TOL, res
+    assert res["max_param_err"] < TOL, res
+    assert res["max_grad_rel"] < 1e-4, res
+    assert res["max_theta_err"] < TOL, res
 
 
 def test_fused_runner_matches_dropin_runner():

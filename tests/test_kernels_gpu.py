@@ -236,6 +236,42 @@ def test_spmm_blocked_vs_dense(device, n, high):
     assert float((out.cpu().double() - ref - 1.0).abs().max() / scale) < RTOL
 
 
+@pytest.mark.parametrize("n,high", [(1, 1.0), (65, 1.0), (700, 1.0), (1500, 1.0), (2600, 0.5), (3000, 0.02)])
+def test_bitmask_agg_vs_dense(device, n, high):
+    """Bitmask aggregation on the int8 matrix cores (lds_aggregate_bitmask) vs
+    the dense fp64 product and the CSR kernel: ragged n (not a multiple of the
+    64-row tile or the 512-column chunk), complete, dense and sparse graphs.
+    Per-column tolerance 1e-5 of max_i Σ_k |Â_ik z_kf| (the quantisation is
+    2^-31 of the column maximum; integer sums are exact)."""
+    g = torch.Generator().manual_seed(n + 17)
+    theta = torch.rand(n * (n + 1) // 2, generator=g) * high
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n), track_grad=False)
+    z = torch.randn(n, 16, generator=g)
+    z[:, 3] *= 1e-30   # tiny column
+    z[:, 7] *= 1e30    # huge column
+    z[:, 11] = 0.0     # empty column
+    z[: n // 2, 13] *= 1e6   # dynamic range inside a column
+    zd = z.to(device)
+    y = graph.spmm_bitmask(zd).cpu().double()
+    a = graph.normalized_dense().cpu().double()
+    ref = a @ z.double()
+    scale = (a.abs() @ z.double().abs()).max(0).values.clamp(min=1e-300)
+    assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL
+    assert torch.all(y[:, 11] == 0)
+    y_csr = graph.spmm(zd, blocked=False).cpu().double()
+    assert float(((y - y_csr).abs().max(0).values / scale).max()) < RTOL
+    # beta = 1 and strided Z / Y
+    zs = torch.zeros(n, 24, device=device)
+    zs[:, :16] = zd
+    out = torch.ones(n, 20, device=device)
+    ws = torch.empty(int(nat.lib.lds_bitmask_agg_ws_bytes(n)), dtype=torch.uint8, device=device)
+    nat.call("lds_aggregate_bitmask", nat.ptr(graph.bits), graph.bits.size(1), nat.ptr(graph.s), n, nat.ptr(zs), 24,
+             nat.ptr(out), 20, 1, nat.ptr(ws), nat.stream_of(zd.device))
+    o = out.cpu().double()
+    assert float(((o[:, :16] - ref - 1.0).abs().max(0).values / scale.clamp(min=1.0)).max()) < RTOL
+    assert torch.all(o[:, 16:] == 1.0)
+
+
 def test_pretrain_step_vs_oracle(device):
     """Fused pre-training epoch (weighted BCE + clamp/symmetrisation backward +
     Adam on packed θ, one launch) against the reference's dense restatement
@@ -301,3 +337,35 @@ def test_theta_grad_ex_wide_k(device, n, k, mode):
         assert float((grad.cpu().double() - ref).abs().max()) < tol
         want = (theta.double() - lr * ref).clamp(0, 1)
         assert float((th.cpu().double() - want).abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("n,count,samples", [(300, 3, 2), (6000, 3, 1), (6000, 2, 2)])
+def test_batched_sampler_equals_single_draws(device, n, count, samples):
+    """lds_sample_graphs_multi (graph g draws counter base + g, sample b tag +
+    b·tag_step) is bit-identical to single lds_sample_bitmask draws, in both
+    launch forms: one block per (tile, graph) and, past the MALL (θ > 64 MB at
+    n = 6000), one block per tile looping over every (graph, sample) on one θ
+    load.  col = NULL (bitmask + degrees only) is accepted."""
+    g = torch.Generator().manual_seed(n)
+    theta = (torch.rand(n * (n + 1) // 2, generator=g) * 0.6).to(device)
+    words = nat.lib.lds_bitmask_words(n)
+    st = nat.stream_of(theta.device)
+    base = torch.tensor([7, 0, 0, 0], dtype=torch.int32, device=device)
+    bits = torch.empty((count, samples, n, words), dtype=torch.int64, device=device)
+    deg = torch.empty((count, samples, n), dtype=torch.int32, device=device)
+    s = torch.empty((count, samples, n), dtype=torch.float32, device=device)
+    seed, tag = 1234, tag_for(TAG_GRAPH, 5)
+    nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 2, count, samples,
+             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, st)
+    one = torch.empty((n, words), dtype=torch.int64, device=device)
+    nb = (n + 63) // 64
+    for gi in range(count):
+        for b in range(samples):
+            nat.call("lds_sample_bitmask", nat.ptr(theta), n, seed, tag + b, 7 + 2 + gi, 0, nat.ptr(one), words, st)
+            assert torch.equal(bits[gi, b, :, :nb], one[:, :nb]), (gi, b)
+            pc = torch.zeros(n, dtype=torch.int64, device=device)
+            for w in range(nb):
+                x = one[:, w]
+                for k in range(64):
+                    pc += (x >> k) & 1
+            assert torch.equal(deg[gi, b].long(), pc), (gi, b)
