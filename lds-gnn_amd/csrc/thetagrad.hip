@@ -440,9 +440,11 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
     const int ntiles = nb * (nb + 1) / 2;
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     const double* lr = mode >= 2 ? reinterpret_cast<const double*>((const char*)scalars + 16) : nullptr;
-    // (a 128×128-tile variant — 8 MFMAs per 8 LDS reads — measured slower here:
-    //  at n = 2708 it has 253 tiles, one 4-wave block per CU; MFMA busy of this
-    //  form at S = 16 is 63 % of the cycles at a 2.26 GHz DVFS clock, r01 PMC)
+    // (a 128×128-tile variant — 8 MFMAs per 8 LDS reads, 4 accumulators per
+    //  wave — measured slower at both ends: at n = 2708 it has 253 tiles, one
+    //  4-wave block per CU; at n = 20 000 (12 k tiles) 3.12 ms against 2.27 ms,
+    //  196 VGPRs and 66 KB LDS leave 2 waves per SIMD.  MFMA busy of this form
+    //  at S = 16 is 63 % of the cycles at a 2.26 GHz DVFS clock, r01 PMC)
     hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u, v, ld, k, r,
                        ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale);
     LDS_RETURN_LAST_ERROR();
