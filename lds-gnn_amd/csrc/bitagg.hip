@@ -42,8 +42,10 @@ constexpr int kSteps = kChunk / 64;   // MFMA k-steps per chunk
 constexpr int kLimbs = 4;         // base-256 digits of the fixed-point s⊙Z
 constexpr int kChunkBytes = kChunk * kF * kLimbs;   // 32 KB
 constexpr int kMaxBlocks = 256;   // column-max partial blocks
-constexpr int kTiles = 4;         // 16-row tiles per wave
-constexpr int kRowsPerWg = 4 * 16 * kTiles;   // 256
+constexpr int kWaves = 8;         // waves per workgroup (share one LDS stage)
+constexpr int kTiles = 2;         // 16-row tiles per wave
+constexpr int kThreads = 64 * kWaves;
+constexpr int kRowsPerWg = kWaves * 16 * kTiles;   // 256
 constexpr int kResidentWgs = 512;  // 2 workgroups per CU (64 KB LDS, <= 256 VGPRs each)
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -178,13 +180,27 @@ __device__ __forceinline__ void load_mask(const uint64_t* __restrict__ bits, int
     }
 }
 
-// Grid (row groups of 256, column splits); 4 waves, each 4 tiles of 16 rows.
+// Grid (row groups of 256, column splits); 8 waves, each 2 tiles of 16 rows
+// (the 64 KB LDS stage allows 2 workgroups per CU: 8-wave groups at ~116
+// VGPRs give 4 waves per SIMD, against 2 for 4 waves × 4 tiles at 212 VGPRs;
+// 28.5 vs 30.2 µs at N = 20 000).  Measured and not kept:
+//  - the 32×32×32 i8 form (A = 32 rows × 32 columns, B = two limbs × 16
+//    features; a quarter of the issue slots held instead of half): 33 µs;
+//  - the mask prefetched two chunks deep in registers with counted vmcnt
+//    waits: hipcc drains vmcnt to 0 at the use of an ordinary load while a
+//    direct-to-LDS load is in flight (loop head, .s);
+//  - mask and digits both through direct-to-LDS loads from inline asm (the
+//    builtin makes hipcc wait vmcnt(0) before every ds_read), 3-deep mask
+//    ring, counted waits, 112 KB LDS, 1 workgroup per CU: 27.9 µs — 2 %, not
+//    worth hand-counted vmcnt.
+// PMC at N = 20 000 (r01): MFMA busy 42 % of the cycles, 40 % of the wave
+// time waiting; per chunk and wave 64 MFMAs, ~130 VALU, 34 LDS reads.
 // Per 512-column chunk the workgroup stages the chunk's digits (32 KB) in
 // LDS by direct global->LDS loads, double-buffered (chunk c+1 streams in
 // while chunk c is multiplied); every wave reads its B fragments from there
 // and its mask bits from HBM into registers, also one chunk ahead (64
 // contiguous bytes per row per chunk).  Partials per split in fp32.
-__global__ __launch_bounds__(256) void bitagg_main_kernel(const uint64_t* __restrict__ bits, int words, int n,
+__global__ __launch_bounds__(kThreads) void bitagg_main_kernel(const uint64_t* __restrict__ bits, int words, int n,
                                                           const int8_t* __restrict__ zq, int chunks, int splits,
                                                           float* __restrict__ part, const uint32_t* __restrict__ colmax) {
     __shared__ __attribute__((aligned(16))) int8_t bsh[2 * kChunkBytes];
@@ -200,11 +216,11 @@ __global__ __launch_bounds__(256) void bitagg_main_kernel(const uint64_t* __rest
 #pragma unroll
         for (int L = 0; L < kLimbs; ++L) acc[t][L] = v4i{0, 0, 0, 0};
 
-    // wave w stages the 1-KB blocks 4i + w of a chunk (64 lanes x 16 B each)
+    // wave w stages the 1-KB blocks kWaves·i + w of a chunk (64 lanes x 16 B each)
     auto stage = [&](int c, int buf) {
 #pragma unroll
-        for (int i = 0; i < kChunkBytes / 1024 / 4; ++i) {
-            const int kb = 4 * i + wave;
+        for (int i = 0; i < kChunkBytes / 1024 / kWaves; ++i) {
+            const int kb = kWaves * i + wave;
             __builtin_amdgcn_global_load_lds(
                 (const void*)(zq + (int64_t)c * kChunkBytes + kb * 1024 + lane * 16),
                 (__attribute__((address_space(3))) void*)(bsh + buf * kChunkBytes + kb * 1024), 16, 0, 0);
@@ -314,7 +330,7 @@ extern "C" int lds_aggregate_bitmask(const uint64_t* bits, int words, const floa
     hipLaunchKernelGGL(bitagg_colmax_kernel, dim3(kMaxBlocks), dim3(256), 0, st, s, n, z, ldz, w.colmax);
     hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st,
                        s, n, z, ldz, (const uint32_t*)w.colmax, w.zq, nc);
-    hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(256), 0, st, bits, words, n,
+    hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(kThreads), 0, st, bits, words, n,
                        (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax);
     hipLaunchKernelGGL(bitagg_final_kernel, dim3((unsigned)(((int64_t)n * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)w.part, ks, n, s, y, ldy, beta);

@@ -369,4 +369,3 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
                 for k in range(64):
                     pc += (x >> k) & 1
             assert torch.equal(deg[gi, b].long(), pc), (gi, b)
-
