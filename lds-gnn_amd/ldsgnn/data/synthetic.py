@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from ..utils.graph import DenseData
+from ..utils.graph import DenseData, knn_graph_dense
 
 SHAPES = {
     "cora": dict(n=2708, f_in=1433, classes=7, density=0.0127, edges=5278),
@@ -59,20 +59,6 @@ def make_dataset(name: str = "cora", seed: int = 0, device="cpu", n_train: int =
     data = DenseData(x=x, y=y, dense_adj=adj, train_mask=masks[0], val_mask=masks[1],
                      test_mask=masks[2], num_classes=c, name=f"{name}-synthetic")
     return data.to(device)
-
-
-def knn_graph_dense(x: torch.Tensor, k: int, loop: bool = False) -> torch.Tensor:
-    """Cosine k-nearest-neighbour connectivity graph (directed rows), as
-    sklearn's kneighbors_graph(metric='cosine', include_self=loop) which the
-    reference calls (src/data/utils.py:165-175).  Ties broken by index."""
-    xn = x / x.norm(dim=1, keepdim=True).clamp(min=1e-12)
-    sim = xn @ xn.t()
-    if not loop:
-        sim.fill_diagonal_(-float("inf"))
-    idx = torch.topk(sim, k, dim=1).indices
-    a = torch.zeros_like(sim)
-    a.scatter_(1, idx, 1.0)
-    return a
 
 
 def knn_init(data: DenseData, k: int = 10) -> DenseData:

@@ -4,8 +4,15 @@ BernoulliGraphModel keeps θ exactly as the reference does — a Parameter holdi
 the row-major upper triangle incl. the diagonal (get_triu_values of the
 initial adjacency) — but `sample()` never builds the dense P: it calls the
 fused θ -> CSR sampler (Sampler.sample_triu).  `forward()` still returns the
-dense symmetric P for API parity/inspection.  PairwiseEmbeddingSampler and
-GraphProposalNetwork (the report's GAE models) are out of scope.
+dense symmetric P for API parity/inspection.
+
+PairwiseEmbeddingSampler and GraphProposalNetwork (src/models/graph.py:81-200,
+SURVEY §8(f) item 4): P comes from node embeddings (σ(E·Eᵀ), or the affine /
+sigmoid / tanh / clamp of a GCN's similarity matrix) as dense torch ops —
+E·Eᵀ is the rocBLAS GEMM — and is sampled by the same HIP sampler from its
+upper triangle, with the KNN / EPS sparsification of the draw as a keep mask.
+The straight-through gradient reaches P's upper triangle through the
+sampled graph's θ-gradient assembly, and autograd carries it on to E.
 """
 from __future__ import annotations
 
@@ -17,8 +24,9 @@ from torch import Tensor, nn
 from torch.nn import Parameter
 
 from .. import rng as _rng
-from ..utils.graph import get_triu_values, is_square_matrix, num_nodes_from_triu_shape, \
+from ..utils.graph import cosine_similarity, get_triu_values, is_square_matrix, num_nodes_from_triu_shape, \
     triu_values_to_symmetric_matrix
+from .gcn import MetaDenseGCN
 from .sampling import Sampler
 
 
@@ -97,3 +105,103 @@ class BernoulliGraphModel(GraphGenerativeModel):
         n_edges = n ** 2
         return {"expected_num_edges": vals[0], "percentage_edges_expected": vals[0] / n_edges,
                 "mean_prob": vals[1], "min_prob": vals[2], "max_prob": vals[3]}
+
+
+class PairwiseEmbeddingSampler(GraphGenerativeModel):
+    """src/models/graph.py:81-112: P = σ(E·Eᵀ)^prob_pow."""
+
+    def __init__(self, n_nodes: int, embedding_dim: int, prob_pow: float = 1.0, init_bounds: float = 0.001,
+                 generator: "_rng.Generator" = None):
+        super().__init__()
+        self.embeddings = Parameter(torch.empty((n_nodes, embedding_dim)), requires_grad=True)
+        self.prob_pow = prob_pow
+        self.n_edges = n_nodes ** 2
+        self.init_bounds = init_bounds
+        self.generator = generator
+        self.reset_embeddings()
+
+    def reset_embeddings(self):
+        self.embeddings.data.uniform_(-self.init_bounds, self.init_bounds)
+
+    def forward(self, *args, **kwargs) -> Tensor:
+        return torch.sigmoid(self.embeddings @ self.embeddings.t()) ** self.prob_pow
+
+    def sample(self, *args, **kwargs):
+        return Sampler.sample(self.forward(), embeddings=self.embeddings, generator=self.generator)
+
+    def statistics(self) -> Dict[str, float]:
+        with torch.no_grad():
+            total = self.forward().sum().item()
+        return {"expected_num_edges": total, "percentage_edges_expected": total / self.n_edges}
+
+
+class GraphProposalNetwork(GraphGenerativeModel):
+    """src/models/graph.py:115-200: a GCN embeds the nodes, P = clamp(
+    [tanh|σ](factor · sim(E) + bias) [+ A], 0, 1) with sim the cosine or the
+    dot-product similarity; sample() caches (graph, embeddings) for refine()."""
+
+    def __init__(self, features: Tensor, dense_adj, dropout: float = 0.0, add_original: bool = False,
+                 embedding_dim: int = 128, probs_bias_init: float = 0.0, probs_factor_init: float = 1.0,
+                 prob_power: float = 1.0, use_sigmoid: bool = True, use_tanh: bool = False,
+                 normalize_similarities: bool = False, generator: "_rng.Generator" = None):
+        super().__init__()
+        assert features.size(0) == dense_adj.size(0)
+        assert is_square_matrix(dense_adj)
+        assert not (use_sigmoid and use_tanh)
+        assert probs_factor_init > 0.0
+        self.original_features = features
+        self.original_adj = dense_adj
+        self.features = features
+        self.adj = dense_adj
+        self.n_edges = dense_adj.size(0) * dense_adj.size(1)
+        self.num_features = features.size(1)
+        self.add_original = add_original
+        self.prob_power = prob_power   # stored, not applied (as in the reference)
+        self.use_sigmoid = use_sigmoid
+        self.use_tanh = use_tanh
+        self.normalize_similarities = normalize_similarities
+        self.gcn = MetaDenseGCN(in_features=self.num_features, hidden_features=embedding_dim * 2,
+                                out_features=embedding_dim, dropout=dropout)
+        self.probs_factor = Parameter(torch.tensor(probs_factor_init), requires_grad=True)
+        self.probs_bias = Parameter(torch.tensor(probs_bias_init), requires_grad=True)
+        self.embeddings_cached = None
+        self.adj_cached = None
+        self.generator = generator
+
+    def forward(self, *args, return_embeddings: bool = False, **kwargs) -> Tensor:
+        new_adj, _ = self.calculate_edges_and_embeddings()
+        return new_adj
+
+    def calculate_edges_and_embeddings(self, *args, **kwargs):
+        new_embeddings = self.gcn.forward_to_last_layer(self.features, self.adj)
+        if self.normalize_similarities:
+            similarity_matrix = cosine_similarity(new_embeddings, new_embeddings)
+        else:
+            similarity_matrix = new_embeddings @ new_embeddings.t()
+        new_adj = self.probs_factor * similarity_matrix + self.probs_bias
+        new_adj = torch.sigmoid(new_adj) if self.use_sigmoid else new_adj
+        new_adj = torch.tanh(new_adj) if self.use_tanh else new_adj
+        if self.add_original:
+            orig = self.adj.to_dense() if hasattr(self.adj, "to_dense") and not torch.is_tensor(self.adj) \
+                else self.adj
+            new_adj = new_adj + orig
+        new_adj = torch.clamp(new_adj, 0.0, 1.0)
+        return new_adj, new_embeddings
+
+    def sample(self, *args, **kwargs):
+        edge_probs, embeddings = self.calculate_edges_and_embeddings()
+        edges = Sampler.sample(edge_probs, embeddings=embeddings, generator=self.generator)
+        self.adj_cached, self.embeddings_cached = edges, embeddings
+        return edges
+
+    def refine(self):
+        if self.adj_cached is not None and self.embeddings_cached is not None:
+            self.features = self.embeddings_cached
+            self.adj = self.adj_cached
+
+    def statistics(self) -> Dict[str, float]:
+        with torch.no_grad():
+            total = self.forward().sum().item()
+        return {"expected_num_edges": total, "percentage_edges_expected": total / self.n_edges,
+                "probs_factor": self.probs_factor.item(), "probs_bias": self.probs_bias.item()}
+

@@ -212,17 +212,25 @@ class SampledGraph(CsrGraph):
 
 
 def sample_graph_from_triu(theta: torch.Tensor, n: int, generator: Optional[Generator] = None,
-                           u_inject: Optional[torch.Tensor] = None, track_grad: bool = True
-                           ) -> SampledGraph:
+                           u_inject: Optional[torch.Tensor] = None, track_grad: bool = True,
+                           keep: Optional[torch.Tensor] = None) -> SampledGraph:
     """Draw A ~ Bernoulli(clamp(θ, 0, 1)) on the upper triangle, symmetrise, add
     self-loops, build CSR + s (lds_sample_graph).  `u_inject`: n×n uniforms
-    replacing the keyed Philox draws (reference-RNG parity mode)."""
+    replacing the keyed Philox draws (reference-RNG parity mode).  `keep`
+    (packed triu, 0/1): sparsification of the SAMPLE (src/models/sampling.py:
+    19-44 applied to the Bernoulli draw) — entry (i, j) is drawn as
+    u_ij < θ_ij·keep_ij, i.e. exactly sample ⊙ keep with the same uniforms,
+    while the straight-through gradient still reaches every θ_ij."""
     nat.require_device(theta, "sample")
     if theta.dim() != 1 or theta.numel() != n * (n + 1) // 2 or theta.dtype != torch.float32:
         raise ValueError("theta must be the float32 packed upper triangle incl. diagonal")
     th = theta.detach()
     if not th.is_contiguous():
         th = th.contiguous()
+    if keep is not None:
+        if keep.shape != th.shape:
+            raise ValueError("keep must be a packed upper-triangle mask like theta")
+        th = (th.clamp(0.0, 1.0) * (keep.detach().to(th.device) != 0).to(th.dtype)).contiguous()
     gen = generator or default_generator
     seed, tag, counter = gen.next_graph()
     dev = theta.device

@@ -127,3 +127,27 @@ def cosine_similarity(a: torch.Tensor, b: torch.Tensor = None, eps: float = 1e-8
     else:
         b_norm = b.norm(p=2, dim=1, keepdim=True)
     return (torch.mm(a, b.t()) / (a_norm * b_norm.t()).clamp(min=eps)).clamp_max(1.0)
+
+
+def knn_graph_dense(x: torch.Tensor, k: int, loop: bool = True, metric: str = "cosine") -> torch.Tensor:
+    """src/data/utils.py:165-175: sklearn's kneighbors_graph(mode='connectivity',
+    include_self=loop) as a dense 0/1 matrix, directed rows (row i marks its k
+    nearest), on x's device.  metric "cosine": distance 1 - cos; "dot" (the
+    reference passes np.dot as a callable metric, sklearn then treats the dot
+    product as a distance): the k smallest dot products.  Ties broken by
+    index.  The query point counts as its own neighbour when loop=True."""
+    x = x.detach().float()
+    n = x.size(0)
+    if metric == "cosine":   # nearest = largest cosine
+        xn = x / x.norm(dim=1, keepdim=True).clamp(min=1e-12)
+        score = xn @ xn.t()
+    elif metric == "dot":    # nearest = smallest dot product (sklearn reads it as a distance)
+        score = -(x @ x.t())
+    else:
+        raise NotImplementedError(f"knn metric {metric}")
+    score.fill_diagonal_(float("inf") if loop else -float("inf"))
+    idx = torch.topk(score, k, dim=1).indices
+    a = torch.zeros((n, n), dtype=torch.float32, device=x.device)
+    a.scatter_(1, idx, 1.0)
+    return a
+

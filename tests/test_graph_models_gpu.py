@@ -1,0 +1,212 @@
+"""The embedding / GAE graph models and the KNN / EPS sparsification of the
+Bernoulli draw (src/models/graph.py:81-200,
+src/models/sampling.py:19-79) against the dense oracle:
+
+- forward(): P as the reference computes it (fp32, 1e-6);
+- sample(): bit-exact edges for injected uniforms (oracle.sample_graph on the
+  same P, then the sample ⊙ kNN pattern / EPS rule);
+- gradients: the straight-through hypergradient through a normalised
+  aggregation reaches E (or the GCN / affine parameters) as dense autograd of
+  the reference formulation does, within 1e-4 relative.
+"""
+import pytest
+import torch
+
+from ldsgnn import ops
+from ldsgnn.models.factory import GraphGenerativeModelFactory
+from ldsgnn.models.graph import GraphProposalNetwork, PairwiseEmbeddingSampler
+from ldsgnn.models.sampling import Sampler
+from ldsgnn.utils.graph import DenseData, knn_graph_dense
+from oracle import lds_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _dense_aggregate_loss(adj_ste, z, w):
+    """L = Σ (normalize(A) Z) ⊙ W, dense (the oracle's normalisation)."""
+    return ((O.normalize_adjacency_matrix(adj_ste) @ z) * w).sum()
+
+
+def _problem(n, d, seed):
+    g = torch.Generator().manual_seed(seed)
+    e = (torch.rand(n, d, generator=g) * 2 - 1)
+    u = torch.rand(n, n, generator=g)
+    z = torch.randn(n, 16, generator=g)
+    w = torch.randn(n, 16, generator=g)
+    return e, u, z, w
+
+
+@pytest.mark.parametrize("prob_pow", [1.0, 2.0])
+def test_pairwise_embedding_sampler_matches_dense(device, prob_pow):
+    n, d = 70, 8
+    e, u, z, w = _problem(n, d, 3)
+    model = PairwiseEmbeddingSampler(n_nodes=n, embedding_dim=d, prob_pow=prob_pow).to(device)
+    with torch.no_grad():
+        model.embeddings.copy_(e.to(device))
+    p = model.forward()
+    ref_p = torch.sigmoid(e @ e.t()) ** prob_pow
+    assert torch.allclose(p.detach().cpu(), ref_p, atol=1e-6)
+    st = model.statistics()
+    assert abs(st["expected_num_edges"] - float(ref_p.sum())) < 1e-2 and set(st) == {
+        "expected_num_edges", "percentage_edges_expected"}
+
+    # sample with injected uniforms: same edges as the dense oracle on the same P
+    graph = Sampler.sample(p, embeddings=model.embeddings, u_inject=u.to(device))
+    p_cpu = p.detach().cpu()
+    ref_a = O.sample_graph(p_cpu, u).detach()
+    got = graph.to_dense().cpu()
+    ref_full = ref_a.clone()
+    ref_full.fill_diagonal_(1.0)
+    assert torch.equal(got, ref_full)
+
+    # hypergradient to E through one aggregation
+    y = ops.aggregate(z.to(device), graph)
+    (y * w.to(device)).sum().backward()
+    e_ref = e.clone().requires_grad_(True)
+    p_ref = torch.sigmoid(e_ref @ e_ref.t()) ** prob_pow
+    a_ref = O.straight_through_estimator(O.to_undirected((u < p_cpu).float(), from_triu_only=True), p_ref)
+    _dense_aggregate_loss(a_ref, z, w).backward()
+    ge, gr = model.embeddings.grad.cpu(), e_ref.grad
+    assert float((ge - gr).abs().max() / gr.abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_knn_sparsified_sample_matches_dense(device, metric):
+    """KNN: the Bernoulli draw keeps (i, j) only where j is among row i's k
+    nearest embeddings; to_undirected then reads the upper triangle."""
+    n, d, k = 64, 6, 7
+    e, u, z, w = _problem(n, d, 5)
+    ed = e.to(device).requires_grad_(True)
+    p = torch.sigmoid(ed @ ed.t())
+    graph = Sampler.sample(p, sparsification="KNN", k=k, knn_metric=metric, embeddings=ed,
+                           u_inject=u.to(device))
+    knn = knn_graph_dense(e, k, loop=False, metric=metric)
+    assert torch.equal(knn.sum(1), torch.full((n,), float(k)))
+    sample = (u < p.detach().cpu()).float() * knn
+    ref = O.to_undirected(sample, from_triu_only=True)
+    ref.fill_diagonal_(1.0)
+    assert torch.equal(graph.to_dense().cpu(), ref)
+    # gradient still reaches every P_ij (zeroed draws included), as the STE does
+    y = ops.aggregate(z.to(device), graph)
+    (y * w.to(device)).sum().backward()
+    e_ref = e.clone().requires_grad_(True)
+    p_ref = torch.sigmoid(e_ref @ e_ref.t())
+    a_ref = O.straight_through_estimator(O.to_undirected(sample, from_triu_only=True), p_ref)
+    _dense_aggregate_loss(a_ref, z, w).backward()
+    assert float((ed.grad.cpu() - e_ref.grad).abs().max() / e_ref.grad.abs().max()) < 1e-4
+
+
+def test_knn_dot_metric_is_a_distance():
+    """np.dot passed to sklearn as a metric is read as a distance: the k
+    smallest dot products are the neighbours (src/models/sampling.py:30-32)."""
+    x = torch.tensor([[1.0, 0.0], [2.0, 0.0], [-1.0, 0.0], [0.0, 1.0]])
+    a = knn_graph_dense(x, 1, loop=False, metric="dot")
+    # row 0: dots with rows 1..3 = 2, -1, 0 -> nearest is row 2
+    assert torch.equal(a[0], torch.tensor([0.0, 0.0, 1.0, 0.0]))
+    c = knn_graph_dense(x, 1, loop=False, metric="cosine")
+    assert torch.equal(c[0], torch.tensor([0.0, 1.0, 0.0, 0.0]))
+
+
+@pytest.mark.parametrize("eps,edges", [(0.5, True), (1.0, True), (1.5, False)])
+def test_eps_sparsified_sample(device, eps, edges):
+    """EPS zeroes sampled entries < eps: a 0/1 draw survives iff 1 >= eps."""
+    n = 50
+    e, u, _, _ = _problem(n, 4, 9)
+    p = torch.sigmoid(e @ e.t()).to(device)
+    graph = Sampler.sample(p, sparsification="EPS", eps=eps, u_inject=u.to(device))
+    ref = O.to_undirected((u < p.cpu()).float(), from_triu_only=True) * (1.0 if edges else 0.0)
+    ref.fill_diagonal_(1.0)
+    assert torch.equal(graph.to_dense().cpu(), ref)
+
+
+def test_dense_sparsify_keeps_reference_semantics(device):
+    """dense=True: sparsify the probabilities themselves (clone, zero, no
+    gradient through zeroed entries), to_undirected from the upper triangle."""
+    n = 30
+    e, _, _, _ = _problem(n, 4, 11)
+    p = torch.sigmoid(e @ e.t()).to(device).requires_grad_(True)
+    out = Sampler.sample(p, sparsification="EPS", eps=0.6, dense=True)
+    ref = p.detach().clone()
+    ref[ref < 0.6] = 0.0
+    ref = O.to_undirected(ref.cpu(), from_triu_only=True)
+    assert torch.allclose(out.detach().cpu(), ref)
+    out.sum().backward()
+    assert torch.all(p.grad[p.detach() < 0.6] == 0)
+
+
+@pytest.mark.parametrize("normalize,add_original", [(True, False), (False, True)])
+def test_graph_proposal_network_matches_dense(device, normalize, add_original):
+    n, f_in, emb = 48, 12, 8
+    g = torch.Generator().manual_seed(21)
+    x = torch.rand(n, f_in, generator=g)
+    a = (torch.rand(n, n, generator=g) < 0.1).float()
+    a = torch.maximum(a, a.t())
+    a.fill_diagonal_(0.0)
+    u = torch.rand(n, n, generator=g)
+    z = torch.randn(n, 16, generator=g)
+    w = torch.randn(n, 16, generator=g)
+    torch.manual_seed(4)
+    model = GraphProposalNetwork(x.to(device), a.to(device), dropout=0.0, add_original=add_original,
+                                 embedding_dim=emb, probs_bias_init=-0.5, probs_factor_init=2.0,
+                                 normalize_similarities=normalize).to(device)
+    p, emb_out = model.calculate_edges_and_embeddings()
+    # dense restatement with the same GCN weights (oracle GCN, dropout 0)
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.gcn.named_parameters()}
+    factor = torch.tensor(2.0, requires_grad=True)
+    bias = torch.tensor(-0.5, requires_grad=True)
+
+    def ref_probs():
+        a_hat = O.normalize_adjacency_matrix(a)
+        h = torch.relu(a_hat @ (x @ params["layer_in.fc.weight"].t() + params["layer_in.fc.bias"]))
+        e_ref = a_hat @ (h @ params["layer_out.fc.weight"].t() + params["layer_out.fc.bias"])
+        sim = O_cos(e_ref) if normalize else e_ref @ e_ref.t()
+        pr = torch.sigmoid(factor * sim + bias)
+        if add_original:
+            pr = pr + a
+        return pr.clamp(0.0, 1.0), e_ref
+
+    def O_cos(m):
+        nrm = m.norm(p=2, dim=1, keepdim=True)
+        return (m @ m.t() / (nrm * nrm.t()).clamp(min=1e-8)).clamp_max(1.0)
+
+    pr, e_ref = ref_probs()
+    assert torch.allclose(emb_out.detach().cpu(), e_ref.detach(), atol=1e-5)
+    assert torch.allclose(p.detach().cpu(), pr.detach(), atol=1e-5)
+
+    graph = Sampler.sample(p, embeddings=emb_out, u_inject=u.to(device))
+    sample = O.to_undirected((u < p.detach().cpu()).float(), from_triu_only=True)
+    ref_a = sample.clone()
+    ref_a.fill_diagonal_(1.0)
+    assert torch.equal(graph.to_dense().cpu(), ref_a)
+    y = ops.aggregate(z.to(device), graph)
+    (y * w.to(device)).sum().backward()
+    _dense_aggregate_loss(O.straight_through_estimator(sample, pr), z, w).backward()
+    assert abs(float(model.probs_factor.grad) - float(factor.grad)) < 1e-4 * max(1.0, abs(float(factor.grad)))
+    assert abs(float(model.probs_bias.grad) - float(bias.grad)) < 1e-4 * max(1.0, abs(float(bias.grad)))
+    for k, v in model.gcn.named_parameters():
+        ref = params[k].grad
+        assert float((v.grad.cpu() - ref).abs().max()) <= 1e-4 * max(1.0, float(ref.abs().max())), k
+
+
+def test_factory_builds_every_model(device):
+    n = 40
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(n, 10, generator=g).to(device)
+    a = (torch.rand(n, n, generator=g) < 0.1).float()
+    a = torch.maximum(a, a.t()).to(device)
+    y = torch.randint(0, 3, (n,), generator=g).to(device)
+    m = torch.ones(n, dtype=torch.bool, device=device)
+    data = DenseData(x=x, y=y, dense_adj=a, train_mask=m, val_mask=m, test_mask=m, num_classes=3)
+    fac = GraphGenerativeModelFactory(data)
+    emb = fac.create("embedding")
+    assert isinstance(emb, PairwiseEmbeddingSampler) and emb.embeddings.shape == (n, 16)
+    assert emb.embeddings.device.type == "cuda"
+    assert type(fac.optimizer(emb)).__name__ == "SGD"
+    gae = fac.create("gae")
+    assert isinstance(gae, GraphProposalNetwork)
+    opt = fac.optimizer(gae)
+    assert len(opt.param_groups) == 2 and opt.param_groups[0]["weight_decay"] == 0.0005
+    with pytest.raises(NotImplementedError):
+        fac.create("nope")
+    # both models sample through the HIP sampler
+    assert emb.sample().n == n and gae.sample().n == n
