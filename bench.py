@@ -64,9 +64,15 @@ def build(args, rank, device):
     torch.manual_seed(args.seed)
     gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(device)
     inner = InnerProblemTrainer(gcn, data, lr=0.01, weight_decay=5e-4)
-    gm = BernoulliGraphModel(data.dense_adj)
-    outer = OuterProblemTrainer(torch.optim.SGD(gm.parameters(), lr=0.1), data, opt_mask, gm,
-                                lr_decay=0.99, grad_reducer=allreduce_mean)
+    if args.graph_model == "lds":
+        gm = BernoulliGraphModel(data.dense_adj)
+        opt = torch.optim.SGD(gm.parameters(), lr=0.1)
+    else:  # the embedding / GAE models: drop-in trainers only
+        from ldsgnn.models.factory import GraphGenerativeModelFactory
+        fac = GraphGenerativeModelFactory(data)
+        gm = fac.create(args.graph_model)
+        opt = fac.optimizer(gm)
+    outer = OuterProblemTrainer(opt, data, opt_mask, gm, lr_decay=0.99, grad_reducer=allreduce_mean)
     return data, BilevelProblemRunner(inner, outer, data), opt_mask
 
 
@@ -165,6 +171,8 @@ def main():
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
                     "for rehearsing several ranks on one device)")
+    ap.add_argument("--graph-model", default="lds", choices=["lds", "embedding", "gae"],
+                    help="graph generative model (embedding / gae: P from node embeddings, autograd path)")
     ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
                     help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
@@ -194,6 +202,8 @@ def main():
         torch.cuda.synchronize()
 
     use_engine = args.path == "engine"
+    if args.graph_model != "lds" and use_engine:
+        raise SystemExit("--graph-model embedding/gae runs on --path autograd (the fused engine is the LDS θ path)")
     if args.kernel == "auto":
         if use_engine and args.samples > 1:
             args.kernel = "lds_theta_grad_ex"
@@ -304,7 +314,7 @@ def main():
                                                                "knn-init") + f"-S{args.samples}-tau{args.tau}", "path": args.path, "nodes": n,
                        "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
-                       "sampled_nnz": nnz, "replicas_in_sync": in_sync,
+                       "sampled_nnz": nnz, "replicas_in_sync": in_sync, "graph_model": args.graph_model,
                        "aggregation": (("bitmask x fixed-point s*Z on int8 MFMA (pre-pass)" if eng.bitmask_agg
                                         else "column-blocked LDS SpMM pre-pass")
                                        if use_engine and eng.long_rows else "in-kernel CSR")},
