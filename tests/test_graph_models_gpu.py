@@ -96,17 +96,6 @@ def test_knn_sparsified_sample_matches_dense(device, metric):
     assert float((ed.grad.cpu() - e_ref.grad).abs().max() / e_ref.grad.abs().max()) < 1e-4
 
 
-def test_knn_dot_metric_is_a_distance():
-    """np.dot passed to sklearn as a metric is read as a distance: the k
-    smallest dot products are the neighbours (src/models/sampling.py:30-32)."""
-    x = torch.tensor([[1.0, 0.0], [2.0, 0.0], [-1.0, 0.0], [0.0, 1.0]])
-    a = knn_graph_dense(x, 1, loop=False, metric="dot")
-    # row 0: dots with rows 1..3 = 2, -1, 0 -> nearest is row 2
-    assert torch.equal(a[0], torch.tensor([0.0, 0.0, 1.0, 0.0]))
-    c = knn_graph_dense(x, 1, loop=False, metric="cosine")
-    assert torch.equal(c[0], torch.tensor([0.0, 1.0, 0.0, 0.0]))
-
-
 @pytest.mark.parametrize("eps,edges", [(0.5, True), (1.0, True), (1.5, False)])
 def test_eps_sparsified_sample(device, eps, edges):
     """EPS zeroes sampled entries < eps: a 0/1 draw survives iff 1 >= eps."""
