@@ -36,6 +36,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
 
 
@@ -162,6 +163,8 @@ def main():
     ap.add_argument("--seed", type=int, default=597905255 % (2 ** 31))
     ap.add_argument("--cpu-steps", type=int, default=11)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--theta-form", default=None, help="θ-grad assembly form (ldsgnn.ops.THETA_GRAD_FORMS; "
+                    "default: bf16x3, the split-bf16 MFMA form picked by shape)")
     ap.add_argument("--kernel", default="auto", help="entry point for the roofline leg (auto: the θ-grad "
                     "assembly the path uses)")
     ap.add_argument("--split", action="store_true", help="engine: per-graph dθ chunks on a side stream beside "
@@ -191,6 +194,9 @@ def main():
 
     import ldsgnn
     from ldsgnn import _native as nat
+    if args.theta_form is not None:
+        from ldsgnn import ops as ldsops
+        ldsops.theta_grad_form(args.theta_form)
 
     data, runner, opt_mask = build(args, rank, device)
     n = data.num_nodes
@@ -290,9 +296,17 @@ def main():
         else:  # one launch per graph: 4 uses (16 + 8 + 8 + 16 columns)
             k = 16 + 8 + 8 + 16
         flops = 4.0 * k * tri
-        achieved = flops / (ksum["avg_us"] * 1e-6) / 1e12
-        roof = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None}
+        fp32_equiv = flops / (ksum["avg_us"] * 1e-6) / 1e12
+        from ldsgnn import ops as ldsops
+        form = ldsops.theta_grad_form()
+        if form == "fp32":
+            roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": fp32_equiv / FP32_PEAK_TFLOPS, "traffic": None}
+        else:  # split-bf16: six bf16 MFMA products per fp32 product, priced against the bf16 dense peak
+            achieved = 6.0 * fp32_equiv
+            roof = {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / BF16_PEAK_TFLOPS, "traffic": None}
+        roof.update(form=form, fp32_equiv_tflops=fp32_equiv)
     roof.update(kernel=args.kernel, avg_us=ksum["avg_us"], launches=ksum["launches"])
     roof["traffic"], roof["traffic_source"] = pmc_traffic(args.kernel, use_engine, world, args)
 

@@ -230,6 +230,17 @@ int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k,
 int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                       int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
                       int mode, const void* scalars, float gscale, void* stream);
+/* Arithmetic form of every θ-gradient assembly above (process-wide; a
+ * captured HIP graph keeps the form it was captured with):
+ *   0 fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains);
+ *   1 split-bf16 MFMA (default), tile shape by problem size: each fp32
+ *     operand as three bf16 words, six v_mfma_f32_32x32x16_bf16 per product
+ *     (fp32 accuracy, |error| <= ~2^-22 |U||V| per term, fp32 accumulation);
+ *   2 split-bf16, 64 × 64 tiles, 16-wide k chunks;  3 the same, 32-wide;
+ *   4 split-bf16, 128 × 128 tiles;  5 the same in XCD-grouped tile order.
+ * form = -1 only reads the current form into *prev (prev may be NULL). */
+int lds_theta_grad_set_form(int form, int* prev);
+
 /* Slot factors for lds_theta_grad from one aggregation Y = ÂZ and its
  * cotangent G (dZ = ÂG):  U = s⊙G, V = s⊙Z, r = -½ s² (G·Y + Z·dZ) rowwise.
  * Columns [f, fpad) of U and V are zero-filled. */

@@ -181,6 +181,23 @@ __device__ __forceinline__ void store4(float (*dst)[kLdsRow], int kq, int row, c
     dst[kq + 3][row] = x.w;
 }
 
+// R_i = Σ_c r[i·ldr + c·ldrc], summed in c order; the loads of four terms are
+// issued together (one wait per four, not one per term: nr = S at S samples).
+__device__ __forceinline__ float row_r_sum(const float* __restrict__ r, int64_t base, int ldrc, int nr) {
+    float acc = 0.f;
+    int c = 0;
+    for (; c + 4 <= nr; c += 4) {
+        const float a0 = r[base + (int64_t)c * ldrc], a1 = r[base + (int64_t)(c + 1) * ldrc];
+        const float a2 = r[base + (int64_t)(c + 2) * ldrc], a3 = r[base + (int64_t)(c + 3) * ldrc];
+        acc += a0;
+        acc += a1;
+        acc += a2;
+        acc += a3;
+    }
+    for (; c < nr; ++c) acc += r[base + (int64_t)c * ldrc];
+    return acc;
+}
+
 // ---------------------------------------------------------------------------
 // MFMA form: C_IJ = U_I V_Jᵀ + V_I U_Jᵀ on fp32-in v_mfma_f32_32x32x2_f32
 // (exact f32 FMA chains, 64 FLOP/clk/SIMD = the fp32 peak with one VGPR per
@@ -237,7 +254,7 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
         const int row = (t < kTile ? i0 : j0) + rr;
         float acc = 0.f;
         if (row < n)
-            for (int c = 0; c < nr; ++c) acc += r[(int64_t)row * ldr + (int64_t)c * ldrc];
+            acc = row_r_sum(r, (int64_t)row * ldr, ldrc, nr);
         (t < kTile ? Ri : Rj)[rr] = acc;
     }
 
@@ -294,6 +311,502 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
         } else {
             grad[idx] = g;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Split-bf16 MFMA form of the same assembly (the default).  Every fp32
+// operand x is cut at staging time into three bf16 words x = x0 + x1 + x2
+// (truncations: x0 = top 8 significand bits, x1 = the next 8 of the exact
+// remainder, x2 = the next 8 of what is left), so x0 + x1 + x2 carries all
+// 24 bits to within one truncation of x2 (≤ 2⁻²³|x|).  A product keeps the
+// six terms down to order 2⁻¹⁶: a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0; the
+// dropped three are ≤ 2⁻²⁴|ab| — fp32 accuracy at fp32 accumulation.  Six
+// v_mfma_f32_32x32x16_bf16 (32 cycles each) replace eight
+// v_mfma_f32_32x32x2_f32 (64 cycles each) per 16-wide k-step: 2.67× fewer
+// MFMA cycles.
+// LDS: 12 planes (U_I, V_I, U_J, V_J × three splits) of [64 rows][KC bf16],
+// row stride KC/2 + 4 dwords (4 × odd: the 16 rows of a ds_read_b128 lane
+// group land on 16 distinct 4-bank slots).  A lane's fragment (row r, 8
+// consecutive k) is one ds_read_b128.  Global loads of chunk c+1 are in
+// flight during chunk c's MFMAs, as in the fp32 form.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Upper halves of two dwords packed (b0 -> low half, b1 -> high half).
+__device__ __forceinline__ uint32_t pack_hi16(uint32_t b0, uint32_t b1) {
+    return __builtin_amdgcn_perm(b1, b0, 0x07060302u);
+}
+
+// Split a pair of fp32 values into three packed bf16 pairs.
+__device__ __forceinline__ void split3_pair(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+    const uint32_t b0 = __float_as_uint(x0), b1 = __float_as_uint(x1);
+    const float r0 = x0 - __uint_as_float(b0 & 0xffff0000u);
+    const float r1 = x1 - __uint_as_float(b1 & 0xffff0000u);
+    const uint32_t c0 = __float_as_uint(r0), c1 = __float_as_uint(r1);
+    const float q0 = r0 - __uint_as_float(c0 & 0xffff0000u);
+    const float q1 = r1 - __uint_as_float(c1 & 0xffff0000u);
+    h = pack_hi16(b0, b1);
+    m = pack_hi16(c0, c1);
+    l = pack_hi16(__float_as_uint(q0), __float_as_uint(q1));
+}
+
+// Zero block that out-of-range lanes load from (rows past n, k past the end).
+__device__ __attribute__((aligned(16))) float g_zero8[8];
+
+template <int KC>
+struct Bf3Stage {
+    // thread t stages row t >> 2 of each block, k = (t & 3)·(KC/4) … + KC/4 - 1
+    static constexpr int kPer = KC / 4;       // fp32 values per thread per array
+    static constexpr int kStr = KC / 2 + 4;   // dwords per LDS row
+    static constexpr int kPlane = 64 * kStr;  // dwords per plane
+    float x[4][kPer];                         // U_I, V_I, U_J, V_J
+};
+
+template <int KC, bool VEC>
+__device__ __forceinline__ void bf3_load(const float* __restrict__ u, const float* __restrict__ v, int ld,
+                                         int k, int n, int gi, int gj, int k0, Bf3Stage<KC>& st) {
+    constexpr int P = Bf3Stage<KC>::kPer;
+    const int gk = k0 + (threadIdx.x & 3) * P;
+    const float* src[4] = {u + (int64_t)gi * ld, v + (int64_t)gi * ld, u + (int64_t)gj * ld,
+                           v + (int64_t)gj * ld};
+    const bool rowok[4] = {gi < n, gi < n, gj < n, gj < n};
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        if constexpr (VEC) {  // branch-free, as in the 128-tile kernel below
+            const float* p = (rowok[a] && gk < k) ? src[a] + gk : g_zero8;
+#pragma unroll
+            for (int q = 0; q < P; q += 4) {
+                const float4 f = *reinterpret_cast<const float4*>(p + q);
+                st.x[a][q] = f.x; st.x[a][q + 1] = f.y; st.x[a][q + 2] = f.z; st.x[a][q + 3] = f.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < P; ++q) st.x[a][q] = (rowok[a] && gk + q < k) ? src[a][gk + q] : 0.f;
+        }
+    }
+}
+
+template <int KC>
+__device__ __forceinline__ void bf3_store(uint32_t* lds, const Bf3Stage<KC>& st) {
+    constexpr int P = Bf3Stage<KC>::kPer;
+    constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane;
+    const int row = threadIdx.x >> 2, kq = threadIdx.x & 3;
+    const int off = row * S + kq * (P / 2);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        uint32_t h[P / 2], m[P / 2], l[P / 2];
+#pragma unroll
+        for (int q = 0; q < P / 2; ++q) split3_pair(st.x[a][2 * q], st.x[a][2 * q + 1], h[q], m[q], l[q]);
+        uint32_t* p0 = lds + (3 * a + 0) * PL + off;
+        uint32_t* p1 = lds + (3 * a + 1) * PL + off;
+        uint32_t* p2 = lds + (3 * a + 2) * PL + off;
+        if constexpr (P == 8) {
+            *reinterpret_cast<u32x4*>(p0) = u32x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u32x4*>(p1) = u32x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u32x4*>(p2) = u32x4{l[0], l[1], l[2], l[3]};
+        } else {
+            *reinterpret_cast<uint2*>(p0) = uint2{h[0], h[1]};
+            *reinterpret_cast<uint2*>(p1) = uint2{m[0], m[1]};
+            *reinterpret_cast<uint2*>(p2) = uint2{l[0], l[1]};
+        }
+    }
+}
+
+template <int KC, bool VEC>
+__global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
+    float gscale) {
+    constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[12 * PL];
+    __shared__ float Ri[kTile], Rj[kTile];
+
+    int a, b;
+    tri_tile(blockIdx.x, a, b);
+    const int i0 = b * kTile, j0 = a * kTile;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int64_t nn = n;
+    const int lj = wc * 32 + (lane & 31);
+    const int j = j0 + lj;
+
+    const int gi = i0 + (t >> 2), gj = j0 + (t >> 2);
+    Bf3Stage<KC> st;
+    if (k > 0) bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, 0, st);
+
+    float th[16], part[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int i = i0 + wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const bool in = i < n && j < n && j >= i;
+        const int64_t idx = in ? tri_index(i, i, nn) + (j - i) : 0;
+        th[e] = (in && theta != nullptr) ? theta[idx] : 0.f;
+        part[e] = (in && (mode == 1 || mode == 3)) ? grad[idx] : 0.f;
+    }
+
+    if (t < 2 * kTile) {
+        const int rr = t & (kTile - 1);
+        const int row = (t < kTile ? i0 : j0) + rr;
+        float acc = 0.f;
+        if (row < n)
+            acc = row_r_sum(r, (int64_t)row * ldr, ldrc, nr);
+        (t < kTile ? Ri : Rj)[rr] = acc;
+    }
+
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+
+    // fragment offsets (dwords): row (wave's 32-row half + lane & 31), k-half 8·(lane >> 5)
+    const int ra = (wr * 32 + (lane & 31)) * S + 4 * (lane >> 5);
+    const int rb = (wc * 32 + (lane & 31)) * S + 4 * (lane >> 5);
+    for (int k0 = 0; k0 < k; k0 += KC) {
+        __syncthreads();
+        bf3_store<KC>(lds, st);
+        __syncthreads();
+        if (k0 + KC < k) bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, k0 + KC, st);
+#pragma unroll
+        for (int kk = 0; kk < KC; kk += 16) {
+            if (k0 + kk < k) {  // zero-filled past k: whole k-steps beyond it are skipped
+                const int o = kk / 2;
+                bf16x8 fa[3], fb[3];
+                // U_I × V_J
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    fa[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (0 + s) * PL + ra + o));
+                    fb[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (9 + s) * PL + rb + o));
+                }
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc, 0, 0, 0);
+                // V_I × U_J
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    fa[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (3 + s) * PL + ra + o));
+                    fb[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (6 + s) * PL + rb + o));
+                }
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc, 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();
+
+    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int li = wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int i = i0 + li;
+        if (i >= n || j >= n || j < i) continue;
+        const int64_t idx = tri_index(i, i, nn) + (j - i);
+        float g = 0.f;
+        if (j > i) {
+            const float gs = gscale * (acc[e] + Ri[li] + Rj[lj]);
+            g = mode == 3 ? part[e] + gs : gs;
+            if (theta != nullptr && !(th[e] >= 0.f && th[e] <= 1.f)) g = 0.f;  // clamp backward
+        }
+        if (mode == 3) {
+            grad[idx] = g;
+            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
+        } else if (mode == 2) {
+            if (grad != nullptr) grad[idx] = g;
+            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
+        } else if (mode == 1) {
+            grad[idx] = part[e] + g;
+        } else {
+            grad[idx] = g;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Split-bf16, 128 × 128 tiles: the 64 × 64 forms above re-read U and V once
+// per 64 output columns, 16 fp32-equivalent flop per staged byte, and at
+// n = 20 000 (42 MB of U, V against a 4 MB L2 per XCD) that stream from the
+// Infinity Cache, not the MFMAs, sets the time.  Here a 256-thread block owns
+// a 128 × 128 tile (each wave a 64 × 64 quarter: 2 × 2 accumulators of
+// 32 × 32), staging 16-wide k chunks of the 12 bf16 planes (72 KB of LDS,
+// 2 blocks per CU): 32 flop per byte, 48 MFMAs per wave between barriers.
+// Tile order (`group` > 0): the triangle's block columns are cut into strips
+// of `group` columns, a strip enumerated row block by row block, and each XCD
+// (blocks b, b + 8, … share one) takes a contiguous range of that order, so
+// the ≈64 tiles an XCD runs at once span ≈8 row blocks × `group` column
+// blocks and share their U, V rows in its L2.
+// ---------------------------------------------------------------------------
+constexpr int kT2 = 128;
+constexpr int kS2 = 12;             // dwords per LDS row (8 data + 4 pad: 4 × odd)
+constexpr int kPL2 = kT2 * kS2;     // dwords per plane
+
+__device__ __forceinline__ void grouped_tile(int L, int nb, int G, int& bi, int& bj) {
+    // strips s of columns [sG, sG + g), g = min(G, nb - sG); tiles before strip s: T(sG)
+    int s = 0;
+    while (true) {
+        const int c1 = min((s + 1) * G, nb);
+        const int before_next = c1 * (c1 + 1) / 2;
+        if (L < before_next) break;
+        ++s;
+    }
+    const int c0 = s * G, g = min(G, nb - c0);
+    int rem = L - c0 * (c0 + 1) / 2;
+    if (rem < c0 * g) {  // rows above the strip's diagonal: g tiles each
+        bi = rem / g;
+        bj = c0 + rem % g;
+        return;
+    }
+    rem -= c0 * g;
+    int i = c0;          // diagonal part: row c0 + q has g - q tiles
+    while (rem >= c0 + g - i) {
+        rem -= c0 + g - i;
+        ++i;
+    }
+    bi = i;
+    bj = i + rem;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
+    float gscale, int group, int per_xcd) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[12 * kPL2];
+    __shared__ float Ri[kT2], Rj[kT2];
+
+    const int nb = (n + kT2 - 1) / kT2;
+    const int ntiles = nb * (nb + 1) / 2;
+    int bi, bj;
+    if (group > 0) {
+        const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+        if (L >= ntiles) return;  // whole block: no barrier reached
+        grouped_tile(L, nb, group, bi, bj);
+    } else {
+        int a, b;
+        tri_tile(blockIdx.x, a, b);
+        bi = b;
+        bj = a;
+    }
+    const int i0 = bi * kT2, j0 = bj * kT2;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int64_t nn = n;
+
+    // staging: thread t owns row t >> 1 of both blocks, k = 8·(t & 1) … + 7 of the chunk
+    const int srow = t >> 1, sk = (t & 1) * 8;
+    const int gi = i0 + srow, gj = j0 + srow;
+    const float* src[4] = {u + (int64_t)gi * ld, v + (int64_t)gi * ld, u + (int64_t)gj * ld,
+                           v + (int64_t)gj * ld};
+    const bool rowok[4] = {gi < n, gi < n, gj < n, gj < n};
+    // two register sets: chunk c + 2 loads while chunk c is staged and computed
+    float xa[4][8], xb[4][8];
+    // VEC (k % 8 == 0, 16-byte aligned rows): branch-free — rows past n and k
+    // past the end load from a zero block instead, so nothing consumes the
+    // loaded values before the next barrier and the next chunk's loads stay in
+    // flight through this chunk's MFMAs (divergent load paths, or a select on
+    // the loaded value, made the compiler wait on them right away).
+    auto load = [&](float (&x)[4][8], int k0) {
+        const int gk = k0 + sk;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            if constexpr (VEC) {
+                const float* p = (rowok[a] && gk < k) ? src[a] + gk : g_zero8;
+                const float4 f0 = *reinterpret_cast<const float4*>(p);
+                const float4 f1 = *reinterpret_cast<const float4*>(p + 4);
+                x[a][0] = f0.x; x[a][1] = f0.y; x[a][2] = f0.z; x[a][3] = f0.w;
+                x[a][4] = f1.x; x[a][5] = f1.y; x[a][6] = f1.z; x[a][7] = f1.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[a][q] = (rowok[a] && gk + q < k) ? src[a][gk + q] : 0.f;
+            }
+        }
+    };
+    if (k > 0) load(xa, 0);
+    if (k > 16) load(xb, 16);
+
+    if (t < 2 * kT2) {
+        const int rr = t & (kT2 - 1);
+        const int row = (t < kT2 ? i0 : j0) + rr;
+        float acc = 0.f;
+        if (row < n)
+            acc = row_r_sum(r, (int64_t)row * ldr, ldrc, nr);
+        (t < kT2 ? Ri : Rj)[rr] = acc;
+    }
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[m][q][e] = 0.f;
+
+    const int soff = srow * kS2 + (t & 1) * 4;
+    const int fo = 4 * (lane >> 5);
+    const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
+    const int rb0 = (wc * 64 + (lane & 31)) * kS2 + fo, rb1 = rb0 + 32 * kS2;
+    auto stage = [&](const float (&x)[4][8]) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            uint32_t h[4], m[4], l[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) split3_pair(x[a][2 * q], x[a][2 * q + 1], h[q], m[q], l[q]);
+            *reinterpret_cast<u32x4*>(lds + (3 * a + 0) * kPL2 + soff) = u32x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u32x4*>(lds + (3 * a + 1) * kPL2 + soff) = u32x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u32x4*>(lds + (3 * a + 2) * kPL2 + soff) = u32x4{l[0], l[1], l[2], l[3]};
+        }
+    };
+    auto compute = [&]() {
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {  // pr 0: U_I × V_J (planes 0-2, 9-11); pr 1: V_I × U_J (3-5, 6-8)
+            const int pa = pr == 0 ? 0 : 3, pb = pr == 0 ? 9 : 6;
+            bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                fa[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pa + s) * kPL2 + ra0));
+                fa[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pa + s) * kPL2 + ra1));
+                fb[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pb + s) * kPL2 + rb0));
+                fb[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pb + s) * kPL2 + rb1));
+            }
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    f32x16 c = acc[m][q];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][1], fb[q][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[q][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][2], fb[q][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[q][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][1], fb[q][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[q][0], c, 0, 0, 0);
+                    acc[m][q] = c;
+                }
+        }
+    };
+    for (int k0 = 0; k0 < k; k0 += 32) {
+        __syncthreads();  // the previous chunk's fragment reads are done
+        stage(xa);
+        __syncthreads();
+        if (k0 + 32 < k) load(xa, k0 + 32);
+        compute();
+        if (k0 + 16 >= k) break;
+        __syncthreads();
+        stage(xb);
+        __syncthreads();
+        if (k0 + 48 < k) load(xb, k0 + 48);
+        compute();
+    }
+    // Epilogue: every θ (and partial-grad) operand of the wave's 64 outputs is
+    // loaded before the first store — a load after a store to the same array
+    // cannot be hoisted above it, and per-element load → store chains cost one
+    // memory latency each (1.1 ms of 2.5 at n = 20 000 before this).
+    const bool need_part = mode == 1 || mode == 3;
+    float th[2][2][16], part[2][2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = j0 + wc * 64 + q * 32 + (lane & 31);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int i = i0 + wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const bool in = i < n && j < n && j >= i;
+                const int64_t id = in ? tri_index(i, i, nn) + (j - i) : 0;
+                th[m][q][e] = (in && theta != nullptr) ? theta[id] : 0.f;
+                part[m][q][e] = (in && need_part) ? grad[id] : 0.f;
+            }
+        }
+    __syncthreads();  // Ri / Rj written by other waves
+
+    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int lj = wc * 64 + q * 32 + (lane & 31);
+            const int j = j0 + lj;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const int i = i0 + li;
+                if (i >= n || j >= n || j < i) continue;
+                const int64_t id = tri_index(i, i, nn) + (j - i);
+                const float t0 = th[m][q][e];
+                float g = 0.f;
+                if (j > i) {
+                    const float gs = gscale * (acc[m][q][e] + Ri[li] + Rj[lj]);
+                    g = mode == 3 ? part[m][q][e] + gs : gs;
+                    if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+                }
+                if (mode == 3) {
+                    grad[id] = g;
+                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                } else if (mode == 2) {
+                    if (grad != nullptr) grad[id] = g;
+                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                } else if (mode == 1) {
+                    grad[id] = part[m][q][e] + g;
+                } else {
+                    grad[id] = g;
+                }
+            }
+        }
+}
+
+// Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
+// shape (below), 2 = 64-tile with 16-wide k chunks, 3 = 64-tile with 32-wide
+// k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
+// order.  Read at launch (a captured HIP graph keeps the form it was
+// captured with).
+static int g_theta_form = 1;
+constexpr int kGroup = 8;
+
+static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const float* v, int ld, int k,
+                              const float* r, int ldr, int nr, float* theta, int n, float* grad, int mode,
+                              const double* lr, int vec4, int ldrc, float gscale) {
+    int form = g_theta_form;
+    const int nb2 = (n + kT2 - 1) / kT2;
+    const int nt2 = nb2 * (nb2 + 1) / 2;
+    // by shape (tools/thetagrad_forms.py, MI355X): 64-tiles while the 128-tile
+    // grid cannot fill the chip with short k (Cora S = 1: 48 vs 65 µs);
+    // 128-tiles in XCD-grouped order for long k (Cora / Citeseer S = 16:
+    // 577 / 695 vs 604 / 895 µs) or large n (n = 20 000: 2.01 vs 2.27 ms)
+    if (form == 1) form = (nt2 >= 1024 || k >= 1024) ? 5 : 2;
+    // the branch-free staging needs whole 8-wide k groups in 16-byte aligned rows
+    const bool fast = vec4 && (k & 7) == 0;
+#define LDS_TG_ARGS u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, vec4, ldrc, gscale
+    if (form == 4 || form == 5) {
+        const int per = (nt2 + 7) / 8;
+        const int grid = form == 5 ? 8 * per : nt2;
+        const int grp = form == 5 ? kGroup : 0;
+        if (fast)
+            hipLaunchKernelGGL(theta_grad_bf3_t128_kernel<true>, dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
+        else
+            hipLaunchKernelGGL(theta_grad_bf3_t128_kernel<false>, dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
+    } else if (form == 3) {
+        if (fast)
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+        else
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+    } else if (form == 2) {
+        if (fast)
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+        else
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+#undef LDS_TG_ARGS
+    } else {
+        hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, st, u, v, ld, k, r, ldr, nr,
+                           theta, n, grad, mode, lr, vec4, ldrc, gscale);
     }
 }
 
@@ -377,9 +890,7 @@ extern "C" int lds_theta_grad(const float* u, const float* v, int ld, int k, con
     const int nb = (n + kTile - 1) / kTile;
     const int ntiles = nb * (nb + 1) / 2;
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
-    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
-                       v, ld, k, r, ldr, nr, const_cast<float*>(theta), n, grad, accumulate ? 1 : 0,
-                       (const double*)nullptr, vec4, 1, 1.0f);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, const_cast<float*>(theta), n, grad, accumulate ? 1 : 0, (const double*)nullptr, vec4, 1, 1.0f);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -408,8 +919,7 @@ extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     // EngineScalars: f64 outer_lr at byte offset 16
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
-    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
-                       v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4, 1, 1.0f);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4, 1, 1.0f);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -423,8 +933,7 @@ extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, 
     const int ntiles = nb * (nb + 1) / 2;
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
-    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u,
-                       v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4, 1, 1.0f);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4, 1, 1.0f);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -445,9 +954,15 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
     //  4-wave block per CU; at n = 20 000 (12 k tiles) 3.12 ms against 2.27 ms,
     //  196 VGPRs and 66 KB LDS leave 2 waves per SIMD.  MFMA busy of this form
     //  at S = 16 is 63 % of the cycles at a 2.26 GHz DVFS clock, r01 PMC)
-    hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream, u, v, ld, k, r,
-                       ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale);
     LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_set_form(int form, int* prev) {
+    LDS_CHECK_ARG(form >= -1 && form <= 5);
+    if (prev != nullptr) *prev = g_theta_form;
+    if (form >= 0) g_theta_form = form;
+    return 0;
 }
 
 extern "C" int lds_slot_factors(const float* g, int ldg, const float* z, int ldz, const float* y,

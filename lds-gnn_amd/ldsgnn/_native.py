@@ -47,6 +47,7 @@ SIGNATURES = {
     "lds_aggregate_bitmask": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
+    "lds_theta_grad_set_form": [c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
     "lds_theta_grad_sgd_accum": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
     "lds_slot_factors": [P, c_int, P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, P, c_int, P,

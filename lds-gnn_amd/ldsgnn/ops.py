@@ -18,6 +18,7 @@ never need their own gradient ("closure of the kernel set").
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Tuple
 
 import torch
@@ -423,6 +424,24 @@ def theta_grad(u: torch.Tensor, v: torch.Tensor, r: torch.Tensor, n: int,
     return out
 
 
+THETA_GRAD_FORMS = {"fp32": 0, "bf16x3": 1, "bf16x3-t64k16": 2, "bf16x3-t64k32": 3, "bf16x3-t128": 4,
+                    "bf16x3-t128-grouped": 5}
+
+
+def theta_grad_form(form: Optional[str] = None) -> str:
+    """Select the θ-gradient assembly's arithmetic form (lds_theta_grad_set_form):
+    "bf16x3" (default: fp32 operands split into three bf16 words, six bf16
+    MFMAs per product, fp32 accuracy; tile shape chosen by problem size), one
+    pinned split-bf16 variant (64-tiles with 16- or 32-wide k chunks, 128-tiles
+    in plain or XCD-grouped order), or "fp32" (fp32-in MFMA).
+    Returns the previous form.  Process-wide; HIP graphs keep the form they
+    were captured with."""
+    prev = ctypes.c_int(0)
+    code = -1 if form is None else THETA_GRAD_FORMS[form]
+    nat.call("lds_theta_grad_set_form", code, ctypes.addressof(prev))
+    return {v: k for k, v in THETA_GRAD_FORMS.items()}[prev.value]
+
+
 def philox_uniform(seed: int, tag: int, counter: int, rows: int, cols: int,
                    device="cuda") -> torch.Tensor:
     out = torch.empty((rows, cols), dtype=torch.float32, device=device)
@@ -432,5 +451,5 @@ def philox_uniform(seed: int, tag: int, counter: int, rows: int, cols: int,
 
 __all__ = [
     "CsrGraph", "SampledGraph", "sample_graph_from_triu", "csr_graph_from_dense", "aggregate",
-    "keyed_dropout", "sgd_clamp_", "theta_grad", "philox_uniform", "TAG_DROP_X", "TAG_DROP_H",
+    "keyed_dropout", "sgd_clamp_", "theta_grad", "theta_grad_form", "philox_uniform", "TAG_DROP_X", "TAG_DROP_H",
 ]

@@ -369,3 +369,61 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
                 for k in range(64):
                     pc += (x >> k) & 1
             assert torch.equal(deg[gi, b].long(), pc), (gi, b)
+
+
+@pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16", "bf16x3-t64k32", "bf16x3-t128",
+                                  "bf16x3-t128-grouped", "fp32"])
+@pytest.mark.parametrize("n,k,ld,mode", [(1, 4, 4, 0), (65, 17, 17, 0), (130, 33, 35, 1), (200, 0, 4, 0),
+                                         (257, 48, 48, 2), (300, 264, 264, 3), (129, 1030, 1032, 0),
+                                         (1100, 40, 40, 3)])
+def test_theta_grad_forms_vs_dense(device, form, n, k, ld, mode):
+    """Every arithmetic form of the θ-grad assembly (fp32 MFMA; split-bf16 with
+    32- and 16-wide k chunks) against the dense fp64 formula, across modes,
+    ragged k (partial chunks and k-steps), an unaligned row stride (scalar
+    staging), k = 0 (R only) and n = 1.  Tolerance 1e-5 × max |g| (north_star's
+    fp32 tolerance; split-bf16 keeps products to ~2⁻²² relative)."""
+    g = torch.Generator().manual_seed(7 * n + k)
+    ub = torch.randn(n, ld, generator=g)
+    vb = torch.randn(n, ld, generator=g) * 0.3
+    r = torch.randn(2, n, generator=g)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    theta[::9] = -0.5
+    u, v = ub[:, :k], vb[:, :k]
+    ud, vd, rd = u.double(), v.double(), r.double().sum(0)
+    mfull = ud @ vd.t() + vd @ ud.t() + rd[:, None] + rd[None, :]
+    iu = torch.triu_indices(n, n)
+    ref = mfull[iu[0], iu[1]]
+    ref[iu[0] == iu[1]] = 0.0
+    ref[(theta.double() < 0) | (theta.double() > 1)] = 0.0
+    base = torch.randn(n * (n + 1) // 2, generator=g)
+    grad = base.clone().to(device)
+    th = theta.clone().to(device)
+    lr = 0.05
+    scal = torch.zeros(32, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(lr)
+    ub_, vb_, r_ = ub.to(device), vb.to(device), r.to(device)
+    prev = ops.theta_grad_form(form)
+    try:
+        nat.call("lds_theta_grad_ex", nat.ptr(ub_), nat.ptr(vb_), ld, k, nat.ptr(r_), 1, n, 2, nat.ptr(th), n,
+                 nat.ptr(grad), mode, nat.ptr(scal), 1.0, nat.stream_of(th.device))
+        torch.cuda.synchronize()
+    finally:
+        assert ops.theta_grad_form(prev) == form
+    tol = 1e-5 * max(float(ref.abs().max()), 1.0)
+    got = grad.cpu().double()
+    if mode == 1:
+        got = got - base.double()
+    elif mode == 3:
+        ref = ref + base.double()
+        ref[(theta.double() < 0) | (theta.double() > 1)] = 0.0
+        ref[iu[0] == iu[1]] = 0.0  # mode 3 writes g (0 on the diagonal), not grad + g
+    assert float((got - ref).abs().max()) < tol
+    if mode >= 2:
+        want = (theta.double() - lr * ref).clamp(0, 1)
+        assert float((th.cpu().double() - want).abs().max()) < 1e-5
+
+
+def test_theta_grad_form_default_and_errors(device):
+    assert ops.theta_grad_form() == "bf16x3"
+    with pytest.raises(nat.NativeError):
+        nat.call("lds_theta_grad_set_form", 6, 0)

@@ -1,0 +1,99 @@
+"""θ-gradient assembly: the fp32-MFMA form against the split-bf16 forms.
+
+Times lds_theta_grad_ex (mode 2: fused SGD + clamp, the engine's call) with
+HIP events at the shapes the engine launches — Cora S = 1 (n = 2708,
+k = 264), Cora S = 16 (k = 4224), Citeseer S = 16 (n = 3327), config 5
+(n = 20 000, k = 264) — and checks every form's gradient (mode 0) against an
+fp64 restatement on sampled rows.  Prints one JSON line per shape."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "lds-gnn_amd")):
+    sys.path.insert(0, p)
+import torch  # noqa: E402
+
+import ldsgnn  # noqa: E402,F401
+from ldsgnn import _native as nat  # noqa: E402
+from ldsgnn import ops  # noqa: E402
+
+FP32_PEAK_TF = 157.3
+BF16_PEAK_TF = 2500.0
+FORMS = ("fp32", "bf16x3-t64k16", "bf16x3-t64k32", "bf16x3-t128", "bf16x3-t128-grouped")
+
+
+def time_it(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return 1000.0 * a.elapsed_time(b) / reps  # µs
+
+
+def run(name, n, k, S, reps):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(n + k)
+    u = torch.randn((n, k), generator=g, device=dev)
+    v = torch.randn((n, k), generator=g, device=dev) * 0.1
+    r = torch.randn((S, n), generator=g, device=dev)
+    m = n * (n + 1) // 2
+    theta0 = torch.rand(m, generator=g, device=dev)
+    theta = theta0.clone()
+    grad = torch.empty(m, device=dev)
+    scal = torch.zeros(32, dtype=torch.uint8, device=dev)
+    scal[16:24].view(torch.float64).fill_(1e-9)
+    st = nat.stream_of(dev)
+    gs = 1.0 / S
+
+    def call(mode):
+        nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, S, nat.ptr(theta), n,
+                 nat.ptr(grad), mode, nat.ptr(scal), gs, st)
+
+    rows = torch.randint(0, n, (12,), generator=g, device=dev).tolist()
+    ud, vd, rd = u.double(), v.double(), r.double().sum(0)
+    flop = 4.0 * k * m
+    out = {"workload": name, "n": n, "k": k, "samples": S, "flop_per_launch": flop}
+    prev = ops.theta_grad_form()
+    try:
+        for form in FORMS:
+            ops.theta_grad_form(form)
+            t = time_it(lambda: call(2), reps)
+            theta.copy_(theta0)
+            call(0)
+            torch.cuda.synchronize()
+            err = 0.0
+            for i in rows:
+                base = i * (2 * n - i + 1) // 2
+                ref = gs * (ud[i] @ vd[i:].T + vd[i] @ ud[i:].T + rd[i] + rd[i:])
+                ref[0] = 0.0
+                got = grad[base:base + n - i].double()
+                err = max(err, float((got - ref).abs().max() / ref.abs().max()))
+            bf = 6.0 if form != "fp32" else 1.0
+            out[form] = {"avg_us": t, "fp32_equiv_TFs": flop / t / 1e6,
+                         "mfma_frac": (flop / t / 1e6) / FP32_PEAK_TF if form == "fp32"
+                         else (bf * flop / t / 1e6) / BF16_PEAK_TF,
+                         "max_rel_vs_fp64_rows": err}
+    finally:
+        ops.theta_grad_form(prev)
+    best = min(FORMS[1:], key=lambda f: out[f]["avg_us"])
+    out["best"] = best
+    out["speedup_best_vs_fp32"] = out["fp32"]["avg_us"] / out[best]["avg_us"]
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    shapes = [("cora-S1", 2708, 264, 1, 50), ("cora-S16", 2708, 4224, 16, 10),
+              ("citeseer-S16", 3327, 4224, 16, 10), ("synthetic20k-S1", 20000, 264, 1, 5)]
+    only = sys.argv[1:]
+    for name, n, k, S, reps in shapes:
+        if not only or name in only:
+            run(name, n, k, S, reps)
+
+
+if __name__ == "__main__":
+    main()
