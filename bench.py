@@ -126,7 +126,12 @@ def pmc_traffic(kernel, use_engine, world, args):
             not os.path.exists(PMC_RECORD):
         return None, None
     with open(PMC_RECORD) as f:
-        rec = json.load(f).get(KERNEL_SYMBOL[kernel])
+        recs = json.load(f)
+    if "theta_grad" in kernel:  # whichever θ-grad kernel the form in force launched (one per record)
+        names = [k for k in recs if "theta_grad" in k]
+        rec = recs[names[0]] if len(names) == 1 else None
+    else:
+        rec = recs.get(KERNEL_SYMBOL[kernel])
     if rec is None:
         return None, None
     return rec["traffic_bytes"], os.path.relpath(PMC_RECORD, ROOT)
