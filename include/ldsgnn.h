@@ -237,7 +237,8 @@ int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float
  *     operand as three bf16 words, six v_mfma_f32_32x32x16_bf16 per product
  *     (fp32 accuracy, |error| <= ~2^-22 |U||V| per term, fp32 accumulation);
  *   2 split-bf16, 64 × 64 tiles, 16-wide k chunks;  3 the same, 32-wide;
- *   4 split-bf16, 128 × 128 tiles;  5 the same in XCD-grouped tile order.
+ *   4 split-bf16, 128 × 128 tiles;  5 the same in XCD-grouped tile order;
+ *   6 form 2 in XCD-grouped tile order.
  * form = -1 only reads the current form into *prev (prev may be NULL). */
 int lds_theta_grad_set_form(int form, int* prev);
 

@@ -414,18 +414,54 @@ __device__ __forceinline__ void bf3_store(uint32_t* lds, const Bf3Stage<KC>& st)
     }
 }
 
+// Linear id L of the XCD-grouped order -> upper-triangle block (bi <= bj):
+// the nb block columns are cut into strips of G, a strip enumerated row block
+// by row block (G tiles per row above its diagonal block, fewer on it).
+__device__ __forceinline__ void grouped_tile(int L, int nb, int G, int& bi, int& bj) {
+    // strips s of columns [sG, sG + g), g = min(G, nb - sG); tiles before strip s: T(sG)
+    int s = 0;
+    while (true) {
+        const int c1 = min((s + 1) * G, nb);
+        const int before_next = c1 * (c1 + 1) / 2;
+        if (L < before_next) break;
+        ++s;
+    }
+    const int c0 = s * G, g = min(G, nb - c0);
+    int rem = L - c0 * (c0 + 1) / 2;
+    if (rem < c0 * g) {  // rows above the strip's diagonal: g tiles each
+        bi = rem / g;
+        bj = c0 + rem % g;
+        return;
+    }
+    rem -= c0 * g;
+    int i = c0;          // diagonal part: row c0 + q has g - q tiles
+    while (rem >= c0 + g - i) {
+        rem -= c0 + g - i;
+        ++i;
+    }
+    bi = i;
+    bj = i + rem;
+}
+
 template <int KC, bool VEC>
 __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
-    float gscale) {
+    float gscale, int group, int per_xcd) {
     constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane;
     __shared__ __attribute__((aligned(16))) uint32_t lds[12 * PL];
     __shared__ float Ri[kTile], Rj[kTile];
 
     int a, b;
-    tri_tile(blockIdx.x, a, b);
+    if (group > 0) {  // XCD-grouped order, as in the 128-tile kernel below
+        const int nb = (n + kTile - 1) / kTile;
+        const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+        if (L >= nb * (nb + 1) / 2) return;  // whole block: no barrier reached
+        grouped_tile(L, nb, group, b, a);
+    } else {
+        tri_tile(blockIdx.x, a, b);
+    }
     const int i0 = b * kTile, j0 = a * kTile;
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
@@ -547,32 +583,6 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
 constexpr int kT2 = 128;
 constexpr int kS2 = 12;             // dwords per LDS row (8 data + 4 pad: 4 × odd)
 constexpr int kPL2 = kT2 * kS2;     // dwords per plane
-
-__device__ __forceinline__ void grouped_tile(int L, int nb, int G, int& bi, int& bj) {
-    // strips s of columns [sG, sG + g), g = min(G, nb - sG); tiles before strip s: T(sG)
-    int s = 0;
-    while (true) {
-        const int c1 = min((s + 1) * G, nb);
-        const int before_next = c1 * (c1 + 1) / 2;
-        if (L < before_next) break;
-        ++s;
-    }
-    const int c0 = s * G, g = min(G, nb - c0);
-    int rem = L - c0 * (c0 + 1) / 2;
-    if (rem < c0 * g) {  // rows above the strip's diagonal: g tiles each
-        bi = rem / g;
-        bj = c0 + rem % g;
-        return;
-    }
-    rem -= c0 * g;
-    int i = c0;          // diagonal part: row c0 + q has g - q tiles
-    while (rem >= c0 + g - i) {
-        rem -= c0 + g - i;
-        ++i;
-    }
-    bi = i;
-    bj = i + rem;
-}
 
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
@@ -766,7 +776,7 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
 // Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
 // shape (below), 2 = 64-tile with 16-wide k chunks, 3 = 64-tile with 32-wide
 // k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
-// order.  Read at launch (a captured HIP graph keeps the form it was
+// order, 6 = form 2 in XCD-grouped order.  Read at launch (a captured HIP graph keeps the form it was
 // captured with).
 static int g_theta_form = 1;
 constexpr int kGroup = 8;
@@ -777,11 +787,12 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
     int form = g_theta_form;
     const int nb2 = (n + kT2 - 1) / kT2;
     const int nt2 = nb2 * (nb2 + 1) / 2;
-    // by shape (tools/thetagrad_forms.py, MI355X): 64-tiles while the 128-tile
-    // grid cannot fill the chip with short k (Cora S = 1: 48 vs 65 µs);
+    // by shape (tools/thetagrad_forms.py, MI355X): 64-tiles in XCD-grouped
+    // order while the 128-tile grid cannot fill the chip with short k (Cora
+    // S = 1: 44.7 vs 65 µs; 46.8 in plain order);
     // 128-tiles in XCD-grouped order for long k (Cora / Citeseer S = 16:
     // 577 / 695 vs 604 / 895 µs) or large n (n = 20 000: 2.01 vs 2.27 ms)
-    if (form == 1) form = (nt2 >= 1024 || k >= 1024) ? 5 : 2;
+    if (form == 1) form = (nt2 >= 1024 || k >= 1024) ? 5 : 6;
     // the branch-free staging needs whole 8-wide k groups in 16-byte aligned rows
     const bool fast = vec4 && (k & 7) == 0;
 #define LDS_TG_ARGS u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, vec4, ldrc, gscale
@@ -795,14 +806,17 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
             hipLaunchKernelGGL(theta_grad_bf3_t128_kernel<false>, dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
     } else if (form == 3) {
         if (fast)
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0);
         else
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
-    } else if (form == 2) {
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0);
+    } else if (form == 2 || form == 6) {
+        const int per = (ntiles + 7) / 8;
+        const int grid = form == 6 ? 8 * per : ntiles;
+        const int grp = form == 6 ? kGroup : 0;
         if (fast)
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
         else
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS);
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
 #undef LDS_TG_ARGS
     } else {
         hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, st, u, v, ld, k, r, ldr, nr,
@@ -959,7 +973,7 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
 }
 
 extern "C" int lds_theta_grad_set_form(int form, int* prev) {
-    LDS_CHECK_ARG(form >= -1 && form <= 5);
+    LDS_CHECK_ARG(form >= -1 && form <= 6);
     if (prev != nullptr) *prev = g_theta_form;
     if (form >= 0) g_theta_form = form;
     return 0;

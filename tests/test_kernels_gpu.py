@@ -371,8 +371,8 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
             assert torch.equal(deg[gi, b].long(), pc), (gi, b)
 
 
-@pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16", "bf16x3-t64k32", "bf16x3-t128",
-                                  "bf16x3-t128-grouped", "fp32"])
+@pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16", "bf16x3-t64k16-grouped", "bf16x3-t64k32",
+                                  "bf16x3-t128", "bf16x3-t128-grouped", "fp32"])
 @pytest.mark.parametrize("n,k,ld,mode", [(1, 4, 4, 0), (65, 17, 17, 0), (130, 33, 35, 1), (200, 0, 4, 0),
                                          (257, 48, 48, 2), (300, 264, 264, 3), (129, 1030, 1032, 0),
                                          (1100, 40, 40, 3)])
@@ -426,4 +426,4 @@ def test_theta_grad_forms_vs_dense(device, form, n, k, ld, mode):
 def test_theta_grad_form_default_and_errors(device):
     assert ops.theta_grad_form() == "bf16x3"
     with pytest.raises(nat.NativeError):
-        nat.call("lds_theta_grad_set_form", 6, 0)
+        nat.call("lds_theta_grad_set_form", 7, 0)
