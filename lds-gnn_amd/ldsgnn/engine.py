@@ -346,6 +346,14 @@ class LdsEngine:
         averaged over samples; one host sync.  Single-sample engines."""
         if self.S != 1:
             raise NotImplementedError("empirical_mean runs on single-sample engines")
+        if not self.long_rows:
+            return self._empirical_mean_batched(flat, n_samples, val_mask, test_mask)
+        return self._empirical_mean_seq(flat, n_samples, val_mask, test_mask)
+
+    def _empirical_mean_seq(self, flat: torch.Tensor, n_samples: int, val_mask: torch.Tensor,
+                            test_mask: torch.Tensor):
+        """empirical_mean one evaluation graph at a time (long rows: the
+        aggregation pre-pass buffers are single-sample)."""
         st, n, c = self._stream(), self.n, self.c
         if getattr(self, "_eval", None) is None:
             self._eval = _Slot(n, self.cap, self.dev, x_nnz=0, samples=1, bptr_len=self.bptr_len, words=self.words)
@@ -367,6 +375,44 @@ class LdsEngine:
             sums.append(torch.stack([sl.lossrow[0].sum(), sl.corrrow[0].sum(), self._eval_rows[0].sum(),
                                      self._eval_rows[1].sum()]))
         host = torch.stack(sums).double().cpu().numpy()
+        return (float(np.mean(host[:, 0] * inv_v)), float(np.mean(host[:, 1] * inv_v)),
+                float(np.mean(host[:, 2] * inv_t)), float(np.mean(host[:, 3] * inv_t)))
+
+    def _empirical_mean_batched(self, flat: torch.Tensor, n_samples: int, val_mask: torch.Tensor,
+                                test_mask: torch.Tensor):
+        """empirical_mean with the n_samples evaluation graphs as one batch
+        (short rows): one lds_sample_graphs_multi launch set draws them with
+        the counters the sequential draws would take (graph g: counter
+        base + pending + g), and every eval-mode forward kernel runs once with
+        grid.y = sample over LdsBatch strides whose parameter stride is 0 (all
+        samples read the same weights)."""
+        st, n, c, E = self._stream(), self.n, self.c, int(n_samples)
+        if getattr(self, "_evb_E", 0) != E:
+            self._evb = _Slot(n, self.cap, self.dev, x_nnz=0, samples=E, bptr_len=0, words=self.words)
+            self._evb_deg = torch.empty((E, n), dtype=torch.int32, device=self.dev)
+            self._evb_rows = torch.zeros((2, E, n), dtype=torch.float32, device=self.dev)
+            self._evb_w = torch.zeros((1, self.np), dtype=torch.float32, device=self.dev)
+            self._evb_bt_obj = nat.LdsBatch(samples=E, tag_step=1, act=n * HID, row=n, rp=n + 1, col=self.cap,
+                                            ell=n * 2 * HID, par=0, xval=0, xd=0, uv=0, part=0, met=2)
+            self._evb_bt = nat.batch_ptr(self._evb_bt_obj)
+            self._evb_E = E
+        sl, g, bt = self._evb, self._evb.g, self._evb_bt
+        self._evb_w[0].copy_(flat)
+        vm = val_mask.to(device=self.dev, dtype=torch.uint8).contiguous()
+        tm = test_mask.to(device=self.dev, dtype=torch.uint8).contiguous()
+        inv_v = float(np.float32(1.0) / np.float32(int(val_mask.sum())))
+        inv_t = float(np.float32(1.0) / np.float32(int(test_mask.sum())))
+        nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), n, self.seed, self.tag_graph, 1,
+                 nat.ptr(self.scalars), self.pending_graph, E, 1, nat.ptr(g.bits), self.words,
+                 nat.ptr(self._evb_deg), nat.ptr(g.row_ptr), nat.ptr(g.col), self.cap, nat.ptr(g.s),
+                 nat.ptr(g.ell), st)
+        self.pending_graph += E
+        self._forward(sl, self._evb_w, vm, inv_v, 0, 0, bt=bt)  # val rows -> sl.lossrow / corrrow [E, n]
+        rl, rc = self._evb_rows[0], self._evb_rows[1]
+        nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n,
+                 nat.ptr(sl.h2), 0, 0, 0, nat.ptr(self.label), nat.ptr(tm), inv_t, nat.ptr(rl), nat.ptr(rc), c, 0,
+                 bt, st)
+        host = torch.stack([sl.lossrow.sum(1), sl.corrrow.sum(1), rl.sum(1), rc.sum(1)], 1).double().cpu().numpy()
         return (float(np.mean(host[:, 0] * inv_v)), float(np.mean(host[:, 1] * inv_v)),
                 float(np.mean(host[:, 2] * inv_t)), float(np.mean(host[:, 3] * inv_t)))
 
@@ -454,8 +500,9 @@ class LdsEngine:
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
         return nat.ptr(self.agg)
 
-    def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int):
+    def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int, bt=None):
         st, n, c = self._stream(), self.n, self.c
+        bt = self.bt if bt is None else bt
         w0t, b0, w1, b1 = self._views(w)
         g = sl.g
         # training forwards keep Xd (CSR + CSC order) and the relu/dropout mask
@@ -464,14 +511,14 @@ class LdsEngine:
         xd = (nat.ptr(sl.xd_csr), nat.ptr(sl.xd_csc), nat.ptr(self.csr2csc)) if keep_xd else (0, 0, 0)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
                  nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, train, self.keep, self.scale, *xd, self.bt, st)
+                 fwd_off, train, self.keep, self.scale, *xd, bt, st)
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
                  self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask),
-                 self._agg(g, sl.h0), self.bt, st)
+                 self._agg(g, sl.h0), bt, st)
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
-                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self._agg(g, sl.h2), self.bt, st)
+                 nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self._agg(g, sl.h2), bt, st)
 
     def set_xt_splits(self, splits: int):
         """Entry ranges per X column for the W0 products (1: one wave per

@@ -142,6 +142,38 @@ def test_engine_batched_sample_equals_single_chain():
             assert torch.equal(v, big.get_params(b)[k]), (b, k)
 
 
+@pytest.mark.parametrize("n_samples", [1, 4, 16])
+def test_batched_empirical_mean_equals_sequential(n_samples):
+    """The batched evaluation (n_samples graphs in one sampler launch set,
+    eval forwards with grid.y = sample over shared weights) equals the
+    one-graph-at-a-time evaluation: same graph counters, same losses and
+    accuracies (fp32 row sums in a different order: 1e-6 relative)."""
+    from collections import OrderedDict
+
+    import ldsgnn
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from oracle import lds_oracle as O
+    from tests.parity_harness import synthetic_problem
+    prob = synthetic_problem(150, 24, 4, 21, 0.05)
+    theta0 = O.get_triu_values(prob["adj"]).cuda().contiguous()
+    torch.manual_seed(0)
+    gcn = MetaDenseGCN(24, 16, 4, dropout=0.5)
+    params = OrderedDict((k, v.detach().cuda()) for k, v in gcn.named_parameters())
+    eng = LdsEngine(prob["x"].cuda(), prob["y"].cuda(), prob["train"].cuda(), prob["opt"].cuda(), theta0, 4,
+                    outer_lr=0.1, tau=3, generator=ldsgnn.rng.Generator(21, 0), params=params)
+    eng.run_window(3)
+    flat = eng.flat_params().clone()
+    vm, tm = prob["val"].cuda(), prob["test"].cuda()
+    start = eng.pending_graph
+    a = eng._empirical_mean_batched(flat, n_samples, vm, tm)
+    assert eng.pending_graph == start + n_samples
+    eng.pending_graph = start
+    b = eng._empirical_mean_seq(flat, n_samples, vm, tm)
+    for x, y in zip(a, b):
+        assert abs(x - y) <= 1e-6 * max(1.0, abs(y)), (a, b)
+
+
 def test_batched_graph_replay_equals_eager():
     """A batched (S = 4) window captured as a HIP graph replays exactly like
     eager batched windows."""
