@@ -264,6 +264,7 @@ class LdsEngine:
     # ------------------------------------------------------------------ setup
     def _alloc_factors(self):
         """U, V: n × (S·ldk), sample b in columns [b·ldk, (b+1)·ldk); R: [S, n]."""
+        self._layout_version = getattr(self, "_layout_version", 0) + 1  # captured step graphs are stale
         self.ktot = self.tau * self.kg + HID + self.cw
         self.ldk = (self.ktot + 3) & ~3
         self.ldu = self.S * self.ldk  # row stride of U / V (the kernels' `ldk` argument)
@@ -286,6 +287,7 @@ class LdsEngine:
         self.btx = nat.batch_ptr(self._btx)
 
     def _grow(self, slots: int):
+        self._layout_version = getattr(self, "_layout_version", 0) + 1
         if slots > _TAB_MAX:
             raise NotImplementedError(f"LdsEngine: at most {_TAB_MAX} inner steps per hyper step")
         while len(self.slots) < slots:
@@ -758,6 +760,52 @@ class LdsEngine:
                  self.off_b1, 0, *adam, t - 1, *self._xt_split(xcsc, self.h0bar, fwd_off), self.btx, st)
 
     # ------------------------------------------------------------- graphs
+    # ------------------------------------------------------ per-step graphs
+    def _graphed(self, kind: str, fn):
+        """Run fn() (inner_step or hyper_step) from a HIP graph captured for
+        this exact launch sequence: the step's position and pending counter
+        offsets (baked into the launch arguments), the Adam-table length and
+        the buffer layout.  A key runs eagerly the first time it is seen
+        (buffers grow then), is captured and replayed the second time and
+        replayed after that; the host-side state the eager call would leave
+        (position, pending offsets) is restored from the capture."""
+        key = (kind, self.t, self.pending_graph, self.pending_fwd, self.train_flag, self._tab_count(),
+               getattr(self, "_layout_version", 0))
+        cache = self.__dict__.setdefault("_step_graphs", {})
+        hit = cache.get(key)
+        if hit is None:
+            if key not in self.__dict__.setdefault("_step_seen", set()):
+                self._step_seen.add(key)
+                return fn()
+            s = torch.cuda.Stream(self.dev)
+            s.wait_stream(torch.cuda.current_stream(self.dev))
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(graph, stream=s):
+                    ret = fn()
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            if getattr(self, "_layout_version", 0) != key[-1]:  # the call re-laid buffers: never replay it
+                raise RuntimeError("engine buffers were re-allocated during step capture")
+            hit = cache[key] = (graph, (self.t, self.pending_graph, self.pending_fwd), ret)
+        graph, post, ret = hit
+        graph.replay()
+        self.t, self.pending_graph, self.pending_fwd = post
+        return ret
+
+    def inner_step_graphed(self):
+        """inner_step() from a per-position HIP graph (see _graphed); the
+        first step at a new position grows the tape eagerly."""
+        if self.t >= len(self.slots):
+            return self.inner_step()
+        return self._graphed("inner", self.inner_step)
+
+    def hyper_step_graphed(self):
+        """hyper_step() (single replica, no reducer) from a HIP graph keyed
+        by the window length."""
+        if self.t * self.kg + HID + self.cw > self.ldk or self.split_theta_grad:
+            return self.hyper_step()
+        return self._graphed("hyper", self.hyper_step)
+
     def run_window(self, tau: int, grad_reducer=None):
         """τ inner steps followed by the hyper step.  A full window from a
         window start draws its τ+1 graphs in one batched launch set."""

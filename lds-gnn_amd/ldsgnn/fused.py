@@ -44,16 +44,19 @@ class FusedBilevelRunner:
     supply the initial state and the weight re-initialisation
     (MetaDenseGCN.reset_weights consumes the torch RNG exactly as there); the
     per-step train loss is read back for the inner early stopping (one sync per
-    inner step, as the reference's `.item()`), so windows run eagerly rather
-    than as replayed HIP graphs."""
+    inner step, as the reference's `.item()`), so the unit of replay is the
+    step: with `step_graphs` (default) every inner step position and hyper
+    step length is captured as a HIP graph at its second use and replayed
+    after that (LdsEngine.inner_step_graphed / hyper_step_graphed)."""
 
     def __init__(self, inner_trainer, outer_trainer, data, n_samples_empirical_mean: int = 16,
-                 generator: "_rng.Generator" = None):
+                 generator: "_rng.Generator" = None, step_graphs: bool = True):
         self.inner_trainer = inner_trainer
         self.outer_trainer = outer_trainer
         self.data = data
         self.n_samples_empirical_mean = n_samples_empirical_mean
         self.generator = generator
+        self.step_graphs = step_graphs
         self.engine = None
         self.gcn_params = None
         self.graph_state_dict = None
@@ -77,14 +80,20 @@ class FusedBilevelRunner:
             eng.set_params(self.inner_trainer.model_params)
             while not inner_stop.abort:
                 t = eng.t
-                eng.inner_step()
+                if self.step_graphs:
+                    eng.inner_step_graphed()
+                else:
+                    eng.inner_step()
                 loss, acc = eng.inner_metrics(t)
                 inner_stop.update(loss, model_params=eng.flat_params())
                 if log is not None:
                     log("loss.train", loss, step)
                     log("acc.train", acc, step)
                 if tau == 0 or step % tau == 0:
-                    eng.hyper_step()
+                    if self.step_graphs:
+                        eng.hyper_step_graphed()
+                    else:
+                        eng.hyper_step()
                     if log is not None:
                         ol, oa = eng.outer_metrics()
                         log("loss.outer", ol, step)

@@ -241,7 +241,8 @@ def test_engine_split_x_products_match_oracle(dropout):
     assert res["max_theta_err"] < TOL, res
 
 
-def test_fused_runner_matches_dropin_runner():
+@pytest.mark.parametrize("step_graphs", [True, False])
+def test_fused_runner_matches_dropin_runner(step_graphs):
     """FusedBilevelRunner (every step, hyper step and the 16-sample empirical
     evaluation on the fused engine) against the drop-in BilevelProblemRunner
     (autograd path) on the same seeded problem: identical control flow (inner
@@ -255,7 +256,7 @@ def test_fused_runner_matches_dropin_runner():
         runner = build_product(prob, dropout=0.5, seed=17)
         if fused:
             runner = FusedBilevelRunner(runner.inner_trainer, runner.outer_trainer, runner.data,
-                                        n_samples_empirical_mean=4)
+                                        n_samples_empirical_mean=4, step_graphs=step_graphs)
         else:
             runner.n_samples_empirical_mean = 4
         rec = []
