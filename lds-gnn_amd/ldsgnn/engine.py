@@ -104,6 +104,10 @@ class _Slot:
         self.corrrow = torch.zeros((S, n), dtype=torch.float32, device=dev)
 
 
+def _identity_reducer(grad: torch.Tensor) -> None:
+    """Single GPU: the hypergradient needs no exchange."""
+
+
 def _csr_of(dense: torch.Tensor):
     sp = dense.to_sparse_csr()
     return (sp.crow_indices().to(torch.int32).contiguous(), sp.col_indices().to(torch.int32).contiguous(),
@@ -249,6 +253,10 @@ class LdsEngine:
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
         self.keep_grad = True  # write dθ (θ.grad) even when it is fused with the update
+        # outer_update(grad): replaces the SGD + clamp step on θ — a graph model
+        # whose θ is a function of its own parameters (the embedding model)
+        # takes dθ, steps its optimizer and rewrites self.theta in place
+        self.outer_update = None
         # dθ assembly split per graph: chunks of finished graphs run on a side
         # stream beside the (latency-bound) reverse pass.  Off by default: on
         # MI355X the replayed graph did not overlap the branches and the
@@ -632,6 +640,11 @@ class LdsEngine:
         """OuterProblemTrainer.train_step + both detaches.  Returns the device
         metrics row [Σ NLL over opt rows, #correct]."""
         st, n, c = self._stream(), self.n, self.c
+        if self.outer_update is not None:
+            if self.S > 1:
+                raise NotImplementedError("outer_update (θ as a function of model parameters) is single-sample")
+            if grad_reducer is None:
+                grad_reducer = _identity_reducer
         T = self.t
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
@@ -676,8 +689,11 @@ class LdsEngine:
             nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
                      nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, st)
             grad_reducer(self.grad)
-            nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
-                     nat.ptr(self.scalars), st)
+            if self.outer_update is None:
+                nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
+                         nat.ptr(self.scalars), st)
+            else:  # θ = P(parameters): the model's own optimizer step rewrites θ
+                self.outer_update(self.grad)
         # detach: the window restarts from the latest weights / Adam state
         P = nat.ptr
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
@@ -802,7 +818,7 @@ class LdsEngine:
     def hyper_step_graphed(self):
         """hyper_step() (single replica, no reducer) from a HIP graph keyed
         by the window length."""
-        if self.t * self.kg + HID + self.cw > self.ldk or self.split_theta_grad:
+        if self.t * self.kg + HID + self.cw > self.ldk or self.split_theta_grad or self.outer_update is not None:
             return self.hyper_step()
         return self._graphed("hyper", self.hyper_step)
 

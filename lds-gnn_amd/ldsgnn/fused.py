@@ -14,11 +14,21 @@ from .engine import LdsEngine
 def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator" = None,
                          samples: int = 1) -> LdsEngine:
     """samples > 1: S replica chains (replicas generator.replica + b) batched
-    in one engine; θ moves by their mean hypergradient."""
-    from .models.graph import BernoulliGraphModel
+    in one engine; θ moves by their mean hypergradient.
+    The embedding model (PairwiseEmbeddingSampler, src/models/graph.py:81-112)
+    runs the inner loop and the hypergradient dθ on the engine with θ = the
+    upper triangle of P = σ(E·Eᵀ)^pow; its outer step (OuterProblemTrainer.
+    train_step after the backward: optimizer, StepLR, projection) runs on E
+    from dθ by autograd through P, and rewrites θ (`LdsEngine.outer_update`)."""
+    from .models.graph import BernoulliGraphModel, PairwiseEmbeddingSampler
     gm = outer.model
+    gcn = inner.model
+    data = inner.data
+    if isinstance(gm, PairwiseEmbeddingSampler):
+        return _embedding_engine(inner, outer, tau, generator, samples)
     if not isinstance(gm, BernoulliGraphModel) or gm.directed:
-        raise NotImplementedError("the fused engine implements the undirected LDS Bernoulli model")
+        raise NotImplementedError("the fused engine implements the undirected LDS Bernoulli model "
+                                  "and the embedding model")
     opt = outer.optimizer
     if len(opt.param_groups) != 1:
         raise NotImplementedError("one θ parameter group expected")
@@ -28,12 +38,52 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
         raise NotImplementedError("the fused engine implements plain SGD on θ")
     if outer.lr_decay is not None and outer.lr_decay_step_size != 1:
         raise NotImplementedError("StepLR with step_size 1 only")
-    gcn = inner.model
-    data = inner.data
     return LdsEngine(data.x, data.y, data.train_mask, outer.opt_mask, gm.probs.data, data.num_classes,
                      dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=grp["lr"],
                      lr_decay=outer.lr_decay, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
                      params=inner.model_params, samples=samples)
+
+
+def _embedding_engine(inner, outer, tau, generator, samples) -> LdsEngine:
+    import torch
+
+    from .models.sampling import Sampler
+    gm, gcn, data = outer.model, inner.model, inner.data
+    if samples != 1:
+        raise NotImplementedError("the embedding model runs single-sample on the engine")
+    cfg = Sampler.config
+    if not cfg.get("undirected", True) or str(cfg.get("sparsification", "NONE")).upper() != "NONE" or \
+            cfg.get("dense", False):
+        raise NotImplementedError("the engine draws undirected, unsparsified graphs")
+    if outer.refine_embeddings:
+        raise NotImplementedError("refine_embeddings is a GAE option")
+    n = data.num_nodes
+    iu = torch.triu_indices(n, n, device=gm.embeddings.device)
+
+    def theta_of_model() -> torch.Tensor:
+        with torch.no_grad():
+            return gm.forward()[iu[0], iu[1]].contiguous()
+
+    eng = LdsEngine(data.x, data.y, data.train_mask, outer.opt_mask, theta_of_model(), data.num_classes,
+                    dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=0.0,
+                    lr_decay=None, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
+                    params=inner.model_params, samples=1)
+
+    def outer_update(grad: torch.Tensor) -> None:
+        # OuterProblemTrainer.train_step (src/trainers/outer.py:57-87) from the backward on:
+        # dθ -> E through P's upper triangle, optimizer, StepLR, projection
+        outer.optimizer.zero_grad()
+        gm.forward()[iu[0], iu[1]].backward(grad)
+        if outer.grad_reducer is not None:
+            outer.grad_reducer(gm)
+        outer.optimizer.step()
+        if outer.lr_decayer is not None:
+            outer.lr_decayer.step()
+        gm.project_parameters()
+        eng.theta.copy_(theta_of_model())
+
+    eng.outer_update = outer_update
+    return eng
 
 
 class FusedBilevelRunner:

@@ -53,6 +53,31 @@ def build_product(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_
     return runner
 
 
+def build_product_embedding(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.5,
+                            lr_decay=0.99, seed=0, embedding_dim=8, init_bounds=0.3, device="cuda"):
+    """build_product with the embedding graph model (P = σ(E·Eᵀ), SGD on E,
+    src/models/graph.py:81-112, src/models/factory.py embeddings_optimizer)."""
+    import ldsgnn
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from ldsgnn.models.graph import PairwiseEmbeddingSampler
+    from ldsgnn.trainers.bilevel import BilevelProblemRunner
+    from ldsgnn.trainers.inner import InnerProblemTrainer
+    from ldsgnn.trainers.outer import OuterProblemTrainer
+    from ldsgnn.utils.graph import DenseData
+
+    data = DenseData(x=prob["x"], y=prob["y"], dense_adj=prob["adj"], train_mask=prob["train"],
+                     val_mask=prob["val"], test_mask=prob["test"],
+                     num_classes=int(prob["y"].max()) + 1).to(device)
+    ldsgnn.rng.manual_seed(seed, 0)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.num_features, hidden, data.num_classes, dropout=dropout).to(device)
+    inner = InnerProblemTrainer(gcn, data, lr=gcn_lr, weight_decay=gcn_wd)
+    gm = PairwiseEmbeddingSampler(data.num_nodes, embedding_dim, init_bounds=init_bounds).to(device)
+    opt = torch.optim.SGD(gm.parameters(), lr=outer_lr)
+    outer = OuterProblemTrainer(opt, data, prob["opt"].to(device), gm, lr_decay=lr_decay)
+    return BilevelProblemRunner(inner, outer, data)
+
+
 def build_oracle(prob, runner, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1,
                  lr_decay=0.99, seed=0):
     params = OrderedDict((k, v.detach().cpu()) for k, v in runner.inner_trainer.model_params.items())
