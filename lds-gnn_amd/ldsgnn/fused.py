@@ -20,15 +20,19 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
     upper triangle of P = σ(E·Eᵀ)^pow; its outer step (OuterProblemTrainer.
     train_step after the backward: optimizer, StepLR, projection) runs on E
     from dθ by autograd through P, and rewrites θ (`LdsEngine.outer_update`)."""
-    from .models.graph import BernoulliGraphModel, PairwiseEmbeddingSampler
+    from .models.graph import BernoulliGraphModel, GraphProposalNetwork, PairwiseEmbeddingSampler
     gm = outer.model
     gcn = inner.model
     data = inner.data
     if isinstance(gm, PairwiseEmbeddingSampler):
         return _embedding_engine(inner, outer, tau, generator, samples)
+    if isinstance(gm, GraphProposalNetwork):
+        if gm.gcn.dropout != 0.0:  # P would be redrawn per sample: not fixed within a window
+            raise NotImplementedError("the GAE model runs on the engine with a dropout-free proposal GCN")
+        return _embedding_engine(inner, outer, tau, generator, samples)
     if not isinstance(gm, BernoulliGraphModel) or gm.directed:
-        raise NotImplementedError("the fused engine implements the undirected LDS Bernoulli model "
-                                  "and the embedding model")
+        raise NotImplementedError("the fused engine implements the undirected LDS Bernoulli model, "
+                                  "the embedding model and the dropout-free GAE model")
     opt = outer.optimizer
     if len(opt.param_groups) != 1:
         raise NotImplementedError("one θ parameter group expected")
@@ -56,9 +60,9 @@ def _embedding_engine(inner, outer, tau, generator, samples) -> LdsEngine:
             cfg.get("dense", False):
         raise NotImplementedError("the engine draws undirected, unsparsified graphs")
     if outer.refine_embeddings:
-        raise NotImplementedError("refine_embeddings is a GAE option")
+        raise NotImplementedError("refine_embeddings changes the GAE inputs per sample")
     n = data.num_nodes
-    iu = torch.triu_indices(n, n, device=gm.embeddings.device)
+    iu = torch.triu_indices(n, n, device=data.x.device)
 
     def theta_of_model() -> torch.Tensor:
         with torch.no_grad():

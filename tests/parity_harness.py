@@ -78,6 +78,33 @@ def build_product_embedding(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e
     return BilevelProblemRunner(inner, outer, data)
 
 
+def build_product_gae(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, lr_decay=0.99, seed=0,
+                      embedding_dim=8, device="cuda"):
+    """build_product with the GAE graph model (a dropout-free proposal GCN,
+    P = clamp(σ(a·E·Eᵀ + b), 0, 1); Adam on the GCN, SGD-rate on a, b as
+    src/models/factory.py:51-57 groups them)."""
+    import ldsgnn
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from ldsgnn.models.graph import GraphProposalNetwork
+    from ldsgnn.trainers.bilevel import BilevelProblemRunner
+    from ldsgnn.trainers.inner import InnerProblemTrainer
+    from ldsgnn.trainers.outer import OuterProblemTrainer
+    from ldsgnn.utils.graph import DenseData
+
+    data = DenseData(x=prob["x"], y=prob["y"], dense_adj=prob["adj"], train_mask=prob["train"],
+                     val_mask=prob["val"], test_mask=prob["test"],
+                     num_classes=int(prob["y"].max()) + 1).to(device)
+    ldsgnn.rng.manual_seed(seed, 0)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.num_features, hidden, data.num_classes, dropout=dropout).to(device)
+    inner = InnerProblemTrainer(gcn, data, lr=gcn_lr, weight_decay=gcn_wd)
+    gm = GraphProposalNetwork(data.x, data.dense_adj, dropout=0.0, embedding_dim=embedding_dim).to(device)
+    opt = torch.optim.Adam([{"params": gm.gcn.parameters(), "weight_decay": 5e-4, "lr": 0.01},
+                            {"params": [gm.probs_factor, gm.probs_bias], "lr": 0.01}])
+    outer = OuterProblemTrainer(opt, data, prob["opt"].to(device), gm, lr_decay=lr_decay)
+    return BilevelProblemRunner(inner, outer, data)
+
+
 def build_oracle(prob, runner, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1,
                  lr_decay=0.99, seed=0):
     params = OrderedDict((k, v.detach().cpu()) for k, v in runner.inner_trainer.model_params.items())

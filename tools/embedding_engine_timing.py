@@ -1,5 +1,5 @@
 """The embedding graph model (P = σ(E·Eᵀ), 16-dim E, init ±0.001: P ≈ 0.5,
-dense sampled graphs) at Cora shape: inner steps/s of the drop-in trainers
+dense sampled graphs) and the GAE model (factory defaults) at Cora shape: inner steps/s of the drop-in trainers
 against FusedBilevelRunner (inner loop + dθ on the engine, long-row bitmask
 aggregation; outer SGD on E by autograd through P).  Fixed epoch budget;
 one JSON line."""
@@ -18,8 +18,8 @@ import bench  # noqa: E402
 from ldsgnn.fused import FusedBilevelRunner  # noqa: E402
 
 
-def run(fused, inner_max, outer_max):
-    args = argparse.Namespace(dataset="cora", seed=1, samples=1, graph_model="embedding", tau=5, path="autograd")
+def run(fused, inner_max, outer_max, model="embedding"):
+    args = argparse.Namespace(dataset="cora", seed=1, samples=1, graph_model=model, tau=5, path="autograd")
     data, runner, _ = bench.build(args, 0, torch.device("cuda:0"))
     if fused:
         runner = FusedBilevelRunner(runner.inner_trainer, runner.outer_trainer, runner.data,
@@ -36,16 +36,17 @@ def run(fused, inner_max, outer_max):
 
 def main():
     inner_max, outer_max = 60, 2
-    out = {"workload": f"cora-shaped embedding model, tau=5, inner max {inner_max}, outer max {outer_max} "
-                       "(second of two runs each: one-time setup excluded)"}
-    for fused in (True, False):
-        run(fused, 5, 0)
-        dt, steps = run(fused, inner_max, outer_max)
-        out["fused" if fused else "dropin"] = {"seconds": dt}
-        if steps:
-            out["inner_steps"] = steps
-    out["speedup"] = out["dropin"]["seconds"] / out["fused"]["seconds"]
-    print(json.dumps(out), flush=True)
+    for model in ("embedding", "gae"):
+        out = {"workload": f"cora-shaped {model} model, tau=5, inner max {inner_max}, outer max {outer_max} "
+                           "(second of two runs each: one-time setup excluded)"}
+        for fused in (True, False):
+            run(fused, 5, 0, model)
+            dt, steps = run(fused, inner_max, outer_max, model)
+            out["fused" if fused else "dropin"] = {"seconds": dt}
+            if steps:
+                out["inner_steps"] = steps
+        out["speedup"] = out["dropin"]["seconds"] / out["fused"]["seconds"]
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
