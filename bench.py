@@ -213,10 +213,16 @@ def main():
         torch.cuda.synchronize()
 
     use_engine = args.path == "engine"
-    if args.graph_model != "lds" and use_engine:
-        raise SystemExit("--graph-model embedding/gae runs on --path autograd (the fused engine is the LDS θ path)")
+    # embedding / GAE on the engine: θ = P(model parameters), the outer step
+    # (autograd through P + the model's optimizer) runs eagerly between the
+    # dθ assembly and the detach (LdsEngine.outer_update): eager windows
+    param_theta = args.graph_model != "lds"
+    if param_theta and use_engine and (world > 1 or args.samples > 1):
+        raise SystemExit("--graph-model embedding/gae on the engine: one GPU, one sample")
     if args.kernel == "auto":
-        if use_engine and args.samples > 1:
+        if use_engine and param_theta:
+            args.kernel = "lds_theta_grad"
+        elif use_engine and args.samples > 1:
             args.kernel = "lds_theta_grad_ex"
         elif use_engine and world == 1:
             args.kernel = "lds_theta_grad_sgd_accum" if args.split else "lds_theta_grad_sgd"
@@ -229,7 +235,7 @@ def main():
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
-        use_graph = not args.eager
+        use_graph = not args.eager and not param_theta
         if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
             eng.capture_window(args.tau, grad_reducer=reducer)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)
