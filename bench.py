@@ -215,7 +215,7 @@ def main():
     use_engine = args.path == "engine"
     # embedding / GAE on the engine: θ = P(model parameters), the outer step
     # (autograd through P + the model's optimizer) runs eagerly between the
-    # dθ assembly and the detach (LdsEngine.outer_update): eager windows
+    # two replayed graphs of a window, where N>1 runs the all-reduce
     param_theta = args.graph_model != "lds"
     if param_theta and use_engine and (world > 1 or args.samples > 1):
         raise SystemExit("--graph-model embedding/gae on the engine: one GPU, one sample")
@@ -235,7 +235,9 @@ def main():
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
-        use_graph = not args.eager and not param_theta
+        if param_theta:  # the model's outer step runs eagerly between graph A and graph B
+            reducer = eng.outer_update
+        use_graph = not args.eager
         if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
             eng.capture_window(args.tau, grad_reducer=reducer)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)

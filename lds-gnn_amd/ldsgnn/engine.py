@@ -104,10 +104,6 @@ class _Slot:
         self.corrrow = torch.zeros((S, n), dtype=torch.float32, device=dev)
 
 
-def _identity_reducer(grad: torch.Tensor) -> None:
-    """Single GPU: the hypergradient needs no exchange."""
-
-
 def _csr_of(dense: torch.Tensor):
     sp = dense.to_sparse_csr()
     return (sp.crow_indices().to(torch.int32).contiguous(), sp.col_indices().to(torch.int32).contiguous(),
@@ -643,8 +639,8 @@ class LdsEngine:
         if self.outer_update is not None:
             if self.S > 1:
                 raise NotImplementedError("outer_update (θ as a function of model parameters) is single-sample")
-            if grad_reducer is None:
-                grad_reducer = _identity_reducer
+            if grad_reducer is None:  # the model's outer step takes the reducer's place (capture: the split point)
+                grad_reducer = self.outer_update
         T = self.t
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
@@ -688,12 +684,10 @@ class LdsEngine:
         else:  # replicas: dθ, all-reduce (mean), then the identical update everywhere
             nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
                      nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, st)
-            grad_reducer(self.grad)
+            grad_reducer(self.grad)  # with outer_update: the model's optimizer step, which rewrites θ
             if self.outer_update is None:
                 nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
                          nat.ptr(self.scalars), st)
-            else:  # θ = P(parameters): the model's own optimizer step rewrites θ
-                self.outer_update(self.grad)
         # detach: the window restarts from the latest weights / Adam state
         P = nat.ptr
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)

@@ -320,6 +320,33 @@ def test_fused_runner_embedding_model_matches_dropin():
         assert abs(a[k] - b[k]) < 1e-4, (k, a[k], b[k])
 
 
+def test_embedding_engine_graph_replay_equals_eager():
+    """Embedding model on the engine, windows replayed from HIP graphs split
+    at the model's outer step (graph A, outer_update eagerly, graph B) equal
+    eager windows: same θ (= P(E)), same E, same GCN weights."""
+    from ldsgnn.fused import engine_from_trainers
+    from tests.parity_harness import build_product_embedding, synthetic_problem
+    prob = synthetic_problem(100, 20, 3, 11, 0.08)
+
+    def make():
+        r = build_product_embedding(prob, dropout=0.5, seed=11, outer_lr=5.0)
+        e = engine_from_trainers(r.inner_trainer, r.outer_trainer, tau=4)
+        e.inner_step()
+        e.hyper_step()
+        return r, e
+
+    (ra, a), (rb, b) = make(), make()
+    a.capture_window(4, grad_reducer=a.outer_update)
+    a.replay(3)
+    for _ in range(3):
+        b.run_window(4)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    assert torch.equal(ra.outer_trainer.model.embeddings, rb.outer_trainer.model.embeddings)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+
+
 def test_fused_runner_gae_model_matches_dropin():
     """The GAE graph model (dropout-free proposal GCN) on the fused engine:
     the outer Adam step on the proposal GCN and the affine parameters by
