@@ -584,7 +584,20 @@ constexpr int kT2 = 128;
 constexpr int kS2 = 12;             // dwords per LDS row (8 data + 4 pad: 4 × odd)
 constexpr int kPL2 = kT2 * kS2;     // dwords per plane
 
-template <bool VEC>
+// Packed index of (i, j), i <= j, in 32-bit arithmetic while n(n+1) < 2^32
+// (n <= 46 340: the epilogue's 64 index computations per lane are 64-bit
+// multiplies otherwise).
+template <bool SMALL>
+__device__ __forceinline__ int64_t tri_at_t(int i, int j, int64_t n) {
+    if constexpr (SMALL) {
+        const uint32_t ui = (uint32_t)i, un = (uint32_t)n;
+        return (int64_t)((ui * (2u * un - ui + 1u)) >> 1) + (j - i);
+    } else {
+        return tri_index(i, i, n) + (j - i);
+    }
+}
+
+template <bool VEC, bool SMALL = false>
 __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
@@ -611,6 +624,7 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const int lane = t & 63, wave = t >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int64_t nn = n;
+    auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
 
     // staging: thread t owns row t >> 1 of both blocks, k = 8·(t & 1) … + 7 of the chunk
     const int srow = t >> 1, sk = (t & 1) * 8;
@@ -731,7 +745,7 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
             for (int e = 0; e < 16; ++e) {
                 const int i = i0 + wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
                 const bool in = i < n && j < n && j >= i;
-                const int64_t id = in ? tri_index(i, i, nn) + (j - i) : 0;
+                const int64_t id = in ? tri_at(i, j, nn) : 0;
                 th[m][q][e] = (in && theta != nullptr) ? theta[id] : 0.f;
                 part[m][q][e] = (in && need_part) ? grad[id] : 0.f;
             }
@@ -750,7 +764,7 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
                 const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
                 const int i = i0 + li;
                 if (i >= n || j >= n || j < i) continue;
-                const int64_t id = tri_index(i, i, nn) + (j - i);
+                const int64_t id = tri_at(i, j, nn);
                 const float t0 = th[m][q][e];
                 float g = 0.f;
                 if (j > i) {
@@ -800,10 +814,16 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
         const int per = (nt2 + 7) / 8;
         const int grid = form == 5 ? 8 * per : nt2;
         const int grp = form == 5 ? kGroup : 0;
-        if (fast)
-            hipLaunchKernelGGL(theta_grad_bf3_t128_kernel<true>, dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
+        const bool small = n <= 46340;
+        if (fast && small)
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp,
+                               per);
+        else if (fast)
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS,
+                               grp, per);
         else
-            hipLaunchKernelGGL(theta_grad_bf3_t128_kernel<false>, dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<false, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS,
+                               grp, per);
     } else if (form == 3) {
         if (fast)
             hipLaunchKernelGGL((theta_grad_bf3_kernel<32, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0);
