@@ -232,6 +232,9 @@ class LdsEngine:
             else:
                 nb = nat.lib.lds_spmm_block_count(n)
                 self.spmm_part = torch.zeros((nb, n, HID), dtype=torch.float32, device=dev)
+        # per-step HIP graphs (inner_step_graphed / hyper_step_graphed): keyed
+        # captures, keys seen once, and the buffer-layout version they hold
+        self._step_graphs, self._step_seen, self._layout_version = {}, set(), 0
         self._grow(self.tau)
         self.outer = _Slot(n, self.cap, dev, graph=self.gbatch.graphs[self.tau], x_nnz=self.x_nnz, samples=S)
         self.t = 0  # inner steps in the current window
@@ -268,7 +271,7 @@ class LdsEngine:
     # ------------------------------------------------------------------ setup
     def _alloc_factors(self):
         """U, V: n × (S·ldk), sample b in columns [b·ldk, (b+1)·ldk); R: [S, n]."""
-        self._layout_version = getattr(self, "_layout_version", 0) + 1  # captured step graphs are stale
+        self._layout_version += 1  # captured step graphs are stale
         self.ktot = self.tau * self.kg + HID + self.cw
         self.ldk = (self.ktot + 3) & ~3
         self.ldu = self.S * self.ldk  # row stride of U / V (the kernels' `ldk` argument)
@@ -291,7 +294,7 @@ class LdsEngine:
         self.btx = nat.batch_ptr(self._btx)
 
     def _grow(self, slots: int):
-        self._layout_version = getattr(self, "_layout_version", 0) + 1
+        self._layout_version += 1
         if slots > _TAB_MAX:
             raise NotImplementedError(f"LdsEngine: at most {_TAB_MAX} inner steps per hyper step")
         while len(self.slots) < slots:
@@ -780,11 +783,11 @@ class LdsEngine:
         replayed after that; the host-side state the eager call would leave
         (position, pending offsets) is restored from the capture."""
         key = (kind, self.t, self.pending_graph, self.pending_fwd, self.train_flag, self._tab_count(),
-               getattr(self, "_layout_version", 0))
-        cache = self.__dict__.setdefault("_step_graphs", {})
+               self._layout_version)
+        cache = self._step_graphs
         hit = cache.get(key)
         if hit is None:
-            if key not in self.__dict__.setdefault("_step_seen", set()):
+            if key not in self._step_seen:
                 self._step_seen.add(key)
                 return fn()
             s = torch.cuda.Stream(self.dev)
@@ -794,7 +797,7 @@ class LdsEngine:
                 with torch.cuda.graph(graph, stream=s):
                     ret = fn()
             torch.cuda.current_stream(self.dev).wait_stream(s)
-            if getattr(self, "_layout_version", 0) != key[-1]:  # the call re-laid buffers: never replay it
+            if self._layout_version != key[-1]:  # the call re-laid buffers: never replay it
                 raise RuntimeError("engine buffers were re-allocated during step capture")
             hit = cache[key] = (graph, (self.t, self.pending_graph, self.pending_fwd), ret)
         graph, post, ret = hit
