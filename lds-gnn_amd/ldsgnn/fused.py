@@ -25,11 +25,11 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
     gcn = inner.model
     data = inner.data
     if isinstance(gm, PairwiseEmbeddingSampler):
-        return _embedding_engine(inner, outer, tau, generator, samples)
+        return _param_theta_engine(inner, outer, tau, generator, samples)
     if isinstance(gm, GraphProposalNetwork):
         if gm.gcn.dropout != 0.0:  # P would be redrawn per sample: not fixed within a window
             raise NotImplementedError("the GAE model runs on the engine with a dropout-free proposal GCN")
-        return _embedding_engine(inner, outer, tau, generator, samples)
+        return _param_theta_engine(inner, outer, tau, generator, samples)
     if not isinstance(gm, BernoulliGraphModel) or gm.directed:
         raise NotImplementedError("the fused engine implements the undirected LDS Bernoulli model, "
                                   "the embedding model and the dropout-free GAE model")
@@ -48,7 +48,10 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
                      params=inner.model_params, samples=samples)
 
 
-def _embedding_engine(inner, outer, tau, generator, samples) -> LdsEngine:
+def _param_theta_engine(inner, outer, tau, generator, samples) -> LdsEngine:
+    """Engine for a graph model whose θ is a function of its own parameters
+    (embedding, dropout-free GAE): θ = triu(P(params)), and the model's outer
+    step, by autograd through P, runs as LdsEngine.outer_update."""
     import torch
 
     from .models.sampling import Sampler
