@@ -54,3 +54,23 @@ def test_product_path_refuses_cpu_tensors():
     from ldsgnn import ops
     with pytest.raises(RuntimeError, match="HIP device"):
         ops.sample_graph_from_triu(torch.rand(6), 3)
+
+
+def test_theta_grad_form_selection_needs_no_gpu():
+    """The θ-grad assembly form is host-side state (lds_theta_grad_set_form):
+    default split bf16, every named form round-trips, out-of-range codes are
+    rejected."""
+    import ctypes as C
+
+    import ldsgnn._native as nat
+    from ldsgnn import ops
+    assert ops.theta_grad_form() == "bf16x3"
+    try:
+        for name in ops.THETA_GRAD_FORMS:
+            ops.theta_grad_form(name)
+            assert ops.theta_grad_form() == name
+    finally:
+        ops.theta_grad_form("bf16x3")
+    prev = C.c_int(-7)
+    assert nat.lib.lds_theta_grad_set_form(len(ops.THETA_GRAD_FORMS), C.byref(prev)) == 1
+    assert nat.lib.lds_theta_grad_set_form(-1, C.byref(prev)) == 0 and prev.value == 1
