@@ -1,27 +1,40 @@
 """Benchmark: LDS inner-loop steps/s on Cora-sized LDS (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): Cora-shaped LDS bilevel, kNN-initialised
-θ (k=10, cosine, symmetrised), 1 sampled graph per inner step, hidden 16,
-dropout 0.5, Adam 0.01 / wd 5e-4, hyper step every τ=5 inner steps (SGD
-lr 0.1, decay 0.99), fp32.  Early stopping disabled: W untimed warm-up inner
-steps, then exactly K timed inner steps with their hyper steps inside the
-timed region.  Synthetic data of Cora's shape (no network).
+Workload (BASELINE.json configs[1], the default): the real Cora Planetoid split
+(NormalizeFeatures), θ₀ = the symmetrised cosine kNN graph (k = 10) from the
+reference's own sklearn call, committed as tests/golden/knn_cora.npz so every
+machine samples the same workload; 1 sampled graph per inner step, hidden 16,
+dropout 0.5, Adam 0.01 / wd 5e-4, hyper step every τ = 5 inner steps (SGD lr
+0.1, decay 0.99), fp32 (the θ-grad assembly in split bf16, fp32-accurate:
+DESIGN §4c).  Early stopping disabled: W untimed warm-up inner steps, then
+exactly K timed inner steps with their hyper steps inside the timed region
+(SURVEY §8(d)); the fused engine replays captured τ-windows.
 
-N>1 (torchrun, one process per GPU): every rank runs its own Monte-Carlo
-replica (keyed RNG stream = rank) and the ranks all-reduce θ.grad once per
-hyper step over RCCL — per-GPU work fixed ("weak"); value = inner steps of all
-ranks / max-over-ranks wall time.
+N > 1 (torchrun, one process per GPU): every rank runs S Monte-Carlo replicas
+(keyed RNG streams rank·S … rank·S+S−1) and the ranks all-reduce θ.grad
+(mean) once per hyper step over RCCL — per-GPU work fixed ("weak"); value =
+inner steps of all ranks ÷ max-over-ranks wall time.  The line also carries
+`strong_scaling` (BASELINE config 4): S_total = 64 samples split over the
+ranks, timed against rank 0 running all 64 alone on its GPU first.
 
-Also reported: `roofline` of the dominant kernel (HIP-event average launch
-time over a second, instrumented pass of the same K steps) and
-`cpu_baseline` — the CPU oracle (dense PyTorch restatement of the reference)
-timed on this host over a bounded sample (rank 0, N=1 only).
+Also reported:
+  * `window`: per-entry-point GPU time of one τ-window (HIP events around
+    every launch in an eager pass of the same K steps), top entries with
+    their algorithmic bytes;
+  * `roofline`: the entry point with the most GPU time per window, against
+    its bound (HBM for the memory kernels, MFMA for the θ-grad assembly);
+  * `cpu_baseline`: the CPU oracle (dense PyTorch restatement of the
+    reference) on this host over a bounded sample (rank 0, N = 1 only).
+
+`--model gcn` (BASELINE config 1): fixed-adjacency GCN training epochs/s on
+the real Cora graph (src/scripts/gcn.py:75-91: train step + evaluate).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -38,11 +51,19 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
+METRIC = "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X"
+PMC_RECORD = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 
 
-def build(args, rank, device):
+def world_info():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def build(args, rank, device, samples=None):
+    """The drop-in trainers of the workload (src/scripts/bilevel.py:74-99)."""
     import ldsgnn
-    from ldsgnn.data.synthetic import knn_init, make_dataset
+    from ldsgnn.data.workloads import load_workload
     from ldsgnn.models.gcn import MetaDenseGCN
     from ldsgnn.models.graph import BernoulliGraphModel
     from ldsgnn.replicas import allreduce_mean
@@ -51,43 +72,39 @@ def build(args, rank, device):
     from ldsgnn.trainers.outer import OuterProblemTrainer
     from ldsgnn.utils.graph import split_mask
 
-    data = make_dataset(args.dataset, seed=args.seed)
-    if args.dataset == "synthetic20k":  # config 5: dense θ_ij ~ U(0, 1) i.i.d. (seed 20000), no kNN graph
-        g = torch.Generator(device=device).manual_seed(20000)
-        data.dense_adj = torch.rand((data.num_nodes, data.num_nodes), generator=g, device=device)
-    else:
-        data = knn_init(data, k=10)
+    S = args.samples if samples is None else samples
+    data = load_workload(args.dataset, seed=args.seed, device=device)
     np.random.seed(args.seed)
-    data.val_mask, opt_mask = split_mask(data.val_mask, 0.5, shuffle=True)
+    data.val_mask, opt_mask = split_mask(data.val_mask.cpu(), 0.5, shuffle=True)
     data = data.to(device)
     opt_mask = opt_mask.to(device)
-    ldsgnn.rng.manual_seed(args.seed, replica=rank * args.samples)  # rank r: replicas r·S .. r·S+S-1
+    ldsgnn.rng.manual_seed(args.seed, replica=rank * S)  # rank r: replicas r·S .. r·S+S-1
     torch.manual_seed(args.seed)
     gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(device)
     inner = InnerProblemTrainer(gcn, data, lr=0.01, weight_decay=5e-4)
     if args.graph_model == "lds":
         gm = BernoulliGraphModel(data.dense_adj)
         opt = torch.optim.SGD(gm.parameters(), lr=0.1)
-    else:  # the embedding / GAE models: drop-in trainers only
+    else:  # the embedding / GAE models
         from ldsgnn.models.factory import GraphGenerativeModelFactory
         fac = GraphGenerativeModelFactory(data)
         gm = fac.create(args.graph_model)
         opt = fac.optimizer(gm)
-    outer = OuterProblemTrainer(opt, data, opt_mask, gm, lr_decay=0.99, grad_reducer=allreduce_mean)
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    outer = OuterProblemTrainer(opt, data, opt_mask, gm, lr_decay=0.99,
+                                grad_reducer=allreduce_mean if multi else None)
     return data, BilevelProblemRunner(inner, outer, data), opt_mask
 
 
 def make_engine(runner, tau, world, samples=1):
+    """Fused engine over the trainers; with world > 1 the exchange is the
+    trainer's reducer (all-reduce mean of θ.grad over RCCL), set on the engine
+    by engine_from_trainers."""
     import ldsgnn
     from ldsgnn.fused import engine_from_trainers
     eng = engine_from_trainers(runner.inner_trainer, runner.outer_trainer, tau=tau,
                                generator=ldsgnn.rng.default_generator, samples=samples)
-    reducer = None
-    if world > 1:
-        def reducer(grad):
-            dist.all_reduce(grad, op=dist.ReduceOp.SUM)
-            grad.div_(world)
-    return eng, reducer
+    return eng, eng.grad_reducer if world > 1 else None
 
 
 def run_engine_windows(eng, reducer, windows, tau, use_graph):
@@ -109,39 +126,132 @@ def run_steps(runner, start: int, count: int, tau: int) -> int:
     return step
 
 
-# entry point -> HIP kernel symbol (for the PMC traffic record)
-KERNEL_SYMBOL = {"lds_theta_grad_ex": "lds::theta_grad_mfma_kernel", "lds_theta_grad_sgd": "lds::theta_grad_mfma_kernel", "lds_theta_grad": "lds::theta_grad_mfma_kernel",
-                 "lds_theta_grad_sgd_accum": "lds::theta_grad_mfma_kernel", "lds_spmm_norm": "lds::spmm_norm_group_kernel",
-                 "lds_sample_bitmask": "lds::sample_tiles_kernel"}
-PMC_RECORD = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# ---------------------------------------------------------------------------
+# algorithmic bytes / flops per launch
+# ---------------------------------------------------------------------------
+
+def algo_cost(name, eng, n_calls_per_window):
+    """(bound, algorithmic bytes or flops of ONE launch) of an engine entry
+    point: every array the launch must touch, counted once."""
+    from ldsgnn import _native as nat
+    n, S = eng.n, eng.S
+    nnz = eng.sampled_nnz_mean()
+    xnnz = int(eng.xcol.numel())
+    act = 4 * 16 * n * S                      # one n × 16 fp32 activation array (all samples)
+    graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)  # row_ptr, col, s, ELL head
+    tri = n * (n + 1) // 2
+    P = eng.np
+    if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex"):
+        k = eng.S * eng.ldk if eng.S > 1 else eng.window_columns(eng.tau, eng.c)
+        return "mfma", 6.0 * 4.0 * k * tri   # split bf16: six bf16 MFMA products per fp32 product
+    if name == "lds_sample_graphs_multi":
+        g = eng.tau + 1
+        words = nat.lib.lds_bitmask_words(n)
+        per = S * (3 * 8 * n * words + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)  # bits w/r/r, CSR, s, ELL
+        return "hbm", 4 * tri + g * per      # θ read once per window
+    if name == "lds_engine_x_linear":
+        return "hbm", S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act
+    if name == "lds_engine_xt_adam":
+        return "hbm", S * (4 * (eng.fin + 1) + 8 * xnnz) + act + S * 28 * P + 4 * eng.nred * 304 * S
+    if name in ("lds_engine_fwd_layer1", "lds_engine_rev_a", "lds_engine_rev_c"):
+        return "hbm", graph + 5 * act
+    if name in ("lds_engine_fwd_layer2", "lds_engine_bwd_layer2", "lds_engine_rev_b"):
+        return "hbm", graph + 4 * act
+    if name in ("lds_engine_bwd1_reduce", "lds_engine_rev_d_reduce"):
+        return "hbm", graph + 7 * act + 4 * eng.nred * 304 * S
+    if name in ("lds_engine_sgd_clamp",):
+        return "hbm", 12 * tri
+    if name == "lds_engine_end_window":
+        return "hbm", S * 24 * P
+    return "hbm", 0
 
 
-def pmc_traffic(kernel, use_engine, world, args):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
-    PMC record (tools/gpu_pmc.sh + tools/pmc_summary.py: 2 x FETCH_SIZE +
-    WRITE_SIZE, separate passes, gfx950 read correction), measured on this
-    default workload (Cora-shaped, S = 1, τ = 5); None for any other."""
-    default = args.dataset == "cora" and args.samples == 1 and args.tau == 5
-    if not (default and use_engine and world == 1 and kernel == "lds_theta_grad_sgd") or \
-            not os.path.exists(PMC_RECORD):
+def pmc_traffic(name, args):
+    """HBM bytes per launch of an entry point from the committed rocprofv3 PMC
+    record of THIS default workload (tools/gpu_pmc.sh + tools/pmc_summary.py:
+    2 x FETCH_SIZE + WRITE_SIZE in separate passes, gfx950 read correction)."""
+    default = (args.dataset == "cora" and args.samples == 1 and args.tau == 5 and args.model == "lds")
+    if not default or not os.path.exists(PMC_RECORD):
         return None, None
     with open(PMC_RECORD) as f:
         recs = json.load(f)
-    if "theta_grad" in kernel:  # whichever θ-grad kernel the form in force launched (one per record)
-        names = [k for k in recs if "theta_grad" in k]
-        rec = recs[names[0]] if len(names) == 1 else None
-    else:
-        rec = recs.get(KERNEL_SYMBOL[kernel])
+    rec = recs.get(name)
     if rec is None:
         return None, None
     return rec["traffic_bytes"], os.path.relpath(PMC_RECORD, ROOT)
 
 
+def window_breakdown(eng, reducer, args, windows):
+    """HIP events around every launch of `windows` eager windows: per entry
+    point launches / µs per window, its algorithmic cost and rate."""
+    from ldsgnn import _native as nat
+    nat.timer.enable_all()
+    run_engine_windows(eng, reducer, windows, args.tau, False)
+    summ = nat.timer.summary()
+    nat.timer.disable()
+    rows = []
+    for name, s in summ.items():
+        per_win = s["total_ms"] * 1000.0 / windows
+        calls = s["launches"] / windows
+        bound, cost = algo_cost(name, eng, calls)
+        row = {"entry": name, "launches_per_window": calls, "us_per_window": per_win, "avg_us": s["avg_us"],
+               "bound": bound}
+        if cost:
+            if bound == "mfma":
+                row["algorithmic_flop"] = cost
+                row["achieved_tflops"] = cost / (s["avg_us"] * 1e-6) / 1e12
+            else:
+                row["algorithmic_bytes"] = cost
+                row["achieved_GBs"] = cost / (s["avg_us"] * 1e-6) / 1e9
+        rows.append(row)
+    rows.sort(key=lambda r: -r["us_per_window"])
+    return rows, summ
+
+
+def roofline_of(row, args):
+    if row["bound"] == "mfma":
+        achieved = row["achieved_tflops"]
+        from ldsgnn import ops as ldsops
+        roof = {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / BF16_PEAK_TFLOPS, "form": ldsops.theta_grad_form(),
+                "fp32_equiv_tflops": achieved / 6.0}
+    else:
+        achieved = row.get("achieved_GBs", 0.0)
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS}
+    roof.update(kernel=row["entry"], avg_us=row["avg_us"], launches_per_window=row["launches_per_window"],
+                share_of_window=None)
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(row["entry"], args)
+    return roof
+
+
+def host_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    # the GPU box's share of its host is 16 cores (OMP_NUM_THREADS there);
+    # nproc / os.cpu_count() report the whole machine
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, cap) if cap > 0 else avail
+    return model, threads, avail
+
+
 def cpu_baseline(args, data, opt_mask):
     """The oracle (dense CPU restatement of the reference) on a bounded sample:
-    `cpu_steps` inner steps incl. their τ-hyper steps, host threads."""
+    `cpu_steps` inner steps incl. their τ-hyper steps, all host threads this
+    process may use."""
     from oracle import lds_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    model, threads, avail = host_info()
     torch.set_num_threads(threads)
     cpu = data.to("cpu")
     theta = O.get_triu_values(cpu.dense_adj)
@@ -153,9 +263,133 @@ def cpu_baseline(args, data, opt_mask):
     prob.run_steps(args.cpu_steps, args.tau)
     dt = time.perf_counter() - t0
     return {"value": args.cpu_steps / dt, "unit": "steps/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "cpus_visible": avail,
             "sample": f"{args.cpu_steps} inner steps incl. hyper steps every tau={args.tau} "
-                      f"(oracle/lds_oracle.py, dense torch-CPU fp32, {threads} threads), "
-                      f"{dt:.1f} s"}
+                      f"(oracle/lds_oracle.py, dense torch-CPU fp32, {threads} threads), {dt:.1f} s"}
+
+
+def cpu_baseline_gcn(args, data, epochs):
+    """Config 1 on the CPU: the reference's fixed-graph GCN epoch
+    (src/scripts/gcn.py:75-91) as the oracle's dense torch-CPU restatement."""
+    from oracle import lds_oracle as O
+    model, threads, avail = host_info()
+    torch.set_num_threads(threads)
+    cpu = data.to("cpu")
+    run = O.FixedGcnTraining(cpu.x, cpu.y, cpu.dense_adj, cpu.train_mask, cpu.val_mask, cpu.test_mask,
+                             hidden=16, dropout_p=0.5, lr=0.01, wd=5e-4, rnd=O.Randomness(args.seed, 0),
+                             init_generator=torch.Generator().manual_seed(args.seed))
+    run.epoch()
+    t0 = time.perf_counter()
+    for _ in range(epochs):
+        run.epoch()
+    dt = time.perf_counter() - t0
+    return {"value": epochs / dt, "unit": "epochs/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "cpus_visible": avail,
+            "sample": f"{epochs} epochs (train step + evaluate, oracle/lds_oracle.py FixedGcnTraining, dense "
+                      f"torch-CPU fp32, {threads} threads), {dt:.1f} s"}
+
+
+def strong_scaling_leg(args, world, rank, device, barrier_sync):
+    """BASELINE config 4: S_total samples per hyper step split over the
+    ranks (S_total / world each).  Rank 0 first times S_total alone on its GPU
+    (T1), then all ranks time their shards with the all-reduce (TN)."""
+    total = args.strong_total
+    if total % world:
+        raise SystemExit(f"--strong-total {total} must divide by the world size {world}")
+    windows = max(1, args.strong_steps // args.tau)
+
+    def timed(S, reducer_world):
+        data, runner, _ = build(args, rank, device, samples=S)
+        eng, reducer = make_engine(runner, args.tau, reducer_world, S)
+        eng.inner_step()
+        eng.hyper_step(grad_reducer=reducer)
+        eng.capture_window(args.tau, grad_reducer=reducer)
+        eng.replay(1)
+        if reducer_world > 1:
+            barrier_sync()
+        else:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.replay(windows)
+        if reducer_world > 1:
+            barrier_sync()
+        else:
+            torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        del eng, runner, data
+        torch.cuda.empty_cache()
+        return el
+
+    t1 = None
+    if rank == 0:  # the single-GPU time of the whole S_total, before the group syncs
+        t1 = timed(total, 1)
+    if world > 1:
+        dist.barrier()
+    tn = timed(total // world, world)
+    if world > 1:
+        t = torch.tensor([tn], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tn = float(t.item())
+    steps = windows * args.tau
+    out = {"samples_total": total, "samples_per_rank": total // world, "steps": steps,
+           "t1_ms_per_step": None if t1 is None else 1000.0 * t1 / steps,
+           "tN_ms_per_step": 1000.0 * tn / steps,
+           "value": total * steps / tn, "unit": "sample-steps/s"}
+    if t1 is not None:
+        out["speedup_vs_1gpu"] = t1 / tn
+    return out
+
+
+def bench_gcn(args, world, rank, device, barrier_sync):
+    """BASELINE config 1: fixed-graph GCN epochs/s on the real Cora graph
+    through the drop-in API (MetaDenseGCN on a hot-path CSR graph, the
+    reference's Adam groups, evaluate() per epoch)."""
+    import torch.nn.functional as F
+    import ldsgnn
+    from ldsgnn.data.workloads import load_workload
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from ldsgnn.utils.evaluation import evaluate
+    data = load_workload("cora-given", device=device)
+    ldsgnn.rng.manual_seed(args.seed, replica=rank)
+    torch.manual_seed(args.seed)
+    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(device)
+    opt = torch.optim.Adam([{"params": gcn.layer_in.parameters(), "weight_decay": 5e-4},
+                            {"params": gcn.layer_out.parameters()}], lr=0.01)
+
+    def epoch():
+        opt.zero_grad()
+        gcn.train()
+        out = gcn(data.x, data.dense_adj)
+        loss = F.nll_loss(out[data.train_mask], data.y[data.train_mask])
+        loss.backward()
+        opt.step()
+        return evaluate(gcn, data)
+
+    for _ in range(args.warmup):
+        epoch()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = epoch()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_gcn(args, data, args.cpu_gcn_epochs)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "fixed-adjacency GCN training epochs/sec on Cora (BASELINE config 1)",
+            "value": world * args.steps / elapsed, "unit": "epochs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "real Cora Planetoid split, given graph (tests/golden/planetoid_cora.npz)",
+            "config": {"workload": "cora-gcn-fixed-adjacency", "path": "drop-in MetaDenseGCN + torch Adam",
+                       "val_acc_last_epoch": m["val.accuracy"]},
+            "roofline": None, "cpu_baseline": cpu}))
 
 
 def main():
@@ -164,30 +398,32 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--tau", type=int, default=5)
-    ap.add_argument("--dataset", default="cora")
+    ap.add_argument("--model", default="lds", choices=["lds", "gcn"],
+                    help="lds: the LDS bilevel hot path (configs 2-5); gcn: config 1, fixed-graph GCN training")
+    ap.add_argument("--dataset", default="cora", help="ldsgnn.data.workloads: cora (config 2, default), "
+                    "citeseer (config 3), synthetic20k (config 5), cora-synthetic")
     ap.add_argument("--seed", type=int, default=597905255 % (2 ** 31))
     ap.add_argument("--cpu-steps", type=int, default=11)
+    ap.add_argument("--cpu-gcn-epochs", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--theta-form", default=None, help="θ-grad assembly form (ldsgnn.ops.THETA_GRAD_FORMS; "
                     "default: bf16x3, the split-bf16 MFMA form picked by shape)")
-    ap.add_argument("--kernel", default="auto", help="entry point for the roofline leg (auto: the θ-grad "
-                    "assembly the path uses)")
-    ap.add_argument("--split", action="store_true", help="engine: per-graph dθ chunks on a side stream beside "
-                    "the reverse pass instead of one assembly launch per window (measured slower on MI355X)")
     ap.add_argument("--samples", type=int, default=1, help="Monte-Carlo replica samples per GPU, batched in "
                     "every launch (BASELINE configs 3/4); value is then sample-steps/s")
+    ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
+                    "the ranks, against rank 0 alone (default 64 when N > 1, off at N = 1)")
+    ap.add_argument("--strong-steps", type=int, default=50)
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
+    ap.add_argument("--no-breakdown", action="store_true", help="skip the per-launch window breakdown leg")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
                     "for rehearsing several ranks on one device)")
     ap.add_argument("--graph-model", default="lds", choices=["lds", "embedding", "gae"],
-                    help="graph generative model (embedding / gae: P from node embeddings, autograd path)")
+                    help="graph generative model (embedding / gae: P from node embeddings)")
     ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
                     help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local_rank = world_info()
     dev_index = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
@@ -196,15 +432,8 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.backend)
-
-    import ldsgnn
-    from ldsgnn import _native as nat
-    if args.theta_form is not None:
-        from ldsgnn import ops as ldsops
-        ldsops.theta_grad_form(args.theta_form)
-
-    data, runner, opt_mask = build(args, rank, device)
-    n = data.num_nodes
+    if args.strong_total is None:
+        args.strong_total = 64 if world > 1 and args.model == "lds" and args.path == "engine" else 0
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -212,6 +441,18 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    import ldsgnn  # noqa: F401
+    from ldsgnn import ops as ldsops
+    if args.theta_form is not None:
+        ldsops.theta_grad_form(args.theta_form)
+    if args.model == "gcn":
+        bench_gcn(args, world, rank, device, barrier_sync)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    data, runner, opt_mask = build(args, rank, device)
+    n = data.num_nodes
     use_engine = args.path == "engine"
     # embedding / GAE on the engine: θ = P(model parameters), the outer step
     # (autograd through P + the model's optimizer) runs eagerly between the
@@ -219,19 +460,10 @@ def main():
     param_theta = args.graph_model != "lds"
     if param_theta and use_engine and (world > 1 or args.samples > 1):
         raise SystemExit("--graph-model embedding/gae on the engine: one GPU, one sample")
-    if args.kernel == "auto":
-        if use_engine and param_theta:
-            args.kernel = "lds_theta_grad"
-        elif use_engine and args.samples > 1:
-            args.kernel = "lds_theta_grad_ex"
-        elif use_engine and world == 1:
-            args.kernel = "lds_theta_grad_sgd_accum" if args.split else "lds_theta_grad_sgd"
-        else:
-            args.kernel = "lds_theta_grad"
+    eng = reducer = None
     if use_engine:
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
         eng, reducer = make_engine(runner, args.tau, world, args.samples)
-        eng.split_theta_grad = args.split
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
@@ -256,72 +488,56 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * args.samples * args.steps / elapsed
+
+    # steady state: the same replays over a longer stretch (>= ~0.2 s), reported beside `value`
+    steady = None
+    if use_engine and use_graph:
+        reps = max(args.steps // args.tau, int(0.2 / max(elapsed / max(1, args.steps // args.tau), 1e-6)))
+        barrier_sync()
+        t1 = time.perf_counter()
+        run_engine_windows(eng, reducer, reps, args.tau, True)
+        barrier_sync()
+        el = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        steady = {"steps": reps * args.tau, "value": world * args.samples * reps * args.tau / el,
+                  "ms_per_step": 1000.0 * el / (reps * args.tau)}
+
     in_sync = None
     if world > 1:  # replicas must hold bit-identical θ after every update
         th = eng.theta if use_engine else runner.outer_trainer.model.probs.data
-        mine = torch.tensor([th.double().sum().item(), th.double().square().sum().item()], dtype=torch.float64)
-        allv = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allv, mine.to(device) if args.backend == "nccl" else mine)
+        mine = torch.stack([th.double().sum(), th.double().square().sum()])  # on this rank's device
+        if args.backend == "nccl":
+            allv = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allv, mine)
+        else:
+            mine = mine.cpu()
+            allv = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allv, mine)
         in_sync = all(torch.equal(v.cpu(), allv[0].cpu()) for v in allv)
 
-    # roofline leg: the same K steps again with HIP events around the kernel
-    nat.timer.enable(args.kernel)
-    if use_engine:
-        run_engine_windows(eng, reducer, args.steps // args.tau, args.tau, False)
-    else:
-        step = run_steps(runner, step, args.steps, args.tau)
-    ksum = nat.timer.summary()[args.kernel]
-    nat.timer.disable()
-    if use_engine:
-        nnz = eng.sampled_nnz()
-    else:
-        g = runner.outer_trainer.model.sample()  # a representative graph for byte counts
-        nnz = g.nnz()
-    tri = n * (n + 1) // 2
-    if args.kernel in ("lds_spmm_norm", "lds_spmm_norm_blocked"):
-        f = 16
-        algo = 4 * (n + 1) + 4 * nnz + 4 * n + 8 * n * f
-        achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
-    elif args.kernel == "lds_aggregate_bitmask":  # int8 MFMA: 4 limbs x 2 ops per (row, column, feature)
-        rows, cols = -(-n // 256) * 256, -(-n // 512) * 512
-        ops = 2.0 * rows * cols * 16 * 4
-        achieved = ops / (ksum["avg_us"] * 1e-6) / 1e12
-        roof = {"bound": "mfma", "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TOP/s",
-                "frac": achieved / INT8_PEAK_TOPS, "traffic": None,
-                "hbm_algorithmic_GBs": (8 * n * nat.lib.lds_bitmask_words(n) + 4 * n + 8 * n * 16)
-                / (ksum["avg_us"] * 1e-6) / 1e9}
-    elif args.kernel == "lds_sample_bitmask":
-        words = nat.lib.lds_bitmask_words(n)
-        algo = 4 * tri + 8 * n * words
-        achieved = algo / (ksum["avg_us"] * 1e-6) / 1e9
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
-    else:  # lds_theta_grad[_sgd]: rank-2k update of the packed triangle
-        from ldsgnn.engine import LdsEngine
-        if use_engine and args.kernel == "lds_theta_grad_ex":  # S factor blocks of ldk columns
-            k = eng.S * eng.ldk
-        elif use_engine and args.kernel in ("lds_theta_grad_sgd", "lds_theta_grad"):  # one launch per window
-            k = LdsEngine.window_columns(args.tau, data.num_classes)
-        elif use_engine:  # split assembly: the timed launch is one graph's chunk (+ R, SGD)
-            k = LdsEngine.window_columns(1, data.num_classes) - LdsEngine.window_columns(0, data.num_classes)
-        else:  # one launch per graph: 4 uses (16 + 8 + 8 + 16 columns)
-            k = 16 + 8 + 8 + 16
-        flops = 4.0 * k * tri
-        fp32_equiv = flops / (ksum["avg_us"] * 1e-6) / 1e12
-        from ldsgnn import ops as ldsops
-        form = ldsops.theta_grad_form()
-        if form == "fp32":
-            roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": fp32_equiv / FP32_PEAK_TFLOPS, "traffic": None}
-        else:  # split-bf16: six bf16 MFMA products per fp32 product, priced against the bf16 dense peak
-            achieved = 6.0 * fp32_equiv
-            roof = {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / BF16_PEAK_TFLOPS, "traffic": None}
-        roof.update(form=form, fp32_equiv_tflops=fp32_equiv)
-    roof.update(kernel=args.kernel, avg_us=ksum["avg_us"], launches=ksum["launches"])
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.kernel, use_engine, world, args)
+    nnz = eng.sampled_nnz_mean() if use_engine else None
+    roof, window = None, None
+    if use_engine and not args.no_breakdown:
+        rows, summ = window_breakdown(eng, reducer, args, max(1, args.steps // args.tau))
+        total = sum(r["us_per_window"] for r in rows)
+        window = {"kernel_us_per_window": total,
+                  "launch_calls_per_window": sum(r["launches_per_window"] for r in rows),
+                  "wall_us_per_window": 1000.0 * elapsed / max(1, args.steps // args.tau),
+                  "top": [{k: v for k, v in r.items()} for r in rows[:4]]}
+        roof = roofline_of(rows[0], args)
+        roof["share_of_window"] = rows[0]["us_per_window"] / total if total else None
+        theta_rows = [r for r in rows if r["bound"] == "mfma"]
+        if theta_rows:
+            window["theta_grad"] = roofline_of(theta_rows[0], args)
+
+    strong = None
+    if use_engine and args.strong_total and not param_theta:
+        del eng
+        torch.cuda.empty_cache()
+        strong = strong_scaling_leg(args, world, rank, device, barrier_sync)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -329,22 +545,19 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": value, "unit": "steps/s" if args.samples == 1 else "sample-steps/s", "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": f"synthetic {args.dataset}-shaped (N={n}, F_in={data.num_features}, "
-                    f"C={data.num_classes}), " + ("theta ~ U(0,1)" if args.dataset == "synthetic20k"
-                                                  else "kNN-initialised theta"),
-            "config": {"workload": f"{args.dataset}-lds-" + ("uniform" if args.dataset == "synthetic20k" else
-                                                               "knn-init") + f"-S{args.samples}-tau{args.tau}", "path": args.path, "nodes": n,
-                       "features": data.num_features, "classes": data.num_classes, "hidden": 16,
+            "data": data.name + f" (N={n}, F_in={data.num_features}, C={data.num_classes})",
+            "config": {"workload": f"{args.dataset}-lds-S{args.samples}-tau{args.tau}", "path": args.path,
+                       "nodes": n, "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
-                       "sampled_nnz": nnz, "replicas_in_sync": in_sync, "graph_model": args.graph_model,
-                       "aggregation": (("bitmask x fixed-point s*Z on int8 MFMA (pre-pass)" if eng.bitmask_agg
-                                        else "column-blocked LDS SpMM pre-pass")
-                                       if use_engine and eng.long_rows else "in-kernel CSR")},
+                       "theta_grad_form": ldsops.theta_grad_form(), "sampled_nnz": nnz,
+                       "replicas_in_sync": in_sync, "graph_model": args.graph_model},
+            "steady_state": steady,
+            "strong_scaling": strong,
+            "window": window,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -238,7 +238,9 @@ int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float
  *     (fp32 accuracy, |error| <= ~2^-22 |U||V| per term, fp32 accumulation);
  *   2 split-bf16, 64 × 64 tiles, 16-wide k chunks;  3 the same, 32-wide;
  *   4 split-bf16, 128 × 128 tiles;  5 the same in XCD-grouped tile order;
- *   6 form 2 in XCD-grouped tile order.
+ *   6 form 2 in XCD-grouped tile order,
+ *   7 form 5 with 64-bit packed-index arithmetic at every n (the path n > 46 340
+ *     takes; for testing).
  * form = -1 only reads the current form into *prev (prev may be NULL). */
 int lds_theta_grad_set_form(int form, int* prev);
 

@@ -584,9 +584,11 @@ constexpr int kT2 = 128;
 constexpr int kS2 = 12;             // dwords per LDS row (8 data + 4 pad: 4 × odd)
 constexpr int kPL2 = kT2 * kS2;     // dwords per plane
 
-// Packed index of (i, j), i <= j, in 32-bit arithmetic while n(n+1) < 2^32
-// (n <= 46 340: the epilogue's 64 index computations per lane are 64-bit
-// multiplies otherwise).
+// Packed index of (i, j), i <= j, in 32-bit arithmetic (the epilogue's 64
+// index computations per lane are 64-bit multiplies otherwise).  i(2n - i + 1)
+// peaks at (n-1)(n+2) < 2^32 for n <= 65 535; the launch uses it for
+// n <= 46 340, where n(n+1) < 2^31 (so the packed index itself also fits an
+// int32), and the 64-bit path above that (form 7 forces it for testing).
 template <bool SMALL>
 __device__ __forceinline__ int64_t tri_at_t(int i, int j, int64_t n) {
     if constexpr (SMALL) {
@@ -790,7 +792,8 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
 // Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
 // shape (below), 2 = 64-tile with 16-wide k chunks, 3 = 64-tile with 32-wide
 // k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
-// order, 6 = form 2 in XCD-grouped order.  Read at launch (a captured HIP graph keeps the form it was
+// order, 6 = form 2 in XCD-grouped order, 7 = form 5 with 64-bit index
+// arithmetic at every n (the n > 46 340 path; for testing).  Read at launch (a captured HIP graph keeps the form it was
 // captured with).
 static int g_theta_form = 1;
 constexpr int kGroup = 8;
@@ -810,11 +813,11 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
     // the branch-free staging needs whole 8-wide k groups in 16-byte aligned rows
     const bool fast = vec4 && (k & 7) == 0;
 #define LDS_TG_ARGS u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, vec4, ldrc, gscale
-    if (form == 4 || form == 5) {
+    if (form == 4 || form == 5 || form == 7) {
         const int per = (nt2 + 7) / 8;
-        const int grid = form == 5 ? 8 * per : nt2;
-        const int grp = form == 5 ? kGroup : 0;
-        const bool small = n <= 46340;
+        const int grid = form != 4 ? 8 * per : nt2;
+        const int grp = form != 4 ? kGroup : 0;
+        const bool small = n <= 46340 && form != 7;
         if (fast && small)
             hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp,
                                per);
@@ -993,7 +996,7 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
 }
 
 extern "C" int lds_theta_grad_set_form(int form, int* prev) {
-    LDS_CHECK_ARG(form >= -1 && form <= 6);
+    LDS_CHECK_ARG(form >= -1 && form <= 7);
     if (prev != nullptr) *prev = g_theta_form;
     if (form >= 0) g_theta_form = form;
     return 0;

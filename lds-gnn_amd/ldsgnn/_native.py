@@ -136,13 +136,22 @@ class KernelTimer:
     def __init__(self):
         self.names = set()
         self.events = {}
+        self.all = False
 
     def enable(self, *names):
         self.names = set(names)
         self.events = {n: [] for n in names}
+        self.all = False
+
+    def enable_all(self):
+        """Time every entry point (bench.py's per-window breakdown)."""
+        self.names = set(SIGNATURES)
+        self.events = {}
+        self.all = True
 
     def disable(self):
         self.names = set()
+        self.all = False
 
     def summary(self):
         torch.cuda.synchronize()
@@ -166,7 +175,7 @@ def call(name: str, *args) -> None:
         a.record()
         err = getattr(lib, name)(*args)
         b.record()
-        timer.events[name].append((a, b))
+        timer.events.setdefault(name, []).append((a, b))
         check(err, name)
         return
     check(getattr(lib, name)(*args), name)

@@ -256,6 +256,11 @@ class LdsEngine:
         # whose θ is a function of its own parameters (the embedding model)
         # takes dθ, steps its optimizer and rewrites self.theta in place
         self.outer_update = None
+        # grad_reducer(grad): the default exchange of a hyper step (e.g. the
+        # all-reduce mean of dθ over ranks, ldsgnn.replicas); when set, dθ is
+        # written, reduced, then SGD + clamp runs (the assembly is not fused
+        # with the update), and captures split at it
+        self.grad_reducer = None
         # dθ assembly split per graph: chunks of finished graphs run on a side
         # stream beside the (latency-bound) reverse pass.  Off by default: on
         # MI355X the replayed graph did not overlap the branches and the
@@ -536,6 +541,7 @@ class LdsEngine:
         self.xt_splits = max(1, int(splits))
         self.xt_part = (torch.zeros((self.S, self.xt_splits, self.fin, HID), dtype=torch.float32, device=self.dev)
                         if self.xt_splits > 1 else None)
+        self._layout_version = getattr(self, "_layout_version", 0) + 1  # captured step graphs are stale
 
     def _xt_split(self, xcsc: torch.Tensor, d: torch.Tensor, fwd_off: int):
         """Long X columns: run the column products as xt_splits partial ranges
@@ -644,6 +650,8 @@ class LdsEngine:
                 raise NotImplementedError("outer_update (θ as a function of model parameters) is single-sample")
             if grad_reducer is None:  # the model's outer step takes the reducer's place (capture: the split point)
                 grad_reducer = self.outer_update
+        elif grad_reducer is None:
+            grad_reducer = self.grad_reducer  # replicas over ranks: dθ → all-reduce → SGD (never fused)
         T = self.t
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
@@ -782,9 +790,16 @@ class LdsEngine:
         (buffers grow then), is captured and replayed the second time and
         replayed after that; the host-side state the eager call would leave
         (position, pending offsets) is restored from the capture."""
+        from .ops import theta_grad_form
+        # everything the captured launches bake in: position, pending counter
+        # offsets, Adam-table length, the θ-grad form (process-wide), whether
+        # dθ is written, and the buffer layout (last)
         key = (kind, self.t, self.pending_graph, self.pending_fwd, self.train_flag, self._tab_count(),
-               self._layout_version)
+               theta_grad_form(), self.keep_grad, self._layout_version)
         cache = self._step_graphs
+        stale = [k for k in cache if k[-1] != self._layout_version]
+        for k in stale:  # captures over re-laid buffers never replay again: free their pools
+            del cache[k]
         hit = cache.get(key)
         if hit is None:
             if key not in self._step_seen:
@@ -815,7 +830,8 @@ class LdsEngine:
     def hyper_step_graphed(self):
         """hyper_step() (single replica, no reducer) from a HIP graph keyed
         by the window length."""
-        if self.t * self.kg + HID + self.cw > self.ldk or self.split_theta_grad or self.outer_update is not None:
+        if self.t * self.kg + HID + self.cw > self.ldk or self.split_theta_grad or self.outer_update is not None \
+                or self.grad_reducer is not None:  # an eager exchange sits inside the step
             return self.hyper_step()
         return self._graphed("hyper", self.hyper_step)
 
@@ -841,6 +857,8 @@ class LdsEngine:
         assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
         if tau != self.tau:
             raise ValueError(f"engine was built for tau={self.tau}; capture that window length")
+        if grad_reducer is None:
+            grad_reducer = self.grad_reducer
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
@@ -900,6 +918,11 @@ class LdsEngine:
         """Stored entries (self-loops included) of the last window's outer
         graph, sample 0 (host sync)."""
         return int(self.gbatch.deg[self.tau, 0].sum().item())
+
+    def sampled_nnz_mean(self) -> float:
+        """Mean stored entries per sampled graph over the last batched window's
+        τ+1 graphs and replica samples (host sync)."""
+        return float(self.gbatch.deg.double().sum().item()) / (self.gbatch.count * self.S)
 
     @staticmethod
     def window_columns(tau: int, c: int) -> int:

@@ -42,10 +42,19 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
         raise NotImplementedError("the fused engine implements plain SGD on θ")
     if outer.lr_decay is not None and outer.lr_decay_step_size != 1:
         raise NotImplementedError("StepLR with step_size 1 only")
-    return LdsEngine(data.x, data.y, data.train_mask, outer.opt_mask, gm.probs.data, data.num_classes,
-                     dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=grp["lr"],
-                     lr_decay=outer.lr_decay, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
-                     params=inner.model_params, samples=samples)
+    eng = LdsEngine(data.x, data.y, data.train_mask, outer.opt_mask, gm.probs.data, data.num_classes,
+                    dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=grp["lr"],
+                    lr_decay=outer.lr_decay, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
+                    params=inner.model_params, samples=samples)
+    # θ.grad is the engine's dθ buffer, as after the reference's backward
+    # (src/trainers/outer.py:77), so a grad_reducer written for the drop-in
+    # trainer (e.g. ldsgnn.replicas.allreduce_mean(model)) sees the engine's
+    # hypergradient; with one set, every hyper step runs dθ → reducer → SGD
+    gm.probs.grad = eng.grad
+    if outer.grad_reducer is not None:
+        reducer, model = outer.grad_reducer, gm
+        eng.grad_reducer = lambda grad: reducer(model)
+    return eng
 
 
 def _param_theta_engine(inner, outer, tau, generator, samples) -> LdsEngine:

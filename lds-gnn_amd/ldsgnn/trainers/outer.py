@@ -35,8 +35,13 @@ class OuterProblemTrainer:
                  sparsity_factor: float = 0.0, regularize: bool = False, lr_decay: float = None,
                  lr_decay_step_size: int = 1, refine_embeddings: bool = False, pretrain: bool = False,
                  grad_reducer: Callable = None):
-        if regularize:
-            raise NotImplementedError("graph regularisation is outside the LDS hot path (default off)")
+        # src/trainers/outer.py:69-75 adds graph_regularization(...) weighted by
+        # the three factors.  With all factors zero that term is exactly 0 (and
+        # so is its gradient), so regularize=True is accepted as the no-op it
+        # is; non-zero factors are outside the LDS hot path (the final LDS
+        # configuration has regularize=False, src/trainers/outer.py:126).
+        if regularize and (smoothness_factor or disconnection_factor or sparsity_factor):
+            raise NotImplementedError("graph regularisation with non-zero factors is outside the LDS hot path")
         self.lr_decay = lr_decay
         self.lr_decay_step_size = lr_decay_step_size
         self.dataset = data
@@ -106,8 +111,9 @@ class OuterProblemTrainer:
 
 class OuterProblemTrainerFactory:
     """Defaults of the sacred ingredient (src/trainers/outer.py:120-129),
-    with pretrain off (not implemented yet)."""
-    config = dict(lr_decay=1.0, lr_decay_step_size=1, refine_embeddings=False, pretrain=False,
+    pretrain=True included: the trainer pre-trains θ with the fused
+    lds_pretrain_step kernel (ldsgnn.trainers.pretrainer)."""
+    config = dict(lr_decay=1.0, lr_decay_step_size=1, refine_embeddings=False, pretrain=True,
                   regularize=False, smoothness_factor=0.0, disconnection_factor=0.0, sparsity_factor=0.0)
 
     @staticmethod

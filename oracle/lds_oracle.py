@@ -494,3 +494,57 @@ def pretrain_epoch_dense(theta: torch.Tensor, train_adj: torch.Tensor, optimizer
     loss.backward()
     optimizer.step()
     return loss.item()
+
+
+class FixedGcnTraining:
+    """BASELINE config 1: the reference's fixed-graph GCN training loop
+    (src/scripts/gcn.py:56-99) restated — MetaDenseGCN on the constant given
+    adjacency (normalised densely every forward, src/models/gcn.py:24-25),
+    torch.optim.Adam with the two parameter groups of gcn.py:62-67 (weight
+    decay on layer_in only), and per epoch: train forward (dropout from the
+    keyed stream), NLL on the train mask, backward, step, then evaluate()
+    (src/utils/evaluation.py:25-48: eval forward, val/test loss and accuracy)
+    and EarlyStopping on val.loss (src/utils/early_stopping.py:19-36)."""
+
+    def __init__(self, x, y, adj, train_mask, val_mask, test_mask, hidden: int = 16, dropout_p: float = 0.5,
+                 lr: float = 0.01, wd: float = 5e-4, rnd: Optional[Randomness] = None,
+                 init_generator: Optional[torch.Generator] = None, params=None, patience: int = 10):
+        self.x, self.y, self.adj = x, y, adj
+        self.train_mask, self.val_mask, self.test_mask = train_mask, val_mask, test_mask
+        self.n, self.f_in = x.shape
+        self.c = int(y.max()) + 1
+        self.hidden, self.dropout_p = hidden, dropout_p
+        self.rnd = rnd or Randomness(0)
+        if params is None:
+            params = init_params(self.f_in, hidden, self.c, init_generator)
+        self.params = OrderedDict((k, v.detach().clone().requires_grad_(True)) for k, v in params.items())
+        ps = list(self.params.values())
+        self.opt = torch.optim.Adam([{"params": ps[:2], "weight_decay": wd}, {"params": ps[2:]}], lr=lr)
+        self.stopper = EarlyStopping(patience)
+
+    def forward(self, training: bool) -> torch.Tensor:
+        ux, uh = self.rnd.forward_u(self.n, self.f_in, self.hidden, self.dropout_p, training)
+        return gcn_forward(self.x, self.adj, self.params, self.dropout_p, training, ux, uh)
+
+    def evaluate(self) -> Dict[str, float]:
+        with torch.no_grad():
+            out = self.forward(False)
+            vm, tm = self.val_mask, self.test_mask
+            return {"val.accuracy": accuracy(out[vm], self.y[vm]),
+                    "val.loss": F.nll_loss(out[vm], self.y[vm]).item(),
+                    "test.accuracy": accuracy(out[tm], self.y[tm]),
+                    "test.loss": F.nll_loss(out[tm], self.y[tm]).item()}
+
+    def epoch(self) -> Tuple[float, float, Dict[str, float]]:
+        """One iteration of src/scripts/gcn.py:75-91; returns (train loss,
+        train acc, evaluate()) and updates the early stopper."""
+        self.opt.zero_grad()
+        out = self.forward(True)
+        m = self.train_mask
+        loss = F.nll_loss(out[m], self.y[m])
+        acc = accuracy(out[m], self.y[m])
+        loss.backward()
+        self.opt.step()
+        metrics = self.evaluate()
+        self.stopper.update(metrics["val.loss"])
+        return loss.item(), acc, metrics

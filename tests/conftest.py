@@ -8,6 +8,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "lds-gnn_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)

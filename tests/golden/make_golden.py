@@ -451,6 +451,235 @@ def g_hypergrad_cora(out, seed=7):
     out["theta_sum"] = theta.astype(np.float64).sum()
 
 
+def _planetoid(name):
+    """The real Planetoid split from the committed fixture, NormalizeFeatures
+    and MakeUndirected applied (ldsgnn.data.planetoid, pinned by
+    tests/test_planetoid.py against the reference's own data facts)."""
+    sys.path.insert(0, os.path.join(ROOT, "lds-gnn_amd"))
+    from ldsgnn.data.planetoid import load_planetoid_npz
+    return load_planetoid_npz(name)
+
+
+def _triu_edges(adj):
+    n = adj.size(0)
+    iu = torch.triu_indices(n, n, 1)
+    keep = adj[iu[0], iu[1]] != 0
+    return iu[:, keep].numpy().astype(np.int32)
+
+
+def _adj_from_edges(n, edges):
+    a = torch.zeros(n, n)
+    e = torch.from_numpy(edges).long()
+    a[e[0], e[1]] = 1.0
+    a[e[1], e[0]] = 1.0
+    return a
+
+
+def g_knn_cora(out):
+    """θ₀ of BASELINE config 2: the reference's own knn_graph_dense
+    (src/data/utils.py:165-175, sklearn kneighbors_graph, k=10, cosine,
+    include_self=False as KNNGraph(loop=False) passes it,
+    src/data/dataloader.py:104-105) on the real Cora features after
+    NormalizeFeatures, then MakeUndirected (src/data/transforms.py:31-37)."""
+    import sklearn
+    from src.data.utils import knn_graph_dense as reference_knn
+    data = _planetoid("cora")
+    a = reference_knn(data.x, 10, loop=False, metric="cosine")
+    out["directed"] = np.stack(np.nonzero(a.numpy())).astype(np.int32)  # row i -> its 10 nearest
+    out["edges"] = _triu_edges(torch.max(a, a.t()))                       # undirected, i < j
+    out["k"] = np.int64(10)
+    out["sklearn_version"] = np.array(sklearn.__version__)
+
+
+def _spy_grads(runner, grads):
+    orig = runner.outer_trainer.train_step
+
+    def spy(*a, **k):
+        m = orig(*a, **k)
+        grads.append(runner.outer_trainer.model.probs.grad.detach().clone().numpy().astype(np.float64))
+        return m
+
+    runner.outer_trainer.train_step = spy
+
+
+def _store_vec(out, key, v, pick):
+    out[key + "_val"] = v[pick].astype(np.float32)
+    out[key + "_sum"] = np.float64(v.astype(np.float64).sum())
+    out[key + "_l2"] = np.float64(np.sqrt((v.astype(np.float64) ** 2).sum()))
+
+
+def _opt_split(data, seed):
+    """bilevel.py:77: split_mask(val_mask, 0.5, shuffle=True) with numpy's
+    global RNG seeded (the reference's own split_mask)."""
+    from src.utils.graph import split_mask
+    np.random.seed(seed)
+    return split_mask(data.val_mask, 0.5, shuffle=True)
+
+
+def g_hypergrad_cora_real(out, seed=11):
+    """BASELINE config 2 exactly: real Cora, kNN θ₀ (golden knn_cora), the
+    reference's first two hyper steps (step 0: a 1-step window; steps 1-5: the
+    τ=5 window) with dropout 0.5, SGD lr 0.1, decay 0.99."""
+    data = _planetoid("cora")
+    knn = np.load(os.path.join(HERE, "knn_cora.npz"))
+    adj = _adj_from_edges(data.num_nodes, knn["edges"])
+    val, opt = _opt_split(data, seed)
+    prob = dict(x=data.x, y=data.y, train=data.train_mask, val=val, opt=opt, test=data.test_mask, adj=adj)
+    rnd = KeyedRandomness(seed=seed)
+    patch_reference(rnd)
+    runner = build_reference(prob, seed=seed, dropout=0.5)
+    grads, losses, thetas = [], [], []
+    _spy_grads(runner, grads)
+    for step in range(6):
+        losses.append(runner.inner_opt_step().loss)
+        if step % 5 == 0:
+            runner.hyper_opt_step(step)
+            thetas.append(runner.outer_trainer.model.probs.detach().clone().numpy())
+    pick = np.random.default_rng(seed).choice(grads[0].size, 20000, replace=False)
+    out["seed"] = np.int64(seed)
+    out["opt_mask"] = opt.numpy()
+    out["val_mask"] = val.numpy()
+    out["inner_losses"] = np.array(losses)
+    out["idx"] = pick.astype(np.int64)
+    for h in range(2):
+        _store_vec(out, f"grad{h}", grads[h], pick)
+        _store_vec(out, f"theta{h}", thetas[h], pick)
+    params = runner.inner_trainer.model_params
+    out["params_final"] = np.concatenate([params[k].detach().numpy().ravel() for k in params])
+
+
+class _Fp64Products:
+    """The reference's two matrix products — the aggregation torch.mm
+    (src/models/layers.py:44) and the linear layers' F.linear (torchmeta
+    MetaLinear) — accumulated in fp64 and rounded once: a pure rounding
+    change, for the conditioning probes."""
+
+    def __enter__(self):
+        import src.models.layers as layers
+        import torch.nn.functional as F
+        orig_mm = torch.mm
+
+        class TorchProxy:
+            def __getattr__(self, k):
+                return getattr(torch, k)
+
+            @staticmethod
+            def mm(a, b):
+                return orig_mm(a.double(), b.double()).float()
+
+        f_linear = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith("__")})
+        f_linear.linear = lambda x, w, b=None: F.linear(x.double(), w.double(),
+                                                        None if b is None else b.double()).float()
+        # the globals of torchmeta's MetaLinear stand-in (F.linear)
+        self.glob = sys.modules["torchmeta.modules"].MetaLinear.forward.__globals__
+        self.layers, self.F = layers, F
+        layers.torch, self.glob["F"] = TorchProxy(), f_linear
+        return self
+
+    def __exit__(self, *exc):
+        self.layers.torch, self.glob["F"] = torch, self.F
+
+
+def g_hypergrad_cora_real_probe(out):
+    """hypergrad_cora_real again under _Fp64Products.  How far the reference's
+    OWN hypergradients move under reordered fp32 arithmetic at config 2 bounds
+    what any other correct fp32 implementation can be held to: higher's Adam
+    update lr·m̂/(√v̂ + eps) has derivative up to lr/eps = 10⁶ in g for
+    parameters with |g| near eps (at the first Adam step it is ≈ lr·sign(g)),
+    so the hypergradient amplifies the rounding of those gradients
+    (DESIGN §6)."""
+    with _Fp64Products():
+        g_hypergrad_cora_real(out)
+
+
+def g_hypergrad_citeseer_s16_probe(out):
+    """hypergrad_citeseer_s16 again under _Fp64Products (config 3's probe)."""
+    with _Fp64Products():
+        g_hypergrad_citeseer_s16(out)
+
+
+def g_hypergrad_citeseer_s16(out, seed=13, samples=16):
+    """BASELINE config 3: real Citeseer, θ₀ = the given graph, S = 16
+    Monte-Carlo replicas.  Replica b is the reference's own runner with the
+    keyed stream of replica b (tags + b) and the same initial GCN (same torch
+    seed); each runs one τ=5 window (5 inner steps + its hyper step) from θ₀.
+    The engine's batched window moves θ by the MEAN of the 16 hypergradients
+    (SURVEY §8(e)), stored here with θ₁ = clamp(θ₀ − 0.1·mean, 0, 1)."""
+    data = _planetoid("citeseer")
+    val, opt = _opt_split(data, seed)
+    prob = dict(x=data.x, y=data.y, train=data.train_mask, val=val, opt=opt, test=data.test_mask,
+                adj=data.dense_adj)
+    mean, losses, outer = None, [], []
+    theta0 = None
+    for b in range(samples):
+        rnd = KeyedRandomness(seed=seed, replica=b)
+        patch_reference(rnd)
+        runner = build_reference(prob, seed=seed, dropout=0.5)
+        if theta0 is None:
+            theta0 = runner.outer_trainer.model.probs.detach().clone()
+        grads = []
+        _spy_grads(runner, grads)
+        losses.append([runner.inner_opt_step().loss for _ in range(5)])
+        m = runner.outer_trainer.train_step(runner.inner_trainer.model_forward)
+        outer.append(m.loss)
+        mean = grads[0] if mean is None else mean + grads[0]
+        print(f"  citeseer replica {b}: inner {losses[-1][-1]:.6f} outer {m.loss:.6f}", flush=True)
+    mean /= samples
+    theta1 = (theta0 - 0.1 * torch.from_numpy(mean).float()).clamp(0.0, 1.0).numpy()
+    pick = np.random.default_rng(seed).choice(mean.size, 20000, replace=False)
+    out["seed"] = np.int64(seed)
+    out["samples"] = np.int64(samples)
+    out["opt_mask"] = opt.numpy()
+    out["val_mask"] = val.numpy()
+    out["inner_losses"] = np.array(losses)   # [S, 5]
+    out["outer_losses"] = np.array(outer)    # [S]
+    out["idx"] = pick.astype(np.int64)
+    _store_vec(out, "grad", mean, pick)
+    _store_vec(out, "theta1", theta1, pick)
+
+
+def g_gcn_fixed_cora(out, seed=17, epochs=200, patience=10):
+    """BASELINE config 1: the reference's fixed-graph GCN training loop
+    (src/scripts/gcn.py:56-99 statement for statement: Adam groups 62-67,
+    train / backward / step / evaluate / EarlyStopping on val.loss) on the
+    real Cora split and given graph, dropout 0.5 from the keyed stream."""
+    from src.models.gcn import MetaDenseGCN
+    from src.utils.early_stopping import EarlyStopping
+    from src.utils.evaluation import accuracy, evaluate
+    import torch.nn.functional as F
+    data = _planetoid("cora")
+    rnd = KeyedRandomness(seed=seed)
+    patch_reference(rnd)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5)
+    out["params0"] = np.concatenate([p.detach().numpy().ravel() for p in gcn.parameters()])
+    optimizer = torch.optim.Adam([{"params": gcn.layer_in.parameters(), "weight_decay": 5e-4},
+                                  {"params": gcn.layer_out.parameters()}], lr=0.01)
+    stopper = EarlyStopping(patience)
+    rows = []
+    gcn.train()
+    for epoch in range(epochs):
+        optimizer.zero_grad()
+        gcn.train()
+        o = gcn(data.x, data.dense_adj)
+        loss = F.nll_loss(o[data.train_mask], data.y[data.train_mask])
+        acc = accuracy(o[data.train_mask], data.y[data.train_mask])
+        loss.backward()
+        optimizer.step()
+        m = evaluate(gcn, data)
+        rows.append([loss.item(), acc, m["val.loss"], m["val.accuracy"], m["test.loss"], m["test.accuracy"]])
+        stopper.update(m["val.loss"], model=gcn)
+        if stopper.abort:
+            break
+    gcn.load_state_dict(stopper.best_model_state_dict())
+    res = evaluate(gcn, data)
+    out["seed"] = np.int64(seed)
+    out["rows"] = np.array(rows)   # per epoch: train loss, train acc, val loss, val acc, test loss, test acc
+    out["final"] = np.array([res["val.loss"], res["val.accuracy"], res["test.loss"], res["test.accuracy"]])
+    out["params_final"] = np.concatenate([p.detach().numpy().ravel() for p in gcn.parameters()])
+    out["forward_draws"] = np.int64(rnd.forward_counter)
+
+
 def main():
     install_stubs()
     torch.set_num_threads(min(8, os.cpu_count() or 1))
@@ -458,7 +687,11 @@ def main():
             ("gcn_forward", g_gcn_forward), ("adam_first_order", g_adam_first_order),
             ("bilevel_small", g_bilevel),
             ("bilevel_nodrop", lambda o: g_bilevel(o, n=64, f_in=16, classes=3, seed=12, dropout=0.0)),
-            ("hypergrad_cora", g_hypergrad_cora), ("conditioning_probe", g_conditioning_probe)]
+            ("hypergrad_cora", g_hypergrad_cora), ("conditioning_probe", g_conditioning_probe),
+            ("knn_cora", g_knn_cora), ("hypergrad_cora_real", g_hypergrad_cora_real),
+            ("hypergrad_cora_real_probe", g_hypergrad_cora_real_probe),
+            ("hypergrad_citeseer_s16", g_hypergrad_citeseer_s16),
+            ("hypergrad_citeseer_s16_probe", g_hypergrad_citeseer_s16_probe), ("gcn_fixed_cora", g_gcn_fixed_cora)]
     only = set(sys.argv[1:])
     for name, fn in jobs:
         if only and name not in only:

@@ -1,0 +1,102 @@
+"""BASELINE config 1 — the 2-layer GCN on the fixed given Cora adjacency
+(src/scripts/gcn.py:56-99) — on the HIP product, against the reference-made
+golden gcn_fixed_cora (tests/golden/make_golden.py: the reference's own
+MetaDenseGCN, torch Adam with its two groups, evaluate(), EarlyStopping on the
+real Cora split, dropout 0.5 from the keyed stream).
+
+The product runs the same statements: MetaDenseGCN on cuda with the dense
+dataset adjacency, which it converts once to the hot-path CSR graph
+(ldsgnn.models.gcn.fixed_graph → ops.csr_graph_from_dense, cached), so every
+aggregation and its backward is the lds_spmm_norm kernel.  Adam is
+torch.optim.Adam, as in the reference.  fp32 tolerance 1e-5 (north_star) on
+the per-epoch losses while the trajectories are compared step for step."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import ldsgnn
+from ldsgnn import ops
+from ldsgnn.data.workloads import load_workload
+from ldsgnn.models.gcn import MetaDenseGCN, fixed_graph
+from ldsgnn.utils.early_stopping import EarlyStopping
+from ldsgnn.utils.evaluation import accuracy, evaluate
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_csr_graph_from_dense_matches_dense_normalisation():
+    """ops.csr_graph_from_dense on the real Cora graph vs the reference's dense
+    normalize_adjacency_matrix (src/utils/graph.py:136-153): identical
+    stored pattern (self-loops set), s bit-identical to 1/sqrt(deg), Â values
+    and Â·Z within fp32 rounding; asymmetric / weighted input is refused."""
+    from oracle import lds_oracle as O
+    data = load_workload("cora-given")
+    adj = data.dense_adj.clone()
+    adj[3, 3] = 1.0  # a stored self-loop is set, not added
+    g = ops.csr_graph_from_dense(adj.to(DEV))
+    ref = O.normalize_adjacency_matrix(adj)
+    a = g.to_dense().cpu()
+    assert torch.equal(a, (ref != 0).float())
+    deg = a.sum(1)
+    assert torch.equal(g.s.cpu(), (1.0 / deg.double().sqrt()).float())
+    assert float((g.normalized_dense().cpu() - ref).abs().max()) < 1e-7
+    z = torch.randn(adj.size(0), 16, generator=torch.Generator().manual_seed(1))
+    y = g.spmm(z.to(DEV)).cpu().double()
+    assert float((y - ref.double() @ z.double()).abs().max()) < 1e-5 * float((ref.abs() @ z.abs()).max())
+    bad = adj.clone()
+    bad[0, 1], bad[1, 0] = 1.0, 0.0
+    with pytest.raises(ValueError):
+        ops.csr_graph_from_dense(bad.to(DEV))
+    assert fixed_graph(bad.to(DEV)) is None  # the GCN then keeps the dense reference semantics
+    w = adj.clone() * 0.5
+    assert fixed_graph(w.to(DEV)) is None
+
+
+def test_fixed_graph_cache_follows_in_place_edits():
+    data = load_workload("cora-given", device=DEV)
+    a = data.dense_adj
+    g1 = fixed_graph(a)
+    assert fixed_graph(a) is g1
+    a[0, 5] = a[5, 0] = 1.0 - a[0, 5]
+    g2 = fixed_graph(a)
+    assert g2 is not g1 and g2.nnz() != g1.nnz()
+
+
+def test_config1_gcn_training_matches_reference_golden():
+    g = np.load(f"{GOLDEN}/gcn_fixed_cora.npz")
+    seed = int(g["seed"])
+    data = load_workload("cora-given", device=DEV)
+    ldsgnn.rng.manual_seed(seed, 0)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(DEV)
+    p0 = np.concatenate([p.detach().cpu().numpy().ravel() for p in gcn.parameters()])
+    assert np.array_equal(p0, g["params0"])  # the reference's initial draws
+    opt = torch.optim.Adam([{"params": gcn.layer_in.parameters(), "weight_decay": 5e-4},
+                            {"params": gcn.layer_out.parameters()}], lr=0.01)
+    stopper = EarlyStopping(10)
+    rows = []
+    for _ in range(200):
+        opt.zero_grad()
+        gcn.train()
+        out = gcn(data.x, data.dense_adj)
+        loss = F.nll_loss(out[data.train_mask], data.y[data.train_mask])
+        acc = accuracy(out[data.train_mask], data.y[data.train_mask])
+        loss.backward()
+        opt.step()
+        m = evaluate(gcn, data)
+        rows.append([loss.item(), acc, m["val.loss"], m["val.accuracy"], m["test.loss"], m["test.accuracy"]])
+        stopper.update(m["val.loss"], model=gcn)
+        if stopper.abort:
+            break
+    rows, ref = np.array(rows), g["rows"]
+    assert rows.shape == ref.shape  # same early-stopping epoch
+    for c in (0, 2, 4):  # losses
+        assert np.allclose(rows[:, c], ref[:, c], rtol=1e-5, atol=1e-6), (c, np.abs(rows[:, c] - ref[:, c]).max())
+    for c in (1, 3, 5):  # accuracies: identical counts
+        assert np.allclose(rows[:, c], ref[:, c], atol=1e-6), c
+    pf = np.concatenate([p.detach().cpu().numpy().ravel() for p in gcn.parameters()])
+    assert np.allclose(pf, g["params_final"], rtol=1e-4, atol=1e-5)
+    assert ldsgnn.rng.default_generator.forward_counter == int(g["forward_draws"])

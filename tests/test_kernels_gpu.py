@@ -426,4 +426,4 @@ def test_theta_grad_forms_vs_dense(device, form, n, k, ld, mode):
 def test_theta_grad_form_default_and_errors(device):
     assert ops.theta_grad_form() == "bf16x3"
     with pytest.raises(nat.NativeError):
-        nat.call("lds_theta_grad_set_form", 7, 0)
+        nat.call("lds_theta_grad_set_form", 8, 0)
