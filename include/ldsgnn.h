@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 3
+#define LDS_ABI_VERSION 4
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -483,7 +483,11 @@ int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int 
  * launch also runs the final stage of the fused reduction (as lds_engine_final
  * with dst = out), so one launch completes every parameter.  xt_part != NULL:
  * Xdᵀ d is read as the xt_splits partials of lds_engine_xt_partials (summed in
- * range order) instead of one wave per X column running the whole column. */
+ * range order) instead of running the column products.  `order` (fin ints) is
+ * the column plan: the first n_heavy entries are the columns with more than
+ * 128 entries, each run by a whole 1024-thread block (16 waves over its entry
+ * range, partials summed in wave order), then every other column, one wave
+ * each (n_heavy = 0 with xt_part). */
 int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int fin,
                        const float* d, float* out, int accumulate, uint64_t seed,
                        uint32_t tag_x, const void* scalars, int fwd_off, int train, float keep,
@@ -492,7 +496,8 @@ int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int f
                        const float* w0, const float* m0, const float* v0, float* w1, float* m1,
                        float* v1, float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                        const double* hyper, const float* adam_tab, int n_wd, int step_off,
-                       const float* xt_part, int xt_splits, const LdsBatch* batch, void* stream);
+                       const float* xt_part, int xt_splits, const int* order, int n_heavy,
+                       const LdsBatch* batch, void* stream);
 /* Long X columns (dense X, config 5): Xdᵀ d over `splits` entry ranges of every
  * column, one wave each; part[s][p][f][16] per replica sample s (stride
  * splits·fin·16).  Feeds lds_engine_xt_adam's xt_part. */

@@ -78,42 +78,40 @@ __device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr,
     return u01(w);
 }
 
-// Normalised aggregation of one 16-wide row: s_i Σ_j s_j Z[j][lane].
-// Chunks of 16 neighbours: one coalesced load of their column indices, each
-// lane fetches s of its own neighbour, then all 16 row gathers are in flight at
-// once.  With `ell` (the graph's first 16 neighbours per row as {j, s_j} pairs,
-// padding {row, 0}: lds_bitmask_fill_csr) the first chunk needs no row_ptr /
-// col / s round trip: ell, row_ptr and s[row] load together and the gathers
-// follow directly.  Past the row's end the weight is 0 (fmaf(0, z, acc) ==
-// acc), so the sum keeps the plain loop's sequential order either way.
+// Normalised aggregation of one 16-wide row, one wave per row:
+// s_row Σ_j s_j Z[j][h].  The row's CSR entries are taken 64 at a time: lane
+// t of a step loads entry beg + 64·step + t and its s_j, then 16-lane group g
+// gathers the Z rows of the step's entries 16g..16g+15 (lane h: feature h);
+// the four group partials combine by two xor-shuffles (fixed order), so every
+// lane ends with feature h of the row.  A row of degree d costs 1 + 2·⌈d/64⌉
+// dependent memory round trips.  A launch takes as long as its slowest row:
+// with 16 lanes per row and chunks of 16 the kNN-initialised Cora θ₀ (degree
+// up to 175) cost 8.8 µs per aggregation launch, one wave per row 4.2 µs, a
+// trivial launch 1.75 µs (tools/microbench/aggbench.py; batching several steps'
+// loads measured slower, 4.7 µs).  `ell` (the head {j, s_j} pairs) is unused
+// on this path.
 __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* __restrict__ col,
                                          const float* __restrict__ s, const int2* __restrict__ ell,
                                          const float* __restrict__ z, int row, int lane) {
+    (void)ell;
+    (void)lane;
+    const int t = threadIdx.x & 63;
+    const int h = t & (HID - 1);
+    const int g = t >> 4;
+    const int beg = rp[row], end = rp[row + 1];
     float acc = 0.f;
-    int p0;
-    const int end = rp[row + 1];
-    if (ell != nullptr) {
-        const int2 e = ell[row * HID + lane];
-        const float sl = __int_as_float(e.y);
-        float zk[HID];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(e.x, k, HID) * HID + lane];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, k, HID), zk[k], acc);
-        p0 = rp[row] + HID;
-    } else {
-        p0 = rp[row];
-    }
-    for (; p0 < end; p0 += HID) {
-        const int p = p0 + lane;
+    for (int p0 = beg; p0 < end; p0 += 64) {
+        const int p = p0 + t;
         const int jl = p < end ? col[p] : row;
         const float sl = p < end ? s[jl] : 0.f;
         float zk[HID];
 #pragma unroll
-        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, k, HID) * HID + lane];
+        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, g * HID + k) * HID + h];
 #pragma unroll
-        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, k, HID), zk[k], acc);
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
     }
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 32);
     return s[row] * acc;
 }
 
@@ -269,8 +267,9 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -290,17 +289,19 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const float y = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h0, row, lane));
     float hd = fmaxf(y, 0.f);
     if (train) hd = dk != 0.f ? hd * scale : 0.f;
-    y0[row * HID + lane] = y;
-    h1d[row * HID + lane] = hd;
+    if (g0) {
+        y0[row * HID + lane] = y;
+        h1d[row * HID + lane] = hd;
+    }
     // D1 ⊙ [Y0 > 0] (× 1/keep): the mask every later product with this layer's
     // ReLU + dropout Jacobian reads instead of redrawing it
-    if (dmask != nullptr) dmask[row * HID + lane] = y > 0.f ? dk : 0.f;
+    if (dmask != nullptr && g0) dmask[row * HID + lane] = y > 0.f ? dk : 0.f;
     float out = 0.f;
     for (int k = 0; k < c; ++k) {
         const float t = gsum16(hd * w.w1[k * HID + lane]);
         if (lane == k) out = t + w.b1[k];
     }
-    h2[row * HID + lane] = out;
+    if (g0) h2[row * HID + lane] = out;
 }
 
 // O = Â H2; P = softmax(O) (over c classes); dO = (P - onehot(y)) ⊙ m / |m|;
@@ -313,8 +314,9 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
     float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -336,9 +338,9 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const float p = act ? expf(logp) : 0.f;
     const int y = label[row];
     const bool sel = mask != nullptr && mask[row];
-    if (o_out) o_out[row * HID + lane] = act ? o : 0.f;
-    if (p_out) p_out[row * HID + lane] = p;
-    if (d_o) d_o[row * HID + lane] = (sel && act) ? (p - (lane == y ? 1.f : 0.f)) * inv_count : 0.f;
+    if (o_out && g0) o_out[row * HID + lane] = act ? o : 0.f;
+    if (p_out && g0) p_out[row * HID + lane] = p;
+    if (d_o && g0) d_o[row * HID + lane] = (sel && act) ? (p - (lane == y ? 1.f : 0.f)) * inv_count : 0.f;
     // argmax with first-index tie-break (torch.argmax)
     float best = act ? o : -INFINITY;
     int bi = lane;
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
         }
     }
     const float logpy = bcast16(logp, y);
-    if (lane == 0) {
+    if (lane == 0 && g0) {
         lossrow[row] = sel ? -logpy : 0.f;
         corrrow[row] = (sel && bi == y) ? 1.f : 0.f;
     }
@@ -373,8 +375,9 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth,
     int r_assign, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     w.w1 = boff<kB>(w.w1, bt.par);
     bkeys<kB>(keys, bt);
     const float g2 = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, d_o, row, lane));  // zero past c (dO is)
-    dh2[row * HID + lane] = g2;
+    if (g0) dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
     for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
     float mask;
@@ -403,8 +406,8 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
         mask = y0[row * HID + lane] > 0.f ? 1.f : 0.f;
         if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
     }
-    dy0[row * HID + lane] = dh1d * mask;
-    if (U != nullptr)  // outer graph, use 2: G = dO, Z = H2, Y = O, ÂG = dH2
+    if (g0) dy0[row * HID + lane] = dh1d * mask;
+    if (U != nullptr && g0)  // outer graph, use 2: G = dO, Z = H2, Y = O, ÂG = dH2
         emit_factor(U, V, ldk, R, foff, fwidth, row, lane, s[row], d_o[row * HID + lane],
                     h2[row * HID + lane], o_in[row * HID + lane], g2, r_assign != 0);
 }
@@ -417,11 +420,12 @@ __global__ __launch_bounds__(256) void bwd_layer1_kernel(
     const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     const float g = agg_row(rp, col, s, ell, dy0, row, lane);
-    dh0[row * HID + lane] = g;
-    if (U != nullptr)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
+    if (g0) dh0[row * HID + lane] = g;
+    if (U != nullptr && g0)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dy0[row * HID + lane],
                     h0[row * HID + lane], y0[row * HID + lane], g);
 }
@@ -614,8 +618,9 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff,
     const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -640,7 +645,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
     const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh0bar, row, lane));  // dY0bar
-    emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
+    if (g0) emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
     float mask;
     if (dmask != nullptr) {
         mask = dmask[ix];
@@ -649,18 +654,18 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
         if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
     }
     const float a = ag * mask;  // dH1dbar
-    dh1dbar[ix] = a;
+    if (g0) dh1dbar[ix] = a;
     const float hd = h1d[ix];
     float out = 0.f;
     for (int k = 0; k < c; ++k) {
         const float t = gsum16(a * w.w1[k * HID + lane] + hd * gw1bar[k * HID + lane]);
         if (lane == k) out = t + gb1bar[k];
     }
-    dh2bar[ix] = out;
+    if (g0) dh2bar[ix] = out;
     const float g2 = dh2[ix];
     float hb = 0.f;
     for (int k = 0; k < c; ++k) hb = fmaf(bcast16(g2, k), gw1bar[k * HID + lane], hb);
-    h1dbar[ix] = hb;
+    if (g0) h1dbar[ix] = hb;
 }
 
 // dObar = Â dH2bar.  Factor use 3 (G = dH2bar, Z = dO, Y = dH2, ÂG = dObar).
@@ -674,8 +679,9 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, int cw, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -691,12 +697,12 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     R = boff<kB>(R, bt.row);
     const int ix = row * HID + lane;
     const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh2bar, row, lane));  // dObar
-    emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
+    if (g0) emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
     const bool sel = mask[row] != 0;
     const float ub = (sel && lane < c) ? ag * inv_count : 0.f;
     const float pv = p[ix];
     const float dot = gsum16(ub * pv);
-    obar[ix] = (lane < c) ? pv * (ub - dot) : 0.f;
+    if (g0) obar[ix] = (lane < c) ? pv * (ub - dot) : 0.f;
 }
 
 // H2bar = Â Obar.  Factor use 2 (G = Obar, Z = H2, Y = O, ÂG = H2bar).
@@ -711,8 +717,9 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
     int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -733,8 +740,10 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     bkeys<kB>(keys, bt);
     const int ix = row * HID + lane;
     const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, obar, row, lane));  // H2bar (zero past c)
-    emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
-    h2bar[ix] = ag;
+    if (g0) {
+        emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
+        h2bar[ix] = ag;
+    }
     float hb = h1dbar_part[ix];
     for (int k = 0; k < c; ++k) hb = fmaf(bcast16(ag, k), w.w1[k * HID + lane], hb);
     float mask;
@@ -744,7 +753,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
         mask = y0[ix] > 0.f ? 1.f : 0.f;
         if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
     }
-    y0bar[ix] = hb * mask;
+    if (g0) y0bar[ix] = hb * mask;
 }
 
 // H0bar = Â Y0bar.  Factor use 1 (G = Y0bar, Z = H0, Y = Y0, ÂG = H0bar).
@@ -755,12 +764,15 @@ __global__ __launch_bounds__(256) void rev_d_kernel(
     float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     if (row >= n) return;
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     const int ix = row * HID + lane;
     const float ag = agg_row(rp, col, s, ell, y0bar, row, lane);
-    emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
-    h0bar[ix] = ag;
+    if (g0) {
+        emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
+        h0bar[ix] = ag;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -877,7 +889,7 @@ __device__ __forceinline__ void refresh_adam_table(int adam_step, const double* 
     }
 }
 
-constexpr int RG1K = 1024 / HID;  // row groups (rows) per 1024-thread block
+constexpr int kRowsPer1K = 1024 / 64;  // rows per 1024-thread block, one wave per row
 constexpr int kAdamTabMax = 256;  // step offsets covered by one Adam table
 
 // One row per 16-lane group (`valid` false past n); per-row terms as
@@ -937,7 +949,8 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials,
     const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 1024 + threadIdx.x) >> 6;  // one wave per row (agg_row)
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores and reduces; groups 1-3 hold copies
     const bool valid = row < n;
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -960,16 +973,16 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     if (valid) {
         const int ix = row * HID + lane;
         g = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dy0, row, lane));
-        dh0[ix] = g;
+        if (g0) dh0[ix] = g;
         a1 = dh2[ix];
         b1 = h1d[ix];
         lr = lossrow[row];
         qr = corrrow[row];
     }
-    if (U != nullptr && valid)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
+    if (U != nullptr && valid && g0)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dy0[row * HID + lane],
                     h0[row * HID + lane], y0[row * HID + lane], g);
-    block_reduce_1024(c, valid, a1, b1, 0.f, 0.f, g, a1, lr, qr, partials);
+    block_reduce_1024(c, valid && g0, a1, b1, 0.f, 0.f, g, a1, lr, qr, partials);
 }
 
 // H0bar = Â Y0bar (+ factor use 1); block partials of
@@ -984,7 +997,8 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials,
     const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 1024 + threadIdx.x) / HID;
+    const int row = (blockIdx.x * 1024 + threadIdx.x) >> 6;  // one wave per row (agg_row)
+    const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores and reduces; groups 1-3 hold copies
     const bool valid = row < n;
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -1007,14 +1021,16 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     if (valid) {
         const int ix = row * HID + lane;
         ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, y0bar, row, lane));
-        emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
-        h0bar[ix] = ag;
+        if (g0) {
+            emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
+            h0bar[ix] = ag;
+        }
         a1 = dh2[ix];
         b1 = dh1dbar[ix];
         a2 = h2bar[ix];
         b2 = h1d[ix];
     }
-    block_reduce_1024(c, valid, a1, b1, a2, b2, ag, a2, 0.f, 0.f, partials);
+    block_reduce_1024(c, valid && g0, a1, b1, a2, b2, ag, a2, 0.f, 0.f, partials);
 }
 
 // Sum the block partials (fixed order) into the flat parameter-shaped buffer
@@ -1122,12 +1138,20 @@ __global__ __launch_bounds__(256) void xt_partials_kernel(
     if (lane < HID) part[((int64_t)p * fin + f) * HID + lane] = acc;
 }
 
+// Columns of X are very uneven (Cora: 34 entries on average, up to 1083), and
+// one wave walking a long column one 64-entry step per round trip set the
+// launch's time.  The column plan (built once per X by the host,
+// LdsEngine._xt_plan) lists the `n_heavy` columns longer than 128 entries first:
+// each gets a 1024-thread block whose 16 waves take consecutive 64-aligned
+// entry ranges, their partial sums combined through LDS in wave order; the
+// remaining columns go 16 per block, one wave each.
+
 template <bool kB>
-__global__ __launch_bounds__(256) void xt_adam_kernel(
+__global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
     const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
     float keep, float scale, FinalArgs fin_args, AdamArgs adam, const float* __restrict__ xt_part,
-    int xt_splits, Batch bt) {
+    int xt_splits, const int* __restrict__ order, int n_heavy, Batch bt) {
     fin_args.partials = boff<kB>(fin_args.partials, bt.part);
     fin_args.dst = boff<kB>(fin_args.dst, bt.par);
     fin_args.metrics = boff<kB>(fin_args.metrics, bt.met);
@@ -1146,32 +1170,56 @@ __global__ __launch_bounds__(256) void xt_adam_kernel(
     d = boff<kB>(d, bt.act);
     bkeys<kB>(keys, bt);
     if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
-        const int e1 = threadIdx.x + 256;
-        final_pair(fin_args, threadIdx.x, e1 < kRedLen ? e1 : -1, adam, sc);
+        if (threadIdx.x < kRedLen) final_pair(fin_args, threadIdx.x, -1, adam, sc);
         return;
     }
-    const int f = (blockIdx.x * 256 + threadIdx.x) >> 6;
-    if (f >= fin) return;
+    const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
+    const bool heavy = (int)blockIdx.x < n_heavy;
+    int f, beg, end;
+    if (heavy) {
+        f = order[blockIdx.x];
+        const int cb = xcp[f], ce = xcp[f + 1];
+        const int seg = ((ce - cb + 15) / 16 + 63) / 64 * 64;
+        beg = min(ce, cb + wave * seg);
+        end = min(ce, beg + seg);
+    } else {
+        const int i = n_heavy + ((int)blockIdx.x - n_heavy) * 16 + wave;
+        if (i >= fin) return;  // light blocks never reach a barrier
+        f = order[i];
+        beg = xcp[f];
+        end = xcp[f + 1];
+    }
     const int idx = f * HID + (lane & (HID - 1));
+    const bool owner = lane < HID && (!heavy || wave == 0);
     // Adam operands and constants first: they overlap the product's loads
     AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
     float prev = 0.f;
-    if (lane < HID) {
+    if (owner) {
         o = adam_load(adam, idx);
         if (fin_args.accumulate) prev = fin_args.dst[idx];
     }
     float step_size, c2;
     adam_step_consts(adam, sc, step_size, c2);
     float acc = 0.f;
-    if (xt_part != nullptr) {   // partials of xt_partials_kernel, summed in range order
+    if (xt_part != nullptr) {   // partials of xt_partials_kernel, summed in range order (n_heavy = 0)
         if (kB) xt_part += (int64_t)blockIdx.y * xt_splits * fin * HID;
         if (lane < HID)
             for (int p = 0; p < xt_splits; ++p) acc += xt_part[((int64_t)p * fin + f) * HID + lane];
     } else {
-        acc = x_wave_dot<true>(xcp, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
+        acc = x_wave_dot_range<true>(beg, end, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
     }
-    if (lane < HID) {
+    if (heavy) {
+        __shared__ float part[16][HID];
+        if (lane < HID) part[wave][lane] = acc;
+        __syncthreads();
+        if (wave == 0 && lane < HID) {
+            acc = 0.f;
+#pragma unroll
+            for (int w = 0; w < 16; ++w) acc += part[w][lane];
+        }
+    }
+    if (owner) {
         const float val = fin_args.accumulate ? prev + acc : acc;
         fin_args.dst[idx] = val;
         adam_apply(adam, idx, val, o, step_size, c2);
@@ -1249,6 +1297,8 @@ using namespace lds;
 // C-ABI (see include/ldsgnn.h, "Fused engine")
 // ---------------------------------------------------------------------------
 static inline int rows_blocks(int n) { return (n + RG - 1) / RG; }
+// one wave per row (agg_row): 4 rows per 256-thread block, 16 per 1024-thread block
+static inline int wave_blocks(int n) { return (n + 3) / 4; }
 
 // Kernel-side strides of a host LdsBatch (NULL: one sample); returns grid.y.
 static inline int mk_batch(const LdsBatch* b, Batch& bt) {
@@ -1321,7 +1371,7 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, b1};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1336,7 +1386,7 @@ extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float*
     LDS_CHECK_ARG(batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(fwd_layer2_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer2_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c,
                        agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1354,7 +1404,7 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(bwd_layer2_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(bwd_layer2_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
                        foff, fwidth, r_assign, dmask, agg, bt);
@@ -1366,7 +1416,7 @@ extern "C" int lds_engine_bwd_layer1(const int* rp, const int* col, const float*
                                      float* U, float* V, int ldk, float* R, int foff, void* stream) {
     LDS_CHECK_ARG(rp && col && s && dy0 && dh0 && n > 0);
     LDS_CHECK_ARG(U == nullptr || (V && R && y0 && h0));
-    hipLaunchKernelGGL(bwd_layer1_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
+    hipLaunchKernelGGL(bwd_layer1_kernel, dim3(wave_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff);
     LDS_RETURN_LAST_ERROR();
 }
@@ -1429,7 +1479,7 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_a_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_a_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar,
                        h1dbar, mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
                        scale, U, V, ldk, R, foff, dmask, agg, bt);
@@ -1445,7 +1495,7 @@ extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, c
     LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_b_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_b_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw,
                        agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1464,7 +1514,7 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_c_kernel, ns, agg, dim3(rows_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_c_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V,
                        ldk, R, foff, cw, dmask, agg, bt);
@@ -1475,7 +1525,7 @@ extern "C" int lds_engine_rev_d(const int* rp, const int* col, const float* s, c
                                 const float* y0bar, const float* h0, const float* y0, float* h0bar,
                                 float* U, float* V, int ldk, float* R, int foff, void* stream) {
     LDS_CHECK_ARG(rp && col && s && y0bar && h0 && y0 && h0bar && U && V && R && n > 0);
-    hipLaunchKernelGGL(rev_d_kernel, dim3(rows_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
+    hipLaunchKernelGGL(rev_d_kernel, dim3(wave_blocks(n)), dim3(256), 0, (hipStream_t)stream, rp, col, s, (const int2*)ell,
                        n, y0bar, h0, y0, h0bar, U, V, ldk, R, foff);
     LDS_RETURN_LAST_ERROR();
 }
@@ -1533,7 +1583,7 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)) && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(bwd1_reduce_kernel, ns, agg, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0, (hipStream_t)stream,
+    LDS_LAUNCH_BA(bwd1_reduce_kernel, ns, agg, dim3((n + kRowsPer1K - 1) / kRowsPer1K, ns), dim3(1024), 0, (hipStream_t)stream,
                        rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow,
                        corrrow, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1548,7 +1598,7 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
     LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_d_reduce_kernel, ns, agg, dim3((n + RG1K - 1) / RG1K, ns), dim3(1024), 0,
+    LDS_LAUNCH_BA(rev_d_reduce_kernel, ns, agg, dim3((n + kRowsPer1K - 1) / kRowsPer1K, ns), dim3(1024), 0,
                        (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R,
                        foff, dh2, dh1dbar, h2bar, h1d, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1579,8 +1629,10 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                                   const float* m0, const float* v0, float* w1, float* m1, float* v1,
                                   float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                                   const double* hyper, const float* adam_tab, int n_wd, int step_off,
-                                  const float* xt_part, int xt_splits, const LdsBatch* batch, void* stream) {
-    LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && fin > 0 && batch_ok(batch));
+                                  const float* xt_part, int xt_splits, const int* order, int n_heavy,
+                                  const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && order && fin > 0 && batch_ok(batch));
+    LDS_CHECK_ARG(n_heavy >= 0 && n_heavy <= fin && (xt_part == nullptr || n_heavy == 0));
     LDS_CHECK_ARG(partials == nullptr || (nblocks > 0 && c > 0 && c <= HID));
     LDS_CHECK_ARG(xt_part == nullptr || xt_splits > 0);
     LDS_CHECK_ARG(adam_ok(adam_mode, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper, adam_tab,
@@ -1588,12 +1640,12 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
     AdamArgs a = mk_adam_args(adam_mode, first, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper,
                               adam_tab, n_wd, step_off);
     FinalArgs f{partials, nblocks, c, off_b0, off_w1, off_b1, accumulate, out, metrics};
-    const int blocks = (fin + 3) / 4 + (partials != nullptr ? 1 : 0);
+    const int blocks = n_heavy + (fin - n_heavy + 15) / 16 + (partials != nullptr ? 1 : 0);
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(256), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
+    LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(1024), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
-                       a, xt_part, xt_splits, bt);
+                       a, xt_part, xt_splits, order, n_heavy, bt);
     LDS_RETURN_LAST_ERROR();
 }
 

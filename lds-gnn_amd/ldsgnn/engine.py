@@ -247,7 +247,7 @@ class LdsEngine:
         self.obar, self.h2bar, self.y0bar, self.h0bar = z(), z(), z(), z()
         zp = lambda: torch.zeros((S, self.np), dtype=torch.float32, device=dev)  # noqa: E731
         self.wbar, self.mbar, self.vbar, self.gbar, self.g = zp(), zp(), zp(), zp(), zp()
-        self.nred = (n + 63) // 64  # first-stage partials of the fused reductions (64 rows per block)
+        self.nred = (n + 15) // 16  # first-stage partials of the fused reductions (16 rows per block)
         self.partials = torch.zeros((S, self.nred, _RED_LEN), dtype=torch.float32, device=dev)
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
@@ -541,17 +541,29 @@ class LdsEngine:
         self.xt_splits = max(1, int(splits))
         self.xt_part = (torch.zeros((self.S, self.xt_splits, self.fin, HID), dtype=torch.float32, device=self.dev)
                         if self.xt_splits > 1 else None)
+        self._xt_plan()
         self._layout_version = getattr(self, "_layout_version", 0) + 1  # captured step graphs are stale
+
+    def _xt_plan(self):
+        """lds_engine_xt_adam's column plan (X is fixed): the columns with more
+        than 128 entries first (a 1024-thread block each), then the rest (one
+        wave each); with split products (xt_splits > 1) no heavy columns."""
+        lens = (self.xcp[1:] - self.xcp[:-1]).long()
+        heavy = (lens > 128) if self.xt_splits <= 1 else torch.zeros_like(lens, dtype=torch.bool)
+        idx = torch.arange(self.fin, device=self.dev)
+        self.xt_order = torch.cat([idx[heavy], idx[~heavy]]).to(torch.int32).contiguous()
+        self.xt_heavy = int(heavy.sum())
 
     def _xt_split(self, xcsc: torch.Tensor, d: torch.Tensor, fwd_off: int):
         """Long X columns: run the column products as xt_splits partial ranges
-        (lds_engine_xt_partials) and return xt_adam's (xt_part, xt_splits)."""
+        (lds_engine_xt_partials) and return xt_adam's (xt_part, xt_splits,
+        column order, heavy count)."""
         if self.xt_splits <= 1:
-            return 0, 0
+            return 0, 0, nat.ptr(self.xt_order), self.xt_heavy
         nat.call("lds_engine_xt_partials", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
                  nat.ptr(d), self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off, 0, self.keep, self.scale,
                  self.xt_splits, nat.ptr(self.xt_part), self.btx, self._stream())
-        return nat.ptr(self.xt_part), self.xt_splits
+        return nat.ptr(self.xt_part), self.xt_splits, nat.ptr(self.xt_order), 0
 
     def _adam_args(self, mode: int, t: int, first: int = 0):
         """Trailing Adam arguments of lds_engine_final / lds_engine_xt_adam.
