@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 4
+#define LDS_ABI_VERSION 5
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -100,7 +100,7 @@ int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* s,
                          void* stream);
 
 /* ELL head of a graph (the engine's aggregation layout): for every row its
- * first 16 CSR entries as {j, bits of s_j} int pairs (n × 16 × 2 ints),
+ * first 64 CSR entries as {j, bits of s_j} int pairs (n × 64 × 2 ints),
  * padded with {row, 0}.  lds_bitmask_fill_csr plus the ELL head (s from
  * lds_bitmask_degree). */
 int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
@@ -121,7 +121,7 @@ int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t t
 /* Batched form for a window of graphs drawn from the same θ: graph g
  * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
  * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
- * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·32.  Four launches
+ * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·128.  Four launches
  * for all `count` graphs. */
 int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
                       const uint32_t* counter_base, uint32_t counter_offset, int count,
@@ -320,7 +320,7 @@ int lds_engine_scalars_size(void);
  * batching as the activations) — long rows (config 5), where
  * lds_spmm_norm_blocked runs as a pre-pass.
  *   act : n×16 activation / adjoint arrays      row : n-vectors (s, R, loss rows)
- *   rp  : row_ptr (n+1)   col : CSR capacity     ell : ELL head (n·32 int32)
+ *   rp  : row_ptr (n+1)   col : CSR capacity     ell : ELL head (n·128 int32)
  *   par : flat parameter vectors (w, m, v, g', adjoints)
  *   xval: the X-values argument (0 when it is the shared X, else the Xd stride)
  *   xd  : stored Xd arrays (CSR / CSC order)
@@ -331,6 +331,17 @@ typedef struct LdsBatch {
     int32_t samples;
     uint32_t tag_step;
     int64_t act, row, rp, col, ell, par, xval, xd, uv, part, met;
+    /* Row plan of the aggregating entry points (may be empty: n_heavy = 0).
+     * Every row gets one wave, except the n_heavy rows listed in heavy_rows
+     * (heavy_flag[row] = 1; rows expected to have more than 64 entries), which
+     * run on a block of their own appended after the one-wave-per-row blocks,
+     * all the block's waves splitting the row's entries.  The plan changes
+     * speed only: any row is aggregated correctly either way.  With a plan the
+     * fused reductions write ceil(n / 16) + n_heavy partials. */
+    const int32_t* heavy_rows;
+    const uint8_t* heavy_flag;
+    int32_t n_heavy;
+    int32_t reserved;
 } LdsBatch;
 
 /* lds_sample_bitmask with the draw counter read from device memory:

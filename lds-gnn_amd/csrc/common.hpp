@@ -14,7 +14,7 @@
 namespace lds {
 
 constexpr int kWave = 64;
-constexpr int kEllWidth = 16;  // neighbours per row in a graph's ELL head ({j, s_j} pairs)
+constexpr int kEllWidth = 64;  // neighbours per row in a graph's ELL head ({j, s_j} pairs): one wave's step
 
 // Packed upper-triangle index of (i, j), i <= j, of an n×n matrix in
 // torch.triu_indices(n, n) row-major order (src/utils/graph.py:41-45).

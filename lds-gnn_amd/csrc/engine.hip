@@ -55,6 +55,9 @@ struct Keys {
 struct Batch {
     int64_t act, row, rp, col, ell2, par, xval, xd, uv, part, met;
     uint32_t tag;
+    const int* heavy;       // row plan (include/ldsgnn.h LdsBatch)
+    const uint8_t* hflag;
+    int nh;
 };
 
 // kB = false (single-sample launch): no offset code at all.
@@ -113,6 +116,116 @@ __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* 
     acc += __shfl_xor(acc, 16);
     acc += __shfl_xor(acc, 32);
     return s[row] * acc;
+}
+
+// ---------------------------------------------------------------------------
+// Row plan of the aggregating kernels (include/ldsgnn.h LdsBatch): the first
+// ceil(n / W) blocks give each row one wave (W waves per block); a row the
+// plan marks heavy is skipped there and runs on a block of its own appended
+// after them, its W waves taking the row's entries 64 at a time, W·64 apart,
+// their sums combined through LDS in wave order (every wave of the block ends
+// with the row's value; wave 0 stores).  On the kNN-initialised Cora θ₀ the 17
+// rows of more than 64 entries (up to 175) otherwise set every launch's time:
+// 4.3 -> 3.4 µs per aggregation launch (tools/microbench/aggbench.py).
+// ---------------------------------------------------------------------------
+struct RowSel {
+    int row;          // -1: no row for this wave
+    int first, end;   // this wave's first CSR entry, the row's end
+    int step;         // entry stride between this wave's steps
+    bool heavy;       // a heavy-row block (all its waves share the row)
+    bool lead;        // this wave stores the row's results
+    int2 e;           // light rows: this lane's ELL head entry {j, s_j}
+};
+
+// The ELL head, row_ptr and the plan flag of a light row load together (the
+// head's address must not wait for the flag).
+template <int W, bool kAgg>
+__device__ __forceinline__ RowSel select_row(int n, const int* __restrict__ rp, const int2* __restrict__ ell,
+                                             const Batch& bt) {
+    RowSel r;
+    r.e = make_int2(0, 0);
+    const int wave = threadIdx.x >> 6;
+    const int nlight = (n + W - 1) / W;
+    r.heavy = (int)blockIdx.x >= nlight;
+    r.step = r.heavy ? 64 * W : 64;
+    int row;
+    if (r.heavy) {
+        row = bt.heavy[(int)blockIdx.x - nlight];
+    } else {
+        row = (int)blockIdx.x * W + wave;
+        if (row >= n) {
+            r.row = -1;
+            r.lead = false;
+            r.first = r.end = 0;
+            return r;
+        }
+    }
+    if constexpr (!kAgg) {
+        if (!r.heavy && ell != nullptr) r.e = ell[(int64_t)row * kEllWidth + (threadIdx.x & 63)];
+        const int beg = rp[row];
+        r.end = rp[row + 1];
+        r.first = beg + (r.heavy ? wave * 64 : 0);
+    } else {
+        r.first = r.end = 0;
+    }
+    if (!r.heavy && bt.nh > 0 && bt.hflag[row]) row = -1;  // its own block aggregates it
+    r.row = row;
+    r.lead = row >= 0 && (!r.heavy || wave == 0);
+    return r;
+}
+
+// s_row Σ_j s_j Z[j][h] of the selected row (feature h = lane % 16 in every
+// lane), the heavy-block combine included; 0 for waves without a row.
+// Light rows take their first 64 entries from the graph's ELL head ({j, s_j}
+// pairs, padded with {row, 0}: a zero weight on a finite row), which needs no
+// row_ptr: the head's load and the Z gathers are the row's only dependent
+// round trips up to degree 64 (one fewer than through row_ptr -> col -> s / Z).
+template <int W, bool kAgg>
+__device__ __forceinline__ float agg_value(const RowSel& r, const int* __restrict__ col,
+                                           const float* __restrict__ s, const int2* __restrict__ ell,
+                                           const float* __restrict__ z, const float* __restrict__ agg) {
+    const int t = threadIdx.x & 63;
+    const int h = t & (HID - 1);
+    if constexpr (kAgg) {
+        return r.row >= 0 ? agg[r.row * HID + h] : 0.f;
+    } else {
+        __shared__ float part[W][HID];
+        const int g = t >> 4;
+        float acc = 0.f;
+        if (r.row >= 0) {
+            int p0 = r.first;
+            if (!r.heavy && ell != nullptr) {
+                const int2 e = r.e;
+                const float sl = __int_as_float(e.y);
+                float zk[HID];
+#pragma unroll
+                for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(e.x, g * HID + k) * HID + h];
+#pragma unroll
+                for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
+                p0 += kEllWidth;
+            }
+            for (; p0 < r.end; p0 += r.step) {
+                const int p = p0 + t;
+                const int jl = p < r.end ? col[p] : r.row;
+                const float sl = p < r.end ? s[jl] : 0.f;
+                float zk[HID];
+#pragma unroll
+                for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, g * HID + k) * HID + h];
+#pragma unroll
+                for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
+            }
+            acc += __shfl_xor(acc, 16);
+            acc += __shfl_xor(acc, 32);
+        }
+        if (r.heavy) {  // block-uniform: every wave of the block reaches the barrier
+            if (t < HID) part[threadIdx.x >> 6][t] = acc;
+            __syncthreads();
+            acc = part[0][h];
+#pragma unroll
+            for (int w = 1; w < W; ++w) acc += part[w][h];
+        }
+        return r.row >= 0 ? s[r.row] * acc : 0.f;
+    }
 }
 
 // Write one factor pair (U = s⊙G, V = s⊙Z) into columns [off, off+width) of the
@@ -267,8 +380,6 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
-    if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -283,10 +394,12 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     w.w1 = boff<kB>(w.w1, bt.par);
     w.b1 = boff<kB>(w.b1, bt.par);
     bkeys<kB>(keys, bt);
-    // the dropout draw does not depend on the aggregation: issue it first
+    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    const float y = agg_value<4, kAgg>(rsel, col, s, ell, h0, agg);
+    if (!rsel.lead) return;
+    const int row = rsel.row;
     const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
                            : 1.f;
-    const float y = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h0, row, lane));
     float hd = fmaxf(y, 0.f);
     if (train) hd = dk != 0.f ? hd * scale : 0.f;
     if (g0) {
@@ -314,8 +427,6 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
     float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
-    if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -328,7 +439,10 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     d_o = boff<kB>(d_o, bt.act);
     lossrow = boff<kB>(lossrow, bt.row);
     corrrow = boff<kB>(corrrow, bt.row);
-    const float o = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, h2, row, lane));
+    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    const float o = agg_value<4, kAgg>(rsel, col, s, ell, h2, agg);
+    if (!rsel.lead) return;
+    const int row = rsel.row;
     const bool act = lane < c;
     const float m = gmax16(act ? o : -INFINITY);
     const float e = act ? expf(o - m) : 0.f;
@@ -375,8 +489,6 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth,
     int r_assign, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
-    if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -395,7 +507,10 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     R = boff<kB>(R, bt.row);
     w.w1 = boff<kB>(w.w1, bt.par);
     bkeys<kB>(keys, bt);
-    const float g2 = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, d_o, row, lane));  // zero past c (dO is)
+    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    const float g2 = agg_value<4, kAgg>(rsel, col, s, ell, d_o, agg);  // zero past c (dO is)
+    if (!rsel.lead) return;
+    const int row = rsel.row;
     if (g0) dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
     for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
@@ -618,8 +733,6 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff,
     const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
-    if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -643,8 +756,11 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
+    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh0bar, agg);  // dY0bar
+    if (!rsel.lead) return;
+    const int row = rsel.row;
     const int ix = row * HID + lane;
-    const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh0bar, row, lane));  // dY0bar
     if (g0) emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
     float mask;
     if (dmask != nullptr) {
@@ -679,8 +795,6 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, int cw, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
-    if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -695,8 +809,11 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     U = boff<kB>(U, bt.uv);
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
+    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh2bar, agg);  // dObar
+    if (!rsel.lead) return;
+    const int row = rsel.row;
     const int ix = row * HID + lane;
-    const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dh2bar, row, lane));  // dObar
     if (g0) emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], dh2bar[ix], d_o[ix], dh2[ix], ag);
     const bool sel = mask[row] != 0;
     const float ub = (sel && lane < c) ? ag * inv_count : 0.f;
@@ -717,8 +834,6 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
     int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
-    if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
@@ -738,8 +853,11 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
+    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, obar, agg);  // H2bar (zero past c)
+    if (!rsel.lead) return;
+    const int row = rsel.row;
     const int ix = row * HID + lane;
-    const float ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, obar, row, lane));  // H2bar (zero past c)
     if (g0) {
         emit_factor(U, V, ldk, R, foff, cw, row, lane, s[row], obar[ix], h2[ix], o[ix], ag);
         h2bar[ix] = ag;
@@ -892,49 +1010,51 @@ __device__ __forceinline__ void refresh_adam_table(int adam_step, const double* 
 constexpr int kRowsPer1K = 1024 / 64;  // rows per 1024-thread block, one wave per row
 constexpr int kAdamTabMax = 256;  // step offsets covered by one Adam table
 
-// One row per 16-lane group (`valid` false past n); per-row terms as
-// colreduce_kernel; writes the block's partial (kRedLen floats).
+// One row per wave (its 16-vectors in lanes 0-15; `valid` false for waves
+// without a row): the block's partial of
+//   A[c][h] = Σ_rows av1[c] bh1[h] + av2[c] bh2[h]   (c < c_n)
+//   v1[h] = Σ x1[h],  v2[h] = Σ x2[h],  l0 = Σ l,  l1 = Σ q
+// (layout of colreduce_kernel).  The rows stage their vectors in LDS and
+// thread e < kRedLen sums element e over the 16 rows in row order — no
+// cross-lane broadcasts (the 16-lane-row form needed 64 shuffles per row).
 __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1, float bh1, float av2,
                                                   float bh2, float x1, float x2, float l, float q,
                                                   float* __restrict__ partials) {
-    __shared__ float red[16][kRedLen];
-    const int lane = threadIdx.x & (HID - 1);
-    const int gw = (threadIdx.x >> 4) & 3;
+    __shared__ float vec[16][6][HID];
+    __shared__ float sca[16][2];
+    const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    if (!valid) av1 = bh1 = av2 = bh2 = x1 = x2 = l = q = 0.f;
-    float acc[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const float p1 = bcast16(av1, k), p2 = bcast16(av2, k);
-        acc[k] = k < c_n ? fmaf(p2, bh2, p1 * bh1) : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        acc[k] += __shfl_xor(acc[k], 16);
-        acc[k] += __shfl_xor(acc[k], 32);
-    }
-    x1 += __shfl_xor(x1, 16);
-    x1 += __shfl_xor(x1, 32);
-    x2 += __shfl_xor(x2, 16);
-    x2 += __shfl_xor(x2, 32);
-    l += __shfl_xor(l, 16);
-    l += __shfl_xor(l, 32);
-    q += __shfl_xor(q, 16);
-    q += __shfl_xor(q, 32);
-    if (gw == 0) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) red[wave][k * 16 + lane] = acc[k];
-        red[wave][256 + lane] = x1;
-        red[wave][272 + lane] = x2;
-        red[wave][288 + lane] = lane == 0 ? l : (lane == 1 ? q : 0.f);
+    if (lane < HID) {
+        vec[wave][0][lane] = valid ? av1 : 0.f;
+        vec[wave][1][lane] = valid ? bh1 : 0.f;
+        vec[wave][2][lane] = valid ? av2 : 0.f;
+        vec[wave][3][lane] = valid ? bh2 : 0.f;
+        vec[wave][4][lane] = valid ? x1 : 0.f;
+        vec[wave][5][lane] = valid ? x2 : 0.f;
+        if (lane == 0) {
+            sca[wave][0] = valid ? l : 0.f;
+            sca[wave][1] = valid ? q : 0.f;
+        }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < kRedLen; e += 1024) {
-        float t = 0.f;
+    const int e = threadIdx.x;
+    if (e >= kRedLen) return;
+    float t = 0.f;
+    if (e < 256) {
+        const int c = e >> 4, h = e & (HID - 1);
+        if (c < c_n) {
 #pragma unroll
-        for (int w = 0; w < 16; ++w) t += red[w][e];
-        partials[(int64_t)blockIdx.x * kRedLen + e] = t;
+            for (int r = 0; r < 16; ++r) t += fmaf(vec[r][2][c], vec[r][3][h], vec[r][0][c] * vec[r][1][h]);
+        }
+    } else if (e < 288) {
+        const int k = e < 272 ? 4 : 5, h = (e - 256) & (HID - 1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += vec[r][k][h];
+    } else if (e < 290) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += sca[r][e - 288];
     }
+    partials[(int64_t)blockIdx.x * kRedLen + e] = t;
 }
 
 // dH0 = Â dY0 (+ outer factor (dY0, H0)); block partials of
@@ -949,9 +1069,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials,
     const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 1024 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores and reduces; groups 1-3 hold copies
-    const bool valid = row < n;
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -969,10 +1087,13 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     U = boff<kB>(U, bt.uv);
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
-    float g = 0.f, a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
+    const RowSel rsel = select_row<16, kAgg>(n, rp, ell, bt);
+    float g = agg_value<16, kAgg>(rsel, col, s, ell, dy0, agg);
+    const bool valid = rsel.lead;
+    const int row = rsel.row;
+    float a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        g = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, dy0, row, lane));
         if (g0) dh0[ix] = g;
         a1 = dh2[ix];
         b1 = h1d[ix];
@@ -997,9 +1118,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials,
     const float* __restrict__ agg, Batch bt) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 1024 + threadIdx.x) >> 6;  // one wave per row (agg_row)
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores and reduces; groups 1-3 hold copies
-    const bool valid = row < n;
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
     rp = boff<kB>(rp, bt.rp);
     col = boff<kB>(col, bt.col);
@@ -1017,10 +1136,13 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     U = boff<kB>(U, bt.uv);
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
-    float ag = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
+    const RowSel rsel = select_row<16, kAgg>(n, rp, ell, bt);
+    const float ag = agg_value<16, kAgg>(rsel, col, s, ell, y0bar, agg);
+    const bool valid = rsel.lead;
+    const int row = rsel.row;
+    float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
     if (valid) {
         const int ix = row * HID + lane;
-        ag = (kAgg ? agg[row * HID + lane] : agg_row(rp, col, s, ell, y0bar, row, lane));
         if (g0) {
             emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
             h0bar[ix] = ag;
@@ -1105,6 +1227,55 @@ __device__ __forceinline__ void final_pair(const FinalArgs& f, int e0, int e1, c
     }
 }
 
+// The final stage in a 1024-thread block: three threads per partial element,
+// each summing a third of the first-stage blocks (in order), the thirds then
+// added in order through LDS; thread e < kRedLen completes element e (as
+// final_pair: dst, metrics, Adam).  With one wave per row the fused
+// reductions write ⌈n/16⌉ (+ heavy rows) partials, 187 at Cora.
+__device__ __forceinline__ void final_block_1024(const FinalArgs& f, const AdamArgs& adam,
+                                                 const EngineScalars* __restrict__ sc) {
+    __shared__ float third[3][kRedLen];
+    const int t = threadIdx.x;
+    const int q = t / kRedLen, e = t - q * kRedLen;
+    // the completing thread's Adam operands first (they overlap the sums)
+    const int idx = t < kRedLen ? final_index(f, t) : -1;
+    AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
+    float prev = 0.f;
+    if (idx >= 0) {
+        o = adam_load(adam, idx);
+        if (f.accumulate) prev = f.dst[idx];
+    }
+    if (q < 3) {
+        const int per = (f.nblocks + 2) / 3;
+        const int b0 = q * per, b1 = min(f.nblocks, b0 + per);
+        float v = 0.f;
+        for (int c0 = b0; c0 < b1; c0 += kRedBlocks) {
+            float x[kRedBlocks];
+#pragma unroll
+            for (int b = 0; b < kRedBlocks; ++b)
+                x[b] = c0 + b < b1 ? f.partials[(int64_t)(c0 + b) * kRedLen + e] : 0.f;
+#pragma unroll
+            for (int w = kRedBlocks / 2; w > 0; w >>= 1)
+#pragma unroll
+                for (int b = 0; b < w; ++b) x[b] += x[b + w];
+            v += x[0];
+        }
+        third[q][e] = v;
+    }
+    __syncthreads();
+    if (t >= kRedLen) return;
+    const float tot = (third[0][t] + third[1][t]) + third[2][t];
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
+    if (idx >= 0) {
+        const float val = f.accumulate ? prev + tot : tot;
+        f.dst[idx] = val;
+        adam_apply(adam, idx, val, o, step_size, c2);
+    } else if (idx <= -2 && f.metrics) {
+        f.metrics[-2 - idx] = tot;
+    }
+}
+
 __global__ __launch_bounds__(320) void final_kernel(FinalArgs f, AdamArgs adam,
                                                     const EngineScalars* __restrict__ sc) {
     if (threadIdx.x < kRedLen) final_pair(f, threadIdx.x, -1, adam, sc);
@@ -1170,7 +1341,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     d = boff<kB>(d, bt.act);
     bkeys<kB>(keys, bt);
     if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
-        if (threadIdx.x < kRedLen) final_pair(fin_args, threadIdx.x, -1, adam, sc);
+        final_block_1024(fin_args, adam, sc);
         return;
     }
     const int wave = threadIdx.x >> 6;
@@ -1302,11 +1473,18 @@ static inline int wave_blocks(int n) { return (n + 3) / 4; }
 
 // Kernel-side strides of a host LdsBatch (NULL: one sample); returns grid.y.
 static inline int mk_batch(const LdsBatch* b, Batch& bt) {
-    bt = Batch{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0u};
-    if (b == nullptr || b->samples <= 1) return 1;
-    bt = Batch{b->act, b->row, b->rp, b->col, b->ell / 2, b->par, b->xval, b->xd, b->uv, b->part, b->met,
-               b->tag_step};
+    bt = Batch{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0u, nullptr, nullptr, 0};
+    if (b == nullptr) return 1;
+    bt.heavy = b->heavy_rows;  // the row plan applies to single-sample launches too
+    bt.hflag = b->heavy_flag;
+    bt.nh = b->n_heavy > 0 && b->heavy_rows && b->heavy_flag ? b->n_heavy : 0;
+    if (b->samples <= 1) return 1;
+    bt.act = b->act; bt.row = b->row; bt.rp = b->rp; bt.col = b->col; bt.ell2 = b->ell / 2; bt.par = b->par;
+    bt.xval = b->xval; bt.xd = b->xd; bt.uv = b->uv; bt.part = b->part; bt.met = b->met; bt.tag = b->tag_step;
     return b->samples;
+}
+static inline int plan_heavy(const LdsBatch* b) {
+    return b != nullptr && b->n_heavy > 0 && b->heavy_rows && b->heavy_flag ? b->n_heavy : 0;
 }
 // Launch the batched (kB = true) instantiation only for more than one sample.
 #define LDS_LAUNCH_B(kern, ns, ...)                          \
@@ -1371,7 +1549,7 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, b1};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1386,7 +1564,7 @@ extern "C" int lds_engine_fwd_layer2(const int* rp, const int* col, const float*
     LDS_CHECK_ARG(batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(fwd_layer2_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer2_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h2, o, p, d_o, label, mask, inv_count, lossrow, corrrow, c,
                        agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1404,7 +1582,7 @@ extern "C" int lds_engine_bwd_layer2(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(bwd_layer2_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(bwd_layer2_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, d_o, y0, dh2, dy0, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, o, h2, U, V, ldk, R,
                        foff, fwidth, r_assign, dmask, agg, bt);
@@ -1479,7 +1657,7 @@ extern "C" int lds_engine_rev_a(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_a_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_a_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh0bar, dy0, dh0, y0, h1d, dh2, w, gw1bar, gb1bar, c, dh1dbar, dh2bar,
                        h1dbar, mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep,
                        scale, U, V, ldk, R, foff, dmask, agg, bt);
@@ -1495,7 +1673,7 @@ extern "C" int lds_engine_rev_b(const int* rp, const int* col, const float* s, c
     LDS_CHECK_ARG(c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_b_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_b_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, dh2bar, d_o, dh2, p, mask, inv_count, c, obar, U, V, ldk, R, foff, cw,
                        agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1514,7 +1692,7 @@ extern "C" int lds_engine_rev_c(const int* rp, const int* col, const float* s, c
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_c_kernel, ns, agg, dim3(wave_blocks(n), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
+    LDS_LAUNCH_BA(rev_c_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp, col, s,
                        (const int2*)ell, n, obar, h2, o, h1dbar_part, y0, w, c, h2bar, y0bar,
                        mk_keys(seed, 0, tag_h), (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V,
                        ldk, R, foff, cw, dmask, agg, bt);
@@ -1583,7 +1761,7 @@ extern "C" int lds_engine_bwd1_reduce(const int* rp, const int* col, const float
     LDS_CHECK_ARG(c > 0 && c <= HID && (U == nullptr || (V && R && y0 && h0)) && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(bwd1_reduce_kernel, ns, agg, dim3((n + kRowsPer1K - 1) / kRowsPer1K, ns), dim3(1024), 0, (hipStream_t)stream,
+    LDS_LAUNCH_BA(bwd1_reduce_kernel, ns, agg, dim3((n + kRowsPer1K - 1) / kRowsPer1K + plan_heavy(batch), ns), dim3(1024), 0, (hipStream_t)stream,
                        rp, col, s, (const int2*)ell, n, dy0, dh0, y0, h0, U, V, ldk, R, foff, dh2, h1d, lossrow,
                        corrrow, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -1598,7 +1776,7 @@ extern "C" int lds_engine_rev_d_reduce(const int* rp, const int* col, const floa
     LDS_CHECK_ARG(h1d && partials && n > 0 && c > 0 && c <= HID && batch_ok(batch));
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(rev_d_reduce_kernel, ns, agg, dim3((n + kRowsPer1K - 1) / kRowsPer1K, ns), dim3(1024), 0,
+    LDS_LAUNCH_BA(rev_d_reduce_kernel, ns, agg, dim3((n + kRowsPer1K - 1) / kRowsPer1K + plan_heavy(batch), ns), dim3(1024), 0,
                        (hipStream_t)stream, rp, col, s, (const int2*)ell, n, y0bar, h0, y0, h0bar, U, V, ldk, R,
                        foff, dh2, dh1dbar, h2bar, h1d, c, partials, agg, bt);
     LDS_RETURN_LAST_ERROR();

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -185,7 +185,9 @@ class LdsBatch(ctypes.Structure):
     """include/ldsgnn.h LdsBatch: per-sample element strides of a batched
     engine launch (S replica samples in one launch, grid.y = sample)."""
     _fields_ = [("samples", ctypes.c_int32), ("tag_step", ctypes.c_uint32)] + [
-        (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")]
+        (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")] + [
+        ("heavy_rows", ctypes.c_void_p), ("heavy_flag", ctypes.c_void_p), ("n_heavy", ctypes.c_int32),
+        ("reserved", ctypes.c_int32)]
 
 
 def batch_ptr(b) -> int:

@@ -45,6 +45,7 @@ from . import _native as nat
 from .rng import TAG_DROP_H, TAG_DROP_X, TAG_GRAPH, Generator, tag_for
 
 HID = 16
+ELL = 64  # entries per row in a graph's ELL head (kEllWidth in csrc/common.hpp)
 _RED_LEN = 304
 _TAB_MAX = 256  # Adam table entries (kAdamTabMax in engine.hip)
 _ACT = ("h0", "y0", "h1d", "h2", "o", "p", "d_o", "dh2", "dy0", "dh0")
@@ -63,7 +64,7 @@ class _Graph:
         self.row_ptr = torch.empty((S, n + 1), dtype=torch.int32, device=dev)
         self.col = torch.empty((S, max(cap, 1)), dtype=torch.int32, device=dev)
         self.s = torch.empty((S, n), dtype=torch.float32, device=dev)
-        self.ell = torch.empty((S, n * 2 * HID), dtype=torch.int32, device=dev)  # ELL head {j, s_j}
+        self.ell = torch.empty((S, n * 2 * ELL), dtype=torch.int32, device=dev)  # ELL head {j, s_j}
         # long rows: segment starts per (row, column block) for lds_spmm_norm_blocked
         self.bptr = torch.empty((S, bptr_len), dtype=torch.int32, device=dev) if bptr_len else None
 
@@ -80,7 +81,7 @@ class _GraphBatch:
         self.row_ptr = torch.empty((count, S, n + 1), dtype=torch.int32, device=dev)
         self.col = torch.empty((count, S, max(cap, 1)), dtype=torch.int32, device=dev)
         self.s = torch.empty((count, S, n), dtype=torch.float32, device=dev)
-        self.ell = torch.empty((count, S, n * 2 * HID), dtype=torch.int32, device=dev)
+        self.ell = torch.empty((count, S, n * 2 * ELL), dtype=torch.int32, device=dev)
         self.bptr = torch.empty((count, S, bptr_len), dtype=torch.int32, device=dev) if bptr_len else None
         self.graphs = [_Graph(n, cap, dev, views=(self.row_ptr[g], self.col[g], self.s[g], self.ell[g],
                                                   self.bptr[g] if bptr_len else None, self.bits[g]))
@@ -247,7 +248,10 @@ class LdsEngine:
         self.obar, self.h2bar, self.y0bar, self.h0bar = z(), z(), z(), z()
         zp = lambda: torch.zeros((S, self.np), dtype=torch.float32, device=dev)  # noqa: E731
         self.wbar, self.mbar, self.vbar, self.gbar, self.g = zp(), zp(), zp(), zp(), zp()
-        self.nred = (n + 15) // 16  # first-stage partials of the fused reductions (16 rows per block)
+        self._row_plan()
+        # first-stage partials of the fused reductions: 16 rows per block, plus
+        # one block per heavy row of the plan
+        self.nred = (n + 15) // 16 + self.n_heavy
         self.partials = torch.zeros((S, self.nred, _RED_LEN), dtype=torch.float32, device=dev)
         self._alloc_factors()
         self.grad = torch.zeros_like(theta)
@@ -285,14 +289,46 @@ class LdsEngine:
         self.R = torch.zeros((self.S, self.n), dtype=torch.float32, device=self.dev)
         self._make_batches()
 
+    # rows expected to have more than this many entries get a block of their own
+    HEAVY_DEGREE = 64
+
+    def _row_plan(self):
+        """The aggregating kernels' row plan (include/ldsgnn.h LdsBatch): rows
+        whose expected degree 1 + Σ_j clamp(θ_ij, 0, 1) exceeds HEAVY_DEGREE run on a
+        block of their own.  Decided once from θ at construction: it changes
+        speed only (a row of any degree is aggregated correctly either way).
+        Long-row mode (pre-aggregated Â·Z) has no plan."""
+        n = self.n
+        self.heavy_flag = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+        if self.long_rows:
+            self.heavy_rows = torch.zeros(1, dtype=torch.int32, device=self.dev)
+            self.n_heavy = 0
+            return
+        i = torch.arange(n, device=self.dev)
+        deg = torch.ones(n, device=self.dev)
+        step = max(1, (1 << 24) // n)  # rows per chunk of the packed triangle
+        for r0 in range(0, n, step):
+            r1 = min(n, r0 + step)
+            lo, hi = r0 * (2 * n - r0 + 1) // 2, r1 * (2 * n - r1 + 1) // 2
+            rows = torch.repeat_interleave(i[r0:r1], n - i[r0:r1])  # row of each packed entry
+            cols = rows + (torch.arange(lo, hi, device=self.dev) - (rows * (2 * n - rows + 1)) // 2)
+            p = self.theta[lo:hi].clamp(0.0, 1.0) * (rows != cols)
+            deg.index_add_(0, rows, p).index_add_(0, cols, p)
+        heavy = deg > self.HEAVY_DEGREE
+        self.heavy_rows = i[heavy].to(torch.int32).contiguous() if bool(heavy.any()) else \
+            torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.heavy_flag[heavy] = 1
+        self.n_heavy = int(heavy.sum())
+
     def _make_batches(self):
         """LdsBatch strides for this engine's layout (kept alive on self)."""
         n, S = self.n, self.S
 
         def mk(xval_stride):
             return nat.LdsBatch(samples=S, tag_step=1, act=n * HID, row=n, rp=n + 1, col=self.cap,
-                                ell=n * 2 * HID, par=self.np, xval=xval_stride, xd=self.x_nnz, uv=self.ldk,
-                                part=self.nred * _RED_LEN, met=2)
+                                ell=n * 2 * ELL, par=self.np, xval=xval_stride, xd=self.x_nnz, uv=self.ldk,
+                                part=self.nred * _RED_LEN, met=2, heavy_rows=nat.ptr(self.heavy_rows),
+                                heavy_flag=nat.ptr(self.heavy_flag), n_heavy=self.n_heavy)
         self._bt = mk(0)  # X values argument = the shared X
         self._btx = mk(self.x_nnz if self.train_flag else 0)  # X values argument = the slot's stored Xd
         self.bt = nat.batch_ptr(self._bt)
@@ -407,7 +443,7 @@ class LdsEngine:
             self._evb_rows = torch.zeros((2, E, n), dtype=torch.float32, device=self.dev)
             self._evb_w = torch.zeros((1, self.np), dtype=torch.float32, device=self.dev)
             self._evb_bt_obj = nat.LdsBatch(samples=E, tag_step=1, act=n * HID, row=n, rp=n + 1, col=self.cap,
-                                            ell=n * 2 * HID, par=0, xval=0, xd=0, uv=0, part=0, met=2)
+                                            ell=n * 2 * ELL, par=0, xval=0, xd=0, uv=0, part=0, met=2)
             self._evb_bt = nat.batch_ptr(self._evb_bt_obj)
             self._evb_E = E
         sl, g, bt = self._evb, self._evb.g, self._evb_bt

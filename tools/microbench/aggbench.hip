@@ -8,6 +8,7 @@
 //   2  one wave per row: group 0 takes the ELL head, groups 1-3 the first 48
 //      entries past it, then 64-wide steps over all groups
 //   3  variant 1 with up to 4 of its 64-wide steps loaded at once
+//   4  variant 1 with rows of more than 64 entries on a whole 4-wave block
 //   8  floor: a trivial kernel with variant 0's grid
 //   9  one dependent load round trip per lane, variant 0's grid
 #include <hip/hip_runtime.h>
@@ -163,6 +164,50 @@ __global__ __launch_bounds__(256) void agg_v3(const int* __restrict__ rp, const 
     if (lane < HID) y[row * HID + h] = s[row] * acc;
 }
 
+// variant 1 plus a row plan: the `nh` rows with more than 64 entries first,
+// each taking a whole 4-wave block (256 entries per step, the four wave sums
+// combined through LDS in wave order), then the other rows one wave each
+__global__ __launch_bounds__(256) void agg_v4(const int* __restrict__ rp, const int* __restrict__ col,
+                                              const float* __restrict__ s, const int* __restrict__ plan, int nh,
+                                              int n, const float* __restrict__ z, float* __restrict__ y) {
+    __shared__ float part[4][HID];
+    const int lane = threadIdx.x & 63;
+    const int h = lane & (HID - 1);
+    const int g = lane >> 4;
+    const int wave = threadIdx.x >> 6;
+    const bool heavy = (int)blockIdx.x < nh;
+    int row;
+    if (heavy) {
+        row = plan[blockIdx.x];
+    } else {
+        const int i = nh + ((int)blockIdx.x - nh) * 4 + wave;
+        if (i >= n) return;
+        row = plan[i];
+    }
+    const int beg = rp[row], end = rp[row + 1];
+    const int step = heavy ? 256 : 64;
+    float acc = 0.f;
+    for (int p0 = beg + (heavy ? wave * 64 : 0); p0 < end; p0 += step) {
+        const int p = p0 + lane;
+        const int jl = p < end ? col[p] : row;
+        const float sl = p < end ? s[jl] : 0.f;
+        float zk[HID];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, g * HID + k) * HID + h];
+#pragma unroll
+        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
+    }
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 32);
+    if (heavy) {
+        if (lane < HID) part[wave][lane] = acc;
+        __syncthreads();
+        if (wave != 0) return;
+        acc = ((part[0][h] + part[1][h]) + part[2][h]) + part[3][h];
+    }
+    if (lane < HID) y[row * HID + h] = s[row] * acc;
+}
+
 // trivial kernel with the same grid as v0: the launch / boundary floor
 __global__ __launch_bounds__(256) void agg_floor(const int* __restrict__ rp, int n, float* __restrict__ y) {
     const int row = (blockIdx.x * 256 + threadIdx.x) / HID;
@@ -179,6 +224,13 @@ __global__ __launch_bounds__(256) void agg_one_hop(const int* __restrict__ rp, i
     y[i] = z[i] * 0.5f + 1.0f;
 }
 }  // namespace
+
+extern "C" int aggbench_launch_plan(const int* rp, const int* col, const float* s, const int* plan, int nh, int n,
+                                    const float* z, float* y, void* stream) {
+    hipLaunchKernelGGL(agg_v4, dim3(nh + (n - nh + 3) / 4), dim3(256), 0, (hipStream_t)stream, rp, col, s, plan, nh,
+                       n, z, y);
+    return (int)hipGetLastError();
+}
 
 extern "C" int aggbench_launch(int variant, const int* rp, const int* col, const float* s, const int2* ell, int n,
                                const float* z, float* y, void* stream) {

@@ -26,6 +26,7 @@ LIB = os.path.join(HERE, "libaggbench.so")
 def load():
     lib = ctypes.CDLL(LIB)
     lib.aggbench_launch.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + [ctypes.c_void_p] * 3
+    lib.aggbench_launch_plan.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3
     return lib
 
 
@@ -54,15 +55,26 @@ def main(K=200):
         deg = (g.row_ptr[1:] - g.row_ptr[:-1])
         z0 = torch.randn(n, 16, device=dev)
         ref = None
-        for v in (8, 9, 0, 1, 2, 3):
+        heavy = deg > 64
+        idx = torch.arange(n, device=dev)
+        plan = torch.cat([idx[heavy], idx[~heavy]]).int().contiguous()
+        nh = int(heavy.sum())
+
+        def launch(v, src, dst, st):
+            if v == 4:
+                return lib.aggbench_launch_plan(g.row_ptr.data_ptr(), g.col.data_ptr(), g.s.data_ptr(),
+                                                plan.data_ptr(), nh, n, src.data_ptr(), dst.data_ptr(), st)
+            return lib.aggbench_launch(v, g.row_ptr.data_ptr(), g.col.data_ptr(), g.s.data_ptr(), ell.data_ptr(), n,
+                                       src.data_ptr(), dst.data_ptr(), st)
+
+        for v in (8, 9, 0, 1, 2, 3, 4):
             y = torch.empty_like(z0)
             st = torch.cuda.current_stream().cuda_stream
-            assert lib.aggbench_launch(v, g.row_ptr.data_ptr(), g.col.data_ptr(), g.s.data_ptr(), ell.data_ptr(), n,
-                                       z0.data_ptr(), y.data_ptr(), st) == 0
+            assert launch(v, z0, y, st) == 0
             torch.cuda.synchronize()
             if v == 0:
                 ref = y.clone()
-            err = float((y - ref).abs().max() / ref.abs().max()) if v in (0, 1, 2, 3) else None
+            err = float((y - ref).abs().max() / ref.abs().max()) if v in (0, 1, 2, 3, 4) else None
             a, b = z0.clone(), torch.empty_like(z0)
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -71,8 +83,7 @@ def main(K=200):
                 with torch.cuda.graph(gr, stream=s):
                     for i in range(K):
                         src, dst = (a, b) if i % 2 == 0 else (b, a)
-                        lib.aggbench_launch(v, g.row_ptr.data_ptr(), g.col.data_ptr(), g.s.data_ptr(), ell.data_ptr(),
-                                            n, src.data_ptr(), dst.data_ptr(), s.cuda_stream)
+                        launch(v, src, dst, s.cuda_stream)
             torch.cuda.current_stream().wait_stream(s)
             gr.replay()
             torch.cuda.synchronize()

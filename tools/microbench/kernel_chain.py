@@ -87,6 +87,18 @@ def main():
         t = graph_time(chain) / args.k
         rows.append({"i": i, "call": name, "us": 1e6 * t})
         print(json.dumps(rows[-1]), flush=True)
+    # ablations of the W0-product launch: without the fused final reduction
+    # block, without the heavy-column blocks (every column one wave)
+    xt = [a for name, a in calls if name == "lds_engine_xt_adam"]
+    if xt:
+        a = xt[0]
+        for label, b in (("as recorded", a), ("no final block", a[:14] + (0,) + a[15:]),
+                         ("no heavy columns", a[:-3] + (0,) + a[-2:])):
+            def chain(b=b):
+                for _ in range(args.k):
+                    real("lds_engine_xt_adam", *cur(b))
+            print(json.dumps({"what": "xt_adam ablation", "variant": label, "us": 1e6 * graph_time(chain) / args.k}),
+                  flush=True)
     print(json.dumps({"what": "summary", "calls": len(calls), "window_us": 1e6 * t_window,
                       "sum_self_chain_us": sum(r["us"] for r in rows), "floor_us": 1e6 * floor / args.k,
                       "samples": args.samples}))

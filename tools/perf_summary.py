@@ -11,7 +11,10 @@ try:
     rows = [json.loads(line) for line in open("gpurun_out/kchain.jsonl")]
     agg = defaultdict(list)
     for r in rows[1:-1]:
-        agg[r["call"]].append(r["us"])
+        if "call" in r:
+            agg[r["call"]].append(r["us"])
+        else:
+            print("  ", r)
     print("chain floor", round(rows[0]["us"], 2), "window", round(rows[-1]["window_us"], 1))
     for k, v in agg.items():
         print(f"  {k:28s} x{len(v):2d} {sum(v) / len(v):6.2f} us")
