@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 5
+#define LDS_ABI_VERSION 6
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -107,22 +107,35 @@ int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
                              const int* row_ptr, int* col, int64_t col_capacity,
                              int* overflow, const float* s, int* ell, void* stream);
 
+/* Workspace ints per graph of lds_sample_graphs_multi (the row degrees). */
+int lds_sample_ws_ints(int n);
+
 /* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
  * b < samples, is draw counter *counter_base + counter_offset + g with tag
  * tag + b·tag_step, stored as graph g·samples + b of the batch arrays (one
- * θ tile load per block serves all samples).  col == NULL: bitmask, degrees
- * and s only — no CSR / ELL (dense graphs aggregated by
- * lds_aggregate_bitmask); row_ptr and ell may then be NULL. */
+ * θ tile load per block serves all samples).  Two launches: the tile kernel
+ * draws the bits and counts them (integer atomics into deg_ws: per graph
+ * lds_sample_ws_ints(n) ints, the row degrees), the fill takes each row's
+ * CSR offset from those counts (no scan launch) and writes row_ptr, col, s
+ * and the ELL head.  deg_ws must be zero on entry: ws_zeroed = 1 promises it
+ * (lds_engine_end_window clears it), 0 makes this call clear it first.
+ * col == NULL: bitmask, degrees and s only — no CSR / ELL (dense graphs
+ * aggregated by lds_aggregate_bitmask), degrees by a popcount pass, deg_ws
+ * need not be zero; row_ptr and ell may then be NULL.  node_flags (n bytes,
+ * may be NULL): each ELL entry's j field carries the neighbour's flag byte in
+ * bits 24-31 (index = j & 0xFFFFFF; the engine's bit 0 = train mask, bit 1 =
+ * opt mask, read by the two-hop kernels). */
 int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                             uint32_t tag_step, const uint32_t* counter_base,
                             uint32_t counter_offset, int count, int samples, uint64_t* bits,
                             int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
-                            float* s, int* ell, void* stream);
+                            float* s, int* ell, const uint8_t* node_flags, int ws_zeroed,
+                            void* stream);
 /* Batched form for a window of graphs drawn from the same θ: graph g
  * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
- * writes bits + g·n·words, deg_ws + g·n, row_ptr + g·(n+1),
- * col + g·col_stride, s + g·n and (ell != NULL) ell + g·n·128.  Four launches
- * for all `count` graphs. */
+ * writes bits + g·n·words, deg_ws + g·lds_sample_ws_ints(n),
+ * row_ptr + g·(n+1), col + g·col_stride, s + g·n and (ell != NULL)
+ * ell + g·n·128.  lds_sample_graphs_multi with samples = 1, ws_zeroed = 0. */
 int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint32_t tag,
                       const uint32_t* counter_base, uint32_t counter_offset, int count,
                       uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
@@ -440,6 +453,32 @@ int lds_engine_rev_d(const int* rp, const int* col, const float* s, const int* e
                      const float* y0bar, const float* h0, const float* y0,
                      float* h0bar, float* U, float* V, int ldk, float* R, int foff,
                      void* stream);
+/* Two-hop loss layer (the forward's last aggregation and the backward's
+ * first, one launch; src/models/gcn.py:33-34 + F.nll_loss over the mask,
+ * src/trainers/inner.py:65): the loss rows are the nodes whose flag byte
+ * (the ELL j field's bits 24-31, lds_sample_graphs_multi node_flags) has
+ * mask_bit set.  O, P, dO, loss and correctness at those rows (zeros
+ * elsewhere), dH2 = Â dO computed from the masked neighbours only (their O
+ * recomputed in-kernel), dY0 as lds_engine_bwd_layer2, and (U != NULL) factor
+ * use 2.  Needs the ELL head (short rows). */
+int lds_engine_fwd2_bwd2(const int* rp, const int* col, const float* s, const int* ell, int n,
+                         const uint8_t* node_flags, int mask_bit, const float* h2, float* o, float* p,
+                         float* d_o, const int* label, float inv_count, float* lossrow, float* corrrow,
+                         int c, const float* y0, float* dh2, float* dy0, const float* w1, uint64_t seed,
+                         uint32_t tag_h, const void* scalars, int fwd_off, int train, float keep,
+                         float scale, float* U, float* V, int ldk, float* R, int foff, int fwidth,
+                         int r_assign, const float* dmask, const LdsBatch* batch, void* stream);
+/* lds_engine_rev_b + lds_engine_rev_c in one launch (the masked neighbours'
+ * dŌ / Ōbar recomputed in-kernel): factor uses 3 (columns foff_b) and 2
+ * (foff_c), R += r3 then += r2, H2bar, Y0bar. */
+int lds_engine_rev_bc(const int* rp, const int* col, const float* s, const int* ell, int n,
+                      const uint8_t* node_flags, int mask_bit, const float* dh2bar, const float* d_o,
+                      const float* dh2, const float* p, const float* h2, const float* o, float inv_count,
+                      int c, const float* h1dbar_part, const float* y0, const float* w1, float* h2bar,
+                      float* y0bar, uint64_t seed, uint32_t tag_h, const void* scalars, int fwd_off,
+                      int train, float keep, float scale, float* U, float* V, int ldk, float* R,
+                      int foff_b, int foff_c, int cw, const float* dmask, const LdsBatch* batch,
+                      void* stream);
 /* θ = clamp(θ - lr·grad, 0, 1) with lr = scalars->outer_lr. */
 int lds_engine_sgd_clamp(float* theta, const float* grad, int64_t count,
                          const void* scalars, void* stream);
@@ -518,12 +557,15 @@ int lds_engine_xt_partials(const int* xcp, const int* xrow, const float* xval, i
                            const LdsBatch* batch, void* stream);
 /* Window end (both trainers' detach, src/trainers/bilevel.py:109-114): copy
  * w/m/v of slot T to slot 0 (skipped when wT == NULL), advance the scalars
- * as lds_engine_advance and (adam_tab != NULL) refresh the first tab_count
- * entries of the Adam table for the new adam_step. */
+ * as lds_engine_advance, (adam_tab != NULL) refresh the first tab_count
+ * entries of the Adam table for the new adam_step, and zero ws_count ints at
+ * ws (the next window's sampler workspace, lds_sample_graphs_multi
+ * ws_zeroed = 1; ws may be NULL). */
 int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT,
                           float* w0, float* m0, float* v0, void* scalars, int graphs,
                           int forwards, int adam_steps, int hypers, const double* betas_dev,
-                          float* adam_tab, int tab_count, const LdsBatch* batch, void* stream);
+                          float* adam_tab, int tab_count, int* ws, int64_t ws_count,
+                          const LdsBatch* batch, void* stream);
 /* Adam table for the current scalars->adam_step (betas_dev = {β1, β2, lr}
  * doubles): entry k = {lr/(1-β1^(s+1+k)), sqrt(1-β2^(s+1+k))}, k < tab_count
  * <= 256; the constants of torch/higher's Adam, computed in double. */

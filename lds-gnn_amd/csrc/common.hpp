@@ -15,6 +15,10 @@ namespace lds {
 
 constexpr int kWave = 64;
 constexpr int kEllWidth = 64;  // neighbours per row in a graph's ELL head ({j, s_j} pairs): one wave's step
+// The j field of an ELL entry: node index in the low 24 bits, the node's flag
+// byte (e.g. train / opt mask bits, include/ldsgnn.h) above them.
+constexpr int kEllIndex = 0x00FFFFFF;
+constexpr int kEllFlagShift = 24;
 
 // Packed upper-triangle index of (i, j), i <= j, of an n×n matrix in
 // torch.triu_indices(n, n) row-major order (src/utils/graph.py:41-45).
@@ -70,10 +74,12 @@ __device__ __forceinline__ void philox_quad(uint32_t k0, uint32_t k1, uint32_t t
     u[3] = u01(o.w);
 }
 
-// fl32(1 / fl32(sqrt(d))) with IEEE round-to-nearest at both steps — what
-// torch CPU computes for `1.0 / degree.sqrt()` (src/utils/graph.py:148).
-// Evaluated in fp64 and rounded to fp32: for sqrt and division a 53-bit
-// intermediate rounds to the correctly rounded 24-bit result (53 >= 2·24+2).
+// fl32(1 / fl32(sqrt(d))) with IEEE round-to-nearest at both steps: the
+// correctly rounded value of `1.0 / degree.sqrt()` (src/utils/graph.py:148),
+// as a GPU (and numpy) computes it.  (torch CPU routes `1.0 / t` through a
+// vectorised reciprocal whose last bit depends on the host ISA.)  Evaluated
+// in fp64 and rounded to fp32: for sqrt and division a 53-bit intermediate
+// rounds to the correctly rounded 24-bit result (53 >= 2·24+2).
 __device__ __forceinline__ float inv_sqrt_degree(int d) {
     const float sq = (float)__dsqrt_rn((double)d);
     return (float)__ddiv_rn(1.0, (double)sq);

@@ -23,15 +23,61 @@ namespace lds {
 constexpr int HID = 16;   // hidden width / row-group width
 constexpr int RG = 256 / HID;  // row groups per 256-thread block
 
+// Cross-lane moves on the VALU instead of the LDS crossbar (ds_bpermute, the
+// lowering of __shfl / __shfl_xor: ~100 cycles per dependent hop).  A 16-lane
+// row group is one DPP row: row_newbcast:K broadcasts lane K of the row,
+// row_ror:R rotates it.  Sums / maxima over a row by rotations 8, 4, 2, 1 pair
+// exactly the lanes the xor butterfly 8, 4, 2, 1 pairs (the partial sums are
+// periodic), so results are bit-identical to the __shfl_xor form, in every
+// lane.  Lanes L and L^16 / L^32 swap through v_permlane16/32_swap (gfx950).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(dpp_i<CTRL>(__float_as_int(v))); }
+template <int K>
+__device__ __forceinline__ int rbc_i(int v) { return dpp_i<0x150 + K>(v); }  // row_newbcast:K
+template <int K>
+__device__ __forceinline__ float rbc_f(float v) { return dpp_f<0x150 + K>(v); }
+#define LDS_R16(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
+
 __device__ __forceinline__ float gsum16(float v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, HID);
+    v += dpp_f<0x128>(v);  // row_ror:8
+    v += dpp_f<0x124>(v);
+    v += dpp_f<0x122>(v);
+    v += dpp_f<0x121>(v);
     return v;
 }
 __device__ __forceinline__ float gmax16(float v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, HID));
+    v = fmaxf(v, dpp_f<0x128>(v));
+    v = fmaxf(v, dpp_f<0x124>(v));
+    v = fmaxf(v, dpp_f<0x122>(v));
+    v = fmaxf(v, dpp_f<0x121>(v));
     return v;
+}
+// v + v of lane L^16, then + v of lane L^32 (the wave's four row groups summed,
+// bit-identical to v += __shfl_xor(v, 16); v += __shfl_xor(v, 32))
+__device__ __forceinline__ float xor16_add(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return v + __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float xor32_add(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return v + __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float groups_sum(float v) { return xor32_add(xor16_add(v)); }
+// argmax over the row's lanes (largest value, lowest lane on ties: torch.argmax)
+__device__ __forceinline__ void argmax16_step(float& best, int& bi, float ob, int oi) {
+    if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+    }
+}
+__device__ __forceinline__ int argmax16(float best, int bi) {
+    argmax16_step(best, bi, dpp_f<0x128>(best), dpp_i<0x128>(bi));
+    argmax16_step(best, bi, dpp_f<0x124>(best), dpp_i<0x124>(bi));
+    argmax16_step(best, bi, dpp_f<0x122>(best), dpp_i<0x122>(bi));
+    argmax16_step(best, bi, dpp_f<0x121>(best), dpp_i<0x121>(bi));
+    return bi;
 }
 __device__ __forceinline__ float bcast16(float v, int src) { return __shfl(v, src, HID); }
 
@@ -100,7 +146,6 @@ __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* 
     (void)lane;
     const int t = threadIdx.x & 63;
     const int h = t & (HID - 1);
-    const int g = t >> 4;
     const int beg = rp[row], end = rp[row + 1];
     float acc = 0.f;
     for (int p0 = beg; p0 < end; p0 += 64) {
@@ -108,13 +153,14 @@ __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* 
         const int jl = p < end ? col[p] : row;
         const float sl = p < end ? s[jl] : 0.f;
         float zk[HID];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, g * HID + k) * HID + h];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
+#define LDS_G(K) zk[K] = z[rbc_i<K>(jl) * HID + h];
+        LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(sl), zk[K], acc);
+        LDS_R16(LDS_F)
+#undef LDS_F
     }
-    acc += __shfl_xor(acc, 16);
-    acc += __shfl_xor(acc, 32);
+    acc = groups_sum(acc);
     return s[row] * acc;
 }
 
@@ -190,7 +236,6 @@ __device__ __forceinline__ float agg_value(const RowSel& r, const int* __restric
         return r.row >= 0 ? agg[r.row * HID + h] : 0.f;
     } else {
         __shared__ float part[W][HID];
-        const int g = t >> 4;
         float acc = 0.f;
         if (r.row >= 0) {
             int p0 = r.first;
@@ -198,10 +243,12 @@ __device__ __forceinline__ float agg_value(const RowSel& r, const int* __restric
                 const int2 e = r.e;
                 const float sl = __int_as_float(e.y);
                 float zk[HID];
-#pragma unroll
-                for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(e.x, g * HID + k) * HID + h];
-#pragma unroll
-                for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
+#define LDS_G(K) zk[K] = z[(rbc_i<K>(e.x) & kEllIndex) * HID + h];
+                LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(sl), zk[K], acc);
+                LDS_R16(LDS_F)
+#undef LDS_F
                 p0 += kEllWidth;
             }
             for (; p0 < r.end; p0 += r.step) {
@@ -209,13 +256,14 @@ __device__ __forceinline__ float agg_value(const RowSel& r, const int* __restric
                 const int jl = p < r.end ? col[p] : r.row;
                 const float sl = p < r.end ? s[jl] : 0.f;
                 float zk[HID];
-#pragma unroll
-                for (int k = 0; k < HID; ++k) zk[k] = z[__shfl(jl, g * HID + k) * HID + h];
-#pragma unroll
-                for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(sl, g * HID + k), zk[k], acc);
+#define LDS_G(K) zk[K] = z[rbc_i<K>(jl) * HID + h];
+                LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(sl), zk[K], acc);
+                LDS_R16(LDS_F)
+#undef LDS_F
             }
-            acc += __shfl_xor(acc, 16);
-            acc += __shfl_xor(acc, 32);
+            acc = groups_sum(acc);
         }
         if (r.heavy) {  // block-uniform: every wave of the block reaches the barrier
             if (t < HID) part[threadIdx.x >> 6][t] = acc;
@@ -283,14 +331,14 @@ __device__ __forceinline__ float x_wave_dot_range(int beg, int end, const int* _
             if (xd_perm_out != nullptr) xd_perm_out[perm[p]] = x;
         }
         float sk[HID];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) sk[k] = src[__shfl(j, k, HID) * HID + lane];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(x, k, HID), sk[k], acc);
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+        LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(x), sk[K], acc);
+        LDS_R16(LDS_F)
+#undef LDS_F
     }
-    acc += __shfl_xor(acc, 16);
-    acc += __shfl_xor(acc, 32);
-    return acc;
+    return groups_sum(acc);
 }
 
 template <bool kCsc>
@@ -350,10 +398,12 @@ __global__ __launch_bounds__(256) void xt_linear_kernel(
             if (train) x = u_at(keys, keys.tag_x, ctr, i, f) < keep ? x * scale : 0.f;
         }
         float dk[HID];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) dk[k] = d[__shfl(i, k, HID) * HID + lane];
-#pragma unroll
-        for (int k = 0; k < HID; ++k) acc = fmaf(__shfl(x, k, HID), dk[k], acc);
+#define LDS_G(K) dk[K] = d[rbc_i<K>(i) * HID + lane];
+        LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(x), dk[K], acc);
+        LDS_R16(LDS_F)
+#undef LDS_F
     }
     float* o = out + f * HID + lane;
     if (w != nullptr) acc = acc + wd * w[f * HID + lane];
@@ -456,17 +506,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     if (p_out && g0) p_out[row * HID + lane] = p;
     if (d_o && g0) d_o[row * HID + lane] = (sel && act) ? (p - (lane == y ? 1.f : 0.f)) * inv_count : 0.f;
     // argmax with first-index tie-break (torch.argmax)
-    float best = act ? o : -INFINITY;
-    int bi = lane;
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {
-        const float ob = __shfl_xor(best, off, HID);
-        const int oi = __shfl_xor(bi, off, HID);
-        if (ob > best || (ob == best && oi < bi)) {
-            best = ob;
-            bi = oi;
-        }
-    }
+    const int bi = argmax16(act ? o : -INFINITY, lane);
     const float logpy = bcast16(logp, y);
     if (lane == 0 && g0) {
         lossrow[row] = sel ? -logpy : 0.f;
@@ -513,7 +553,9 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     const int row = rsel.row;
     if (g0) dh2[row * HID + lane] = g2;
     float dh1d = 0.f;
-    for (int k = 0; k < c; ++k) dh1d = fmaf(bcast16(g2, k), w.w1[k * HID + lane], dh1d);
+#define LDS_W(K) if (K < c) dh1d = fmaf(rbc_f<K>(g2), w.w1[K * HID + lane], dh1d);
+    LDS_R16(LDS_W)
+#undef LDS_W
     float mask;
     if (dmask != nullptr) {
         mask = dmask[row * HID + lane];
@@ -780,7 +822,9 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     if (g0) dh2bar[ix] = out;
     const float g2 = dh2[ix];
     float hb = 0.f;
-    for (int k = 0; k < c; ++k) hb = fmaf(bcast16(g2, k), gw1bar[k * HID + lane], hb);
+#define LDS_W(K) if (K < c) hb = fmaf(rbc_f<K>(g2), gw1bar[K * HID + lane], hb);
+    LDS_R16(LDS_W)
+#undef LDS_W
     if (g0) h1dbar[ix] = hb;
 }
 
@@ -863,7 +907,9 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
         h2bar[ix] = ag;
     }
     float hb = h1dbar_part[ix];
-    for (int k = 0; k < c; ++k) hb = fmaf(bcast16(ag, k), w.w1[k * HID + lane], hb);
+#define LDS_W(K) if (K < c) hb = fmaf(rbc_f<K>(ag), w.w1[K * HID + lane], hb);
+    LDS_R16(LDS_W)
+#undef LDS_W
     float mask;
     if (dmask != nullptr) {
         mask = dmask[ix];
@@ -891,6 +937,395 @@ __global__ __launch_bounds__(256) void rev_d_kernel(
         emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
         h0bar[ix] = ag;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Two-hop forms: the loss layer and the aggregation of its gradient in one
+// launch.  dO (and, in the reverse, Ōbar) is non-zero only on the rows of the
+// loss mask M (train: 140 of Cora's 2708 nodes; opt: ~250), so
+//   Â dO at row i = s_i Σ_{j ∈ N(i) ∩ M} s_j dO_j
+// needs dO_j only at the few masked neighbours — and dO_j is a function of
+// row j's own aggregation O_j = s_j Σ_{k ∈ N(j)} s_k H2_k.  Each wave walks
+// its row's entries (ELL head: the neighbour's mask bits ride in the j field),
+// ballots the masked ones and hands them out four at a time, one per 16-lane
+// group; the group recomputes O_j (or dŌ_j) from row j's ELL head / CSR tail,
+// applies the softmax (Jacobian) epilogue and accumulates s_j·(result).  The
+// group that meets j = i itself stores row i's own outputs.  O_j is computed
+// by one routine (group_agg, entries in CSR order) wherever it is needed, so
+// every wave that recomputes it gets the bits row j stored.  This replaces
+// the fwd_layer2 -> bwd_layer2 and rev_b -> rev_c launch pairs (one dependent
+// boundary and one memory level each).
+// ---------------------------------------------------------------------------
+
+// s-weighted sum over row j's entries of z (16-lane group, lane h = feature h),
+// in CSR order: the ELL head (all four 16-entry chunks' gathers issued before
+// the first use: one memory level for degree <= 64), then the CSR tail 64
+// entries at a time (indices, then s and the gathers: two levels per 64).
+// The caller multiplies by s_j.
+__device__ __forceinline__ float group_agg(int j, const int* __restrict__ rp, const int* __restrict__ col,
+                                           const float* __restrict__ s, const int2* __restrict__ ell,
+                                           const float* __restrict__ z) {
+    const int t = threadIdx.x & 63;
+    const int h = t & (HID - 1);
+    const int beg = rp[j], end = rp[j + 1];
+    const int2* __restrict__ eh = ell + (int64_t)j * kEllWidth;
+    int2 e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e[q] = eh[16 * q + h];
+    const int deg = end - beg;
+    float acc = 0.f;
+    {
+        float zk[4][HID];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (16 * q < deg) {  // group-uniform; entries past deg are the head's {j, 0} padding
+#define LDS_G(K) zk[q][K] = z[(rbc_i<K>(e[q].x) & kEllIndex) * HID + h];
+                LDS_R16(LDS_G)
+#undef LDS_G
+            }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (16 * q < deg) {
+#define LDS_F(K) acc = fmaf(__int_as_float(rbc_i<K>(e[q].y)), zk[q][K], acc);
+                LDS_R16(LDS_F)
+#undef LDS_F
+            }
+    }
+    for (int p0 = beg + kEllWidth; p0 < end; p0 += 4 * HID) {
+        int kk[4];
+        float sk[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int p = p0 + 16 * q + h;
+            kk[q] = p < end ? col[p] : j;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sk[q] = p0 + 16 * q + h < end ? s[kk[q]] : 0.f;
+        float zk[4][HID];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (p0 + 16 * q < end) {
+#define LDS_G(K) zk[q][K] = z[rbc_i<K>(kk[q]) * HID + h];
+                LDS_R16(LDS_G)
+#undef LDS_G
+            }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (p0 + 16 * q < end) {
+#define LDS_F(K) acc = fmaf(rbc_f<K>(sk[q]), zk[q][K], acc);
+                LDS_R16(LDS_F)
+#undef LDS_F
+            }
+    }
+    return acc;
+}
+
+// Walk the selected row's entries; for every masked neighbour j call f(j, s_j)
+// in the 16-lane group it is handed to.  Picks go out in entry order, one per
+// group per round: a light row's wave takes four per round; the W waves of a
+// heavy-row block all walk the whole row (same ballots) and wave w's group g
+// takes pick 4w + g of each round of 4W — the plan gives a block to rows with
+// many masked neighbours, not only to long rows.  Uniform control flow: a
+// group without a pick calls f with j = -1.
+template <int W, class F>
+__device__ __forceinline__ void for_masked(const RowSel& r, const int* __restrict__ col, const float* __restrict__ s,
+                                           const uint8_t* __restrict__ nflag, int mbit, F&& f) {
+    if (r.row < 0) return;
+    const int t = threadIdx.x & 63;
+    const int g = t >> 4;
+    const int wave = threadIdx.x >> 6;
+    const int nw = r.heavy ? W : 1;                  // waves sharing the row
+    const int slot = (r.heavy ? wave : 0) * 4 + g;   // this group's pick in each round
+    const int beg = r.heavy ? r.first - 64 * wave : r.first;
+    bool head = !r.heavy;
+    int p0 = beg;
+    for (;;) {
+        int jl;
+        float sl;
+        bool ml;
+        if (head) {
+            jl = r.e.x & kEllIndex;
+            sl = __int_as_float(r.e.y);
+            ml = ((r.e.x >> kEllFlagShift) & mbit) != 0;
+        } else {
+            if (p0 >= r.end) break;
+            const int p = p0 + t;
+            const bool v = p < r.end;
+            jl = v ? col[p] : 0;
+            sl = v ? s[jl] : 0.f;
+            ml = v && (nflag[jl] & mbit) != 0;
+        }
+        uint64_t ball = __ballot(ml);
+        while (ball) {
+            int mine = -1;
+            for (int q = 0; q < 4 * nw; ++q) {
+                if (ball) {
+                    const int b = __ffsll((unsigned long long)ball) - 1;
+                    ball &= ball - 1;
+                    if (q == slot) mine = b;
+                }
+            }
+            const int src = mine >= 0 ? mine : 0;
+            const int j = __shfl(jl, src);
+            const float sj = __shfl(sl, src);
+            f(mine >= 0 ? j : -1, sj);
+        }
+        p0 += kEllWidth;
+        head = false;
+    }
+}
+
+// Sum a per-lane 16-vector over the four groups (fixed order), then over the
+// W waves of a heavy-row block (LDS, wave order): every lane ends with the
+// row's total for feature h.
+template <int W, int NV>
+__device__ __forceinline__ void combine_groups(const RowSel& r, float (&v)[NV]) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = groups_sum(v[k]);
+    if (r.heavy) {  // block-uniform
+        __shared__ float part[W][NV][HID];
+        const int t = threadIdx.x & 63;
+        if (t < HID)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) part[threadIdx.x >> 6][k][t] = v[k];
+        __syncthreads();
+        const int h = t & (HID - 1);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            float a = part[0][k][h];
+#pragma unroll
+            for (int w = 1; w < W; ++w) a += part[w][k][h];
+            v[k] = a;
+        }
+    }
+}
+
+// U/V columns of one factor pair (emit_factor without the R update); returns
+// this pair's r = -½ s² (G·Y + Z·ÂG) (every lane of the group).
+__device__ __forceinline__ float emit_uv(float* __restrict__ U, float* __restrict__ V, int ldk, int off, int width,
+                                         int row, int lane, float si, float g, float z, float y, float ag) {
+    const float d = gsum16(g * y + z * ag);
+    if (lane < width) {
+        U[(int64_t)row * ldk + off + lane] = si * g;
+        V[(int64_t)row * ldk + off + lane] = si * z;
+    }
+    return -0.5f * si * si * d;
+}
+
+// Softmax NLL epilogue of one row of O (16-lane group, lane h < c active):
+// p, dO = (p - onehot(y)) / |M|, -log p_y, argmax == y.
+struct LossRow {
+    float p, d_o, nll, corr;
+};
+__device__ __forceinline__ LossRow loss_row(float o, int y, int c, float inv_count) {
+    const int lane = threadIdx.x & (HID - 1);
+    const bool act = lane < c;
+    const float m = gmax16(act ? o : -INFINITY);
+    const float e = act ? expf(o - m) : 0.f;
+    const float sum = gsum16(e);
+    const float lse = logf(sum);
+    const float logp = o - m - lse;
+    LossRow r;
+    r.p = act ? expf(logp) : 0.f;
+    r.d_o = act ? (r.p - (lane == y ? 1.f : 0.f)) * inv_count : 0.f;
+    const int bi = argmax16(act ? o : -INFINITY, lane);
+    r.nll = -bcast16(logp, y);
+    r.corr = bi == y ? 1.f : 0.f;
+    return r;
+}
+
+// fwd_layer2 + bwd_layer2 for a loss over the rows flagged `mbit`:
+//   O = Â H2 (rows of M: o, p, dO, loss, correct stored; other rows zeros),
+//   dH2 = Â dO;  dY0 = (dH2 W1) ⊙ D1 ⊙ [Y0 > 0];  outer mode: factor (dO, H2).
+template <bool kB>
+__global__ __launch_bounds__(256) void fwd2_bwd2_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n, const uint8_t* __restrict__ nflag, int mbit,
+    const float* __restrict__ h2, float* __restrict__ o_out, float* __restrict__ p_out, float* __restrict__ d_o,
+    const int* __restrict__ label, float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow,
+    int c, const float* __restrict__ y0, float* __restrict__ dh2, float* __restrict__ dy0, GcnW w, Keys keys,
+    const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
+    float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth, int r_assign,
+    const float* __restrict__ dmask, Batch bt) {
+    const int lane = threadIdx.x & (HID - 1);
+    const bool g0 = (threadIdx.x & 63) < HID;
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    h2 = boff<kB>(h2, bt.act);
+    o_out = boff<kB>(o_out, bt.act);
+    p_out = boff<kB>(p_out, bt.act);
+    d_o = boff<kB>(d_o, bt.act);
+    lossrow = boff<kB>(lossrow, bt.row);
+    corrrow = boff<kB>(corrrow, bt.row);
+    y0 = boff<kB>(y0, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    dy0 = boff<kB>(dy0, bt.act);
+    dmask = boff<kB>(dmask, bt.act);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
+    w.w1 = boff<kB>(w.w1, bt.par);
+    bkeys<kB>(keys, bt);
+    const RowSel rsel = select_row<4, false>(n, rp, ell, bt);
+    const int row = rsel.row;
+    // the lead's own-row operands, loaded ahead of the two-hop walk
+    const int ix = row * HID + lane;
+    float si = 0.f, mk = 0.f, h2i = 0.f, w1v[HID];
+    bool in_mask = false;
+    if (rsel.lead) {
+        si = s[row];
+        in_mask = (nflag[row] & mbit) != 0;
+        mk = dmask != nullptr ? dmask[ix] : 0.f;
+        h2i = U != nullptr ? h2[ix] : 0.f;
+#pragma unroll
+        for (int k = 0; k < HID; ++k) w1v[k] = k < c ? w.w1[k * HID + lane] : 0.f;
+    }
+    // v[0]: Σ s_j dO_j;  v[1], v[2]: row i's own dO_i, O_i (one contributor)
+    float v[3] = {0.f, 0.f, 0.f};
+    for_masked<4>(rsel, col, s, nflag, mbit, [&](int j, float sj) {
+        if (j < 0) return;
+        const int y = label[j];
+        const float o = sj * group_agg(j, rp, col, s, ell, h2);
+        const LossRow lr = loss_row(o, y, c, inv_count);
+        v[0] = fmaf(sj, lr.d_o, v[0]);
+        if (j == row) {
+            const float ov = lane < c ? o : 0.f;
+            v[1] = lr.d_o;
+            v[2] = ov;
+            o_out[j * HID + lane] = ov;
+            p_out[j * HID + lane] = lr.p;
+            d_o[j * HID + lane] = lr.d_o;
+            if (lane == 0) {
+                lossrow[j] = lr.nll;
+                corrrow[j] = lr.corr;
+            }
+        }
+    });
+    combine_groups<4, 3>(rsel, v);
+    if (!rsel.lead) return;
+    if (g0 && !in_mask) {  // rows outside the mask: no loss, dO = 0
+        o_out[ix] = 0.f;
+        p_out[ix] = 0.f;
+        d_o[ix] = 0.f;
+        if (lane == 0) {
+            lossrow[row] = 0.f;
+            corrrow[row] = 0.f;
+        }
+    }
+    const float g2 = si * v[0];
+    if (g0) dh2[ix] = g2;
+    float dh1d = 0.f;
+#define LDS_W(K) if (K < c) dh1d = fmaf(rbc_f<K>(g2), w1v[K], dh1d);
+    LDS_R16(LDS_W)
+#undef LDS_W
+    float mask;
+    if (dmask != nullptr) {
+        mask = mk;
+    } else {
+        mask = y0[ix] > 0.f ? 1.f : 0.f;
+        if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    }
+    if (g0) dy0[ix] = dh1d * mask;
+    if (U != nullptr && g0) {  // outer graph, use 2: G = dO, Z = H2, Y = O, ÂG = dH2
+        const float r = emit_uv(U, V, ldk, foff, fwidth, row, lane, si, v[1], h2i, v[2], g2);
+        if (lane == 0) R[row] = r_assign ? r : R[row] + r;
+    }
+}
+
+// rev_b + rev_c (train mask):
+//   dŌ = Â dH2bar (rows of M only), Ōbar = P ⊙ (ū - P·ū), ū = dŌ / |M|;
+//   H2bar = Â Ōbar;  factor uses 3 (dH2bar, dO, dH2, dŌ) and 2 (Ōbar, H2, O, H2bar);
+//   H1dbar = H1dbar_part + H2bar W1;  Y0bar = H1dbar ⊙ D1 ⊙ [Y0 > 0].
+template <bool kB>
+__global__ __launch_bounds__(256) void rev_bc_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, const float* __restrict__ s,
+    const int2* __restrict__ ell, int n, const uint8_t* __restrict__ nflag, int mbit,
+    const float* __restrict__ dh2bar, const float* __restrict__ d_o, const float* __restrict__ dh2,
+    const float* __restrict__ p, const float* __restrict__ h2, const float* __restrict__ o, float inv_count, int c,
+    const float* __restrict__ h1dbar_part, const float* __restrict__ y0, GcnW w, float* __restrict__ h2bar,
+    float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
+    float scale, float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff_b,
+    int foff_c, int cw, const float* __restrict__ dmask, Batch bt) {
+    const int lane = threadIdx.x & (HID - 1);
+    const bool g0 = (threadIdx.x & 63) < HID;
+    rp = boff<kB>(rp, bt.rp);
+    col = boff<kB>(col, bt.col);
+    s = boff<kB>(s, bt.row);
+    ell = boff<kB>(ell, bt.ell2);
+    dh2bar = boff<kB>(dh2bar, bt.act);
+    d_o = boff<kB>(d_o, bt.act);
+    dh2 = boff<kB>(dh2, bt.act);
+    p = boff<kB>(p, bt.act);
+    h2 = boff<kB>(h2, bt.act);
+    o = boff<kB>(o, bt.act);
+    h1dbar_part = boff<kB>(h1dbar_part, bt.act);
+    y0 = boff<kB>(y0, bt.act);
+    h2bar = boff<kB>(h2bar, bt.act);
+    y0bar = boff<kB>(y0bar, bt.act);
+    dmask = boff<kB>(dmask, bt.act);
+    U = boff<kB>(U, bt.uv);
+    V = boff<kB>(V, bt.uv);
+    R = boff<kB>(R, bt.row);
+    w.w1 = boff<kB>(w.w1, bt.par);
+    bkeys<kB>(keys, bt);
+    const RowSel rsel = select_row<4, false>(n, rp, ell, bt);
+    const int row = rsel.row;
+    // the lead's own-row operands, loaded ahead of the two-hop walk
+    const int ix = row * HID + lane;
+    float si = 0.f, a_dh2bar = 0.f, a_do = 0.f, a_dh2 = 0.f, a_h2 = 0.f, a_o = 0.f, a_hb = 0.f, mk = 0.f;
+    float w1v[HID];
+    if (rsel.lead) {
+        si = s[row];
+        a_dh2bar = dh2bar[ix];
+        a_do = d_o[ix];
+        a_dh2 = dh2[ix];
+        a_h2 = h2[ix];
+        a_o = o[ix];
+        a_hb = h1dbar_part[ix];
+        mk = dmask != nullptr ? dmask[ix] : 0.f;
+#pragma unroll
+        for (int k = 0; k < HID; ++k) w1v[k] = k < c ? w.w1[k * HID + lane] : 0.f;
+    }
+    // v[0]: Σ s_j Ōbar_j;  v[1], v[2]: row i's own dŌ_i, Ōbar_i
+    float v[3] = {0.f, 0.f, 0.f};
+    for_masked<4>(rsel, col, s, nflag, mbit, [&](int j, float sj) {
+        if (j < 0) return;
+        const float pv = p[j * HID + lane];
+        const float dob = sj * group_agg(j, rp, col, s, ell, dh2bar);
+        const float ub = lane < c ? dob * inv_count : 0.f;
+        const float dot = gsum16(ub * pv);
+        const float ob = lane < c ? pv * (ub - dot) : 0.f;
+        v[0] = fmaf(sj, ob, v[0]);
+        if (j == row) {
+            v[1] = dob;
+            v[2] = ob;
+        }
+    });
+    combine_groups<4, 3>(rsel, v);
+    if (!rsel.lead) return;
+    const float ag = si * v[0];  // H2bar (zero past c)
+    if (g0) {
+        // use 3: G = dH2bar, Z = dO, Y = dH2, ÂG = dŌ (dO = 0 off the mask);
+        // use 2: G = Ōbar, Z = H2, Y = O, ÂG = H2bar — R += r3, then += r2 (rev_b, rev_c order)
+        const float r3 = emit_uv(U, V, ldk, foff_b, cw, row, lane, si, a_dh2bar, a_do, a_dh2, v[1]);
+        const float r2 = emit_uv(U, V, ldk, foff_c, cw, row, lane, si, v[2], a_h2, a_o, ag);
+        if (lane == 0) R[row] = (R[row] + r3) + r2;
+        h2bar[ix] = ag;
+    }
+    float hb = a_hb;
+#define LDS_W(K) if (K < c) hb = fmaf(rbc_f<K>(ag), w1v[K], hb);
+    LDS_R16(LDS_W)
+#undef LDS_W
+    float mask;
+    if (dmask != nullptr) {
+        mask = mk;
+    } else {
+        mask = y0[ix] > 0.f ? 1.f : 0.f;
+        if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    }
+    if (g0) y0bar[ix] = hb * mask;
 }
 
 // ---------------------------------------------------------------------------
@@ -1405,8 +1840,14 @@ __global__ __launch_bounds__(256) void end_window_kernel(int np, const float* __
                                                          float* __restrict__ v0, EngineScalars* sc,
                                                          int graphs, int forwards, int adam_steps,
                                                          int hypers, const double* __restrict__ betas,
-                                                         float* __restrict__ tab, int tab_count, int64_t par) {
+                                                         float* __restrict__ tab, int tab_count, int64_t par,
+                                                         int* __restrict__ ws, int64_t ws_count) {
     const int e = blockIdx.x * 256 + threadIdx.x;
+    if (ws != nullptr) {  // the next window's sampler workspace (lds_sample_graphs_multi, ws_zeroed)
+        const int64_t stride = (int64_t)gridDim.x * gridDim.y * 256;
+        for (int64_t k = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; k < ws_count; k += stride)
+            ws[k] = 0;
+    }
     if (wT != nullptr && e < np) {
         const int64_t o = (int64_t)blockIdx.y * par;
         w0[o + e] = wT[o + e];
@@ -1708,6 +2149,49 @@ extern "C" int lds_engine_rev_d(const int* rp, const int* col, const float* s, c
     LDS_RETURN_LAST_ERROR();
 }
 
+extern "C" int lds_engine_fwd2_bwd2(const int* rp, const int* col, const float* s, const int* ell, int n,
+                                     const uint8_t* node_flags, int mask_bit, const float* h2, float* o, float* p,
+                                     float* d_o, const int* label, float inv_count, float* lossrow, float* corrrow,
+                                     int c, const float* y0, float* dh2, float* dy0, const float* w1, uint64_t seed,
+                                     uint32_t tag_h, const void* scalars, int fwd_off, int train, float keep,
+                                     float scale, float* U, float* V, int ldk, float* R, int foff, int fwidth,
+                                     int r_assign, const float* dmask, const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && ell && node_flags && h2 && o && p && d_o && label && lossrow && corrrow);
+    LDS_CHECK_ARG(y0 && dh2 && dy0 && w1 && scalars && n > 0 && n <= kEllIndex + 1 && mask_bit > 0 && mask_bit < 256);
+    LDS_CHECK_ARG(c > 0 && c <= HID && batch_ok(batch) && (U == nullptr || (V && R && fwidth <= HID)));
+    GcnW w{nullptr, nullptr, w1, nullptr};
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    LDS_LAUNCH_B(fwd2_bwd2_kernel, ns, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0,
+                 (hipStream_t)stream, rp, col, s, (const int2*)ell, n, node_flags, mask_bit, h2, o, p, d_o, label,
+                 inv_count, lossrow, corrrow, c, y0, dh2, dy0, w, mk_keys(seed, 0, tag_h),
+                 (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff, fwidth, r_assign,
+                 dmask, bt);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_rev_bc(const int* rp, const int* col, const float* s, const int* ell, int n,
+                                 const uint8_t* node_flags, int mask_bit, const float* dh2bar, const float* d_o,
+                                 const float* dh2, const float* p, const float* h2, const float* o,
+                                 float inv_count, int c, const float* h1dbar_part, const float* y0,
+                                 const float* w1, float* h2bar, float* y0bar, uint64_t seed, uint32_t tag_h,
+                                 const void* scalars, int fwd_off, int train, float keep, float scale, float* U,
+                                 float* V, int ldk, float* R, int foff_b, int foff_c, int cw, const float* dmask,
+                                 const LdsBatch* batch, void* stream) {
+    LDS_CHECK_ARG(rp && col && s && ell && node_flags && dh2bar && d_o && dh2 && p && h2 && o && h1dbar_part);
+    LDS_CHECK_ARG(y0 && w1 && h2bar && y0bar && scalars && U && V && R && n > 0 && n <= kEllIndex + 1);
+    LDS_CHECK_ARG(mask_bit > 0 && mask_bit < 256 && c > 0 && c <= HID && cw >= c && cw <= HID && batch_ok(batch));
+    GcnW w{nullptr, nullptr, w1, nullptr};
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    LDS_LAUNCH_B(rev_bc_kernel, ns, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0,
+                 (hipStream_t)stream, rp, col, s, (const int2*)ell, n, node_flags, mask_bit, dh2bar, d_o, dh2, p, h2,
+                 o, inv_count, c, h1dbar_part, y0, w, h2bar, y0bar, mk_keys(seed, 0, tag_h),
+                 (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff_b, foff_c, cw, dmask,
+                 bt);
+    LDS_RETURN_LAST_ERROR();
+}
+
 extern "C" int lds_engine_sgd_clamp(float* theta, const float* grad, int64_t count, const void* scalars,
                                     void* stream) {
     LDS_CHECK_ARG(theta && grad && scalars && count >= 0);
@@ -1845,14 +2329,16 @@ extern "C" int lds_engine_xt_partials(const int* xcp, const int* xrow, const flo
 extern "C" int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT, float* w0,
                                      float* m0, float* v0, void* scalars, int graphs, int forwards,
                                      int adam_steps, int hypers, const double* betas_dev, float* adam_tab,
-                                     int tab_count, const LdsBatch* batch, void* stream) {
+                                     int tab_count, int* ws, int64_t ws_count, const LdsBatch* batch,
+                                     void* stream) {
     LDS_CHECK_ARG(scalars && np > 0 && (wT == nullptr || (mT && vT && w0 && m0 && v0)) && batch_ok(batch));
+    LDS_CHECK_ARG(ws_count >= 0 && (ws != nullptr || ws_count == 0));
     LDS_CHECK_ARG(adam_tab == nullptr || (betas_dev && tab_count > 0 && tab_count <= kAdamTabMax));
     Batch bt;
     const int ns = mk_batch(batch, bt);
     hipLaunchKernelGGL(end_window_kernel, dim3((np + 255) / 256, ns), dim3(256), 0, (hipStream_t)stream, np, wT,
                        mT, vT, w0, m0, v0, (EngineScalars*)scalars, graphs, forwards, adam_steps, hypers,
-                       betas_dev, adam_tab, tab_count, bt.par);
+                       betas_dev, adam_tab, tab_count, bt.par, ws, ws_count);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -31,11 +31,19 @@ namespace lds {
 // far past the 256 MB MALL) the re-reads are the kernel's HBM traffic, so
 // there the loop runs over every (graph, sample) of the batch (kLoop with
 // `graphs` = count: 1.24 ms -> see DESIGN §4b for 6 graphs at N = 20 000).
-template <bool kInj, bool kLoop>
+//
+// kDeg: the tile also counts what it stores into the row degrees dacc[graph]
+// (integer atomics, no-return, one per non-zero word: about a dozen per row
+// at Cora density), so the CSR fill needs no degree pass.  dacc must be zero
+// on entry.  (Per-64-row-block totals kept the same way cost 2x the kernel's
+// time: ~10^4 atomics per graph on three cache lines serialise at the memory
+// side.)
+template <bool kInj, bool kLoop, bool kDeg>
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
-    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs) {
+    uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs,
+    int* __restrict__ dacc, int wsi) {
     __shared__ uint64_t colpart[4][64];
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
@@ -75,6 +83,8 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
         const uint32_t ctr = counter + (uint32_t)gl;
         const uint32_t tg = tag + (uint32_t)z * tag_step;
         uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
+        int* __restrict__ da = kDeg ? dacc + ((int64_t)gidx * nsamp + z) * wsi : nullptr;
+        int rowpc = 0;  // kDeg: lane r's row count
         uint64_t colword = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -100,6 +110,10 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                 if (i < n) {
                     if (!diag_tile) {
                         if (lane == 0) gb[(int64_t)i * words + bj] = w;
+                        if constexpr (kDeg) {
+                            const int pc = __popcll(w);
+                            if (lane == 4 * q + r) rowpc = pc;
+                        }
                     } else if (lane == 0) {
                         rowword[i - bi * 64] = w;
                     }
@@ -107,12 +121,22 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                 if (e) colword |= 1ull << (i - bi * 64);
             }
         }
+        if constexpr (kDeg) {  // row part of an off-diagonal tile (diagonal tiles: column part only)
+            if (lane < 16 && rowpc != 0) atomicAdd(&da[r0 + lane], rowpc);
+        }
         colpart[wave][lane] = colword;
         __syncthreads();
-        if (wave == 0 && j < n) {
-            uint64_t out = colpart[0][lane] | colpart[1][lane] | colpart[2][lane] | colpart[3][lane];
-            if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
-            gb[(int64_t)j * words + bi] = out;
+        if (wave == 0) {
+            int pc = 0;
+            if (j < n) {
+                uint64_t out = colpart[0][lane] | colpart[1][lane] | colpart[2][lane] | colpart[3][lane];
+                if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
+                gb[(int64_t)j * words + bi] = out;
+                pc = __popcll(out);
+            }
+            if constexpr (kDeg) {
+                if (pc != 0) atomicAdd(&da[j], pc);
+            }
         }
         if (it + 1 < z1) __syncthreads();  // colpart / rowword are reused by the next item
     }
@@ -121,11 +145,11 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
 // One wave per row: popcount of the row's words.
 __global__ __launch_bounds__(256) void degree_kernel(const uint64_t* __restrict__ bits, int n,
                                                       int words, int* __restrict__ deg,
-                                                      float* __restrict__ s) {
+                                                      float* __restrict__ s, int deg_stride) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
     bits += (int64_t)blockIdx.y * n * words;  // batched: graph blockIdx.y
-    deg += (int64_t)blockIdx.y * n;
+    deg += (int64_t)blockIdx.y * deg_stride;
     s += (int64_t)blockIdx.y * n;
     const int lane = wave_lane();
     const int nbw = (n + 63) / 64;
@@ -167,6 +191,11 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ deg,
     if (t == 1023) row_ptr[n] = partial[1023];
 }
 
+// ELL j field: index | node flags (common.hpp kEllIndex); no flags: the index.
+__device__ __forceinline__ int ell_index(int j, const uint8_t* __restrict__ flags) {
+    return flags != nullptr ? (j | ((int)flags[j] << kEllFlagShift)) : j;
+}
+
 // Rows with at least this many entries use the word-at-a-time compaction.
 constexpr int kDenseRowFill = 1024;
 
@@ -184,7 +213,8 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
                                                         int* __restrict__ col, int64_t capacity,
                                                         int* __restrict__ overflow,
                                                         const float* __restrict__ s,
-                                                        int2* __restrict__ ell) {
+                                                        int2* __restrict__ ell,
+                                                        const uint8_t* __restrict__ flags) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n) return;
     bits += (int64_t)blockIdx.y * n * words;  // batched: graph blockIdx.y, col stride = capacity
@@ -222,7 +252,7 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
                 if (pos < capacity) col[pos] = j;
                 else over = true;
                 if (ell != nullptr && pos - row_beg < kEllWidth)
-                    ell[pos - row_beg] = make_int2(j, __float_as_int(s[j]));
+                    ell[pos - row_beg] = make_int2(ell_index(j, flags), __float_as_int(s[j]));
                 ++pos;
                 word &= word - 1;
             }
@@ -248,12 +278,104 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
                 if (pos < capacity) col[pos] = j;
                 else over = true;
                 if (ell != nullptr && pos - row_beg < kEllWidth)
-                    ell[pos - row_beg] = make_int2(j, __float_as_int(s[j]));
+                    ell[pos - row_beg] = make_int2(ell_index(j, flags), __float_as_int(s[j]));
             }
             base += __popcll(wd);
         }
     }
     if (over && overflow != nullptr) *overflow = 1;
+}
+
+// The CSR fill of the fused sampler: the tile kernel's degree counts give
+// each row its CSR offset directly — the block's 256 threads sum the degrees
+// of all rows before its first row (one coalesced pass, a block reduction),
+// each wave adds its predecessors in the block — so no scan launch runs
+// between the draw and the fill.  Also writes row_ptr, s = deg^-1/2 and the
+// ELL head, whose s_j is computed here from deg[j] (inv_sqrt_degree).
+__global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __restrict__ bits, int n, int words,
+                                                              const int* __restrict__ dacc, int wsi,
+                                                              int* __restrict__ row_ptr, int* __restrict__ col,
+                                                              int64_t capacity, float* __restrict__ s,
+                                                              int2* __restrict__ ell,
+                                                              const uint8_t* __restrict__ flags) {
+    __shared__ int red[4];
+    const int wave = threadIdx.x >> 6;
+    const int row0 = blockIdx.x * 4;
+    const int row = row0 + wave;
+    const int g = blockIdx.y;
+    bits += (int64_t)g * n * words;
+    dacc += (int64_t)g * wsi;
+    row_ptr += (int64_t)g * (n + 1);
+    col += (int64_t)g * capacity;
+    s += (int64_t)g * n;
+    const int lane = wave_lane();
+    int acc = 0;
+    for (int r = threadIdx.x; r < row0; r += 256) acc += dacc[r];
+    acc = wave_sum(acc);
+    if (lane == 0) red[wave] = acc;
+    __syncthreads();
+    if (row >= n) return;
+    int pre = red[0] + red[1] + red[2] + red[3];
+    for (int w = 0; w < wave; ++w) pre += dacc[row0 + w];
+    const int deg = dacc[row];
+    if (lane == 0) {  // (clamped: a workspace that was not zero on entry cannot send readers past col)
+        row_ptr[row] = (int)min((int64_t)pre, capacity);
+        if (row == n - 1) row_ptr[n] = (int)min((int64_t)pre + deg, capacity);
+        s[row] = inv_sqrt_degree(deg);
+    }
+    if (ell != nullptr) {
+        ell += ((int64_t)g * n + row) * kEllWidth;
+        if (lane < kEllWidth && lane >= deg) ell[lane] = make_int2(row, 0);  // padding: weight 0
+    }
+    const uint64_t* rb_bits = bits + (int64_t)row * words;
+    const int nbw = (n + 63) / 64;
+    int64_t base = pre;
+    if (deg < kDenseRowFill) {  // short rows: each lane pops its own word's bits
+        for (int w0 = 0; w0 < nbw; w0 += 64) {
+            const int w = w0 + lane;
+            uint64_t word = w < nbw ? rb_bits[w] : 0ull;
+            const int cnt = __popcll(word);
+            int incl = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            int64_t pos = base + (incl - cnt);
+            while (word) {
+                const int bit = __ffsll((unsigned long long)word) - 1;
+                const int j = w * 64 + bit;
+                if (pos < capacity) col[pos] = j;
+                if (ell != nullptr && pos - pre < kEllWidth)
+                    ell[pos - pre] = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+                ++pos;
+                word &= word - 1;
+            }
+            base += __shfl(incl, 63);
+        }
+        return;
+    }
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int w0 = 0; w0 < nbw; w0 += 64) {
+        const int w = w0 + lane;
+        const uint64_t word = w < nbw ? rb_bits[w] : 0ull;
+        uint64_t nz = __ballot(word != 0ull);
+        while (nz) {
+            const int src = __ffsll((unsigned long long)nz) - 1;
+            nz &= nz - 1;
+            const uint32_t lo = __shfl((uint32_t)word, src), hi = __shfl((uint32_t)(word >> 32), src);
+            const uint64_t wd = ((uint64_t)hi << 32) | lo;
+            const bool set = (wd >> lane) & 1ull;
+            const int64_t pos = base + __popcll(wd & below);
+            if (set) {
+                const int j = (w0 + src) * 64 + lane;
+                if (pos < capacity) col[pos] = j;
+                if (ell != nullptr && pos - pre < kEllWidth)
+                    ell[pos - pre] = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+            }
+            base += __popcll(wd);
+        }
+    }
 }
 
 __global__ void csr_degree_scale_kernel(const int* __restrict__ row_ptr, int n,
@@ -305,13 +427,15 @@ extern "C" int lds_sample_bitmask(const float* theta, int n, uint64_t seed, uint
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
     if (u_inject != nullptr)
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<true, false>), dim3(ntiles), dim3(256), 0,
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<true, false, false>), dim3(ntiles), dim3(256), 0,
                            (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1, 1);
+                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1, 1,
+                           (int*)nullptr, 0);
     else
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles), dim3(256), 0,
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false, false>), dim3(ntiles), dim3(256), 0,
                            (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1, 1);
+                           counter, (const uint32_t*)nullptr, u_inject, bits, words, ntiles, 0u, 1, 1,
+                           (int*)nullptr, 0);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -322,9 +446,10 @@ extern "C" int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, 
     LDS_CHECK_ARG(n > 0 && n <= (1 << 20) && words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles), dim3(256), 0,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false, false>), dim3(ntiles), dim3(256), 0,
                        (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u, 1, 1);
+                       counter_offset, counter_base, (const float*)nullptr, bits, words, ntiles, 0u, 1, 1,
+                       (int*)nullptr, 0);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -333,7 +458,7 @@ extern "C" int lds_bitmask_degree(const uint64_t* bits, int n, int words, int* d
     LDS_CHECK_ARG(bits != nullptr && deg != nullptr && s != nullptr && n > 0);
     LDS_CHECK_ARG(words >= (n + 63) / 64);
     hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, bits,
-                       n, words, deg, s);
+                       n, words, deg, s, n);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -350,7 +475,7 @@ extern "C" int lds_bitmask_fill_csr(const uint64_t* bits, int n, int words, cons
     LDS_CHECK_ARG(words >= (n + 63) / 64 && col_capacity >= 0);
     hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                        bits, n, words, row_ptr, col, col_capacity, overflow, (const float*)nullptr,
-                       (int2*)nullptr);
+                       (int2*)nullptr, (const uint8_t*)nullptr);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -360,7 +485,8 @@ extern "C" int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words, 
     LDS_CHECK_ARG(bits != nullptr && row_ptr != nullptr && col != nullptr && n > 0);
     LDS_CHECK_ARG(words >= (n + 63) / 64 && col_capacity >= 0 && s != nullptr && ell != nullptr);
     hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                       bits, n, words, row_ptr, col, col_capacity, overflow, s, (int2*)ell);
+                       bits, n, words, row_ptr, col, col_capacity, overflow, s, (int2*)ell,
+                       (const uint8_t*)nullptr);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -372,39 +498,67 @@ extern "C" int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* 
     LDS_RETURN_LAST_ERROR();
 }
 
+extern "C" int lds_sample_ws_ints(int n) { return n; }
+
 extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                                        uint32_t tag_step, const uint32_t* counter_base,
                                        uint32_t counter_offset, int count, int samples, uint64_t* bits,
                                        int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
-                                       float* s, int* ell, void* stream) {
+                                       float* s, int* ell, const uint8_t* node_flags, int ws_zeroed,
+                                       void* stream) {
     // col == NULL: bitmask, degrees and s only (the bitmask aggregation of
-    // dense graphs reads no CSR); row_ptr / ell are then not written
+    // dense graphs reads no CSR); row_ptr / ell are then not written.
+    // deg_ws: lds_sample_ws_ints(n) ints per graph (degrees first); with CSR
+    // the tile kernel accumulates into it, so it must be zero on entry —
+    // ws_zeroed = 1 promises that (the engine zeroes it at the end of every
+    // window, lds_engine_end_window), 0 lets this call clear it first.
     LDS_CHECK_ARG(theta && bits && deg_ws && s && n > 0 && n <= (1 << 20));
     LDS_CHECK_ARG(col == nullptr || (row_ptr != nullptr && col_stride > 0));
     LDS_CHECK_ARG(count > 0 && samples > 0 && samples <= 65535 && (int64_t)count * samples <= 65535);
-    LDS_CHECK_ARG(words >= (n + 63) / 64);
+    LDS_CHECK_ARG(words >= (n + 63) / 64 && n <= kEllIndex + 1);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
     const int graphs = count * samples;
+    const int wsi = lds_sample_ws_ints(n);
     hipStream_t st = (hipStream_t)stream;
+    const bool fused = col != nullptr;  // degrees counted by the tiles, scan folded into the fill
+    if (fused && !ws_zeroed) {
+        const hipError_t e = hipMemsetAsync(deg_ws, 0, (size_t)graphs * wsi * sizeof(int), st);
+        if (e != hipSuccess) return (int)e;
+    }
+    int* dacc = fused ? deg_ws : nullptr;
     // replica samples loop inside the block over one θ tile load; past the
     // MALL (θ > ~64 MB) the window's graphs join that loop too
     const bool big = (int64_t)n * (n + 1) / 2 * 4 > ((int64_t)64 << 20);
     const int loop_graphs = big ? count : 1;
-    if (samples > 1 || (big && count > 1))
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true>), dim3(ntiles, count / loop_graphs, 1),
-                           dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
-                           counter_base, (const float*)nullptr, bits, words, ntiles, tag_step, samples, loop_graphs);
-    else
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false>), dim3(ntiles, count, 1), dim3(256), 0, st, theta,
-                           n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
-                           (const float*)nullptr, bits, words, ntiles, tag_step, 1, 1);
-    hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
-                       deg_ws, s);
-    if (col == nullptr) LDS_RETURN_LAST_ERROR();
-    hipLaunchKernelGGL(scan_kernel, dim3(1, graphs), dim3(1024), 0, st, deg_ws, n, row_ptr);
-    hipLaunchKernelGGL(fill_csr_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
-                       row_ptr, col, col_stride, (int*)nullptr, (const float*)s, (int2*)ell);
+    if (samples > 1 || (big && count > 1)) {
+        if (fused)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true>), dim3(ntiles, count / loop_graphs, 1),
+                               dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
+                               counter_base, (const float*)nullptr, bits, words, ntiles, tag_step, samples, loop_graphs,
+                               dacc, wsi);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, false>), dim3(ntiles, count / loop_graphs, 1),
+                               dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
+                               counter_base, (const float*)nullptr, bits, words, ntiles, tag_step, samples, loop_graphs,
+                               dacc, wsi);
+    } else {
+        if (fused)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false, true>), dim3(ntiles, count, 1), dim3(256), 0,
+                               st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
+                               (const float*)nullptr, bits, words, ntiles, tag_step, 1, 1, dacc, wsi);
+        else
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, false, false>), dim3(ntiles, count, 1), dim3(256), 0,
+                               st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset, counter_base,
+                               (const float*)nullptr, bits, words, ntiles, tag_step, 1, 1, dacc, wsi);
+    }
+    if (!fused) {
+        hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
+                           deg_ws, s, wsi);
+        LDS_RETURN_LAST_ERROR();
+    }
+    hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
+                       (const int*)deg_ws, wsi, row_ptr, col, col_stride, s, (int2*)ell, node_flags);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -413,7 +567,7 @@ extern "C" int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint3
                                  uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
                                  int64_t col_stride, float* s, int* ell, void* stream) {
     return lds_sample_graphs_multi(theta, n, seed, tag, 0u, counter_base, counter_offset, count, 1, bits,
-                                   words, deg_ws, row_ptr, col, col_stride, s, ell, stream);
+                                   words, deg_ws, row_ptr, col, col_stride, s, ell, nullptr, 0, stream);
 }
 
 extern "C" int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32_t tag,

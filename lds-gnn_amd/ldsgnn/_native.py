@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -34,7 +34,8 @@ SIGNATURES = {
     "lds_sample_graphs": [P, c_int, c_uint64, c_uint32, P, c_uint32, c_int, P, c_int, P, P, P, c_int64, P, P,
                           P],
     "lds_sample_graphs_multi": [P, c_int, c_uint64, c_uint32, c_uint32, P, c_uint32, c_int, c_int, P, c_int, P,
-                                P, P, c_int64, P, P, P],
+                                P, P, c_int64, P, P, P, c_int, P],
+    "lds_sample_ws_ints": [c_int],
     "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
     "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
@@ -92,7 +93,13 @@ SIGNATURES = {
                            c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, c_int, P, c_int, P, P],
     "lds_engine_xt_partials": [P, P, P, c_int, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float, c_int, P,
                                P, P],
-    "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
+    "lds_engine_fwd2_bwd2": [P, P, P, P, c_int, P, c_int, P, P, P, P, P, c_float, P, P, c_int, P, P, P, P,
+                             c_uint64, c_uint32, P, c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, c_int,
+                             c_int, P, P, P],
+    "lds_engine_rev_bc": [P, P, P, P, c_int, P, c_int, P, P, P, P, P, P, c_float, c_int, P, P, P, P, P, c_uint64,
+                          c_uint32, P, c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, c_int, c_int, P, P, P],
+    "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int64,
+                              P, P],
     "lds_engine_adam_table": [P, P, P, c_int, P],
 }
 

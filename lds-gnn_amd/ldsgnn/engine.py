@@ -77,7 +77,9 @@ class _GraphBatch:
         self.count, self.cap = count, cap
         S = samples
         self.bits = torch.empty((count, S, n, words), dtype=torch.int64, device=dev)
-        self.deg = torch.empty((count, S, n), dtype=torch.int32, device=dev)
+        # sampler workspace (degrees + row-block totals, lds_sample_ws_ints):
+        # zero on entry to a window's draw, cleared again by lds_engine_end_window
+        self.deg = torch.zeros((count, S, int(nat.lib.lds_sample_ws_ints(n))), dtype=torch.int32, device=dev)
         self.row_ptr = torch.empty((count, S, n + 1), dtype=torch.int32, device=dev)
         self.col = torch.empty((count, S, max(cap, 1)), dtype=torch.int32, device=dev)
         self.s = torch.empty((count, S, n), dtype=torch.float32, device=dev)
@@ -171,6 +173,8 @@ class LdsEngine:
         self.label = y.to(device=dev, dtype=torch.int32).contiguous()
         self.train_mask = train_mask.to(device=dev, dtype=torch.uint8).contiguous()
         self.opt_mask = opt_mask.to(device=dev, dtype=torch.uint8).contiguous()
+        # node flags carried in every ELL entry (include/ldsgnn.h): bit 0 train, bit 1 opt
+        self.nflag = (self.train_mask | (self.opt_mask << 1)).contiguous()
         self.inv_train = float(np.float32(1.0) / np.float32(int(train_mask.sum())))
         self.inv_opt = float(np.float32(1.0) / np.float32(int(opt_mask.sum())))
 
@@ -201,6 +205,12 @@ class LdsEngine:
                          .clamp(0, 1).double().sum().item())
             long_rows = n >= 1024 and 1.0 + 2.0 * (tsum - diag) / n >= 256.0
         self.long_rows = bool(long_rows)
+        # two-hop loss kernels (lds_engine_fwd2_bwd2 / lds_engine_rev_bc): need the
+        # ELL head with node flags, i.e. in-kernel aggregation (short rows)
+        self.two_hop = not self.long_rows
+        # the outer step's loss (opt mask, ~2x the train rows): separate launches
+        # measured faster (more masked neighbours per row -> more rounds)
+        self.two_hop_outer = False
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
         if long_rows_kernel not in ("bitmask", "blocked"):
@@ -214,7 +224,8 @@ class LdsEngine:
         self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) if self.long_rows and not self.bitmask_agg else 0
         self.words = nat.lib.lds_bitmask_words(n)
         S = self.S
-        self.deg = torch.empty((S, n), dtype=torch.int32, device=dev)
+        self.deg = torch.empty((S, int(nat.lib.lds_sample_ws_ints(n))), dtype=torch.int32, device=dev)
+        self._ws_clean = True  # gbatch.deg is zero (fresh, or cleared by the last end_window)
 
         # tape
         self.tau = max(1, int(tau))
@@ -291,21 +302,29 @@ class LdsEngine:
 
     # rows expected to have more than this many entries get a block of their own
     HEAVY_DEGREE = 64
+    # ... and so do rows expected to have more than this many neighbours in a
+    # loss mask (the two-hop kernels recompute each such neighbour's row)
+    HEAVY_MASKED = 4
 
     def _row_plan(self):
         """The aggregating kernels' row plan (include/ldsgnn.h LdsBatch): rows
-        whose expected degree 1 + Σ_j clamp(θ_ij, 0, 1) exceeds HEAVY_DEGREE run on a
-        block of their own.  Decided once from θ at construction: it changes
-        speed only (a row of any degree is aggregated correctly either way).
-        Long-row mode (pre-aggregated Â·Z) has no plan."""
+        whose expected degree 1 + Σ_j clamp(θ_ij, 0, 1) exceeds HEAVY_DEGREE,
+        or whose expected count of train (or opt) neighbours, self included,
+        exceeds HEAVY_MASKED, run on a block of their own.  Decided once from θ
+        at construction: it changes speed only (a row of any degree is
+        aggregated correctly either way).  Long-row mode (pre-aggregated Â·Z)
+        has no plan."""
         n = self.n
         self.heavy_flag = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+        self.heavy_flag2 = torch.zeros(n, dtype=torch.uint8, device=self.dev)
         if self.long_rows:
-            self.heavy_rows = torch.zeros(1, dtype=torch.int32, device=self.dev)
-            self.n_heavy = 0
+            self.heavy_rows = self.heavy_rows2 = torch.zeros(1, dtype=torch.int32, device=self.dev)
+            self.n_heavy = self.n_heavy2 = 0
             return
         i = torch.arange(n, device=self.dev)
         deg = torch.ones(n, device=self.dev)
+        mt = self.train_mask.float()
+        et = mt.clone()  # expected train neighbours (self-loop included)
         step = max(1, (1 << 24) // n)  # rows per chunk of the packed triangle
         for r0 in range(0, n, step):
             r1 = min(n, r0 + step)
@@ -314,7 +333,15 @@ class LdsEngine:
             cols = rows + (torch.arange(lo, hi, device=self.dev) - (rows * (2 * n - rows + 1)) // 2)
             p = self.theta[lo:hi].clamp(0.0, 1.0) * (rows != cols)
             deg.index_add_(0, rows, p).index_add_(0, cols, p)
+            et.index_add_(0, rows, p * mt[cols]).index_add_(0, cols, p * mt[rows])
         heavy = deg > self.HEAVY_DEGREE
+        # the two-hop kernels' own plan (their LdsBatch, bt2): also rows with
+        # many train neighbours (no block reductions there, so nred is unaffected)
+        heavy2 = heavy | (et > self.HEAVY_MASKED)
+        self.heavy_rows2 = i[heavy2].to(torch.int32).contiguous() if bool(heavy2.any()) else \
+            torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.heavy_flag2[heavy2] = 1
+        self.n_heavy2 = int(heavy2.sum())
         self.heavy_rows = i[heavy].to(torch.int32).contiguous() if bool(heavy.any()) else \
             torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.heavy_flag[heavy] = 1
@@ -331,8 +358,12 @@ class LdsEngine:
                                 heavy_flag=nat.ptr(self.heavy_flag), n_heavy=self.n_heavy)
         self._bt = mk(0)  # X values argument = the shared X
         self._btx = mk(self.x_nnz if self.train_flag else 0)  # X values argument = the slot's stored Xd
+        self._bt2 = mk(0)  # the two-hop kernels: their own row plan
+        self._bt2.heavy_rows, self._bt2.heavy_flag = nat.ptr(self.heavy_rows2), nat.ptr(self.heavy_flag2)
+        self._bt2.n_heavy = self.n_heavy2
         self.bt = nat.batch_ptr(self._bt)
         self.btx = nat.batch_ptr(self._btx)
+        self.bt2 = nat.batch_ptr(self._bt2)
 
     def _grow(self, slots: int):
         self._layout_version += 1
@@ -439,7 +470,7 @@ class LdsEngine:
         st, n, c, E = self._stream(), self.n, self.c, int(n_samples)
         if getattr(self, "_evb_E", 0) != E:
             self._evb = _Slot(n, self.cap, self.dev, x_nnz=0, samples=E, bptr_len=0, words=self.words)
-            self._evb_deg = torch.empty((E, n), dtype=torch.int32, device=self.dev)
+            self._evb_deg = torch.empty((E, int(nat.lib.lds_sample_ws_ints(n))), dtype=torch.int32, device=self.dev)
             self._evb_rows = torch.zeros((2, E, n), dtype=torch.float32, device=self.dev)
             self._evb_w = torch.zeros((1, self.np), dtype=torch.float32, device=self.dev)
             self._evb_bt_obj = nat.LdsBatch(samples=E, tag_step=1, act=n * HID, row=n, rp=n + 1, col=self.cap,
@@ -455,7 +486,7 @@ class LdsEngine:
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, E, 1, nat.ptr(g.bits), self.words,
                  nat.ptr(self._evb_deg), nat.ptr(g.row_ptr), nat.ptr(g.col), self.cap, nat.ptr(g.s),
-                 nat.ptr(g.ell), st)
+                 nat.ptr(g.ell), nat.ptr(self.nflag), 0, st)
         self.pending_graph += E
         self._forward(sl, self._evb_w, vm, inv_v, 0, 0, bt=bt)  # val rows -> sl.lossrow / corrrow [E, n]
         rl, rc = self._evb_rows[0], self._evb_rows[1]
@@ -523,7 +554,7 @@ class LdsEngine:
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(g.bits), self.words,
                  nat.ptr(self.deg), nat.ptr(g.row_ptr), self._col_arg(g.col), self.cap, nat.ptr(g.s),
-                 nat.ptr(g.ell), self._stream())
+                 nat.ptr(g.ell), nat.ptr(self.nflag), 0, self._stream())
         self._block_ptrs([g])
         self.pending_graph += 1
 
@@ -550,7 +581,10 @@ class LdsEngine:
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
         return nat.ptr(self.agg)
 
-    def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int, bt=None):
+    def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int, bt=None,
+                 loss_in_backward: bool = False):
+        """X-linear, layer 1 and (unless loss_in_backward: the two-hop
+        backward computes it) the loss layer."""
         st, n, c = self._stream(), self.n, self.c
         bt = self.bt if bt is None else bt
         w0t, b0, w1, b1 = self._views(w)
@@ -566,6 +600,8 @@ class LdsEngine:
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
                  self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask),
                  self._agg(g, sl.h0), bt, st)
+        if loss_in_backward and self.two_hop:
+            return
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
                  nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), nat.ptr(mask), inv_count,
                  nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, self._agg(g, sl.h2), bt, st)
@@ -622,10 +658,13 @@ class LdsEngine:
         return self.xval, self.xtval
 
     def _backward(self, sl: _Slot, w: torch.Tensor, gout: torch.Tensor, train: int, fwd_off: int,
-                  metrics_row: torch.Tensor, outer_factors: bool, adam_mode: int, adam_t: int):
+                  metrics_row: torch.Tensor, outer_factors: bool, adam_mode: int, adam_t: int,
+                  mask_bit: int = 0, inv_count: float = 0.0):
         """First-order backward into `gout` (data gradient, no weight decay),
         fused with the Adam forward of inner step adam_t (adam_mode 1) or the
-        Adam reverse of inner step adam_t (adam_mode 2, hyper step)."""
+        Adam reverse of inner step adam_t (adam_mode 2, hyper step).  With the
+        two-hop kernels the loss layer over the rows of `mask_bit` runs here
+        (lds_engine_fwd2_bwd2)."""
         st, n, c = self._stream(), self.n, self.c
         _, _, w1, _ = self._views(w)
         g = sl.g
@@ -635,10 +674,17 @@ class LdsEngine:
         else:
             base, U, V, R = 0, 0, 0, 0
         rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
-        nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
-                 nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
-                 self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldu, R, base + HID, self.cw,
-                 1, nat.ptr(sl.dmask), self._agg(g, sl.d_o), self.bt, st)
+        if self.two_hop and (mask_bit == 1 or self.two_hop_outer):
+            nat.call("lds_engine_fwd2_bwd2", rp, cl, s, el, n, nat.ptr(self.nflag), mask_bit, nat.ptr(sl.h2),
+                     nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), inv_count,
+                     nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, nat.ptr(sl.y0), nat.ptr(sl.dh2), nat.ptr(sl.dy0),
+                     nat.ptr(w1), self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep,
+                     self.scale, U, V, self.ldu, R, base + HID, self.cw, 1, nat.ptr(sl.dmask), self.bt2, st)
+        else:
+            nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
+                     nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
+                     self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldu, R, base + HID, self.cw,
+                     1, nat.ptr(sl.dmask), self._agg(g, sl.d_o), self.bt, st)
         # dH0 + first stage of gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
         nat.call("lds_engine_bwd1_reduce", rp, cl, s, el, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
                  nat.ptr(sl.h0), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
@@ -662,7 +708,8 @@ class LdsEngine:
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
                  nat.ptr(gb.deg), nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s),
-                 nat.ptr(gb.ell), self._stream())
+                 nat.ptr(gb.ell), nat.ptr(self.nflag), 1 if self._ws_clean else 0, self._stream())
+        self._ws_clean = False
         self._block_ptrs(gb.graphs[:count])
 
     def inner_step(self, presampled: bool = False):
@@ -682,8 +729,10 @@ class LdsEngine:
         else:
             self._sample(sl.g)
         fwd_off = self.pending_fwd
-        self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off)
-        self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False, 1, t)
+        self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off,
+                      loss_in_backward=True)
+        self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False, 1, t,
+                       mask_bit=1, inv_count=self.inv_train)
         if self.train_flag:
             self.pending_fwd += 1
         self.t = t + 1
@@ -709,11 +758,12 @@ class LdsEngine:
         else:
             self._sample(out.g)
         fwd_off = self.pending_fwd
-        self._forward(out, self.w[T], self.opt_mask, self.inv_opt, self.train_flag, fwd_off)
+        self._forward(out, self.w[T], self.opt_mask, self.inv_opt, self.train_flag, fwd_off,
+                      loss_in_backward=self.two_hop_outer)
         # R is assigned by the outer layer-2 backward (first emitter); the
         # Adam reverse of step T-1 starts from zero m̄ / v̄ (`first`)
         self._backward(out, self.w[T], self.wbar, self.train_flag, fwd_off, self.metrics[self.tau], True,
-                       2 if T else 0, T - 1 if T else 0)
+                       2 if T else 0, T - 1 if T else 0, mask_bit=2, inv_count=self.inv_opt)
         if self.train_flag:
             self.pending_fwd += 1
         split = self.split_theta_grad and T > 0
@@ -752,7 +802,8 @@ class LdsEngine:
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
         nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
                  P(self.scalars), self.pending_graph, self.pending_fwd, T, 1, P(self.betas_dev), P(self.adam_tab),
-                 self._tab_count(), self.bt, st)
+                 self._tab_count(), P(self.gbatch.deg), self.gbatch.deg.numel(), self.bt, st)
+        self._ws_clean = True
         self.pending_graph = 0
         self.pending_fwd = 0
         self.t = 0
@@ -810,13 +861,20 @@ class LdsEngine:
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
                  nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldu, R,
                  base + HID + 2 * self.cw, nat.ptr(sl.dmask), self._agg(g, self.dh0bar), self.bt, st)
-        nat.call("lds_engine_rev_b", rp, cl, s, el, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
-                 nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldu,
-                 R, base + HID + self.cw, self.cw, self._agg(g, self.dh2bar), self.bt, st)
-        nat.call("lds_engine_rev_c", rp, cl, s, el, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
-                 nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
-                 self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
-                 self.ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self._agg(g, self.obar), self.bt, st)
+        if self.two_hop:  # dŌ, Ōbar on the train rows only, H2bar from them: one launch
+            nat.call("lds_engine_rev_bc", rp, cl, s, el, n, nat.ptr(self.nflag), 1, nat.ptr(self.dh2bar),
+                     nat.ptr(sl.d_o), nat.ptr(sl.dh2), nat.ptr(sl.p), nat.ptr(sl.h2), nat.ptr(sl.o), self.inv_train, c,
+                     nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), nat.ptr(self.h2bar), nat.ptr(self.y0bar),
+                     self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
+                     self.ldu, R, base + HID + self.cw, base + HID, self.cw, nat.ptr(sl.dmask), self.bt2, st)
+        else:
+            nat.call("lds_engine_rev_b", rp, cl, s, el, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
+                     nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldu,
+                     R, base + HID + self.cw, self.cw, self._agg(g, self.dh2bar), self.bt, st)
+            nat.call("lds_engine_rev_c", rp, cl, s, el, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
+                     nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
+                     self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
+                     self.ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self._agg(g, self.obar), self.bt, st)
         # H0bar + first stage of W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
         nat.call("lds_engine_rev_d_reduce", rp, cl, s, el, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
                  nat.ptr(self.h0bar), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
@@ -965,12 +1023,18 @@ class LdsEngine:
     def sampled_nnz(self) -> int:
         """Stored entries (self-loops included) of the last window's outer
         graph, sample 0 (host sync)."""
-        return int(self.gbatch.deg[self.tau, 0].sum().item())
+        if self.bitmask_agg:  # no CSR: the degrees of the popcount pass
+            return int(self.gbatch.deg[self.tau, 0, :self.n].sum().item())
+        return int(self.gbatch.row_ptr[self.tau, 0, self.n].item())
 
     def sampled_nnz_mean(self) -> float:
         """Mean stored entries per sampled graph over the last batched window's
         τ+1 graphs and replica samples (host sync)."""
-        return float(self.gbatch.deg.double().sum().item()) / (self.gbatch.count * self.S)
+        if self.bitmask_agg:
+            tot = self.gbatch.deg[:, :, :self.n].double().sum()
+        else:
+            tot = self.gbatch.row_ptr[:, :, self.n].double().sum()
+        return float(tot.item()) / (self.gbatch.count * self.S)
 
     @staticmethod
     def window_columns(tau: int, c: int) -> int:

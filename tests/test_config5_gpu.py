@@ -114,11 +114,11 @@ def test_batched_sampler_n20000_equals_single_draws(device):
     st = nat.stream_of(device)
     base = torch.tensor([3, 0, 0, 0], dtype=torch.int32, device=device)
     bits = torch.empty((count, 1, n, words), dtype=torch.int64, device=device)
-    deg = torch.empty((count, 1, n), dtype=torch.int32, device=device)
+    deg = torch.empty((count, 1, nat.lib.lds_sample_ws_ints(n)), dtype=torch.int32, device=device)
     s = torch.empty((count, 1, n), dtype=torch.float32, device=device)
     seed, tag = 99, tag_for(TAG_GRAPH, 0)
     nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 1, count, 1,
-             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, st)
+             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, 0, 0, st)
     one = torch.empty((n, words), dtype=torch.int64, device=device)
     nb = (n + 63) // 64
     for gi in range(count):

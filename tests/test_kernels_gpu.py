@@ -352,11 +352,12 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
     st = nat.stream_of(theta.device)
     base = torch.tensor([7, 0, 0, 0], dtype=torch.int32, device=device)
     bits = torch.empty((count, samples, n, words), dtype=torch.int64, device=device)
-    deg = torch.empty((count, samples, n), dtype=torch.int32, device=device)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    deg = torch.empty((count, samples, wsi), dtype=torch.int32, device=device)
     s = torch.empty((count, samples, n), dtype=torch.float32, device=device)
     seed, tag = 1234, tag_for(TAG_GRAPH, 5)
     nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 2, count, samples,
-             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, st)
+             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, 0, 0, st)
     one = torch.empty((n, words), dtype=torch.int64, device=device)
     nb = (n + 63) // 64
     for gi in range(count):
@@ -368,7 +369,60 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
                 x = one[:, w]
                 for k in range(64):
                     pc += (x >> k) & 1
-            assert torch.equal(deg[gi, b].long(), pc), (gi, b)
+            assert torch.equal(deg[gi, b, :n].long(), pc), (gi, b)
+
+
+@pytest.mark.parametrize("n,count,samples,dense", [(300, 3, 2, 0.3), (1000, 2, 1, 0.05), (2100, 2, 1, 0.9)])
+def test_fused_sampler_csr_equals_staged_path(device, n, count, samples, dense):
+    """The two-launch CSR sampler (degrees counted by the tile kernel, the scan
+    folded into the fill) against the staged path (draw -> popcount degrees /
+    s -> scan -> fill + ELL head): bit-identical row_ptr, col, s and ELL, with
+    a dirty workspace cleared by the call (ws_zeroed = 0) and with a zeroed one
+    (ws_zeroed = 1).  dense = 0.9 takes the word-at-a-time fill of rows past
+    1024 entries."""
+    g = torch.Generator().manual_seed(n + count)
+    theta = (torch.rand(n * (n + 1) // 2, generator=g) * dense).to(device)
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    st = nat.stream_of(theta.device)
+    base = torch.tensor([5, 0, 0, 0], dtype=torch.int32, device=device)
+    G = count * samples
+    cap = n * n
+    seed, tag = 77, tag_for(TAG_GRAPH, 2)
+    outs = []
+    for zeroed in (0, 1):
+        bits = torch.empty((G, n, words), dtype=torch.int64, device=device)
+        ws = torch.full((G, wsi), 0 if zeroed else 7, dtype=torch.int32, device=device)
+        rp = torch.empty((G, n + 1), dtype=torch.int32, device=device)
+        col = torch.full((G, cap), -1, dtype=torch.int32, device=device)
+        s = torch.empty((G, n), dtype=torch.float32, device=device)
+        ell = torch.empty((G, n * 128), dtype=torch.int32, device=device)
+        nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 1, count, samples,
+                 nat.ptr(bits), words, nat.ptr(ws), nat.ptr(rp), nat.ptr(col), cap, nat.ptr(s), nat.ptr(ell), 0, zeroed, st)
+        outs.append((rp.clone(), col.clone(), s.clone(), ell.clone(), ws[:, :n].clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    rp, col, s, ell, deg = outs[0]
+    for gi in range(count):
+        for b in range(samples):
+            k = gi * samples + b
+            one = torch.empty((n, words), dtype=torch.int64, device=device)
+            nat.call("lds_sample_bitmask", nat.ptr(theta), n, seed, tag + b, 5 + 1 + gi, 0, nat.ptr(one), words, st)
+            d1 = torch.empty(n, dtype=torch.int32, device=device)
+            s1 = torch.empty(n, dtype=torch.float32, device=device)
+            rp1 = torch.empty(n + 1, dtype=torch.int32, device=device)
+            col1 = torch.full((cap,), -1, dtype=torch.int32, device=device)
+            ell1 = torch.empty(n * 128, dtype=torch.int32, device=device)
+            nat.call("lds_bitmask_degree", nat.ptr(one), n, words, nat.ptr(d1), nat.ptr(s1), st)
+            nat.call("lds_exclusive_scan", nat.ptr(d1), n, nat.ptr(rp1), st)
+            nat.call("lds_bitmask_fill_csr_ell", nat.ptr(one), n, words, nat.ptr(rp1), nat.ptr(col1), cap, 0,
+                     nat.ptr(s1), nat.ptr(ell1), st)
+            assert torch.equal(deg[k], d1), (gi, b)
+            assert torch.equal(rp[k], rp1), (gi, b)
+            assert torch.equal(s[k], s1), (gi, b)
+            nnz = int(rp1[n])
+            assert torch.equal(col[k, :nnz], col1[:nnz]), (gi, b)
+            assert torch.equal(ell[k], ell1), (gi, b)
 
 
 @pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16", "bf16x3-t64k16-grouped", "bf16x3-t64k32",

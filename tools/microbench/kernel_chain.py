@@ -80,7 +80,13 @@ def main():
                                 for _ in range(args.k)])
     print(json.dumps({"what": "floor", "kernel": "lds_engine_advance (1 block)", "us": 1e6 * floor / args.k}))
     rows = []
+    ws_bytes = eng.gbatch.deg.numel() * 4
+    memset = graph_time(lambda: [torch.cuda.current_stream() and eng.gbatch.deg.zero_() for _ in range(args.k)])
+    print(json.dumps({"what": "memset chain", "bytes": ws_bytes, "us": 1e6 * memset / args.k}), flush=True)
     for i, (name, a) in enumerate(calls):
+        if name == "lds_sample_graphs_multi":  # repeated draws: the call clears its workspace (ws_zeroed = 0)
+            a = a[:-2] + (0,) + a[-1:]
+
         def chain(name=name, a=a):
             for _ in range(args.k):
                 real(name, *cur(a))
@@ -99,6 +105,16 @@ def main():
                     real("lds_engine_xt_adam", *cur(b))
             print(json.dumps({"what": "xt_adam ablation", "variant": label, "us": 1e6 * graph_time(chain) / args.k}),
                   flush=True)
+    # two-hop kernels without picks (mask bit no node has): the walk + epilogue alone
+    for name in ("lds_engine_fwd2_bwd2", "lds_engine_rev_bc"):
+        for i, a in enumerate([a for nm, a in calls if nm == name][:1] + [a for nm, a in calls if nm == name][-1:]):
+            b = a[:6] + (128,) + a[7:]
+            for label, x in (("as recorded", a), ("no picks", b)):
+                def chain(x=x, name=name):
+                    for _ in range(args.k):
+                        real(name, *cur(x))
+                print(json.dumps({"what": "two-hop ablation", "call": name, "which": "first" if i == 0 else "last",
+                                  "variant": label, "us": 1e6 * graph_time(chain) / args.k}), flush=True)
     print(json.dumps({"what": "summary", "calls": len(calls), "window_us": 1e6 * t_window,
                       "sum_self_chain_us": sum(r["us"] for r in rows), "floor_us": 1e6 * floor / args.k,
                       "samples": args.samples}))

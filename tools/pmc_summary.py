@@ -19,6 +19,38 @@ def load(path):
     return per
 
 
+# engine entry point -> the kernels one call of it dispatches (name substrings)
+ENTRY_KERNELS = {
+    "lds_sample_graphs_multi": ["sample_tiles_kernel", "degree_kernel", "scan_kernel", "fill_csr_kernel",
+                                "fill_csr_fused_kernel"],
+    "lds_theta_grad_sgd": ["theta_grad"],
+    "lds_engine_x_linear": ["x_linear_kernel"],
+    "lds_engine_fwd_layer1": ["fwd_layer1_kernel"],
+    "lds_engine_fwd_layer2": ["fwd_layer2_kernel"],
+    "lds_engine_bwd_layer2": ["bwd_layer2_kernel"],
+    "lds_engine_bwd1_reduce": ["bwd1_reduce_kernel"],
+    "lds_engine_xt_adam": ["xt_adam_kernel"],
+    "lds_engine_rev_a": ["rev_a_kernel"],
+    "lds_engine_rev_b": ["rev_b_kernel"],
+    "lds_engine_rev_c": ["rev_c_kernel"],
+    "lds_engine_rev_d_reduce": ["rev_d_reduce_kernel"],
+    "lds_engine_end_window": ["end_window_kernel"],
+}
+
+
+def entries(per_kernel):
+    """Bytes per call of each entry point: the sum over its kernels of their
+    per-dispatch means."""
+    out = {}
+    for entry, subs in ENTRY_KERNELS.items():
+        ks = [k for k in per_kernel if any(s in k for s in subs)]
+        if not ks:
+            continue
+        out[entry] = {f: sum(per_kernel[k][f] for k in ks) for f in ("read_bytes", "write_bytes", "traffic_bytes")}
+        out[entry]["kernels"] = ks
+    return out
+
+
 def main():
     base = sys.argv[1]
     want = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else None
@@ -35,9 +67,12 @@ def main():
         wr = 1024 * sum(w) / len(w)
         out[name] = dict(launches=len(f), read_bytes=rd, write_bytes=wr, traffic_bytes=rd + wr)
         print(f"{len(f):6d} read {rd / 1e6:9.3f} MB  write {wr / 1e6:9.3f} MB  per launch  {name}")
+    ent = entries(out)
+    for name, e in ent.items():
+        print(f"entry {name}: read {e['read_bytes'] / 1e6:.3f} MB write {e['write_bytes'] / 1e6:.3f} MB per call")
     if "--json" in sys.argv:
         with open(sys.argv[sys.argv.index("--json") + 1], "w") as fh:
-            json.dump(out, fh, indent=1)
+            json.dump({**ent, "_kernels": out}, fh, indent=1)
 
 
 if __name__ == "__main__":
