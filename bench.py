@@ -408,6 +408,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--theta-form", default=None, help="θ-grad assembly form (ldsgnn.ops.THETA_GRAD_FORMS; "
                     "default: bf16x3, the split-bf16 MFMA form picked by shape)")
+    ap.add_argument("--sample-loop", type=int, default=None, help="1: the window's graphs loop inside each sampler "
+                    "tile block over one θ load (lds_sample_loop_graphs); 0: one block per (tile, graph)")
     ap.add_argument("--samples", type=int, default=1, help="Monte-Carlo replica samples per GPU, batched in "
                     "every launch (BASELINE configs 3/4); value is then sample-steps/s")
     ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
@@ -445,6 +447,9 @@ def main():
     from ldsgnn import ops as ldsops
     if args.theta_form is not None:
         ldsops.theta_grad_form(args.theta_form)
+    if args.sample_loop is not None:
+        from ldsgnn import _native as nat
+        nat.lib.lds_sample_loop_graphs(int(args.sample_loop))
     if args.model == "gcn":
         bench_gcn(args, world, rank, device, barrier_sync)
         if world > 1:

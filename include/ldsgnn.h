@@ -109,6 +109,11 @@ int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
 
 /* Workspace ints per graph of lds_sample_graphs_multi (the row degrees). */
 int lds_sample_ws_ints(int n);
+/* on = 1 (default): lds_sample_graphs_multi draws all `count` graphs of a
+ * call from one θ tile load per block (a loop over graphs in the block);
+ * 0: one block per (tile, graph) unless θ exceeds 64 MB; -1: query.  Returns
+ * the previous setting.  Process-wide, host-only. */
+int lds_sample_loop_graphs(int on);
 
 /* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
  * b < samples, is draw counter *counter_base + counter_offset + g with tag

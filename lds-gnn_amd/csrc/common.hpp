@@ -45,12 +45,16 @@ struct U32x4 {
 __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        // (a v_mad_u64_u32 form was 1.31x faster in isolation,
-        // tools/microbench/philox_rate.hip, but slower inside the sampler)
-        const uint32_t lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
-        const uint32_t lo1 = 0xCD9E8D57u * c.z;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
+        // one v_mad_u64_u32 per 32x32->64 product instead of v_mul_lo_u32 +
+        // v_mul_hi_u32 (both quarter rate); non-volatile asm so the four quads
+        // of a thread still interleave
+        uint64_t p0, p1, cc0, cc1;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p0), "=s"(cc0) : "s"(0xD2511F53u), "v"(c.x));
+        asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p1), "=s"(cc1) : "s"(0xCD9E8D57u), "v"(c.z));
+        (void)cc0;
+        (void)cc1;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         c = U32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -86,6 +90,37 @@ __device__ __forceinline__ float inv_sqrt_degree(int d) {
 }
 
 __device__ __forceinline__ int wave_lane() { return threadIdx.x & (kWave - 1); }
+// The wave's index in its block, as a wave-uniform (SGPR) value: the compiler
+// cannot prove threadIdx.x >> 6 uniform, and everything derived from it (row
+// indices, row offsets, 64-bit addresses, branches) would otherwise run
+// per lane on the VALU under exec masks.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// 64-lane integer sum and inclusive scan on the VALU: DPP within 16-lane rows
+// (row_ror / row_shr), row_bcast15/31 or v_permlane16/32_swap across rows —
+// no LDS-crossbar round trips (the __shfl forms cost ~100 cycles per hop).
+template <int CTRL>
+__device__ __forceinline__ int dpp_int(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true); }
+__device__ __forceinline__ int wave_sum_int(int v) {
+    v += dpp_int<0x128>(v);  // row_ror:8, 4, 2, 1: every lane of a row holds the row's sum
+    v += dpp_int<0x124>(v);
+    v += dpp_int<0x122>(v);
+    v += dpp_int<0x121>(v);
+    auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    v += (int)((threadIdx.x & 16) ? r[0] : r[1]);
+    r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    v += (int)((threadIdx.x & 32) ? r[0] : r[1]);
+    return v;
+}
+__device__ __forceinline__ int wave_incl_scan_int(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1, 2, 4, 8 (0 past the row start)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+    return v;
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

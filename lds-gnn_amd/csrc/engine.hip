@@ -190,7 +190,7 @@ __device__ __forceinline__ RowSel select_row(int n, const int* __restrict__ rp, 
                                              const Batch& bt) {
     RowSel r;
     r.e = make_int2(0, 0);
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int nlight = (n + W - 1) / W;
     r.heavy = (int)blockIdx.x >= nlight;
     r.step = r.heavy ? 64 * W : 64;
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc, Batch bt) {
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int row = blockIdx.x * 4 + wave_id();
     if (row >= n) return;
     xval = boff<kB>(xval, bt.xval);
     wt = boff<kB>(wt, bt.par);
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void bwd_layer1_kernel(
     const float* __restrict__ h0, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
+    const int row = blockIdx.x * 4 + wave_id();  // one wave per row (agg_row)
     if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     const float g = agg_row(rp, col, s, ell, dy0, row, lane);
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(256) void rev_d_kernel(
     float* __restrict__ h0bar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff) {
     const int lane = threadIdx.x & (HID - 1);
-    const int row = (blockIdx.x * 256 + threadIdx.x) >> 6;  // one wave per row (agg_row)
+    const int row = blockIdx.x * 4 + wave_id();  // one wave per row (agg_row)
     if (row >= n) return;
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     const int ix = row * HID + lane;
@@ -1033,7 +1033,7 @@ __device__ __forceinline__ void for_masked(const RowSel& r, const int* __restric
     if (r.row < 0) return;
     const int t = threadIdx.x & 63;
     const int g = t >> 4;
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int nw = r.heavy ? W : 1;                  // waves sharing the row
     const int slot = (r.heavy ? wave : 0) * 4 + g;   // this group's pick in each round
     const int beg = r.heavy ? r.first - 64 * wave : r.first;
@@ -1458,7 +1458,7 @@ __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1
     __shared__ float vec[16][6][HID];
     __shared__ float sca[16][2];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     if (lane < HID) {
         vec[wave][0][lane] = valid ? av1 : 0.f;
         vec[wave][1][lane] = valid ? bh1 : 0.f;
@@ -1733,7 +1733,7 @@ __global__ __launch_bounds__(256) void xt_partials_kernel(
     d = boff<kB>(d, bt.act);
     bkeys<kB>(keys, bt);
     if (kB) part += (int64_t)blockIdx.y * splits * fin * HID;
-    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6;   // f·splits + p
+    const int w = blockIdx.x * 4 + wave_id();   // f·splits + p
     if (w >= fin * splits) return;
     const int f = w / splits, p = w - f * splits;
     const int beg = xcp[f], end = xcp[f + 1];
@@ -1779,7 +1779,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
         final_block_1024(fin_args, adam, sc);
         return;
     }
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     const int lane = threadIdx.x & 63;
     const bool heavy = (int)blockIdx.x < n_heavy;
     int f, beg, end;

@@ -18,19 +18,20 @@ namespace lds {
 // owns column j = 64*bj + l; wave w owns the tile's rows 16w .. 16w+15 and
 // issues all 16 of its θ loads (each a coalesced 256-B row segment) before any
 // compute, then draws four Philox quads (one call = four rows' uniforms of a
-// column).  Row words come out of __ballot; the transposed (lower-triangle)
-// words collect one bit per row in each lane and are OR-combined across the
-// four waves in LDS.  Every word of `bits` has exactly one writer: no atomics,
+// column; the four chains interleave) and compares them as integers.  Row
+// words come out of __ballot (lane r keeps row r's word: one store per wave);
+// the transposed (lower-triangle) words collect one bit per row in each lane
+// and are OR-combined across the four waves in LDS.  Every word of `bits` has exactly one writer: no atomics,
 // no memset.
 // Batched launches: grid.y = graph (counter + y), grid.z = replica sample (tag +
-// z·tag_step); bit matrix (y·samples + z) of the batch.  Measured
-// on MI355X (r01, 6 Cora graphs per window): drawing all graphs of a window
-// from one θ load inside the block (a loop over graphs) took 41-53 µs against
-// 35 µs here — the loop raised the kernel to 157 VGPRs (occupancy 3 vs 8), and
-// the θ re-read per graph is cheap (MALL-resident).  At config 5 (θ 800 MB,
-// far past the 256 MB MALL) the re-reads are the kernel's HBM traffic, so
-// there the loop runs over every (graph, sample) of the batch (kLoop with
-// `graphs` = count: 1.24 ms -> see DESIGN §4b for 6 graphs at N = 20 000).
+// z·tag_step); bit matrix (y·samples + z) of the batch.  kLoop: the block loops
+// over the (graph, sample) items of the launch on ONE θ tile load (θ read once
+// per window instead of once per graph; lds_sample_loop_graphs).  r01's form
+// of that loop took 157 VGPRs and lost to one block per graph; with the
+// integer-threshold compare and the single row-word store below it takes 69
+// and the loop is the faster form (31.0 µs, 21.9 MB fetched per Cora window of
+// 6 graphs, against 30.8 µs, 113.9 MB).  Philox-bound: 4 calls × 10 rounds of
+// two v_mad_u64_u32 per lane per item.
 //
 // kDeg: the tile also counts what it stores into the row degrees dacc[graph]
 // (integer atomics, no-return, one per non-zero word: about a dozen per row
@@ -44,7 +45,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
     uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs,
     int* __restrict__ dacc, int wsi) {
-    __shared__ uint64_t colpart[4][64];
+    __shared__ uint32_t colpart[4][64];  // wave w's column bits (rows 16w .. 16w+15 of the tile)
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
     // batched launches: graph blockIdx.y draws counter + blockIdx.y; replica
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const int nsamp = kLoop ? samples : (int)gridDim.z;
     (void)ntiles;
     const int lane = wave_lane();
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
     int a, b;
     tri_tile(tile, a, b);
     const int bi = b, bj = a;  // bi <= bj
@@ -71,10 +72,20 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
         const int i = r0 + r;
         th[r] = (i < j && j < n) ? theta[tri_index(i, j, nn)] : -1.0f;  // i < n follows
     }
+    // Edge (i, j) iff u < clamp(θ, 0, 1) (triu_values_to_symmetric_matrix,
+    // src/utils/graph.py:180; θ = -1 marks pairs outside the strict upper
+    // triangle).  With u = m·2^-24 (m = the Philox word >> 8, an integer) that
+    // is m < ceil(clamp(θ)·2^24) exactly (scaling by 2^24 is exact; m < T iff
+    // m < ceil T for an integer m and T >= 0): one integer compare per draw.
+    uint32_t thr[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        thr[r] = th[r] >= 0.0f ? (uint32_t)ceilf(fminf(th[r], 1.0f) * 16777216.0f) : 0u;
     // kLoop: items (graph blockIdx.y + g, sample z), g < graphs, g-major, over
     // this one θ tile load (graph blockIdx.y + g draws counter + g)
     const int z0 = kLoop ? 0 : (int)blockIdx.z;
     const int z1 = kLoop ? samples * graphs : z0 + 1;
+    const bool rvalid = lane < 16 && r0 + lane < n;  // lane r stores row r0 + r's word
 #pragma unroll 1
     for (int it = z0; it < z1; ++it) {
         const int gl = kLoop ? it / samples : 0;
@@ -84,52 +95,56 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
         const uint32_t tg = tag + (uint32_t)z * tag_step;
         uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
         int* __restrict__ da = kDeg ? dacc + ((int64_t)gidx * nsamp + z) * wsi : nullptr;
-        int rowpc = 0;  // kDeg: lane r's row count
-        uint64_t colword = 0;
+        // the draws of all 16 rows first: four independent Philox chains per lane
+        bool e[16];
+        if constexpr (kInj) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i0 = r0 + 4 * q;
-            float u[4];
-            if constexpr (kInj) {
+            for (int r = 0; r < 16; ++r) {
+                const int i = r0 + r;
+                const float u = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
+                e[r] = th[r] >= 0.0f && u < fminf(th[r], 1.0f);
+            }
+        } else {
+            uint32_t x[16];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = i0 + r;
-                    u[r] = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
-                }
-            } else {
-                philox_quad(k0, k1, tg, ctr, (uint32_t)j, (uint32_t)(i0 >> 2), u);
+            for (int q = 0; q < 4; ++q) {
+                const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)((r0 >> 2) + q), tg, ctr}, k0, k1);
+                x[4 * q] = o.x;
+                x[4 * q + 1] = o.y;
+                x[4 * q + 2] = o.z;
+                x[4 * q + 3] = o.w;
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = i0 + r;
-                const float t = th[4 * q + r];
-                // clamp(0, 1) as triu_values_to_symmetric_matrix (src/utils/graph.py:180);
-                // t = -1 marks pairs outside the strict upper triangle
-                const bool e = t >= 0.0f && u[r] < fminf(t, 1.0f);
-                const uint64_t w = __ballot(e);
-                if (i < n) {
-                    if (!diag_tile) {
-                        if (lane == 0) gb[(int64_t)i * words + bj] = w;
-                        if constexpr (kDeg) {
-                            const int pc = __popcll(w);
-                            if (lane == 4 * q + r) rowpc = pc;
-                        }
-                    } else if (lane == 0) {
-                        rowword[i - bi * 64] = w;
-                    }
+            for (int r = 0; r < 16; ++r) e[r] = (x[r] >> 8) < thr[r];
+        }
+        // row words out of ballots (lane r keeps row r's), column bits per lane
+        uint32_t row_lo = 0, row_hi = 0, cw = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint64_t w = __ballot(e[r]);
+            row_lo = lane == r ? (uint32_t)w : row_lo;
+            row_hi = lane == r ? (uint32_t)(w >> 32) : row_hi;
+            cw |= (uint32_t)e[r] << r;
+        }
+        const uint64_t myrow = ((uint64_t)row_hi << 32) | row_lo;
+        if (!diag_tile) {
+            if (rvalid) {
+                gb[(int64_t)(r0 + lane) * words + bj] = myrow;
+                if constexpr (kDeg) {  // row part of an off-diagonal tile (diagonal tiles: column part only)
+                    const int pc = __popcll(myrow);
+                    if (pc != 0) atomicAdd(&da[r0 + lane], pc);
                 }
-                if (e) colword |= 1ull << (i - bi * 64);
             }
+        } else if (rvalid) {
+            rowword[wave * 16 + lane] = myrow;
         }
-        if constexpr (kDeg) {  // row part of an off-diagonal tile (diagonal tiles: column part only)
-            if (lane < 16 && rowpc != 0) atomicAdd(&da[r0 + lane], rowpc);
-        }
-        colpart[wave][lane] = colword;
+        colpart[wave][lane] = cw;
         __syncthreads();
         if (wave == 0) {
             int pc = 0;
             if (j < n) {
-                uint64_t out = colpart[0][lane] | colpart[1][lane] | colpart[2][lane] | colpart[3][lane];
+                uint64_t out = (uint64_t)colpart[0][lane] | ((uint64_t)colpart[1][lane] << 16) |
+                               ((uint64_t)colpart[2][lane] << 32) | ((uint64_t)colpart[3][lane] << 48);
                 if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
                 gb[(int64_t)j * words + bi] = out;
                 pc = __popcll(out);
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
 __global__ __launch_bounds__(256) void degree_kernel(const uint64_t* __restrict__ bits, int n,
                                                       int words, int* __restrict__ deg,
                                                       float* __restrict__ s, int deg_stride) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int row = blockIdx.x * 4 + wave_id();
     if (row >= n) return;
     bits += (int64_t)blockIdx.y * n * words;  // batched: graph blockIdx.y
     deg += (int64_t)blockIdx.y * deg_stride;
@@ -215,7 +230,7 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
                                                         const float* __restrict__ s,
                                                         int2* __restrict__ ell,
                                                         const uint8_t* __restrict__ flags) {
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int row = blockIdx.x * 4 + wave_id();
     if (row >= n) return;
     bits += (int64_t)blockIdx.y * n * words;  // batched: graph blockIdx.y, col stride = capacity
     row_ptr += (int64_t)blockIdx.y * (n + 1);
@@ -290,8 +305,12 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
 // each row its CSR offset directly — the block's 256 threads sum the degrees
 // of all rows before its first row (one coalesced pass, a block reduction),
 // each wave adds its predecessors in the block — so no scan launch runs
-// between the draw and the fill.  Also writes row_ptr, s = deg^-1/2 and the
-// ELL head, whose s_j is computed here from deg[j] (inv_sqrt_degree).
+// between the draw and the fill.  Then one wave per row pops the row's bits
+// into col (no loads: the positions come from a wave scan of the words'
+// counts), keeping the first 64 columns in LDS; the ELL head is written last,
+// lane l for entry l, whose s_j = deg_j^-1/2 (inv_sqrt_degree) and flag byte
+// are one parallel load per lane (in the bit-popping loop they were a chain of
+// dependent loads per lane: 16 µs per 6-graph launch against 6.6 now).
 __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __restrict__ bits, int n, int words,
                                                               const int* __restrict__ dacc, int wsi,
                                                               int* __restrict__ row_ptr, int* __restrict__ col,
@@ -299,7 +318,8 @@ __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __r
                                                               int2* __restrict__ ell,
                                                               const uint8_t* __restrict__ flags) {
     __shared__ int red[4];
-    const int wave = threadIdx.x >> 6;
+    __shared__ int head[4][kEllWidth];
+    const int wave = wave_id();
     const int row0 = blockIdx.x * 4;
     const int row = row0 + wave;
     const int g = blockIdx.y;
@@ -309,73 +329,82 @@ __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __r
     col += (int64_t)g * capacity;
     s += (int64_t)g * n;
     const int lane = wave_lane();
+    const int nbw = (n + 63) / 64;
+    const bool live = row < n;
+    const uint64_t* rb_bits = bits + (int64_t)row * words;
+    // the row's own operands first (independent of the block prefix)
+    int deg = 0, pre = 0;
+    uint64_t word0 = 0;
+    if (live) {
+        deg = dacc[row];
+        for (int w = 0; w < wave; ++w) pre += dacc[row0 + w];
+        word0 = lane < nbw ? rb_bits[lane] : 0ull;
+    }
     int acc = 0;
     for (int r = threadIdx.x; r < row0; r += 256) acc += dacc[r];
-    acc = wave_sum(acc);
+    acc = wave_sum_int(acc);
     if (lane == 0) red[wave] = acc;
     __syncthreads();
-    if (row >= n) return;
-    int pre = red[0] + red[1] + red[2] + red[3];
-    for (int w = 0; w < wave; ++w) pre += dacc[row0 + w];
-    const int deg = dacc[row];
-    if (lane == 0) {  // (clamped: a workspace that was not zero on entry cannot send readers past col)
-        row_ptr[row] = (int)min((int64_t)pre, capacity);
-        if (row == n - 1) row_ptr[n] = (int)min((int64_t)pre + deg, capacity);
-        s[row] = inv_sqrt_degree(deg);
-    }
-    if (ell != nullptr) {
-        ell += ((int64_t)g * n + row) * kEllWidth;
-        if (lane < kEllWidth && lane >= deg) ell[lane] = make_int2(row, 0);  // padding: weight 0
-    }
-    const uint64_t* rb_bits = bits + (int64_t)row * words;
-    const int nbw = (n + 63) / 64;
-    int64_t base = pre;
-    if (deg < kDenseRowFill) {  // short rows: each lane pops its own word's bits
-        for (int w0 = 0; w0 < nbw; w0 += 64) {
-            const int w = w0 + lane;
-            uint64_t word = w < nbw ? rb_bits[w] : 0ull;
-            const int cnt = __popcll(word);
-            int incl = cnt;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o);
-                if (lane >= o) incl += v;
-            }
-            int64_t pos = base + (incl - cnt);
-            while (word) {
-                const int bit = __ffsll((unsigned long long)word) - 1;
-                const int j = w * 64 + bit;
-                if (pos < capacity) col[pos] = j;
-                if (ell != nullptr && pos - pre < kEllWidth)
-                    ell[pos - pre] = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
-                ++pos;
-                word &= word - 1;
-            }
-            base += __shfl(incl, 63);
+    pre += red[0] + red[1] + red[2] + red[3];
+    if (live) {
+        if (lane == 0) {  // (clamped: a workspace that was not zero on entry cannot send readers past col)
+            row_ptr[row] = (int)min((int64_t)pre, capacity);
+            if (row == n - 1) row_ptr[n] = (int)min((int64_t)pre + deg, capacity);
+            s[row] = inv_sqrt_degree(deg);
         }
-        return;
-    }
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int w0 = 0; w0 < nbw; w0 += 64) {
-        const int w = w0 + lane;
-        const uint64_t word = w < nbw ? rb_bits[w] : 0ull;
-        uint64_t nz = __ballot(word != 0ull);
-        while (nz) {
-            const int src = __ffsll((unsigned long long)nz) - 1;
-            nz &= nz - 1;
-            const uint32_t lo = __shfl((uint32_t)word, src), hi = __shfl((uint32_t)(word >> 32), src);
-            const uint64_t wd = ((uint64_t)hi << 32) | lo;
-            const bool set = (wd >> lane) & 1ull;
-            const int64_t pos = base + __popcll(wd & below);
-            if (set) {
-                const int j = (w0 + src) * 64 + lane;
-                if (pos < capacity) col[pos] = j;
-                if (ell != nullptr && pos - pre < kEllWidth)
-                    ell[pos - pre] = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+        int64_t base = pre;
+        if (deg < kDenseRowFill) {  // short rows: each lane pops its own word's bits
+            for (int w0 = 0; w0 < nbw; w0 += 64) {
+                const int w = w0 + lane;
+                uint64_t word = w0 == 0 ? word0 : (w < nbw ? rb_bits[w] : 0ull);
+                const int cnt = __popcll(word);
+                const int incl = wave_incl_scan_int(cnt);
+                int64_t pos = base + (incl - cnt);
+                while (word) {
+                    const int bit = __ffsll((unsigned long long)word) - 1;
+                    const int j = w * 64 + bit;
+                    if (pos < capacity) col[pos] = j;
+                    if (pos - pre < kEllWidth) head[wave][pos - pre] = j;
+                    ++pos;
+                    word &= word - 1;
+                }
+                base += __builtin_amdgcn_readlane(incl, 63);
             }
-            base += __popcll(wd);
+        } else {
+            const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+            for (int w0 = 0; w0 < nbw; w0 += 64) {
+                const int w = w0 + lane;
+                const uint64_t word = w0 == 0 ? word0 : (w < nbw ? rb_bits[w] : 0ull);
+                uint64_t nz = __ballot(word != 0ull);
+                while (nz) {
+                    const int src = __ffsll((unsigned long long)nz) - 1;
+                    nz &= nz - 1;
+                    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)word, src);
+                    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(word >> 32), src);
+                    const uint64_t wd = ((uint64_t)hi << 32) | lo;
+                    const bool set = (wd >> lane) & 1ull;
+                    const int64_t pos = base + __popcll(wd & below);
+                    if (set) {
+                        const int j = (w0 + src) * 64 + lane;
+                        if (pos < capacity) col[pos] = j;
+                        if (pos - pre < kEllWidth) head[wave][pos - pre] = j;
+                    }
+                    base += __popcll(wd);
+                }
+            }
         }
     }
+    if (ell == nullptr || !live) return;
+    // the wave's own head columns are in LDS (written by this wave only)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int2 e = make_int2(row, 0);  // padding: a valid index with weight 0
+    if (lane < deg) {
+        const int j = head[wave][lane];
+        e = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+    }
+    ell[((int64_t)g * n + row) * kEllWidth + lane] = e;
 }
 
 __global__ void csr_degree_scale_kernel(const int* __restrict__ row_ptr, int n,
@@ -500,6 +529,18 @@ extern "C" int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* 
 
 extern "C" int lds_sample_ws_ints(int n) { return n; }
 
+// 1 (default): the window's graphs loop inside the tile block over one θ
+// load; 0: one block per (tile, graph) unless θ is past the MALL.  Measured at
+// Cora (6 graphs per window): 31.0 µs / 21.9 MB fetched per launch looping
+// against 30.8 µs / 113.9 MB, bench 12.64k vs 12.60k steps/s.  Returns the
+// previous setting.
+static int g_sample_loop_graphs = 1;
+extern "C" int lds_sample_loop_graphs(int on) {
+    const int prev = g_sample_loop_graphs;
+    if (on >= 0) g_sample_loop_graphs = on ? 1 : 0;
+    return prev;
+}
+
 extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                                        uint32_t tag_step, const uint32_t* counter_base,
                                        uint32_t counter_offset, int count, int samples, uint64_t* bits,
@@ -530,8 +571,8 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
     // replica samples loop inside the block over one θ tile load; past the
     // MALL (θ > ~64 MB) the window's graphs join that loop too
     const bool big = (int64_t)n * (n + 1) / 2 * 4 > ((int64_t)64 << 20);
-    const int loop_graphs = big ? count : 1;
-    if (samples > 1 || (big && count > 1)) {
+    const int loop_graphs = (big || g_sample_loop_graphs) ? count : 1;
+    if (samples > 1 || (loop_graphs > 1 && count > 1)) {
         if (fused)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true>), dim3(ntiles, count / loop_graphs, 1),
                                dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
