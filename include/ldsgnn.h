@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 6
+#define LDS_ABI_VERSION 7
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -248,6 +248,20 @@ int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k,
 int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                       int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
                       int mode, const void* scalars, float gscale, void* stream);
+/* lds_theta_grad_ex on pre-split operands: every fp32 value x of U and V as
+ * its three truncation-split bf16 words x = hi + mid + lo (lds_split_planes
+ * makes them from fp32; the engine's factor producers write them directly),
+ * so the staging copies instead of splitting.  Chunk-major layout: columns
+ * 16c .. 16c+15 of row i are [hi ×16 | mid ×16 | lo ×16] (uint16) at offset
+ * (c·n + i)·48.  Same arithmetic and result bits as the fp32-operand form.
+ * k a multiple of 8 (columns past k in its last chunk are ignored), ld >= k
+ * bounds the chunks, up / vp 16-byte aligned. */
+int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k, const float* r,
+                          int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad, int mode,
+                          const void* scalars, float gscale, void* stream);
+/* The chunk-major split words of the first k columns of x (rows × ld fp32)
+ * into planes (ceil(k/16) chunks of rows × 48 uint16). */
+int lds_split_planes(const float* x, int rows, int ld, int k, uint16_t* planes, void* stream);
 /* Arithmetic form of every θ-gradient assembly above (process-wide; a
  * captured HIP graph keeps the form it was captured with):
  *   0 fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains);

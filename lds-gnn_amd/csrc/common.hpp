@@ -89,6 +89,19 @@ __device__ __forceinline__ float inv_sqrt_degree(int d) {
     return (float)__ddiv_rn(1.0, (double)sq);
 }
 
+// x = x0 + x1 + x2 as three bf16 words by truncation: x0 = the top 16 bits of
+// x, x1 those of the exact remainder x - x0, x2 those of what is left (the
+// split-bf16 θ-grad assembly, thetagrad.hip; pre-split planes hold these).
+__device__ __forceinline__ void split3_one(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const uint32_t b = __float_as_uint(x);
+    const float r = x - __uint_as_float(b & 0xffff0000u);
+    const uint32_t c = __float_as_uint(r);
+    const float q = r - __uint_as_float(c & 0xffff0000u);
+    h = (uint16_t)(b >> 16);
+    m = (uint16_t)(c >> 16);
+    l = (uint16_t)(__float_as_uint(q) >> 16);
+}
+
 __device__ __forceinline__ int wave_lane() { return threadIdx.x & (kWave - 1); }
 // The wave's index in its block, as a wave-uniform (SGPR) value: the compiler
 // cannot prove threadIdx.x >> 6 uniform, and everything derived from it (row

@@ -340,8 +340,19 @@ __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __r
         for (int w = 0; w < wave; ++w) pre += dacc[row0 + w];
         word0 = lane < nbw ? rb_bits[lane] : 0ull;
     }
+    // degrees of the rows before the block: 8 independent loads per thread
+    // per round (a plain strided loop waited on each load in turn)
     int acc = 0;
-    for (int r = threadIdx.x; r < row0; r += 256) acc += dacc[r];
+    for (int r0b = 0; r0b < row0; r0b += 8 * 256) {
+        int v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int r = r0b + q * 256 + (int)threadIdx.x;
+            v[q] = r < row0 ? dacc[r] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q];
+    }
     acc = wave_sum_int(acc);
     if (lane == 0) red[wave] = acc;
     __syncthreads();

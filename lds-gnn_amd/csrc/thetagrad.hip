@@ -388,6 +388,65 @@ __device__ __forceinline__ void bf3_load(const float* __restrict__ u, const floa
     }
 }
 
+// Pre-split operands (lds_theta_grad_planes): U and V carry the split3
+// words of every fp32 value (split once by whoever writes a column; staging
+// here is a plain copy instead of the ~14 VALU per MFMA of the split),
+// chunk-major: the 16-column chunk c of row i is [hi ×16 | mid ×16 | lo ×16]
+// (96 bytes) at uint16 offset (c·rows + i)·48, so the chunk of 64 (128)
+// consecutive rows a tile stages is one contiguous 6 (12) KB block that a wave
+// copies with fully coalesced 1 KB load instructions.  Measured at Cora S = 1
+// (k = 264, engine factors written pre-split): 42.8-45 µs per launch against
+// 40.7 for the fp32-operand staging, so the engine keeps fp32 factors.  The
+// 64-tile kernel is bound by LDS bandwidth, not by the split VALU: per
+// 16-wide chunk a block writes 24 KB and reads 48 KB of LDS for 48 MFMAs
+// (1.5 KB per 32-cycle MFMA against 128 B per cycle per CU; SQ_WAIT_INST_LDS
+// 15-23 % of wave cycles, MFMA busy ~22 %), the same in both forms.
+struct Planes {
+    const uint16_t* u;
+    const uint16_t* v;
+};
+
+__host__ __device__ __forceinline__ int64_t ci_at(int64_t i, int c, int p, int64_t rows) {
+    return ((int64_t)(c >> 4) * rows + i) * 48 + p * 16 + (c & 15);
+}
+
+// One wave copies NQ KB of chunk k0/16 starting at row r0 of an operand into
+// LDS planes 3a..3a+2 (rows of S dwords, planes of PL dwords): lane l holds
+// bytes 16m + 1024q of the block, m = 15l mod 64 — each load instruction
+// still reads one contiguous KB, and with planes 4 dwords past a multiple of
+// 64 banks every 16-lane group of the b128 LDS writes hits 64 distinct banks
+// (with m = l the writes were 3-way conflicted: 5·10^6 conflict cycles per
+// Cora launch); rows past n and half-chunks at or past k (k a multiple of 8)
+// load zeros.
+template <int NQ>
+struct CiCopy {
+    u32x4 x[NQ];
+};
+template <int NQ>
+__device__ __forceinline__ void ci_load(const uint16_t* __restrict__ op, int rows, int r0, int k, int k0,
+                                        CiCopy<NQ>& c) {
+    const int m = (15 * (threadIdx.x & 63)) & 63;
+    const uint16_t* blk = op + ((int64_t)(k0 >> 4) * rows + r0) * 48;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int o = 16 * m + 1024 * q;  // byte offset in the block
+        const int row = o / 96, half = (o % 32) >> 4;
+        const bool ok = r0 + row < rows && k0 + 8 * half < k;
+        c.x[q] = ok ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(blk) + o)
+                    : *reinterpret_cast<const u32x4*>(g_zero8);
+    }
+}
+template <int NQ, int S, int PL>
+__device__ __forceinline__ void ci_store(uint32_t* lds, int a, const CiCopy<NQ>& c) {
+    const int m = (15 * (threadIdx.x & 63)) & 63;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int o = 16 * m + 1024 * q;
+        const int row = o / 96, w = o % 96;
+        *reinterpret_cast<u32x4*>(lds + (3 * a + w / 32) * PL + row * S + 4 * ((w % 32) >> 4)) = c.x[q];
+    }
+}
+
 template <int KC>
 __device__ __forceinline__ void bf3_store(uint32_t* lds, const Bf3Stage<KC>& st) {
     constexpr int P = Bf3Stage<KC>::kPer;
@@ -443,13 +502,14 @@ __device__ __forceinline__ void grouped_tile(int L, int nb, int G, int& bi, int&
     bj = i + rem;
 }
 
-template <int KC, bool VEC>
+template <int KC, bool VEC, bool PRE = false, bool PART = true>
 __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
-    float gscale, int group, int per_xcd) {
-    constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane;
+    float gscale, int group, int per_xcd, Planes pl) {
+    // (pre-split copies: planes 4 dwords past a multiple of 64 banks, ci_store)
+    constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane + (PRE ? 4 : 0);
     __shared__ __attribute__((aligned(16))) uint32_t lds[12 * PL];
     __shared__ float Ri[kTile], Rj[kTile];
 
@@ -472,8 +532,24 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
 
     const int gi = i0 + (t >> 2), gj = j0 + (t >> 2);
     Bf3Stage<KC> st;
-    if (k > 0) bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, 0, st);
+    // pre-split: wave w copies operand w (U_I, V_I, U_J, V_J) of the chunk
+    // (one chunk in flight: two measured slower — more registers, and the
+    // kernel is bound by LDS bandwidth, ~1.5 KB of LDS traffic per MFMA)
+    CiCopy<6> cc;
+    const int cop = t >> 6;
+    const uint16_t* cbase = (cop & 1) ? pl.v : pl.u;
+    const int crow0 = cop < 2 ? i0 : j0;
+    const int nch = (k + KC - 1) / KC;
+    if (k > 0) {
+        if constexpr (PRE) {
+            ci_load<6>(cbase, n, crow0, k, 0, cc);
+        } else {
+            bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, 0, st);
+        }
+    }
 
+    // PART (modes 1, 3): the partial grad is read too — a template flag so
+    // the SGD-only launch (mode 2) keeps its 16 registers for the staging
     float th[16], part[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -481,7 +557,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
         const bool in = i < n && j < n && j >= i;
         const int64_t idx = in ? tri_index(i, i, nn) + (j - i) : 0;
         th[e] = (in && theta != nullptr) ? theta[idx] : 0.f;
-        part[e] = (in && (mode == 1 || mode == 3)) ? grad[idx] : 0.f;
+        part[e] = (PART && in && (mode == 1 || mode == 3)) ? grad[idx] : 0.f;
     }
 
     if (t < 2 * kTile) {
@@ -500,11 +576,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     // fragment offsets (dwords): row (wave's 32-row half + lane & 31), k-half 8·(lane >> 5)
     const int ra = (wr * 32 + (lane & 31)) * S + 4 * (lane >> 5);
     const int rb = (wc * 32 + (lane & 31)) * S + 4 * (lane >> 5);
-    for (int k0 = 0; k0 < k; k0 += KC) {
-        __syncthreads();
-        bf3_store<KC>(lds, st);
-        __syncthreads();
-        if (k0 + KC < k) bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, k0 + KC, st);
+    auto compute = [&](int k0) {
 #pragma unroll
         for (int kk = 0; kk < KC; kk += 16) {
             if (k0 + kk < k) {  // zero-filled past k: whole k-steps beyond it are skipped
@@ -535,6 +607,24 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc, 0, 0, 0);
             }
+        }
+    };
+    if constexpr (PRE) {
+        static_assert(!PRE || KC == 16, "pre-split staging: 16-wide k chunks");
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();
+            ci_store<6, S, PL>(lds, cop, cc);
+            __syncthreads();
+            if (c + 1 < nch) ci_load<6>(cbase, n, crow0, k, KC * (c + 1), cc);
+            compute(KC * c);
+        }
+    } else {
+        for (int k0 = 0; k0 < k; k0 += KC) {
+            __syncthreads();
+            bf3_store<KC>(lds, st);
+            __syncthreads();
+            if (k0 + KC < k) bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, k0 + KC, st);
+            compute(k0);
         }
     }
     __syncthreads();
@@ -582,7 +672,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kT2 = 128;
 constexpr int kS2 = 12;             // dwords per LDS row (8 data + 4 pad: 4 × odd)
-constexpr int kPL2 = kT2 * kS2;     // dwords per plane
+constexpr int kPL2 = kT2 * kS2;     // dwords per plane (pre-split copies: + 4, see ci_store)
 
 // Packed index of (i, j), i <= j, in 32-bit arithmetic (the epilogue's 64
 // index computations per lane are 64-bit multiplies otherwise).  i(2n - i + 1)
@@ -599,13 +689,14 @@ __device__ __forceinline__ int64_t tri_at_t(int i, int j, int64_t n) {
     }
 }
 
-template <bool VEC, bool SMALL = false>
+template <bool VEC, bool SMALL = false, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
-    float gscale, int group, int per_xcd) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[12 * kPL2];
+    float gscale, int group, int per_xcd, Planes pl) {
+    constexpr int kPL = kPL2 + (PRE ? 4 : 0);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[12 * kPL];
     __shared__ float Ri[kT2], Rj[kT2];
 
     const int nb = (n + kT2 - 1) / kT2;
@@ -657,8 +748,20 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
             }
         }
     };
-    if (k > 0) load(xa, 0);
-    if (k > 16) load(xb, 16);
+    // pre-split: wave w copies operand w (U_I, V_I, U_J, V_J) of the chunk: 12 KB
+    CiCopy<12> pa_, pb_;
+    const int cop = t >> 6;
+    const uint16_t* cbase = (cop & 1) ? pl.v : pl.u;
+    const int crow0 = cop < 2 ? i0 : j0;
+    auto pload = [&](CiCopy<12>& x, int k0) { ci_load<12>(cbase, n, crow0, k, k0, x); };
+    auto pstage = [&](const CiCopy<12>& x) { ci_store<12, kS2, kPL>(lds, cop, x); };
+    if constexpr (PRE) {
+        if (k > 0) pload(pa_, 0);
+        if (k > 16) pload(pb_, 16);
+    } else {
+        if (k > 0) load(xa, 0);
+        if (k > 16) load(xb, 16);
+    }
 
     if (t < 2 * kT2) {
         const int rr = t & (kT2 - 1);
@@ -687,9 +790,9 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
             uint32_t h[4], m[4], l[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) split3_pair(x[a][2 * q], x[a][2 * q + 1], h[q], m[q], l[q]);
-            *reinterpret_cast<u32x4*>(lds + (3 * a + 0) * kPL2 + soff) = u32x4{h[0], h[1], h[2], h[3]};
-            *reinterpret_cast<u32x4*>(lds + (3 * a + 1) * kPL2 + soff) = u32x4{m[0], m[1], m[2], m[3]};
-            *reinterpret_cast<u32x4*>(lds + (3 * a + 2) * kPL2 + soff) = u32x4{l[0], l[1], l[2], l[3]};
+            *reinterpret_cast<u32x4*>(lds + (3 * a + 0) * kPL + soff) = u32x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u32x4*>(lds + (3 * a + 1) * kPL + soff) = u32x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u32x4*>(lds + (3 * a + 2) * kPL + soff) = u32x4{l[0], l[1], l[2], l[3]};
         }
     };
     auto compute = [&]() {
@@ -699,10 +802,10 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
             bf16x8 fa[2][3], fb[2][3];
 #pragma unroll
             for (int s = 0; s < 3; ++s) {
-                fa[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pa + s) * kPL2 + ra0));
-                fa[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pa + s) * kPL2 + ra1));
-                fb[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pb + s) * kPL2 + rb0));
-                fb[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pb + s) * kPL2 + rb1));
+                fa[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pa + s) * kPL + ra0));
+                fa[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pa + s) * kPL + ra1));
+                fb[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pb + s) * kPL + rb0));
+                fb[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(lds + (pb + s) * kPL + rb1));
             }
 #pragma unroll
             for (int m = 0; m < 2; ++m)
@@ -721,15 +824,23 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     };
     for (int k0 = 0; k0 < k; k0 += 32) {
         __syncthreads();  // the previous chunk's fragment reads are done
-        stage(xa);
+        if constexpr (PRE) pstage(pa_);
+        else stage(xa);
         __syncthreads();
-        if (k0 + 32 < k) load(xa, k0 + 32);
+        if (k0 + 32 < k) {
+            if constexpr (PRE) pload(pa_, k0 + 32);
+            else load(xa, k0 + 32);
+        }
         compute();
         if (k0 + 16 >= k) break;
         __syncthreads();
-        stage(xb);
+        if constexpr (PRE) pstage(pb_);
+        else stage(xb);
         __syncthreads();
-        if (k0 + 48 < k) load(xb, k0 + 48);
+        if (k0 + 48 < k) {
+            if constexpr (PRE) pload(pb_, k0 + 48);
+            else load(xb, k0 + 48);
+        }
         compute();
     }
     // Epilogue: every θ (and partial-grad) operand of the wave's 64 outputs is
@@ -800,8 +911,11 @@ constexpr int kGroup = 8;
 
 static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const float* v, int ld, int k,
                               const float* r, int ldr, int nr, float* theta, int n, float* grad, int mode,
-                              const double* lr, int vec4, int ldrc, float gscale) {
+                              const double* lr, int vec4, int ldrc, float gscale,
+                              Planes pl = Planes{nullptr, nullptr}) {
     int form = g_theta_form;
+    const bool pre = pl.u != nullptr;
+    if (pre && (form == 0 || form == 3)) form = 6;  // pre-split: the 16-wide-chunk 64-tile or the 128-tile forms
     const int nb2 = (n + kT2 - 1) / kT2;
     const int nt2 = nb2 * (nb2 + 1) / 2;
     // by shape (tools/thetagrad_forms.py, MI355X): 64-tiles in XCD-grouped
@@ -818,28 +932,40 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
         const int grid = form != 4 ? 8 * per : nt2;
         const int grp = form != 4 ? kGroup : 0;
         const bool small = n <= 46340 && form != 7;
-        if (fast && small)
+        if (pre && small)
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS,
+                               grp, per, pl);
+        else if (pre)
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, false, true>), dim3(grid), dim3(256), 0, st,
+                               LDS_TG_ARGS, grp, per, pl);
+        else if (fast && small)
             hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp,
-                               per);
+                               per, pl);
         else if (fast)
             hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS,
-                               grp, per);
+                               grp, per, pl);
         else
             hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<false, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS,
-                               grp, per);
+                               grp, per, pl);
     } else if (form == 3) {
         if (fast)
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0);
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, true>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0, pl);
         else
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0);
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<32, false>), dim3(ntiles), dim3(256), 0, st, LDS_TG_ARGS, 0, 0, pl);
     } else if (form == 2 || form == 6) {
         const int per = (ntiles + 7) / 8;
         const int grid = form == 6 ? 8 * per : ntiles;
         const int grp = form == 6 ? kGroup : 0;
-        if (fast)
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
+        if (pre && (mode == 1 || mode == 3))
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, true, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS,
+                               grp, per, pl);
+        else if (pre)
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, true, false>), dim3(grid), dim3(256), 0, st,
+                               LDS_TG_ARGS, grp, per, pl);
+        else if (fast)
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per, pl);
         else
-            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per);
+            hipLaunchKernelGGL((theta_grad_bf3_kernel<16, false>), dim3(grid), dim3(256), 0, st, LDS_TG_ARGS, grp, per, pl);
 #undef LDS_TG_ARGS
     } else {
         hipLaunchKernelGGL(theta_grad_mfma_kernel, dim3(ntiles), dim3(256), 0, st, u, v, ld, k, r, ldr, nr,
@@ -992,6 +1118,47 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
     //  196 VGPRs and 66 KB LDS leave 2 waves per SIMD.  MFMA busy of this form
     //  at S = 16 is 63 % of the cycles at a 2.26 GHz DVFS clock, r01 PMC)
     launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k, const float* r,
+                                     int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad, int mode,
+                                     const void* scalars, float gscale, void* stream) {
+    LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
+    LDS_CHECK_ARG(k == 0 || (up != nullptr && vp != nullptr && ld >= k));
+    LDS_CHECK_ARG((k & 7) == 0);
+    LDS_CHECK_ARG(((((uintptr_t)up) | ((uintptr_t)vp)) & 15) == 0);
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
+    LDS_CHECK_ARG(mode < 2 ? grad != nullptr : (theta != nullptr && scalars != nullptr));
+    LDS_CHECK_ARG(mode != 3 || grad != nullptr);
+    const int nb = (n + kTile - 1) / kTile;
+    const int ntiles = nb * (nb + 1) / 2;
+    const double* lr = mode >= 2 ? reinterpret_cast<const double*>((const char*)scalars + 16) : nullptr;
+    launch_theta_grad(ntiles, (hipStream_t)stream, nullptr, nullptr, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr,
+                      1, ldr_col, gscale, Planes{up, vp});
+    LDS_RETURN_LAST_ERROR();
+}
+
+// x (rows × ld fp32, the first k columns) -> its chunk-major split3 words
+// (ci_at; ceil(k/16) chunks of rows × 48 uint16).
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ x, int rows, int ld, int k,
+                                                           uint16_t* __restrict__ planes) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)rows * k) return;
+    const int64_t i = e / k;
+    const int c = (int)(e - i * k);
+    uint16_t h, m, l;
+    split3_one(x[i * ld + c], h, m, l);
+    planes[ci_at(i, c, 0, rows)] = h;
+    planes[ci_at(i, c, 1, rows)] = m;
+    planes[ci_at(i, c, 2, rows)] = l;
+}
+
+extern "C" int lds_split_planes(const float* x, int rows, int ld, int k, uint16_t* planes, void* stream) {
+    LDS_CHECK_ARG(x && planes && rows > 0 && k > 0 && ld >= k);
+    const int64_t tot = (int64_t)rows * k;
+    hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                       rows, ld, k, planes);
     LDS_RETURN_LAST_ERROR();
 }
 

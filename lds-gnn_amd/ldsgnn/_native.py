@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -38,6 +38,8 @@ SIGNATURES = {
     "lds_sample_ws_ints": [c_int],
     "lds_sample_loop_graphs": [c_int],
     "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
+    "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
+    "lds_split_planes": [P, c_int, c_int, c_int, P, P],
     "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],

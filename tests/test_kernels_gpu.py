@@ -477,6 +477,48 @@ def test_theta_grad_forms_vs_dense(device, form, n, k, ld, mode):
         assert float((th.cpu().double() - want).abs().max()) < 1e-5
 
 
+@pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16-grouped", "bf16x3-t128-grouped", "bf16x3-t128-grouped-i64"])
+@pytest.mark.parametrize("n,k,mode", [(300, 264, 2), (2708, 264, 0), (700, 40, 3), (130, 8, 1)])
+def test_theta_grad_planes_bit_exact_vs_fp32_operands(device, form, n, k, mode):
+    """lds_theta_grad_planes on the split planes of U, V (lds_split_planes,
+    the words the engine's factor producers write) gives the same bits as
+    lds_theta_grad_ex on the fp32 operands: the split moves out of the kernel,
+    the arithmetic does not change."""
+    g = torch.Generator().manual_seed(n + k + mode)
+    ld = (k + 15) // 16 * 16 + 16
+    u = torch.randn(n, ld, generator=g).to(device)
+    v = (torch.randn(n, ld, generator=g) * 0.3).to(device)
+    r = torch.randn(2, n, generator=g).to(device)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    theta[::9] = -0.5
+    base = torch.randn(n * (n + 1) // 2, generator=g)
+    scal = torch.zeros(32, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(0.05)
+    st = nat.stream_of(torch.device(device))
+    up = torch.zeros(((ld + 15) // 16) * n * 48, dtype=torch.int16, device=device)
+    vp = torch.zeros_like(up)
+    nat.call("lds_split_planes", nat.ptr(u), n, ld, ld, nat.ptr(up), st)
+    nat.call("lds_split_planes", nat.ptr(v), n, ld, ld, nat.ptr(vp), st)
+    outs = []
+    prev = ops.theta_grad_form(form)
+    try:
+        for planes in (False, True):
+            th = theta.clone().to(device)
+            grad = base.clone().to(device)
+            if planes:
+                nat.call("lds_theta_grad_planes", nat.ptr(up), nat.ptr(vp), ld, k, nat.ptr(r), 1, n, 2,
+                         nat.ptr(th), n, nat.ptr(grad), mode, nat.ptr(scal), 1.0, st)
+            else:
+                nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
+                         nat.ptr(grad), mode, nat.ptr(scal), 1.0, st)
+            torch.cuda.synchronize()
+            outs.append((th.cpu(), grad.cpu()))
+    finally:
+        ops.theta_grad_form(prev)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_theta_grad_form_default_and_errors(device):
     assert ops.theta_grad_form() == "bf16x3"
     with pytest.raises(nat.NativeError):
