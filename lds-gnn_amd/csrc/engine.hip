@@ -293,6 +293,18 @@ __device__ __forceinline__ void emit_factor(float* __restrict__ U, float* __rest
     }
 }
 
+// emit_factor with R[row] loaded beforehand (ahead of the aggregation)
+__device__ __forceinline__ void emit_factor_pre(float* __restrict__ U, float* __restrict__ V, int ldk,
+                                                float* __restrict__ R, float rprev, int off, int width, int row,
+                                                int lane, float si, float g, float z, float y, float ag) {
+    const float d = gsum16(g * y + z * ag);
+    if (lane < width) {
+        U[(int64_t)row * ldk + off + lane] = si * g;
+        V[(int64_t)row * ldk + off + lane] = si * z;
+    }
+    if (lane == 0) R[row] = rprev + (-0.5f * si * si * d);
+}
+
 // ---------------------------------------------------------------------------
 // X-side products (X is CSR / CSC, dropout keyed per (node, feature))
 // ---------------------------------------------------------------------------
@@ -445,11 +457,17 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     w.b1 = boff<kB>(w.b1, bt.par);
     bkeys<kB>(keys, bt);
     const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    // the row's own operands (dropout draw, W1, b1) ahead of the aggregation
+    float dk = 1.f, b1l = 0.f, w1v[HID];
+    if (rsel.lead) {
+        if (train) dk = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, rsel.row, lane) < keep ? scale : 0.f;
+        b1l = lane < c ? w.b1[lane] : 0.f;
+#pragma unroll
+        for (int k = 0; k < HID; ++k) w1v[k] = k < c ? w.w1[k * HID + lane] : 0.f;
+    }
     const float y = agg_value<4, kAgg>(rsel, col, s, ell, h0, agg);
     if (!rsel.lead) return;
     const int row = rsel.row;
-    const float dk = train ? (u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? scale : 0.f)
-                           : 1.f;
     float hd = fmaxf(y, 0.f);
     if (train) hd = dk != 0.f ? hd * scale : 0.f;
     if (g0) {
@@ -460,10 +478,9 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     // ReLU + dropout Jacobian reads instead of redrawing it
     if (dmask != nullptr && g0) dmask[row * HID + lane] = y > 0.f ? dk : 0.f;
     float out = 0.f;
-    for (int k = 0; k < c; ++k) {
-        const float t = gsum16(hd * w.w1[k * HID + lane]);
-        if (lane == k) out = t + w.b1[k];
-    }
+#define LDS_W(K) if (K < c) { const float t = gsum16(hd * w1v[K]); if (lane == K) out = t + b1l; }
+    LDS_R16(LDS_W)
+#undef LDS_W
     if (g0) h2[row * HID + lane] = out;
 }
 
@@ -799,30 +816,44 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
     const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
-    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh0bar, agg);  // dY0bar
-    if (!rsel.lead) return;
+    // the row's own operands ahead of the aggregation (their loads overlap it)
     const int row = rsel.row;
     const int ix = row * HID + lane;
-    if (g0) emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dh0bar[ix], dy0[ix], dh0[ix], ag);
-    float mask;
-    if (dmask != nullptr) {
-        mask = dmask[ix];
-    } else {
-        mask = y0[ix] > 0.f ? 1.f : 0.f;
-        if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+    float si = 0.f, rprev = 0.f, o_dh0bar = 0.f, o_dy0 = 0.f, o_dh0 = 0.f, mask = 0.f, hd = 0.f, g2 = 0.f, gb1l = 0.f;
+    float w1v[HID], gwv[HID];
+    if (rsel.lead) {
+        si = s[row];
+        rprev = R[row];
+        o_dh0bar = dh0bar[ix];
+        o_dy0 = dy0[ix];
+        o_dh0 = dh0[ix];
+        if (dmask != nullptr) {
+            mask = dmask[ix];
+        } else {
+            mask = y0[ix] > 0.f ? 1.f : 0.f;
+            if (train) mask = u_at(keys, keys.tag_h, sc->fwd_ctr + fwd_off, row, lane) < keep ? mask * scale : 0.f;
+        }
+        hd = h1d[ix];
+        g2 = dh2[ix];
+        gb1l = lane < c ? gb1bar[lane] : 0.f;
+#pragma unroll
+        for (int k = 0; k < HID; ++k) {
+            w1v[k] = k < c ? w.w1[k * HID + lane] : 0.f;
+            gwv[k] = k < c ? gw1bar[k * HID + lane] : 0.f;
+        }
     }
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh0bar, agg);  // dY0bar
+    if (!rsel.lead) return;
+    if (g0) emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_dh0bar, o_dy0, o_dh0, ag);
     const float a = ag * mask;  // dH1dbar
     if (g0) dh1dbar[ix] = a;
-    const float hd = h1d[ix];
     float out = 0.f;
-    for (int k = 0; k < c; ++k) {
-        const float t = gsum16(a * w.w1[k * HID + lane] + hd * gw1bar[k * HID + lane]);
-        if (lane == k) out = t + gb1bar[k];
-    }
+#define LDS_W(K) if (K < c) { const float t = gsum16(a * w1v[K] + hd * gwv[K]); if (lane == K) out = t + gb1l; }
+    LDS_R16(LDS_W)
+#undef LDS_W
     if (g0) dh2bar[ix] = out;
-    const float g2 = dh2[ix];
     float hb = 0.f;
-#define LDS_W(K) if (K < c) hb = fmaf(rbc_f<K>(g2), gw1bar[K * HID + lane], hb);
+#define LDS_W(K) if (K < c) hb = fmaf(rbc_f<K>(g2), gwv[K], hb);
     LDS_R16(LDS_W)
 #undef LDS_W
     if (g0) h1dbar[ix] = hb;
@@ -1523,21 +1554,28 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     const RowSel rsel = select_row<16, kAgg>(n, rp, ell, bt);
-    float g = agg_value<16, kAgg>(rsel, col, s, ell, dy0, agg);
     const bool valid = rsel.lead;
     const int row = rsel.row;
-    float a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f;
+    const int ix = row * HID + lane;
+    // the row's own operands ahead of the aggregation
+    float a1 = 0.f, b1 = 0.f, lr = 0.f, qr = 0.f, si = 0.f, rprev = 0.f, o_dy0 = 0.f, o_h0 = 0.f, o_y0 = 0.f;
     if (valid) {
-        const int ix = row * HID + lane;
-        if (g0) dh0[ix] = g;
         a1 = dh2[ix];
         b1 = h1d[ix];
         lr = lossrow[row];
         qr = corrrow[row];
+        if (U != nullptr) {
+            si = s[row];
+            rprev = R[row];
+            o_dy0 = dy0[ix];
+            o_h0 = h0[ix];
+            o_y0 = y0[ix];
+        }
     }
+    float g = agg_value<16, kAgg>(rsel, col, s, ell, dy0, agg);
+    if (valid && g0) dh0[ix] = g;
     if (U != nullptr && valid && g0)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
-        emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], dy0[row * HID + lane],
-                    h0[row * HID + lane], y0[row * HID + lane], g);
+        emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_dy0, o_h0, o_y0, g);
     block_reduce_1024(c, valid && g0, a1, b1, 0.f, 0.f, g, a1, lr, qr, partials);
 }
 
@@ -1572,20 +1610,26 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     const RowSel rsel = select_row<16, kAgg>(n, rp, ell, bt);
-    const float ag = agg_value<16, kAgg>(rsel, col, s, ell, y0bar, agg);
     const bool valid = rsel.lead;
     const int row = rsel.row;
-    float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f;
+    const int ix = row * HID + lane;
+    // the row's own operands ahead of the aggregation
+    float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f, si = 0.f, rprev = 0.f, o_y0bar = 0.f, o_h0 = 0.f, o_y0 = 0.f;
     if (valid) {
-        const int ix = row * HID + lane;
-        if (g0) {
-            emit_factor(U, V, ldk, R, foff, HID, row, lane, s[row], y0bar[ix], h0[ix], y0[ix], ag);
-            h0bar[ix] = ag;
-        }
         a1 = dh2[ix];
         b1 = dh1dbar[ix];
         a2 = h2bar[ix];
         b2 = h1d[ix];
+        si = s[row];
+        rprev = R[row];
+        o_y0bar = y0bar[ix];
+        o_h0 = h0[ix];
+        o_y0 = y0[ix];
+    }
+    const float ag = agg_value<16, kAgg>(rsel, col, s, ell, y0bar, agg);
+    if (valid && g0) {
+        emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_y0bar, o_h0, o_y0, ag);
+        h0bar[ix] = ag;
     }
     block_reduce_1024(c, valid && g0, a1, b1, a2, b2, ag, a2, 0.f, 0.f, partials);
 }
