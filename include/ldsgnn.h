@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 7
+#define LDS_ABI_VERSION 8
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -386,12 +386,18 @@ int lds_sample_bitmask_dev(const float* theta, int n, uint64_t seed, uint32_t ta
  * xd_csr != NULL the dropped values are also stored in CSR order, and when
  * xd_csc != NULL scattered to CSC order via csr2csc (position of each CSR entry
  * in the CSC arrays) — later products of the same step read them with
- * train = 0 instead of redrawing the mask. */
+ * train = 0 instead of redrawing the mask.  xhead != NULL: the rows' heads
+ * (built once per X) replace the row-pointer load: xinfo[row] = {p0, nnz}
+ * (int pairs), xhead[row] = the row's first 64 entries as {column, value bits}
+ * int pairs (zero-padded); head_vals = 1 takes the values from the head (X
+ * itself), 0 from xval[p0 + e] (e.g. the stored Xd); entries past 64 come
+ * from xcol / xval. */
 int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int n,
                         const float* wt, const float* bias, float* out, uint64_t seed,
                         uint32_t tag_x, const void* scalars, int fwd_off, int train,
                         float keep, float scale, float* xd_csr, float* xd_csc,
-                        const int* csr2csc, const LdsBatch* batch, void* stream);
+                        const int* csr2csc, const int* xhead, const int* xinfo, int head_vals,
+                        const LdsBatch* batch, void* stream);
 /* out[f][:] (+)= Σ_i dropout(X)[i][f] · d[i][:]  (+ wd · w)   (X in CSC). */
 int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int fin,
                          const float* d, float* out, const float* w, float wd,
@@ -556,7 +562,10 @@ int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int 
  * the column plan: the first n_heavy entries are the columns with more than
  * 128 entries, each run by a whole 1024-thread block (16 waves over its entry
  * range, partials summed in wave order), then every other column, one wave
- * each (n_heavy = 0 with xt_part). */
+ * each (n_heavy = 0 with xt_part).  xtinfo != NULL: per plan slot s,
+ * xtinfo[s] = {column, p0, nnz, 0} (int4) replaces order[s] -> xcp loads,
+ * and xthead[s] (64 ints, NULL allowed) holds the light column's first 64
+ * row indices (values from xval[p0 + e]). */
 int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int fin,
                        const float* d, float* out, int accumulate, uint64_t seed,
                        uint32_t tag_x, const void* scalars, int fwd_off, int train, float keep,
@@ -566,7 +575,7 @@ int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int f
                        float* v1, float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                        const double* hyper, const float* adam_tab, int n_wd, int step_off,
                        const float* xt_part, int xt_splits, const int* order, int n_heavy,
-                       const LdsBatch* batch, void* stream);
+                       const int* xtinfo, const int* xthead, const LdsBatch* batch, void* stream);
 /* Long X columns (dense X, config 5): Xdᵀ d over `splits` entry ranges of every
  * column, one wave each; part[s][p][f][16] per replica sample s (stride
  * splits·fin·16).  Feeds lds_engine_xt_adam's xt_part. */

@@ -135,6 +135,17 @@ __device__ __forceinline__ int wave_incl_scan_int(int v) {
     return v;
 }
 
+// Inclusive scan within each 16-lane row (DPP row_shr), and lane 15's value
+// of the row broadcast to the row (row_newbcast:15).
+__device__ __forceinline__ int row16_incl_scan_int(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    return v;
+}
+__device__ __forceinline__ int row16_last_int(int v) { return dpp_int<0x15F>(v); }
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -353,6 +353,82 @@ __device__ __forceinline__ float x_wave_dot_range(int beg, int end, const int* _
     return groups_sum(acc);
 }
 
+// The same over a row / column described by its HEAD (the engine builds one
+// per X, LdsEngine._x_heads): {p0, nnz} and the first 64 entries.  kHead 0:
+// {index, value bits} pairs, X's own values used; 1: the same pairs, values
+// from val[p0 + e] (e.g. the dropped Xd a training forward stored); 2: indices
+// only (int), values from val.  The head replaces the
+// dependent row-pointer load: entries and the gathers they index are the
+// only round trips up to 64 entries; entries past 64 come from the CSR /
+// CSC arrays as in x_wave_dot_range.
+template <bool kCsc, int kHead>
+__device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const int* __restrict__ head,
+                                                 const int* __restrict__ idx, const float* __restrict__ val,
+                                                 const float* __restrict__ src, const Keys& keys, uint32_t ctr,
+                                                 int train, float keep, float scale,
+                                                 float* __restrict__ xd_out = nullptr,
+                                                 float* __restrict__ xd_perm_out = nullptr,
+                                                 const int* __restrict__ perm = nullptr) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int q = (threadIdx.x >> 4) & 3;
+    float acc = 0.f;
+    {
+        const int e = 16 * q + lane;  // group q: head entries 16q .. 16q+15
+        const bool v = e < nnz;
+        int j;
+        float x;
+        if constexpr (kHead == 0) {
+            const int2 hv = reinterpret_cast<const int2*>(head)[e];
+            j = hv.x;
+            x = __int_as_float(hv.y);  // 0 past nnz
+        } else {
+            j = kHead == 1 ? reinterpret_cast<const int2*>(head)[e].x : head[e];
+            x = v ? val[p0 + e] : 0.f;
+        }
+        if (v) {
+            if (train) {
+                const int node = kCsc ? j : r, feat = kCsc ? r : j;
+                x = u_at(keys, keys.tag_x, ctr, node, feat) < keep ? x * scale : 0.f;
+            }
+            if (xd_out != nullptr) xd_out[p0 + e] = x;
+            if (xd_perm_out != nullptr) xd_perm_out[perm[p0 + e]] = x;
+        }
+        if (16 * q < nnz) {  // group-uniform: chunks past the row's end are skipped
+            float sk[HID];
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+            LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(x), sk[K], acc);
+            LDS_R16(LDS_F)
+#undef LDS_F
+        }
+    }
+    const int end = p0 + nnz;
+    for (int pb = p0 + 64 + q * HID; pb < end; pb += 4 * HID) {
+        const int p = pb + lane;
+        int j = 0;
+        float x = 0.f;
+        if (p < end) {
+            j = idx[p];
+            x = val[p];
+            if (train) {
+                const int node = kCsc ? j : r, feat = kCsc ? r : j;
+                x = u_at(keys, keys.tag_x, ctr, node, feat) < keep ? x * scale : 0.f;
+            }
+            if (xd_out != nullptr) xd_out[p] = x;
+            if (xd_perm_out != nullptr) xd_perm_out[perm[p]] = x;
+        }
+        float sk[HID];
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+        LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(x), sk[K], acc);
+        LDS_R16(LDS_F)
+#undef LDS_F
+    }
+    return groups_sum(acc);
+}
+
 template <bool kCsc>
 __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const int* __restrict__ idx,
                                             const float* __restrict__ val, int r,
@@ -372,7 +448,8 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
     const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
-    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc, Batch bt) {
+    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc,
+    const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
     const int row = blockIdx.x * 4 + wave_id();
     if (row >= n) return;
     xval = boff<kB>(xval, bt.xval);
@@ -383,9 +460,21 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
     xd_csc = boff<kB>(xd_csc, bt.xd);
     bkeys<kB>(keys, bt);
     const int lane = threadIdx.x & 63;
-    const float acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, sc->fwd_ctr + fwd_off, train, keep,
-                                        scale, xd_csr, xd_csc, csr2csc);
-    if (lane < HID) out[row * HID + lane] = bias != nullptr ? bias[lane] + acc : acc;
+    const float bl = (bias != nullptr && lane < HID) ? bias[lane] : 0.f;
+    const uint32_t ctr = sc->fwd_ctr + fwd_off;
+    float acc;
+    if (xhead != nullptr) {
+        const int2 inf = xinfo[row];  // {p0, nnz}
+        if (head_vals)  // X's own values from the head (forward)
+            acc = x_wave_dot_head<false, 0>(row, inf.x, inf.y, xhead + (int64_t)row * 128, xcol, xval, wt, keys,
+                                               ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
+        else            // values from xval (the Xd a training forward stored)
+            acc = x_wave_dot_head<false, 1>(row, inf.x, inf.y, xhead + (int64_t)row * 128, xcol, xval, wt,
+                                                keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
+    } else {
+        acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
+    }
+    if (lane < HID) out[row * HID + lane] = bl + acc;
 }
 
 // out[f][h] (= or +=) Σ_i Xd[i][f] · D[i][h]  (+ wd · w[f][h])   via CSC of X.
@@ -1801,7 +1890,8 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
     const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
     float keep, float scale, FinalArgs fin_args, AdamArgs adam, const float* __restrict__ xt_part,
-    int xt_splits, const int* __restrict__ order, int n_heavy, Batch bt) {
+    int xt_splits, const int* __restrict__ order, int n_heavy, const int4* __restrict__ xtinfo,
+    const int* __restrict__ xthead, Batch bt) {
     fin_args.partials = boff<kB>(fin_args.partials, bt.part);
     fin_args.dst = boff<kB>(fin_args.dst, bt.par);
     fin_args.metrics = boff<kB>(fin_args.metrics, bt.met);
@@ -1826,19 +1916,39 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
     const bool heavy = (int)blockIdx.x < n_heavy;
-    int f, beg, end;
+    // with the column heads (xtinfo[slot] = {f, p0, nnz}, slot = position in
+    // `order`) one load gives the column, its range and its first 64 rows;
+    // without them: order[slot] -> xcp[f] -> entries, two dependent loads first
+    int f, beg, end, slot;
     if (heavy) {
-        f = order[blockIdx.x];
-        const int cb = xcp[f], ce = xcp[f + 1];
+        slot = blockIdx.x;
+        int cb, ce;
+        if (xtinfo != nullptr) {
+            const int4 inf = xtinfo[slot];
+            f = inf.x;
+            cb = inf.y;
+            ce = inf.y + inf.z;
+        } else {
+            f = order[slot];
+            cb = xcp[f];
+            ce = xcp[f + 1];
+        }
         const int seg = ((ce - cb + 15) / 16 + 63) / 64 * 64;
         beg = min(ce, cb + wave * seg);
         end = min(ce, beg + seg);
     } else {
-        const int i = n_heavy + ((int)blockIdx.x - n_heavy) * 16 + wave;
-        if (i >= fin) return;  // light blocks never reach a barrier
-        f = order[i];
-        beg = xcp[f];
-        end = xcp[f + 1];
+        slot = n_heavy + ((int)blockIdx.x - n_heavy) * 16 + wave;
+        if (slot >= fin) return;  // light blocks never reach a barrier
+        if (xtinfo != nullptr) {
+            const int4 inf = xtinfo[slot];
+            f = inf.x;
+            beg = inf.y;
+            end = inf.y + inf.z;
+        } else {
+            f = order[slot];
+            beg = xcp[f];
+            end = xcp[f + 1];
+        }
     }
     const int idx = f * HID + (lane & (HID - 1));
     const bool owner = lane < HID && (!heavy || wave == 0);
@@ -1856,6 +1966,9 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
         if (kB) xt_part += (int64_t)blockIdx.y * xt_splits * fin * HID;
         if (lane < HID)
             for (int p = 0; p < xt_splits; ++p) acc += xt_part[((int64_t)p * fin + f) * HID + lane];
+    } else if (xthead != nullptr && !heavy) {
+        acc = x_wave_dot_head<true, 2>(f, beg, end - beg, xthead + (int64_t)slot * 64, xrow, xval, d, keys,
+                                       sc->fwd_ctr + fwd_off, train, keep, scale);
     } else {
         acc = x_wave_dot_range<true>(beg, end, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
     }
@@ -2001,14 +2114,17 @@ extern "C" int lds_engine_x_linear(const int* xrp, const int* xcol, const float*
                                    const float* wt, const float* bias, float* out, uint64_t seed,
                                    uint32_t tag_x, const void* scalars, int fwd_off, int train,
                                    float keep, float scale, float* xd_csr, float* xd_csc,
-                                   const int* csr2csc, const LdsBatch* batch, void* stream) {
+                                   const int* csr2csc, const int* xhead, const int* xinfo, int head_vals,
+                                   const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(xrp && xcol && xval && wt && out && scalars && n > 0 && batch_ok(batch));
     LDS_CHECK_ARG(xd_csc == nullptr || (xd_csr && csr2csc));
+    LDS_CHECK_ARG(xhead == nullptr || xinfo != nullptr);
     Batch bt;
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(x_linear_kernel, ns, dim3((n + 3) / 4, ns), dim3(256), 0, (hipStream_t)stream, xrp,
                        xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0),
-                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, bt);
+                       (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, xhead,
+                       (const int2*)xinfo, head_vals, bt);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -2336,8 +2452,9 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                                   float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                                   const double* hyper, const float* adam_tab, int n_wd, int step_off,
                                   const float* xt_part, int xt_splits, const int* order, int n_heavy,
-                                  const LdsBatch* batch, void* stream) {
+                                  const int* xtinfo, const int* xthead, const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && order && fin > 0 && batch_ok(batch));
+    LDS_CHECK_ARG(xthead == nullptr || xtinfo != nullptr);
     LDS_CHECK_ARG(n_heavy >= 0 && n_heavy <= fin && (xt_part == nullptr || n_heavy == 0));
     LDS_CHECK_ARG(partials == nullptr || (nblocks > 0 && c > 0 && c <= HID));
     LDS_CHECK_ARG(xt_part == nullptr || xt_splits > 0);
@@ -2351,7 +2468,7 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
     const int ns = mk_batch(batch, bt);
     LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(1024), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
-                       a, xt_part, xt_splits, order, n_heavy, bt);
+                       a, xt_part, xt_splits, order, n_heavy, (const int4*)xtinfo, xthead, bt);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -301,16 +301,69 @@ __global__ __launch_bounds__(256) void fill_csr_kernel(const uint64_t* __restric
     if (over && overflow != nullptr) *overflow = 1;
 }
 
+// One row of the fused fill with a whole wave (rows of kDenseRowFill or more
+// entries, or a wave that holds one): ascending columns into col from
+// position pre, the first 64 into head.
+__device__ __forceinline__ void fill_row_wave(const uint64_t* __restrict__ rb_bits, int nbw, int64_t pre, int deg,
+                                              int* __restrict__ col, int64_t capacity, int* __restrict__ head) {
+    const int lane = wave_lane();
+    int64_t base = pre;
+    if (deg < kDenseRowFill) {  // each lane pops its own word's bits
+        for (int w0 = 0; w0 < nbw; w0 += 64) {
+            const int w = w0 + lane;
+            uint64_t word = w < nbw ? rb_bits[w] : 0ull;
+            const int cnt = __popcll(word);
+            const int incl = wave_incl_scan_int(cnt);
+            int64_t pos = base + (incl - cnt);
+            while (word) {
+                const int bit = __ffsll((unsigned long long)word) - 1;
+                const int j = w * 64 + bit;
+                if (pos < capacity) col[pos] = j;
+                if (pos - pre < kEllWidth) head[pos - pre] = j;
+                ++pos;
+                word &= word - 1;
+            }
+            base += __builtin_amdgcn_readlane(incl, 63);
+        }
+        return;
+    }
+    // dense rows: for every non-zero word (uniform loop over a ballot) lane l
+    // tests bit l; the word's entries go out as one contiguous store
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int w0 = 0; w0 < nbw; w0 += 64) {
+        const int w = w0 + lane;
+        const uint64_t word = w < nbw ? rb_bits[w] : 0ull;
+        uint64_t nz = __ballot(word != 0ull);
+        while (nz) {
+            const int src = __ffsll((unsigned long long)nz) - 1;
+            nz &= nz - 1;
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)word, src);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(word >> 32), src);
+            const uint64_t wd = ((uint64_t)hi << 32) | lo;
+            const bool set = (wd >> lane) & 1ull;
+            const int64_t pos = base + __popcll(wd & below);
+            if (set) {
+                const int j = (w0 + src) * 64 + lane;
+                if (pos < capacity) col[pos] = j;
+                if (pos - pre < kEllWidth) head[pos - pre] = j;
+            }
+            base += __popcll(wd);
+        }
+    }
+}
+
 // The CSR fill of the fused sampler: the tile kernel's degree counts give
 // each row its CSR offset directly — the block's 256 threads sum the degrees
 // of all rows before its first row (one coalesced pass, a block reduction),
-// each wave adds its predecessors in the block — so no scan launch runs
-// between the draw and the fill.  Then one wave per row pops the row's bits
-// into col (no loads: the positions come from a wave scan of the words'
-// counts), keeping the first 64 columns in LDS; the ELL head is written last,
-// lane l for entry l, whose s_j = deg_j^-1/2 (inv_sqrt_degree) and flag byte
-// are one parallel load per lane (in the bit-popping loop they were a chain of
-// dependent loads per lane: 16 µs per 6-graph launch against 6.6 now).
+// the block's own 16 degrees are scanned in one 16-lane row — so no scan
+// launch runs between the draw and the fill.  A 16-lane group per row: lane
+// h pops the bits of words h, h+16, ... (positions from a 16-lane scan of
+// their counts), keeping the first 64 columns in LDS; the ELL head is
+// written last, four entries per lane, whose s_j = deg_j^-1/2
+// (inv_sqrt_degree) and flag byte are parallel loads.  A wave holding a row
+// of kDenseRowFill or more entries fills its four rows one at a time with the
+// whole wave instead.  (One wave per row: 11.2 µs per Cora window of 6
+// graphs; four rows per wave: see DESIGN.)
 __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __restrict__ bits, int n, int words,
                                                               const int* __restrict__ dacc, int wsi,
                                                               int* __restrict__ row_ptr, int* __restrict__ col,
@@ -318,30 +371,30 @@ __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __r
                                                               int2* __restrict__ ell,
                                                               const uint8_t* __restrict__ flags) {
     __shared__ int red[4];
-    __shared__ int head[4][kEllWidth];
+    __shared__ int dblk[16];  // exclusive scan of the block's 16 row degrees
+    __shared__ int head[16][kEllWidth];
     const int wave = wave_id();
-    const int row0 = blockIdx.x * 4;
-    const int row = row0 + wave;
+    const int lane = wave_lane();
+    const int h = lane & 15, k = wave * 4 + (lane >> 4);  // row k of the block (this lane's group)
+    const int row0 = blockIdx.x * 16;
+    const int row = row0 + k;
     const int g = blockIdx.y;
     bits += (int64_t)g * n * words;
     dacc += (int64_t)g * wsi;
     row_ptr += (int64_t)g * (n + 1);
     col += (int64_t)g * capacity;
     s += (int64_t)g * n;
-    const int lane = wave_lane();
     const int nbw = (n + 63) / 64;
     const bool live = row < n;
     const uint64_t* rb_bits = bits + (int64_t)row * words;
     // the row's own operands first (independent of the block prefix)
-    int deg = 0, pre = 0;
-    uint64_t word0 = 0;
-    if (live) {
-        deg = dacc[row];
-        for (int w = 0; w < wave; ++w) pre += dacc[row0 + w];
-        word0 = lane < nbw ? rb_bits[lane] : 0ull;
+    const int deg = live ? dacc[row] : 0;
+    const uint64_t word0 = (live && h < nbw) ? rb_bits[h] : 0ull;
+    if (wave == 0 && lane < 16) {
+        const int d = row0 + lane < n ? dacc[row0 + lane] : 0;
+        dblk[lane] = row16_incl_scan_int(d) - d;
     }
-    // degrees of the rows before the block: 8 independent loads per thread
-    // per round (a plain strided loop waited on each load in turn)
+    // degrees of the rows before the block: 8 independent loads per thread per round
     int acc = 0;
     for (int r0b = 0; r0b < row0; r0b += 8 * 256) {
         int v[8];
@@ -356,66 +409,56 @@ __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __r
     acc = wave_sum_int(acc);
     if (lane == 0) red[wave] = acc;
     __syncthreads();
-    pre += red[0] + red[1] + red[2] + red[3];
-    if (live) {
-        if (lane == 0) {  // (clamped: a workspace that was not zero on entry cannot send readers past col)
-            row_ptr[row] = (int)min((int64_t)pre, capacity);
-            if (row == n - 1) row_ptr[n] = (int)min((int64_t)pre + deg, capacity);
-            s[row] = inv_sqrt_degree(deg);
-        }
+    const int bpre = red[0] + red[1] + red[2] + red[3];
+    const int pre = bpre + dblk[k];
+    if (live && h == 0) {  // (clamped: a workspace that was not zero on entry cannot send readers past col)
+        row_ptr[row] = (int)min((int64_t)pre, capacity);
+        if (row == n - 1) row_ptr[n] = (int)min((int64_t)pre + deg, capacity);
+        s[row] = inv_sqrt_degree(deg);
+    }
+    if (__ballot(live && deg >= kDenseRowFill) == 0) {
         int64_t base = pre;
-        if (deg < kDenseRowFill) {  // short rows: each lane pops its own word's bits
-            for (int w0 = 0; w0 < nbw; w0 += 64) {
-                const int w = w0 + lane;
-                uint64_t word = w0 == 0 ? word0 : (w < nbw ? rb_bits[w] : 0ull);
-                const int cnt = __popcll(word);
-                const int incl = wave_incl_scan_int(cnt);
-                int64_t pos = base + (incl - cnt);
-                while (word) {
-                    const int bit = __ffsll((unsigned long long)word) - 1;
-                    const int j = w * 64 + bit;
-                    if (pos < capacity) col[pos] = j;
-                    if (pos - pre < kEllWidth) head[wave][pos - pre] = j;
-                    ++pos;
-                    word &= word - 1;
-                }
-                base += __builtin_amdgcn_readlane(incl, 63);
+        for (int w0 = 0; w0 < nbw; w0 += 16) {  // uniform: every group walks the same word count
+            const int w = w0 + h;
+            uint64_t word = w0 == 0 ? word0 : ((live && w < nbw) ? rb_bits[w] : 0ull);
+            const int cnt = __popcll(word);
+            const int incl = row16_incl_scan_int(cnt);
+            int64_t pos = base + (incl - cnt);
+            while (word) {
+                const int bit = __ffsll((unsigned long long)word) - 1;
+                const int j = w * 64 + bit;
+                if (pos < capacity) col[pos] = j;
+                if (pos - pre < kEllWidth) head[k][pos - pre] = j;
+                ++pos;
+                word &= word - 1;
             }
-        } else {
-            const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-            for (int w0 = 0; w0 < nbw; w0 += 64) {
-                const int w = w0 + lane;
-                const uint64_t word = w0 == 0 ? word0 : (w < nbw ? rb_bits[w] : 0ull);
-                uint64_t nz = __ballot(word != 0ull);
-                while (nz) {
-                    const int src = __ffsll((unsigned long long)nz) - 1;
-                    nz &= nz - 1;
-                    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)word, src);
-                    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(word >> 32), src);
-                    const uint64_t wd = ((uint64_t)hi << 32) | lo;
-                    const bool set = (wd >> lane) & 1ull;
-                    const int64_t pos = base + __popcll(wd & below);
-                    if (set) {
-                        const int j = (w0 + src) * 64 + lane;
-                        if (pos < capacity) col[pos] = j;
-                        if (pos - pre < kEllWidth) head[wave][pos - pre] = j;
-                    }
-                    base += __popcll(wd);
-                }
-            }
+            base += row16_last_int(incl);
+        }
+    } else {
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {  // the wave's four rows, one at a time
+            const int kq = wave * 4 + q, rq = row0 + kq;
+            if (rq >= n) break;
+            fill_row_wave(bits + (int64_t)rq * words, nbw, (int64_t)bpre + dblk[kq], dacc[rq], col, capacity,
+                          head[kq]);
         }
     }
     if (ell == nullptr || !live) return;
-    // the wave's own head columns are in LDS (written by this wave only)
+    // the head columns of this wave's rows are in LDS (written by this wave only)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int2 e = make_int2(row, 0);  // padding: a valid index with weight 0
-    if (lane < deg) {
-        const int j = head[wave][lane];
-        e = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+    int2* __restrict__ er = ell + ((int64_t)g * n + row) * kEllWidth;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int e = h + 16 * m;
+        int2 v = make_int2(row, 0);  // padding: a valid index with weight 0
+        if (e < deg) {
+            const int j = head[k][e];
+            v = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+        }
+        er[e] = v;
     }
-    ell[((int64_t)g * n + row) * kEllWidth + lane] = e;
 }
 
 __global__ void csr_degree_scale_kernel(const int* __restrict__ row_ptr, int n,
@@ -609,7 +652,7 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
                            deg_ws, s, wsi);
         LDS_RETURN_LAST_ERROR();
     }
-    hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, bits, n, words,
+    hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 15) / 16, graphs), dim3(256), 0, st, bits, n, words,
                        (const int*)deg_ws, wsi, row_ptr, col, col_stride, s, (int2*)ell, node_flags);
     LDS_RETURN_LAST_ERROR();
 }

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -65,7 +65,7 @@ SIGNATURES = {
     "lds_engine_scalars_size": [],
     "lds_sample_bitmask_dev": [P, c_int, c_uint64, c_uint32, P, c_uint32, P, c_int, P],
     "lds_engine_x_linear": [P, P, P, c_int, P, P, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
-                            P, P, P, P, P],
+                            P, P, P, P, P, c_int, P, P],
     "lds_engine_xt_linear": [P, P, P, c_int, P, P, P, c_float, c_int, c_uint64, c_uint32, P, c_int, c_int,
                              c_float, c_float, P],
     "lds_engine_fwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,
@@ -93,7 +93,8 @@ SIGNATURES = {
                          P, P, P, P, P, P, c_int, P, c_int, P],
     "lds_engine_xt_adam": [P, P, P, c_int, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
                            P, c_int, c_int, c_int, c_int, c_int, P,
-                           c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, c_int, P, c_int, P, P],
+                           c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, c_int, P, c_int, P, P,
+                           P, P],
     "lds_engine_xt_partials": [P, P, P, c_int, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float, c_int, P,
                                P, P],
     "lds_engine_fwd2_bwd2": [P, P, P, P, c_int, P, c_int, P, P, P, P, P, c_float, P, P, c_int, P, P, P, P,

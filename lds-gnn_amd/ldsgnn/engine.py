@@ -163,6 +163,11 @@ class LdsEngine:
         order = torch.argsort(self.xcol.long() * n + rows)
         self.csr2csc = torch.empty(nnz, dtype=torch.int32, device=dev)
         self.csr2csc[order] = torch.arange(nnz, dtype=torch.int32, device=dev)
+        # row heads of X (lds_engine_x_linear xhead / xinfo): {p0, nnz} and the first 64 {column, value}
+        rp0 = self.xrp[:-1].long()
+        rnz = (self.xrp[1:] - self.xrp[:-1]).long()
+        self.xinfo = torch.stack([rp0, rnz], 1).to(torch.int32).contiguous()
+        self.xhead = self._head_of(rp0, rnz, self.xcol, self.xval)
         self.x_nnz = nnz if self.train_flag else 0
         # dense X (config 5: 20 000 entries per column): the W0 products run as
         # partial ranges of ~512 entries per wave instead of one wave per column
@@ -595,7 +600,7 @@ class LdsEngine:
         xd = (nat.ptr(sl.xd_csr), nat.ptr(sl.xd_csc), nat.ptr(self.csr2csc)) if keep_xd else (0, 0, 0)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
                  nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, train, self.keep, self.scale, *xd, bt, st)
+                 fwd_off, train, self.keep, self.scale, *xd, nat.ptr(self.xhead), nat.ptr(self.xinfo), 1, bt, st)
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
                  self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask),
@@ -625,6 +630,30 @@ class LdsEngine:
         idx = torch.arange(self.fin, device=self.dev)
         self.xt_order = torch.cat([idx[heavy], idx[~heavy]]).to(torch.int32).contiguous()
         self.xt_heavy = int(heavy.sum())
+        # column heads by plan slot (lds_engine_xt_adam xtinfo / xthead)
+        f = self.xt_order.long()
+        p0 = self.xcp[f].long()
+        nz = (self.xcp[f + 1] - self.xcp[f]).long()
+        self.xtinfo = torch.stack([f, p0, nz, torch.zeros_like(f)], 1).to(torch.int32).contiguous()
+        self.xthead = self._head_of(p0, nz, self.xrow, None)
+
+    @staticmethod
+    def _head_of(p0: torch.Tensor, nz: torch.Tensor, idx: torch.Tensor, val):
+        """The first 64 entries of every row of a CSR (row starts p0, lengths
+        nz): indices [rows, 64] int32, or {index, value bits} pairs
+        [rows, 64, 2] when `val` is given; zero past each row's end."""
+        e = torch.arange(64, device=p0.device)
+        ok = e[None, :] < nz[:, None]
+        pos = torch.where(ok, p0[:, None] + e[None, :], torch.zeros_like(p0)[:, None])
+        if idx.numel() == 0:
+            cols = torch.zeros(pos.shape, dtype=torch.int32, device=p0.device)
+            vals = torch.zeros(pos.shape, dtype=torch.float32, device=p0.device)
+        else:
+            cols = torch.where(ok, idx[pos].to(torch.int32), 0)
+            vals = torch.where(ok, val[pos], 0.0) if val is not None else None
+        if val is None:
+            return cols.to(torch.int32).contiguous()
+        return torch.stack([cols.to(torch.int32), vals.to(torch.float32).view(torch.int32)], 2).contiguous()
 
     def _xt_split(self, xcsc: torch.Tensor, d: torch.Tensor, fwd_off: int):
         """Long X columns: run the column products as xt_splits partial ranges
@@ -696,8 +725,8 @@ class LdsEngine:
         nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc),
                  self.fin, nat.ptr(sl.dh0), nat.ptr(gout), 0, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
-                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, *self._xt_split(xcsc, sl.dh0, fwd_off), self.btx,
-                 st)
+                 self.off_b1, nat.ptr(metrics_row), *adam, adam_t, *self._xt_split(xcsc, sl.dh0, fwd_off),
+                 nat.ptr(self.xtinfo), nat.ptr(self.xthead), self.btx, st)
 
     # ----------------------------------------------------------------- steps
     def _sample_batch(self, count: int):
@@ -855,7 +884,8 @@ class LdsEngine:
         xcsr, xcsc = self._xvals(sl)  # Xd of step t (no redraw: train = 0 below)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(xcsr), n,
                  nat.ptr(gw0t), nat.ptr(gb0), nat.ptr(self.dh0bar), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, 0, self.keep, self.scale, 0, 0, 0, self.btx, st)
+                 fwd_off, 0, self.keep, self.scale, 0, 0, 0, nat.ptr(self.xhead), nat.ptr(self.xinfo),
+                 1 if xcsr is self.xval else 0, self.btx, st)
         nat.call("lds_engine_rev_a", rp, cl, s, el, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
@@ -880,11 +910,14 @@ class LdsEngine:
                  nat.ptr(self.h0bar), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
                  nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), self._agg(g, self.y0bar), self.bt,
                  st)
-        adam = self._adam_args(2 if t else 0, t - 1 if t else 0)
+        if t == 0:  # W̄ of the window's first weights feeds nothing (only θ is trained): no W0 products
+            return
+        adam = self._adam_args(2, t - 1)
         nat.call("lds_engine_xt_adam", nat.ptr(self.xcp), nat.ptr(self.xrow), nat.ptr(xcsc), self.fin,
                  nat.ptr(self.h0bar), nat.ptr(self.wbar), 1, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
-                 self.off_b1, 0, *adam, t - 1, *self._xt_split(xcsc, self.h0bar, fwd_off), self.btx, st)
+                 self.off_b1, 0, *adam, t - 1, *self._xt_split(xcsc, self.h0bar, fwd_off), nat.ptr(self.xtinfo),
+                 nat.ptr(self.xthead), self.btx, st)
 
     # ------------------------------------------------------------- graphs
     # ------------------------------------------------------ per-step graphs

@@ -99,7 +99,7 @@ def main():
     if xt:
         a = xt[0]
         for label, b in (("as recorded", a), ("no final block", a[:14] + (0,) + a[15:]),
-                         ("no heavy columns", a[:-3] + (0,) + a[-2:])):
+                         ("no heavy columns, no heads", a[:-5] + (0, 0, 0) + a[-2:])):
             def chain(b=b):
                 for _ in range(args.k):
                     real("lds_engine_xt_adam", *cur(b))
