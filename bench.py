@@ -18,9 +18,9 @@ inner steps of all ranks ÷ max-over-ranks wall time.  The line also carries
 ranks, timed against rank 0 running all 64 alone on its GPU first.
 
 Also reported:
-  * `window`: per-entry-point GPU time of one τ-window (HIP events around
-    every launch in an eager pass of the same K steps), top entries with
-    their algorithmic bytes;
+  * `window`: per-entry-point GPU time of one τ-window: every C-ABI call of
+    one window replayed as a dependent chain of itself from a HIP graph (HIP
+    events on the launch stream), with algorithmic bytes / flops and rates;
   * `roofline`: the entry point with the most GPU time per window, against
     its bound (HBM for the memory kernels, MFMA for the θ-grad assembly);
   * `cpu_baseline`: the CPU oracle (dense PyTorch restatement of the
@@ -155,6 +155,8 @@ def algo_cost(name, eng, n_calls_per_window):
         return "hbm", S * (4 * (eng.fin + 1) + 8 * xnnz) + act + S * 28 * P + 4 * eng.nred * 304 * S
     if name in ("lds_engine_fwd_layer1", "lds_engine_rev_a", "lds_engine_rev_c"):
         return "hbm", graph + 5 * act
+    if name in ("lds_engine_fwd2_bwd2", "lds_engine_rev_bc"):  # two hops over one graph read
+        return "hbm", graph + 7 * act
     if name in ("lds_engine_fwd_layer2", "lds_engine_bwd_layer2", "lds_engine_rev_b"):
         return "hbm", graph + 4 * act
     if name in ("lds_engine_bwd1_reduce", "lds_engine_rev_d_reduce"):
@@ -181,31 +183,76 @@ def pmc_traffic(name, args):
     return rec["traffic_bytes"], os.path.relpath(PMC_RECORD, ROOT)
 
 
-def window_breakdown(eng, reducer, args, windows):
-    """HIP events around every launch of `windows` eager windows: per entry
-    point launches / µs per window, its algorithmic cost and rate."""
+def chain_us(fn, dev, k, reps=3):
+    """µs per launch of `fn` (one C-ABI call) as a dependent chain of k copies
+    captured in one HIP graph, timed with HIP events recorded on the stream
+    the graph is replayed on (the stream the kernels run on)."""
     from ldsgnn import _native as nat
-    nat.timer.enable_all()
-    run_engine_windows(eng, reducer, windows, args.tau, False)
-    summ = nat.timer.summary()
-    nat.timer.disable()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(k):
+                fn(nat.stream_of(dev))
+        g.replay()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(reps):
+            g.replay()
+        b.record(s)
+    b.synchronize()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    return 1000.0 * a.elapsed_time(b) / (reps * k)
+
+
+def window_breakdown(eng, reducer, args, device, k=20):
+    """Where one τ-window's GPU time goes.  The C-ABI calls of one eager
+    window are recorded; each recorded call is then replayed as a chain of k
+    dependent copies of itself from one HIP graph (HIP events around the
+    replays, on the launch stream), so a launch's time is its own duration plus
+    the dependent-launch gap it pays inside the real window too — not the
+    event-per-launch skew of timing small kernels eagerly.  Per entry point:
+    launches and µs per window, the average launch, its algorithmic cost and
+    rate.  Runs after every timed leg: the chains re-apply θ / Adam updates,
+    so the engine's state is not used afterwards."""
+    from ldsgnn import _native as nat
+    calls = []
+    real = nat.call
+
+    def rec(name, *a):
+        calls.append((name, a))
+        real(name, *a)
+
+    nat.call = rec
+    try:
+        run_engine_windows(eng, reducer, 1, args.tau, False)
+    finally:
+        nat.call = real
+    torch.cuda.synchronize()
+    per = {}
+    for name, a in calls:
+        if name == "lds_sample_graphs_multi":  # repeated draws clear their own workspace (ws_zeroed = 0)
+            a = a[:-2] + (0,) + a[-1:]
+        us = chain_us(lambda st, name=name, a=a: real(name, *(a[:-1] + (st,))), device, k)
+        per.setdefault(name, []).append(us)
     rows = []
-    for name, s in summ.items():
-        per_win = s["total_ms"] * 1000.0 / windows
-        calls = s["launches"] / windows
-        bound, cost = algo_cost(name, eng, calls)
-        row = {"entry": name, "launches_per_window": calls, "us_per_window": per_win, "avg_us": s["avg_us"],
+    for name, ts in per.items():
+        calls_w = len(ts)
+        avg = sum(ts) / calls_w
+        bound, cost = algo_cost(name, eng, calls_w)
+        row = {"entry": name, "launches_per_window": calls_w, "us_per_window": sum(ts), "avg_us": avg,
                "bound": bound}
         if cost:
             if bound == "mfma":
                 row["algorithmic_flop"] = cost
-                row["achieved_tflops"] = cost / (s["avg_us"] * 1e-6) / 1e12
+                row["achieved_tflops"] = cost / (avg * 1e-6) / 1e12
             else:
                 row["algorithmic_bytes"] = cost
-                row["achieved_GBs"] = cost / (s["avg_us"] * 1e-6) / 1e9
+                row["achieved_GBs"] = cost / (avg * 1e-6) / 1e9
         rows.append(row)
     rows.sort(key=lambda r: -r["us_per_window"])
-    return rows, summ
+    return rows, len(calls)
 
 
 def roofline_of(row, args):
@@ -526,12 +573,15 @@ def main():
     nnz = eng.sampled_nnz_mean() if use_engine else None
     roof, window = None, None
     if use_engine and not args.no_breakdown:
-        rows, summ = window_breakdown(eng, reducer, args, max(1, args.steps // args.tau))
+        rows, ncalls = window_breakdown(eng, reducer, args, device)
         total = sum(r["us_per_window"] for r in rows)
-        window = {"kernel_us_per_window": total,
-                  "launch_calls_per_window": sum(r["launches_per_window"] for r in rows),
-                  "wall_us_per_window": 1000.0 * elapsed / max(1, args.steps // args.tau),
-                  "top": [{k: v for k, v in r.items()} for r in rows[:4]]}
+        wall_win = 1000.0 * (steady["ms_per_step"] if steady else 1000.0 * elapsed / args.steps) * args.tau
+        window = {"method": "per-call dependent chains (20 copies, one HIP graph, HIP events on the launch stream)",
+                  "launch_calls_per_window": ncalls,
+                  "sum_of_launch_us_per_window": total,
+                  "replayed_window_us": wall_win,
+                  "entries": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+                              for r in rows]}
         roof = roofline_of(rows[0], args)
         roof["share_of_window"] = rows[0]["us_per_window"] / total if total else None
         theta_rows = [r for r in rows if r["bound"] == "mfma"]

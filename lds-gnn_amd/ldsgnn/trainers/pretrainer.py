@@ -73,7 +73,11 @@ class Pretrainer:
 
     def __init__(self, model, data, lr: float = 0.01, optimizer: str = "adam", patience: int = 20,
                  max_epochs: int = 400, generator: Optional[torch.Generator] = None,
-                 betas=(0.9, 0.999), eps: float = 1e-8):
+                 betas=(0.9, 0.999), eps: float = 1e-8, split: Optional[Dict[str, torch.Tensor]] = None):
+        """`split`: a precomputed edge split (split_edges' keys) instead of
+        drawing one from data.dense_adj — the reference's split is a
+        torch_geometric draw this repository cannot reproduce, so the golden
+        test hands both sides the same split."""
         assert optimizer.lower() in ["sgd", "adam"]
         if optimizer.lower() != "adam" or getattr(model, "directed", False):
             raise NotImplementedError("fused pre-training implements Adam on the undirected Bernoulli model")
@@ -82,7 +86,7 @@ class Pretrainer:
         nat.require_device(theta, "Pretrainer")
         self.n = n = model.num_nodes
         self.lr, self.betas, self.eps = float(lr), betas, float(eps)
-        self.split = split_edges(data.dense_adj, generator=generator)
+        self.split = dict(split) if split is not None else split_edges(data.dense_adj, generator=generator)
         self.train_bits = edges_to_bits(self.split["train_pos"], n, theta.device)
         t_sum = float(self.split["train_pos"].size(1))
         self.pos_weight = float(np.float32((n * n - t_sum) / t_sum))  # (numel - sum) / sum

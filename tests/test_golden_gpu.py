@@ -201,3 +201,39 @@ def test_hypergradient_cora_golden():
     assert np.isclose(np.sqrt((grad ** 2).sum()), g["grad_l2"], rtol=1e-5)
     th = gm.probs.detach().cpu().numpy()
     assert np.allclose(th[g["theta_idx"]], g["theta_val"], rtol=1e-5, atol=1e-7)
+
+
+def test_pretrainer_golden():
+    """θ pre-training against the reference's own Pretrainer.train /
+    train_step / evaluate (src/trainers/pretrainer.py:49-113; golden
+    `pretrainer`, make_golden.g_pretrainer): the same edge split and θ₀ (with
+    entries at and beyond the clamp bounds), Adam 0.01, patience 20, at most 30
+    epochs.  Per epoch: θ at 1e-5, the weighted BCE at 1e-5 relative, the
+    validation AUC / AP; then the epoch count (early stopping) and the test
+    metrics after the reference's best-state reload."""
+    from ldsgnn.trainers.pretrainer import Pretrainer
+    g = gold("pretrainer")
+    n = int(g["n"])
+    split = {k[len("split_"):]: torch.from_numpy(g[k]) for k in g.files if k.startswith("split_")}
+    model = BernoulliGraphModel(torch.zeros(n, n)).to(DEV)
+    with torch.no_grad():
+        model.probs.copy_(torch.from_numpy(g["theta0"]).to(DEV))
+    p = Pretrainer(model, None, lr=0.01, optimizer="adam", patience=int(g["patience"]),
+                   max_epochs=int(g["max_epochs"]), split=split)
+    thetas, losses = [], []
+    step = p.train_step
+
+    def spy(epoch):
+        losses.append(step(epoch))
+        thetas.append(model.probs.detach().cpu().clone())
+    p.train_step = spy
+    test = p.train()
+    assert len(thetas) == g["thetas"].shape[0]  # the same early-stopping epoch
+    for e, th in enumerate(thetas):
+        ref = torch.from_numpy(g["thetas"][e])
+        assert float((th - ref).abs().max()) < 1e-5, e
+        assert abs(losses[e] - float(g["losses"][e])) <= 1e-5 * abs(float(g["losses"][e])), e
+        h = p.history[e]
+        assert np.allclose([h["val_auc"], h["val_average_precision"]], g["val"][e], rtol=1e-6, atol=1e-7), e
+    assert torch.allclose(model.probs.detach().cpu(), torch.from_numpy(g["theta_final"]), rtol=0, atol=1e-5)
+    assert np.allclose([test["auc"], test["average_precision"]], g["test"], rtol=1e-6, atol=1e-7)

@@ -271,3 +271,21 @@ def test_hypergradient_cora_golden():
     assert np.isclose(np.sqrt((grad ** 2).sum()), g["grad_l2"], rtol=1e-5)
     th = prob.theta.detach().numpy()
     assert np.allclose(th[g["theta_idx"]], g["theta_val"], rtol=1e-5, atol=1e-7)
+
+
+def test_pretrain_epochs_golden():
+    """oracle.pretrain_epoch_dense + torch.optim.Adam against the reference's
+    own Pretrainer.train_step (golden `pretrainer`): θ after every epoch and
+    the epoch's weighted BCE, bit for bit (the same dense ops in the same
+    order on CPU)."""
+    g = gold("pretrainer")
+    n = int(g["n"])
+    tp = torch.from_numpy(g["split_train_pos"])
+    train_adj = torch.zeros(n, n)
+    train_adj[tp[0], tp[1]] = 1
+    theta = torch.nn.Parameter(torch.from_numpy(g["theta0"]).clone())
+    opt = torch.optim.Adam([theta], lr=0.01)
+    for e in range(g["thetas"].shape[0]):
+        loss = O.pretrain_epoch_dense(theta, train_adj, opt)
+        assert loss == float(g["losses"][e]), e
+        assert np.array_equal(theta.detach().numpy(), g["thetas"][e]), e

@@ -21,13 +21,16 @@ def load(path):
 
 # engine entry point -> the kernels one call of it dispatches (name substrings)
 ENTRY_KERNELS = {
-    "lds_sample_graphs_multi": ["sample_tiles_kernel", "degree_kernel", "scan_kernel", "fill_csr_kernel",
-                                "fill_csr_fused_kernel"],
+    # the window's batched draw: graphs looped in the tile kernel (kLoop, kDeg) + the fused fill
+    # (the single-graph <false, false, true> draws of the step-0 window are not this entry's launches)
+    "lds_sample_graphs_multi": ["lds::sample_tiles_kernel<false, true, true>", "lds::fill_csr_fused_kernel"],
     "lds_theta_grad_sgd": ["theta_grad"],
     "lds_engine_x_linear": ["x_linear_kernel"],
     "lds_engine_fwd_layer1": ["fwd_layer1_kernel"],
     "lds_engine_fwd_layer2": ["fwd_layer2_kernel"],
     "lds_engine_bwd_layer2": ["bwd_layer2_kernel"],
+    "lds_engine_fwd2_bwd2": ["fwd2_bwd2_kernel"],
+    "lds_engine_rev_bc": ["rev_bc_kernel"],
     "lds_engine_bwd1_reduce": ["bwd1_reduce_kernel"],
     "lds_engine_xt_adam": ["xt_adam_kernel"],
     "lds_engine_rev_a": ["rev_a_kernel"],
