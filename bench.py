@@ -165,7 +165,27 @@ def algo_cost(name, eng, n_calls_per_window):
         return "hbm", 12 * tri
     if name == "lds_engine_end_window":
         return "hbm", S * 24 * P
+    if name == "lds_aggregate_bitmask":  # int8 MFMA: 0/1 mask x 4 base-256 digits of s*Z, 16 features
+        chunks = (n + 511) // 512
+        return "mfma_i8", 2.0 * n * chunks * 512 * 16 * 4
+    if name == "lds_spmm_norm_blocked":
+        return "hbm", 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n
+    if name == "lds_engine_xt_partials":
+        return "hbm", 8 * xnnz + act
     return "hbm", 0
+
+
+def bitagg_hbm_bytes(n):
+    """Algorithmic HBM bytes of one lds_aggregate_bitmask call (csrc/bitagg.hip):
+    the mask, s and Z once, the int8 digits written once and read once (the
+    row groups' re-reads of them are tiling, served from L2 / MALL), the split
+    partials written and read once (none with one split), Y written."""
+    from ldsgnn import _native as nat
+    words = nat.lib.lds_bitmask_words(n)
+    chunks, groups = (n + 511) // 512, (n + 255) // 256
+    splits = max(1, min(chunks, 512 // groups))
+    part = 2 * splits * 64 * n if splits > 1 else 0
+    return 8 * n * words + 4 * n + 64 * n + 2 * chunks * 32768 + part + 64 * n
 
 
 def pmc_traffic(name, args):
@@ -244,7 +264,12 @@ def window_breakdown(eng, reducer, args, device, k=20):
         row = {"entry": name, "launches_per_window": calls_w, "us_per_window": sum(ts), "avg_us": avg,
                "bound": bound}
         if cost:
-            if bound == "mfma":
+            if bound == "mfma_i8":
+                row["algorithmic_int8_ops"] = cost
+                row["achieved_tops"] = cost / (avg * 1e-6) / 1e12
+                row["algorithmic_bytes"] = bitagg_hbm_bytes(eng.n)
+                row["achieved_GBs"] = row["algorithmic_bytes"] / (avg * 1e-6) / 1e9
+            elif bound == "mfma":
                 row["algorithmic_flop"] = cost
                 row["achieved_tflops"] = cost / (avg * 1e-6) / 1e12
             else:
@@ -256,7 +281,12 @@ def window_breakdown(eng, reducer, args, device, k=20):
 
 
 def roofline_of(row, args):
-    if row["bound"] == "mfma":
+    if row["bound"] == "mfma_i8":  # the config-5 bitmask aggregation: int8 MFMA, HBM fraction alongside
+        achieved = row["achieved_tops"]
+        roof = {"bound": "mfma", "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TOP/s (int8)",
+                "frac": achieved / INT8_PEAK_TOPS, "hbm_GBs": row["achieved_GBs"],
+                "hbm_frac": row["achieved_GBs"] / HBM_PEAK_GBS}
+    elif row["bound"] == "mfma":
         achieved = row["achieved_tflops"]
         from ldsgnn import ops as ldsops
         roof = {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -587,6 +617,10 @@ def main():
         theta_rows = [r for r in rows if r["bound"] == "mfma"]
         if theta_rows:
             window["theta_grad"] = roofline_of(theta_rows[0], args)
+        agg_rows = [r for r in rows if r["bound"] == "mfma_i8"]
+        if agg_rows:  # config 5: the bitmask aggregation, the dense-graph form of the north-star SpMM
+            window["bitmask_aggregation"] = roofline_of(agg_rows[0], args)
+            window["bitmask_aggregation"]["share_of_window"] = agg_rows[0]["us_per_window"] / total
 
     strong = None
     if use_engine and args.strong_total and not param_theta:

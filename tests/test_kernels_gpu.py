@@ -272,6 +272,27 @@ def test_bitmask_agg_vs_dense(device, n, high):
     assert torch.all(o[:, 16:] == 1.0)
 
 
+@pytest.mark.parametrize("n", [65, 1500, 3000])
+def test_bitmask_agg_repeatable_on_dirty_workspace(device, n):
+    """A workspace full of garbage and back-to-back calls give bit-identical
+    Y: one split (n = 65: y written by the main kernel) and several (the
+    split partials summed in fixed order by the final launch)."""
+    g = torch.Generator().manual_seed(n + 5)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n), track_grad=False)
+    z = torch.randn(n, 16, generator=g).to(device)
+    ws = torch.full((int(nat.lib.lds_bitmask_agg_ws_bytes(n)),), 0x7F, dtype=torch.uint8, device=device)
+    outs = []
+    for _ in range(3):
+        y = torch.empty(n, 16, device=device)
+        nat.call("lds_aggregate_bitmask", nat.ptr(graph.bits), graph.bits.size(1), nat.ptr(graph.s), n, nat.ptr(z),
+                 16, nat.ptr(y), 16, 0, nat.ptr(ws), nat.stream_of(z.device))
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ref = graph.normalized_dense().cpu().double() @ z.cpu().double()
+    assert float((outs[0].double() - ref).abs().max() / ref.abs().max()) < RTOL
+
+
 def test_pretrain_step_vs_oracle(device):
     """Fused pre-training epoch (weighted BCE + clamp/symmetrisation backward +
     Adam on packed θ, one launch) against the reference's dense restatement
