@@ -88,6 +88,7 @@ def build(args, rank, device, samples=None):
     else:  # the embedding / GAE models
         from ldsgnn.models.factory import GraphGenerativeModelFactory
         fac = GraphGenerativeModelFactory(data)
+        fac.gae_config = dict(fac.gae_config, dropout=args.gae_dropout)
         gm = fac.create(args.graph_model)
         opt = fac.optimizer(gm)
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -498,6 +499,8 @@ def main():
                     "for rehearsing several ranks on one device)")
     ap.add_argument("--graph-model", default="lds", choices=["lds", "embedding", "gae"],
                     help="graph generative model (embedding / gae: P from node embeddings)")
+    ap.add_argument("--gae-dropout", type=float, default=0.0, help="--graph-model gae: the proposal GCN's "
+                    "dropout (factory default 0; > 0 runs per-draw θ on the engine)")
     ap.add_argument("--path", default="engine", choices=["engine", "autograd"],
                     help="engine: fused HIP engine (HIP-graph replayed tau-windows); autograd: drop-in trainers")
     args = ap.parse_args()
@@ -551,7 +554,7 @@ def main():
         eng.hyper_step(grad_reducer=reducer)
         if param_theta:  # the model's outer step runs eagerly between graph A and graph B
             reducer = eng.outer_update
-        use_graph = not args.eager
+        use_graph = not args.eager and eng.theta_fn is None  # per-draw θ (GAE proposal dropout): eager windows
         if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
             eng.capture_window(args.tau, grad_reducer=reducer)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)

@@ -276,6 +276,10 @@ class LdsEngine:
         # whose θ is a function of its own parameters (the embedding model)
         # takes dθ, steps its optimizer and rewrites self.theta in place
         self.outer_update = None
+        # theta_fn(counter) -> θ of one draw (set_theta_fn): θ redrawn per
+        # sample, as a GAE proposal with dropout makes it (None: one θ)
+        self.theta_fn = None
+        self._fwd_of = {}  # inner step t -> the forward counter offset its classifier forward took
         # grad_reducer(grad): the default exchange of a hyper step (e.g. the
         # all-reduce mean of dθ over ranks, ldsgnn.replicas); when set, dθ is
         # written, reduced, then SGD + clamp runs (the assembly is not fused
@@ -554,9 +558,10 @@ class LdsEngine:
         self.pending_fwd = 0
 
     # --------------------------------------------------------------- pieces
-    def _sample(self, g: _Graph):
-        """Draw the next graph of every replica sample into `g`."""
-        nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
+    def _sample(self, g: _Graph, theta: torch.Tensor = None):
+        """Draw the next graph of every replica sample into `g` (from `theta`,
+        default self.theta)."""
+        nat.call("lds_sample_graphs_multi", nat.ptr(self.theta if theta is None else theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(g.bits), self.words,
                  nat.ptr(self.deg), nat.ptr(g.row_ptr), self._col_arg(g.col), self.cap, nat.ptr(g.s),
                  nat.ptr(g.ell), nat.ptr(self.nflag), 0, self._stream())
@@ -699,7 +704,7 @@ class LdsEngine:
         g = sl.g
         if outer_factors:
             base = self.t * self.kg
-            U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
+            U, V, R = nat.ptr(self.U), nat.ptr(self.V), self._r_of(self.t)
         else:
             base, U, V, R = 0, 0, 0, 0
         rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
@@ -753,11 +758,15 @@ class LdsEngine:
             self.metrics = torch.zeros((self.tau + 1, self.S, 2), dtype=torch.float32, device=self.dev)
             self._refresh_adam_table()  # entries for the new step offsets
         sl = self.slots[t]
-        if presampled:
+        if self.theta_fn is not None:
+            assert not presampled
+            self._sample_per_draw(sl.g, t)
+        elif presampled:
             self.pending_graph += 1
         else:
             self._sample(sl.g)
         fwd_off = self.pending_fwd
+        self._fwd_of[t] = fwd_off
         self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off,
                       loss_in_backward=True)
         self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False, 1, t,
@@ -782,7 +791,10 @@ class LdsEngine:
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
         out = self.outer
-        if presampled:
+        if self.theta_fn is not None:
+            assert not presampled
+            self._sample_per_draw(out.g, T)
+        elif presampled:
             self.pending_graph += 1
         else:
             self._sample(out.g)
@@ -795,6 +807,8 @@ class LdsEngine:
                        2 if T else 0, T - 1 if T else 0, mask_bit=2, inv_count=self.inv_opt)
         if self.train_flag:
             self.pending_fwd += 1
+        if self.theta_fn is not None:
+            return self._hyper_tail_per_draw(T, grad_reducer)
         split = self.split_theta_grad and T > 0
         if split and self.S > 1:
             raise NotImplementedError("split θ-grad assembly is single-sample only")
@@ -868,18 +882,91 @@ class LdsEngine:
         nat.call("lds_theta_grad", nat.ptr(self.U) + off, nat.ptr(self.V) + off, self.ldk, k, 0, 0, 0, 0, self.n,
                  nat.ptr(self.grad), accumulate, side.cuda_stream)
 
+    # ------------------------------------------------------- per-draw θ
+    def set_theta_fn(self, fn):
+        """θ as a function of the draw: every graph of a window is sampled
+        from its own θ_t = fn(counter_t), counter_t the forward counter the
+        model's own forward takes right before the draw (a GAE proposal GCN
+        with dropout: src/models/graph.py:167-186 runs once per sample()).  The
+        hyper step then assembles one dθ_t per draw (its factor columns and its
+        own R row) and hands the stack [T + 1, n(n+1)/2] to the reducer
+        (outer_update), which takes each through its own P_t.  Single sample,
+        eager windows."""
+        if self.S != 1:
+            raise NotImplementedError("per-draw θ is single-sample")
+        self.theta_fn = fn
+        self.theta_counters = {}
+
+    def take_forward_counter(self) -> int:
+        """The next forward counter (absolute), taken by a host-side forward
+        (per-draw θ: the model's statistics() in training mode)."""
+        c = int(self._i32[1].item()) + self.pending_fwd
+        self.pending_fwd += 1
+        return c
+
+    def _per_draw_bufs(self, count: int):
+        tri = self.theta.numel()
+        if getattr(self, "theta_g", None) is None or self.theta_g.size(0) < count:
+            self.theta_g = torch.zeros((count, tri), dtype=torch.float32, device=self.dev)
+            self.grad_g = torch.zeros((count, tri), dtype=torch.float32, device=self.dev)
+            self.Rg = torch.zeros((count, self.n), dtype=torch.float32, device=self.dev)
+
+    def _sample_per_draw(self, g: _Graph, slot: int):
+        """θ_slot = theta_fn(absolute forward counter), then the draw from it;
+        the model's forward takes that counter (pending_fwd += 1)."""
+        self._per_draw_bufs(max(slot + 1, self.tau + 1))
+        c = int(self._i32[1].item()) + self.pending_fwd  # device counter + this window's pending forwards
+        self.theta_g[slot].copy_(self.theta_fn(c))
+        self.theta_counters[slot] = c
+        self.pending_fwd += 1
+        self._sample(g, theta=self.theta_g[slot])
+
+    def _r_of(self, slot: int) -> int:
+        """R of the factors of graph `slot`: one shared vector, or (per-draw
+        θ) graph slot's own row."""
+        if self.theta_fn is None:
+            return nat.ptr(self.R)
+        return nat.ptr(self.Rg[slot])
+
+    def _hyper_tail_per_draw(self, T: int, grad_reducer):
+        """Hyper-step tail for per-draw θ: the reverse pass (each graph's
+        factors and R row), dθ_t per draw (its own columns: graph t < T at
+        [t·kg, (t+1)·kg), the outer graph at [T·kg, T·kg + 16 + cw)), the
+        reducer on the stack, then the detach."""
+        st, n = self._stream(), self.n
+        self.Rg[:T].zero_()  # inner graphs' rows accumulate (the outer row is assigned by its first emitter)
+        for t in range(T - 1, -1, -1):
+            self._reverse_step(t)
+        for t in range(T + 1):
+            k0, k = (t * self.kg, self.kg) if t < T else (T * self.kg, HID + self.cw)
+            nat.call("lds_theta_grad", nat.ptr(self.U) + 4 * k0, nat.ptr(self.V) + 4 * k0, self.ldk, k,
+                     nat.ptr(self.Rg[t]), 1, 1, 0, n, nat.ptr(self.grad_g[t]), 0, st)
+        grad_reducer(self.grad_g[:T + 1])
+        P = nat.ptr
+        wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
+        nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
+                 P(self.scalars), self.pending_graph, self.pending_fwd, T, 1, P(self.betas_dev), P(self.adam_tab),
+                 self._tab_count(), P(self.gbatch.deg), self.gbatch.deg.numel(), self.bt, st)
+        self._ws_clean = True
+        self.pending_graph = 0
+        self.pending_fwd = 0
+        self.t = 0
+        return self.metrics[self.tau]
+
     def _reverse_step(self, t: int):
         """Reverse of inner step t; gbar already holds ḡ of step t (from the
         Adam reverse fused into the previous stage).  Ends with the Adam
         reverse of step t-1 fused into the W̄ completion."""
         st, n, c = self._stream(), self.n, self.c
         sl, g = self.slots[t], self.slots[t].g
-        fwd_off = t if self.train_flag else 0  # forward counter of inner step t within the window
+        # forward counter of inner step t within the window (per-draw θ: a
+        # proposal forward precedes each classifier forward, so recorded)
+        fwd_off = (self._fwd_of[t] if self.theta_fn is not None else t) if self.train_flag else 0
         gw0t, gb0, gw1, gb1 = self._views(self.gbar)
         _, _, w1, _ = self._views(self.w[t])
         base = t * self.kg
         rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
-        U, V, R = nat.ptr(self.U), nat.ptr(self.V), nat.ptr(self.R)
+        U, V, R = nat.ptr(self.U), nat.ptr(self.V), self._r_of(t)
         tr = self.train_flag
         xcsr, xcsc = self._xvals(sl)  # Xd of step t (no redraw: train = 0 below)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(xcsr), n,
@@ -962,7 +1049,7 @@ class LdsEngine:
     def inner_step_graphed(self):
         """inner_step() from a per-position HIP graph (see _graphed); the
         first step at a new position grows the tape eagerly."""
-        if self.t >= len(self.slots):
+        if self.t >= len(self.slots) or self.theta_fn is not None:  # per-draw θ: host-side counters
             return self.inner_step()
         return self._graphed("inner", self.inner_step)
 
@@ -977,7 +1064,7 @@ class LdsEngine:
     def run_window(self, tau: int, grad_reducer=None):
         """τ inner steps followed by the hyper step.  A full window from a
         window start draws its τ+1 graphs in one batched launch set."""
-        batch = self.t == 0 and tau == self.tau and self.gbatch.count == tau + 1
+        batch = self.t == 0 and tau == self.tau and self.gbatch.count == tau + 1 and self.theta_fn is None
         if batch:
             self._sample_batch(tau + 1)
         for _ in range(tau):
@@ -994,6 +1081,9 @@ class LdsEngine:
         between the replays (the collective stays outside the captured work),
         graph B applies SGD + clamp and the detach."""
         assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
+        if self.theta_fn is not None:
+            raise NotImplementedError("per-draw θ (GAE proposal dropout) computes θ of each draw on the host "
+                                      "side's counters: run windows eagerly")
         if tau != self.tau:
             raise ValueError(f"engine was built for tau={self.tau}; capture that window length")
         if grad_reducer is None:

@@ -27,12 +27,10 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
     if isinstance(gm, PairwiseEmbeddingSampler):
         return _param_theta_engine(inner, outer, tau, generator, samples)
     if isinstance(gm, GraphProposalNetwork):
-        if gm.gcn.dropout != 0.0:  # P would be redrawn per sample: not fixed within a window
-            raise NotImplementedError("the GAE model runs on the engine with a dropout-free proposal GCN")
         return _param_theta_engine(inner, outer, tau, generator, samples)
     if not isinstance(gm, BernoulliGraphModel) or gm.directed:
         raise NotImplementedError("the fused engine implements the undirected LDS Bernoulli model, "
-                                  "the embedding model and the dropout-free GAE model")
+                                  "the embedding model and the GAE model")
     opt = outer.optimizer
     if len(opt.param_groups) != 1:
         raise NotImplementedError("one θ parameter group expected")
@@ -59,10 +57,21 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
 
 def _param_theta_engine(inner, outer, tau, generator, samples) -> LdsEngine:
     """Engine for a graph model whose θ is a function of its own parameters
-    (embedding, dropout-free GAE): θ = triu(P(params)), and the model's outer
-    step, by autograd through P, runs as LdsEngine.outer_update."""
+    (embedding, GAE): θ = triu(P(params)), and the model's outer step, by
+    autograd through P, runs as LdsEngine.outer_update.
+
+    A GAE proposal GCN with dropout makes every sample() a new P
+    (src/models/graph.py:167-186: the proposal forward runs in training mode
+    once per draw, src/trainers/bilevel.py:103-106, outer.py:61-63), so the
+    engine runs per-draw θ (LdsEngine.set_theta_fn): draw t of a window is
+    sampled from θ_t = triu(P) of the proposal forward at the forward counter
+    the drop-in's sample() would take (one before the classifier forward of
+    the same step), the hyper step assembles one dθ_t per draw, and the outer
+    step sums Σ_t ⟨triu(P_t), dθ_t⟩ through each draw's own P_t (same
+    dropout masks, same counters).  θ for evaluation is the eval-mode P."""
     import torch
 
+    from .models.graph import GraphProposalNetwork
     from .models.sampling import Sampler
     gm, gcn, data = outer.model, inner.model, inner.data
     if samples != 1:
@@ -77,19 +86,48 @@ def _param_theta_engine(inner, outer, tau, generator, samples) -> LdsEngine:
     iu = torch.triu_indices(n, n, device=data.x.device)
 
     def theta_of_model() -> torch.Tensor:
-        with torch.no_grad():
-            return gm.forward()[iu[0], iu[1]].contiguous()
+        # eval-mode P: what empirical_mean_loss samples from (src/utils/evaluation.py:66-72)
+        was = gm.training
+        gm.eval()
+        try:
+            with torch.no_grad():
+                return gm.forward()[iu[0], iu[1]].contiguous()
+        finally:
+            gm.train(was)
+
+    per_draw = isinstance(gm, GraphProposalNetwork) and gm.gcn.dropout != 0.0
 
     eng = LdsEngine(data.x, data.y, data.train_mask, outer.opt_mask, theta_of_model(), data.num_classes,
                     dropout=gcn.dropout, gcn_lr=inner.lr, gcn_wd=inner.weight_decay, outer_lr=0.0,
                     lr_decay=None, tau=tau, generator=generator or gcn.generator or _rng.default_generator,
                     params=inner.model_params, samples=1)
 
+    def proposal_at(counter: int, grad: bool) -> torch.Tensor:
+        """triu(P) of the proposal forward (training mode) at a forward counter."""
+        was = gm.training
+        gm.train()
+        try:
+            with torch.set_grad_enabled(grad):
+                p, _ = gm.calculate_edges_and_embeddings(dropout_counter=counter)
+            return p[iu[0], iu[1]]
+        finally:
+            gm.train(was)
+
+    if per_draw:
+        if (gm.gcn.generator or _rng.default_generator) is not eng.gen:
+            raise NotImplementedError("per-draw θ needs the proposal GCN and the engine on one generator "
+                                      "(one forward-counter sequence)")
+        eng.set_theta_fn(lambda counter: proposal_at(counter, False))
+
     def outer_update(grad: torch.Tensor) -> None:
         # OuterProblemTrainer.train_step (src/trainers/outer.py:57-87) from the backward on:
         # dθ -> E through P's upper triangle, optimizer, StepLR, projection
         outer.optimizer.zero_grad()
-        gm.forward()[iu[0], iu[1]].backward(grad)
+        if per_draw:  # grad: [draws, n(n+1)/2], draw t through its own P_t
+            for t in range(grad.size(0)):
+                (proposal_at(eng.theta_counters[t], True) * grad[t]).sum().backward()
+        else:
+            gm.forward()[iu[0], iu[1]].backward(grad)
         if outer.grad_reducer is not None:
             outer.grad_reducer(gm)
         outer.optimizer.step()
@@ -164,6 +202,7 @@ class FusedBilevelRunner:
                         ol, oa = eng.outer_metrics()
                         log("loss.outer", ol, step)
                         log("acc.outer", oa, step)
+                        self._log_model_statistics(eng, log, step)
                 step += 1
             self.inner_steps = step
             vl, va, tl, ta = eng.empirical_mean(inner_stop.model_params, self.n_samples_empirical_mean,
@@ -178,6 +217,17 @@ class FusedBilevelRunner:
             outer_stop.update(vl, model_params=[deepcopy(inner_stop.model_params), eng.theta])
         self.gcn_params, self.graph_state_dict = outer_stop.model_params
         eng.sync_generator()
+
+    def _log_model_statistics(self, eng, log, step):
+        """BilevelProblemRunner.hyper_opt_step logs the graph model's
+        statistics() after a hyper step (src/trainers/bilevel.py:117-120).  A
+        GAE proposal with dropout runs a training-mode forward there and takes
+        a forward counter, which the engine's sequence skips likewise (per-draw
+        θ); the other models' statistics draw nothing and are not logged here."""
+        if getattr(eng, "theta_fn", None) is None:
+            return
+        for name, value in self.outer_trainer.model.statistics(dropout_counter=eng.take_forward_counter()).items():
+            log(name, value, step)
 
     def evaluate(self):
         assert self.gcn_params is not None, "Models need to be trained before evaluation."

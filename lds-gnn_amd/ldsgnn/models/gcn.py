@@ -64,11 +64,14 @@ class MetaDenseGCN(MetaModule):
         self.layer_in.reset_weights()
         self.layer_out.reset_weights()
 
-    def _dropout_keys(self):
+    def _dropout_keys(self, counter: int = None):
+        """Keys of this forward's two dropout sites: the generator's next
+        forward counter, or `counter` when given (a replayed forward — the
+        fused engine's per-draw GAE proposals — takes no new counter)."""
         if not self.training or self.dropout == 0.0:
             return None, None
         gen = self.generator or _rng.default_generator
-        c = gen.next_forward()
+        c = gen.next_forward() if counter is None else int(counter)
         return gen.dropout_key(_rng.TAG_DROP_X, c), gen.dropout_key(_rng.TAG_DROP_H, c)
 
     def _drop(self, x, key):
@@ -76,7 +79,7 @@ class MetaDenseGCN(MetaModule):
             return x
         return keyed_dropout(x, self.dropout, key)  # HIP kernel; raises for CPU tensors
 
-    def forward_to_last_layer(self, node_features, dense_adj, params=None):
+    def forward_to_last_layer(self, node_features, dense_adj, params=None, dropout_counter: int = None):
         if isinstance(dense_adj, CsrGraph):
             if not self.normalize_adj:
                 raise NotImplementedError("hot-path graphs are normalised by construction "
@@ -87,7 +90,7 @@ class MetaDenseGCN(MetaModule):
             # CSR graph; anything else keeps the reference's dense semantics
             graph = fixed_graph(dense_adj)
             dense_adj = graph if graph is not None else normalize_adjacency_matrix(dense_adj)
-        kx, kh = self._dropout_keys()
+        kx, kh = self._dropout_keys(dropout_counter)
         embeddings = self._drop(node_features, kx)
         embeddings = F.relu(self.layer_in(embeddings, dense_adj, params=get_subdict(params, "layer_in")))
         embeddings = self._drop(embeddings, kh)

@@ -168,12 +168,15 @@ class GraphProposalNetwork(GraphGenerativeModel):
         self.adj_cached = None
         self.generator = generator
 
-    def forward(self, *args, return_embeddings: bool = False, **kwargs) -> Tensor:
-        new_adj, _ = self.calculate_edges_and_embeddings()
+    def forward(self, *args, return_embeddings: bool = False, dropout_counter: int = None, **kwargs) -> Tensor:
+        new_adj, _ = self.calculate_edges_and_embeddings(dropout_counter=dropout_counter)
         return new_adj
 
-    def calculate_edges_and_embeddings(self, *args, **kwargs):
-        new_embeddings = self.gcn.forward_to_last_layer(self.features, self.adj)
+    def calculate_edges_and_embeddings(self, *args, dropout_counter: int = None, **kwargs):
+        """`dropout_counter`: run the proposal GCN's dropout at that forward
+        counter instead of drawing the next one (the fused engine recomputes
+        the P of a draw it made, ldsgnn.fused)."""
+        new_embeddings = self.gcn.forward_to_last_layer(self.features, self.adj, dropout_counter=dropout_counter)
         if self.normalize_similarities:
             similarity_matrix = cosine_similarity(new_embeddings, new_embeddings)
         else:
@@ -199,9 +202,9 @@ class GraphProposalNetwork(GraphGenerativeModel):
             self.features = self.embeddings_cached
             self.adj = self.adj_cached
 
-    def statistics(self) -> Dict[str, float]:
+    def statistics(self, dropout_counter: int = None) -> Dict[str, float]:
         with torch.no_grad():
-            total = self.forward().sum().item()
+            total = self.forward(dropout_counter=dropout_counter).sum().item()
         return {"expected_num_edges": total, "percentage_edges_expected": total / self.n_edges,
                 "probs_factor": self.probs_factor.item(), "probs_bias": self.probs_bias.item()}
 

@@ -79,10 +79,10 @@ def build_product_embedding(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e
 
 
 def build_product_gae(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, lr_decay=0.99, seed=0,
-                      embedding_dim=8, device="cuda"):
-    """build_product with the GAE graph model (a dropout-free proposal GCN,
-    P = clamp(σ(a·E·Eᵀ + b), 0, 1); Adam on the GCN, SGD-rate on a, b as
-    src/models/factory.py:51-57 groups them)."""
+                      embedding_dim=8, device="cuda", proposal_dropout=0.0):
+    """build_product with the GAE graph model (proposal GCN with dropout
+    `proposal_dropout`, P = clamp(σ(a·E·Eᵀ + b), 0, 1); Adam on the GCN,
+    SGD-rate on a, b as src/models/factory.py:51-57 groups them)."""
     import ldsgnn
     from ldsgnn.models.gcn import MetaDenseGCN
     from ldsgnn.models.graph import GraphProposalNetwork
@@ -98,7 +98,7 @@ def build_product_gae(prob, hidden=16, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, lr
     torch.manual_seed(seed)
     gcn = MetaDenseGCN(data.num_features, hidden, data.num_classes, dropout=dropout).to(device)
     inner = InnerProblemTrainer(gcn, data, lr=gcn_lr, weight_decay=gcn_wd)
-    gm = GraphProposalNetwork(data.x, data.dense_adj, dropout=0.0, embedding_dim=embedding_dim).to(device)
+    gm = GraphProposalNetwork(data.x, data.dense_adj, dropout=proposal_dropout, embedding_dim=embedding_dim).to(device)
     opt = torch.optim.Adam([{"params": gm.gcn.parameters(), "weight_decay": 5e-4, "lr": 0.01},
                             {"params": [gm.probs_factor, gm.probs_bias], "lr": 0.01}])
     outer = OuterProblemTrainer(opt, data, prob["opt"].to(device), gm, lr_decay=lr_decay)

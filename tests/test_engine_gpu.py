@@ -347,11 +347,14 @@ def test_embedding_engine_graph_replay_equals_eager():
         assert torch.equal(v, b.get_params()[k]), k
 
 
-def test_fused_runner_gae_model_matches_dropin():
-    """The GAE graph model (dropout-free proposal GCN) on the fused engine:
-    the outer Adam step on the proposal GCN and the affine parameters by
-    autograd through P's upper triangle, against the drop-in runner: same
-    control flow, losses within 1e-4, same final proposal parameters."""
+@pytest.mark.parametrize("proposal_dropout", [0.0, 0.5])
+def test_fused_runner_gae_model_matches_dropin(proposal_dropout):
+    """The GAE graph model on the fused engine: the outer Adam step on the
+    proposal GCN and the affine parameters by autograd through P's upper
+    triangle, against the drop-in runner: same control flow, losses within
+    1e-4, same final proposal parameters.  With proposal dropout every draw
+    has its own P (per-draw θ: the proposal forward at the counter the
+    drop-in's sample() takes, dθ per draw back through its own P)."""
     from ldsgnn.fused import FusedBilevelRunner
     from tests.parity_harness import build_product_gae, synthetic_problem
     prob = synthetic_problem(96, 20, 3, 9, 0.08)
@@ -361,7 +364,7 @@ def test_fused_runner_gae_model_matches_dropin():
         return torch.cat([p.detach().reshape(-1) for p in gm.parameters()])
 
     def run(fused):
-        runner = build_product_gae(prob, dropout=0.5, seed=9)
+        runner = build_product_gae(prob, dropout=0.5, seed=9, proposal_dropout=proposal_dropout)
         init[fused] = flat(runner.outer_trainer.model).clone()
         if fused:
             runner = FusedBilevelRunner(runner.inner_trainer, runner.outer_trainer, runner.data,
