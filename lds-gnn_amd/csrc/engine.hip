@@ -1799,9 +1799,16 @@ __device__ __forceinline__ void final_pair(const FinalArgs& f, int e0, int e1, c
 // each summing a third of the first-stage blocks (in order), the thirds then
 // added in order through LDS; thread e < kRedLen completes element e (as
 // final_pair: dst, metrics, Adam).  With one wave per row the fused
-// reductions write ⌈n/16⌉ (+ heavy rows) partials, 187 at Cora.
+// reductions write ⌈n/16⌉ (+ heavy rows) partials, 187 at Cora.  A third is
+// summed as consecutive groups of 16 partials (a fixed pairwise tree each),
+// accumulated in order; kBatch (16 or 64) is how many are loaded per round
+// trip — the same sums either way.  The single-sample launch loads 64 at once
+// (its final block is on the critical path); the batched one 16, which keeps
+// xt_adam at 40 VGPRs instead of 86 (two 1024-thread blocks per CU, not one).
+template <int kBatch>
 __device__ __forceinline__ void final_block_1024(const FinalArgs& f, const AdamArgs& adam,
                                                  const EngineScalars* __restrict__ sc) {
+    static_assert(kBatch % 16 == 0 && kBatch <= kRedBlocks, "groups of 16");
     __shared__ float third[3][kRedLen];
     const int t = threadIdx.x;
     const int q = t / kRedLen, e = t - q * kRedLen;
@@ -1817,16 +1824,20 @@ __device__ __forceinline__ void final_block_1024(const FinalArgs& f, const AdamA
         const int per = (f.nblocks + 2) / 3;
         const int b0 = q * per, b1 = min(f.nblocks, b0 + per);
         float v = 0.f;
-        for (int c0 = b0; c0 < b1; c0 += kRedBlocks) {
-            float x[kRedBlocks];
+        for (int c0 = b0; c0 < b1; c0 += kBatch) {
+            float x[kBatch];
 #pragma unroll
-            for (int b = 0; b < kRedBlocks; ++b)
+            for (int b = 0; b < kBatch; ++b)
                 x[b] = c0 + b < b1 ? f.partials[(int64_t)(c0 + b) * kRedLen + e] : 0.f;
 #pragma unroll
-            for (int w = kRedBlocks / 2; w > 0; w >>= 1)
+            for (int g = 0; g < kBatch / 16; ++g) {
+                float* y = x + 16 * g;
 #pragma unroll
-                for (int b = 0; b < w; ++b) x[b] += x[b + w];
-            v += x[0];
+                for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+                    for (int b = 0; b < w; ++b) y[b] += y[b + w];
+                v += y[0];
+            }
         }
         third[q][e] = v;
     }
@@ -1910,7 +1921,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     d = boff<kB>(d, bt.act);
     bkeys<kB>(keys, bt);
     if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
-        final_block_1024(fin_args, adam, sc);
+        final_block_1024<kB ? 16 : 64>(fin_args, adam, sc);
         return;
     }
     const int wave = wave_id();

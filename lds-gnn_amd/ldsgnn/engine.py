@@ -631,7 +631,10 @@ class LdsEngine:
         than 128 entries first (a 1024-thread block each), then the rest (one
         wave each); with split products (xt_splits > 1) no heavy columns."""
         lens = (self.xcp[1:] - self.xcp[:-1]).long()
-        heavy = (lens > 128) if self.xt_splits <= 1 else torch.zeros_like(lens, dtype=torch.bool)
+        # batched samples keep every column one wave: the 1024-thread heavy
+        # blocks then only fragment the CU (measured 59.6 vs 73.4 µs per call,
+        # Citeseer S = 16); with one sample the long columns set the time
+        heavy = (lens > 128) if self.xt_splits <= 1 and self.S == 1 else torch.zeros_like(lens, dtype=torch.bool)
         idx = torch.arange(self.fin, device=self.dev)
         self.xt_order = torch.cat([idx[heavy], idx[~heavy]]).to(torch.int32).contiguous()
         self.xt_heavy = int(heavy.sum())
