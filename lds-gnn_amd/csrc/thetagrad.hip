@@ -447,11 +447,23 @@ __device__ __forceinline__ void ci_store(uint32_t* lds, int a, const CiCopy<NQ>&
     }
 }
 
+// Staging row of thread t.  KC = 16 (4 floats per thread and array, stored
+// as ds_write_b64: lane groups of 16, bank (a/4) mod 32): a group covers rows
+// {a, a+2, a+4, a+6} × the four k-quarters, whose 8-byte slots in 12-dword
+// rows hit 32 distinct banks (rows t >> 2 put a..a+3 in a group: 2-way
+// conflicts).  The four lanes of one row stay adjacent, so each row's 64 B
+// remain one contiguous global read.  KC = 32: row t >> 2.
+template <int KC>
+__device__ __forceinline__ int bf3_srow(int t) {
+    if constexpr (KC == 16) return 16 * (t >> 6) + ((t >> 4) & 1) + 2 * ((t >> 2) & 3) + 8 * ((t >> 5) & 1);
+    return t >> 2;
+}
+
 template <int KC>
 __device__ __forceinline__ void bf3_store(uint32_t* lds, const Bf3Stage<KC>& st) {
     constexpr int P = Bf3Stage<KC>::kPer;
     constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane;
-    const int row = threadIdx.x >> 2, kq = threadIdx.x & 3;
+    const int row = bf3_srow<KC>(threadIdx.x), kq = threadIdx.x & 3;
     const int off = row * S + kq * (P / 2);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -530,7 +542,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     const int lj = wc * 32 + (lane & 31);
     const int j = j0 + lj;
 
-    const int gi = i0 + (t >> 2), gj = j0 + (t >> 2);
+    const int gi = i0 + bf3_srow<KC>(t), gj = j0 + bf3_srow<KC>(t);
     Bf3Stage<KC> st;
     // pre-split: wave w copies operand w (U_I, V_I, U_J, V_J) of the chunk
     // (one chunk in flight: two measured slower — more registers, and the
@@ -719,8 +731,13 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const int64_t nn = n;
     auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
 
-    // staging: thread t owns row t >> 1 of both blocks, k = 8·(t & 1) … + 7 of the chunk
-    const int srow = t >> 1, sk = (t & 1) * 8;
+    // staging: thread t owns row srow of both blocks, k = 8·half … + 7 of the
+    // chunk; the 8-lane groups of its ds_write_b128 (bank (a/4) mod 32) take
+    // 8 rows of one half, whose 16-byte slots in 12-dword rows hit 32 distinct
+    // banks (rows t >> 1, halves t & 1 were 2-way conflicted: 8 extra LDS
+    // cycles per store, SQ_LDS_BANK_CONFLICT 12.8 M per launch at Cora S = 8)
+    const int shalf = (t >> 3) & 1;
+    const int srow = 32 * (t >> 6) + (t & 7) + 8 * ((t >> 4) & 3), sk = shalf * 8;
     const int gi = i0 + srow, gj = j0 + srow;
     const float* src[4] = {u + (int64_t)gi * ld, v + (int64_t)gi * ld, u + (int64_t)gj * ld,
                            v + (int64_t)gj * ld};
@@ -780,7 +797,7 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[m][q][e] = 0.f;
 
-    const int soff = srow * kS2 + (t & 1) * 4;
+    const int soff = srow * kS2 + shalf * 4;
     const int fo = 4 * (lane >> 5);
     const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
     const int rb0 = (wc * 64 + (lane & 31)) * kS2 + fo, rb1 = rb0 + 32 * kS2;
