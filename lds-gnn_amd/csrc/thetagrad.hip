@@ -325,10 +325,16 @@ __global__ __launch_bounds__(256) void theta_grad_mfma_kernel(
 // v_mfma_f32_32x32x16_bf16 (32 cycles each) replace eight
 // v_mfma_f32_32x32x2_f32 (64 cycles each) per 16-wide k-step: 2.67× fewer
 // MFMA cycles.
-// LDS: 12 planes (U_I, V_I, U_J, V_J × three splits) of [64 rows][KC bf16],
-// row stride KC/2 + 4 dwords (4 × odd: the 16 rows of a ds_read_b128 lane
-// group land on 16 distinct 4-bank slots).  A lane's fragment (row r, 8
-// consecutive k) is one ds_read_b128.  Global loads of chunk c+1 are in
+// LDS: 12 planes (U_I, V_I, U_J, V_J × three splits) of [64 rows][KC bf16].
+// A lane's fragment (row r, 8 consecutive k) is one ds_read_b128.  KC = 16:
+// rows of 8 dwords, unpadded, the two 16-byte halves of row r swapped when
+// bit 3 of r is set (swz16).  That keeps both the fragment reads (ds_read_b128
+// lane groups {0-3,12-15,20-27}, ... : 16 rows of one half) and the staging
+// stores (ds_write_b64 groups of 16 lanes: 4 rows × 4 k-quarters, banks mod 32;
+// ds_write_b128 groups of 8: 4 rows × 2 halves) on distinct banks.  The
+// previous 12-dword rows (4 × odd) read conflict-free but stored 2-way
+// conflicted: 12.8 M extra LDS cycles per 128-tile launch at Cora S = 8.  KC =
+// 32: rows of KC/2 + 4 dwords, no swap.  Global loads of chunk c+1 are in
 // flight during chunk c's MFMAs, as in the fp32 form.
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -359,7 +365,8 @@ template <int KC>
 struct Bf3Stage {
     // thread t stages row t >> 2 of each block, k = (t & 3)·(KC/4) … + KC/4 - 1
     static constexpr int kPer = KC / 4;       // fp32 values per thread per array
-    static constexpr int kStr = KC / 2 + 4;   // dwords per LDS row
+    static constexpr bool kSwz = KC == 16;    // unpadded rows, halves swapped by row bit 3
+    static constexpr int kStr = kSwz ? 8 : KC / 2 + 4;   // dwords per LDS row
     static constexpr int kPlane = 64 * kStr;  // dwords per plane
     float x[4][kPer];                         // U_I, V_I, U_J, V_J
 };
@@ -406,6 +413,10 @@ struct Planes {
     const uint16_t* v;
 };
 
+// 16-byte half of row r that holds logical half h in the unpadded 8-dword
+// layout (see the split-bf16 comment above).
+__device__ __forceinline__ int swz16(int r) { return (r >> 3) & 1; }
+
 __host__ __device__ __forceinline__ int64_t ci_at(int64_t i, int c, int p, int64_t rows) {
     return ((int64_t)(c >> 4) * rows + i) * 48 + p * 16 + (c & 15);
 }
@@ -443,28 +454,18 @@ __device__ __forceinline__ void ci_store(uint32_t* lds, int a, const CiCopy<NQ>&
     for (int q = 0; q < NQ; ++q) {
         const int o = 16 * m + 1024 * q;
         const int row = o / 96, w = o % 96;
-        *reinterpret_cast<u32x4*>(lds + (3 * a + w / 32) * PL + row * S + 4 * ((w % 32) >> 4)) = c.x[q];
+        const int half = ((w % 32) >> 4) ^ (S == 8 ? swz16(row) : 0);
+        *reinterpret_cast<u32x4*>(lds + (3 * a + w / 32) * PL + row * S + 4 * half) = c.x[q];
     }
-}
-
-// Staging row of thread t.  KC = 16 (4 floats per thread and array, stored
-// as ds_write_b64: lane groups of 16, bank (a/4) mod 32): a group covers rows
-// {a, a+2, a+4, a+6} × the four k-quarters, whose 8-byte slots in 12-dword
-// rows hit 32 distinct banks (rows t >> 2 put a..a+3 in a group: 2-way
-// conflicts).  The four lanes of one row stay adjacent, so each row's 64 B
-// remain one contiguous global read.  KC = 32: row t >> 2.
-template <int KC>
-__device__ __forceinline__ int bf3_srow(int t) {
-    if constexpr (KC == 16) return 16 * (t >> 6) + ((t >> 4) & 1) + 2 * ((t >> 2) & 3) + 8 * ((t >> 5) & 1);
-    return t >> 2;
 }
 
 template <int KC>
 __device__ __forceinline__ void bf3_store(uint32_t* lds, const Bf3Stage<KC>& st) {
     constexpr int P = Bf3Stage<KC>::kPer;
     constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane;
-    const int row = bf3_srow<KC>(threadIdx.x), kq = threadIdx.x & 3;
-    const int off = row * S + kq * (P / 2);
+    const int row = threadIdx.x >> 2, kq = threadIdx.x & 3;
+    const int off = Bf3Stage<KC>::kSwz ? row * S + 4 * ((kq >> 1) ^ swz16(row)) + 2 * (kq & 1)
+                                       : row * S + kq * (P / 2);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
         uint32_t h[P / 2], m[P / 2], l[P / 2];
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     const int lj = wc * 32 + (lane & 31);
     const int j = j0 + lj;
 
-    const int gi = i0 + bf3_srow<KC>(t), gj = j0 + bf3_srow<KC>(t);
+    const int gi = i0 + (t >> 2), gj = j0 + (t >> 2);
     Bf3Stage<KC> st;
     // pre-split: wave w copies operand w (U_I, V_I, U_J, V_J) of the chunk
     // (one chunk in flight: two measured slower — more registers, and the
@@ -586,8 +587,10 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 
     // fragment offsets (dwords): row (wave's 32-row half + lane & 31), k-half 8·(lane >> 5)
-    const int ra = (wr * 32 + (lane & 31)) * S + 4 * (lane >> 5);
-    const int rb = (wc * 32 + (lane & 31)) * S + 4 * (lane >> 5);
+    // (row bit 3 = lane bit 3: the rows of a fragment read are wr·32 + lane & 31)
+    const int fh = Bf3Stage<KC>::kSwz ? 4 * ((lane >> 5) ^ ((lane >> 3) & 1)) : 4 * (lane >> 5);
+    const int ra = (wr * 32 + (lane & 31)) * S + fh;
+    const int rb = (wc * 32 + (lane & 31)) * S + fh;
     auto compute = [&](int k0) {
 #pragma unroll
         for (int kk = 0; kk < KC; kk += 16) {
@@ -674,8 +677,8 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
 // n = 20 000 (42 MB of U, V against a 4 MB L2 per XCD) that stream from the
 // Infinity Cache, not the MFMAs, sets the time.  Here a 256-thread block owns
 // a 128 × 128 tile (each wave a 64 × 64 quarter: 2 × 2 accumulators of
-// 32 × 32), staging 16-wide k chunks of the 12 bf16 planes (72 KB of LDS,
-// 2 blocks per CU): 32 flop per byte, 48 MFMAs per wave between barriers.
+// 32 × 32), staging 16-wide k chunks of the 12 bf16 planes (48 KB of LDS;
+// 2 blocks per CU, VGPR-bound): 32 flop per byte, 48 MFMAs per wave between barriers.
 // Tile order (`group` > 0): the triangle's block columns are cut into strips
 // of `group` columns, a strip enumerated row block by row block, and each XCD
 // (blocks b, b + 8, … share one) takes a contiguous range of that order, so
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
 // blocks and share their U, V rows in its L2.
 // ---------------------------------------------------------------------------
 constexpr int kT2 = 128;
-constexpr int kS2 = 12;             // dwords per LDS row (8 data + 4 pad: 4 × odd)
+constexpr int kS2 = 8;              // dwords per LDS row, unpadded, halves swapped by row bit 3 (swz16)
 constexpr int kPL2 = kT2 * kS2;     // dwords per plane (pre-split copies: + 4, see ci_store)
 
 // Packed index of (i, j), i <= j, in 32-bit arithmetic (the epilogue's 64
@@ -731,13 +734,8 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const int64_t nn = n;
     auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
 
-    // staging: thread t owns row srow of both blocks, k = 8·half … + 7 of the
-    // chunk; the 8-lane groups of its ds_write_b128 (bank (a/4) mod 32) take
-    // 8 rows of one half, whose 16-byte slots in 12-dword rows hit 32 distinct
-    // banks (rows t >> 1, halves t & 1 were 2-way conflicted: 8 extra LDS
-    // cycles per store, SQ_LDS_BANK_CONFLICT 12.8 M per launch at Cora S = 8)
-    const int shalf = (t >> 3) & 1;
-    const int srow = 32 * (t >> 6) + (t & 7) + 8 * ((t >> 4) & 3), sk = shalf * 8;
+    // staging: thread t owns row t >> 1 of both blocks, k = 8·(t & 1) … + 7 of the chunk
+    const int srow = t >> 1, sk = (t & 1) * 8;
     const int gi = i0 + srow, gj = j0 + srow;
     const float* src[4] = {u + (int64_t)gi * ld, v + (int64_t)gi * ld, u + (int64_t)gj * ld,
                            v + (int64_t)gj * ld};
@@ -797,8 +795,8 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[m][q][e] = 0.f;
 
-    const int soff = srow * kS2 + shalf * 4;
-    const int fo = 4 * (lane >> 5);
+    const int soff = srow * kS2 + 4 * ((t & 1) ^ swz16(srow));
+    const int fo = 4 * ((lane >> 5) ^ ((lane >> 3) & 1));  // rows wr·64 (+32) + lane & 31: bit 3 = lane bit 3
     const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
     const int rb0 = (wc * 64 + (lane & 31)) * kS2 + fo, rb1 = rb0 + 32 * kS2;
     auto stage = [&](const float (&x)[4][8]) {
