@@ -900,6 +900,22 @@ class LdsEngine:
         self.theta_fn = fn
         self.theta_counters = {}
 
+    def detach(self):
+        """InnerProblemTrainer.detach without a hyper step (a training loop
+        with no graph learning, BASELINE config 1): the weights and Adam state
+        of the current step become slot 0, the pending draw counters and Adam
+        steps are applied on device (lds_engine_end_window with no hyper step:
+        no learning-rate decay)."""
+        T, P, st = self.t, nat.ptr, self._stream()
+        wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
+        nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
+                 P(self.scalars), self.pending_graph, self.pending_fwd, T, 0, P(self.betas_dev), P(self.adam_tab),
+                 self._tab_count(), P(self.gbatch.deg), self.gbatch.deg.numel(), self.bt, st)
+        self._ws_clean = True
+        self.pending_graph = 0
+        self.pending_fwd = 0
+        self.t = 0
+
     def take_forward_counter(self) -> int:
         """The next forward counter (absolute), taken by a host-side forward
         (per-draw θ: the model's statistics() in training mode)."""

@@ -234,3 +234,115 @@ class FusedBilevelRunner:
         vl, va, tl, ta = self.engine.empirical_mean(self.gcn_params, self.n_samples_empirical_mean,
                                                     self.data.val_mask, self.data.test_mask)
         return {"loss.val.final": vl, "acc.val.final": va, "loss.test.final": tl, "acc.test.final": ta}
+
+
+class FixedGraphGcn:
+    """BASELINE config 1 — fixed-adjacency GCN training, src/scripts/gcn.py:
+    56-99 — on the fused engine.  θ is the given 0/1 adjacency's upper
+    triangle, whose Bernoulli draws are exactly that graph (u ∈ [0, 1): u < 1
+    always, u < 0 never), drawn once; there is no hyper step.  One epoch is the
+    reference's train step (training-mode forward with dropout, NLL on the
+    train rows, backward, Adam with weight decay on layer_in only,
+    src/scripts/gcn.py:62-67,75-83) and evaluate() (eval-mode forward, NLL and
+    accuracy on the validation and test rows, src/utils/evaluation.py:25-48),
+    with one host read of the epoch's metrics (the reference's `.item()`s).
+    From the second epoch on, train step and evaluation replay as one HIP
+    graph.
+
+    gcn: the MetaDenseGCN whose initial weights and dropout rate are used;
+    data: DenseData with the fixed dense_adj (any symmetric 0/1 matrix)."""
+
+    def __init__(self, gcn, data, lr: float = 0.01, weight_decay: float = 5e-4,
+                 generator: "_rng.Generator" = None, graphs: bool = True):
+        import numpy as np
+        import torch
+
+        from .engine import _Slot
+        n = data.num_nodes
+        iu = torch.triu_indices(n, n, device=data.x.device)
+        theta = data.dense_adj[iu[0], iu[1]].float().contiguous()
+        if not bool(((theta == 0) | (theta == 1)).all()):
+            raise NotImplementedError("FixedGraphGcn takes a 0/1 adjacency (the graph the reference normalises)")
+        params = gcn.model_params if hasattr(gcn, "model_params") else dict(gcn.named_parameters())
+        from collections import OrderedDict
+        params = OrderedDict((k, v.detach()) for k, v in params.items())
+        self.eng = eng = LdsEngine(data.x, data.y, data.train_mask, data.val_mask, theta, data.num_classes,
+                                   dropout=gcn.dropout, gcn_lr=lr, gcn_wd=weight_decay, outer_lr=0.0,
+                                   lr_decay=None, tau=1, generator=generator or gcn.generator or _rng.default_generator,
+                                   params=params, samples=1)
+        if eng.long_rows:
+            raise NotImplementedError("FixedGraphGcn: short-row graphs (the engine's in-kernel aggregation)")
+        self.gcn, self.data = gcn, data
+        self.use_graphs = graphs
+        self._graph = None
+        self._drawn = False
+        self.vm = data.val_mask.to(device=eng.dev, dtype=torch.uint8).contiguous()
+        self.tm = data.test_mask.to(device=eng.dev, dtype=torch.uint8).contiguous()
+        self.inv_v = float(np.float32(1.0) / np.float32(int(data.val_mask.sum())))
+        self.inv_t = float(np.float32(1.0) / np.float32(int(data.test_mask.sum())))
+        # evaluation slot reading the training graph (no draw)
+        self._ev = _Slot(n, eng.cap, eng.dev, x_nnz=0, samples=1, bptr_len=eng.bptr_len, words=eng.words)
+        self._test_rows = torch.zeros((2, n), dtype=torch.float32, device=eng.dev)
+
+    def _train_step(self):
+        eng = self.eng
+        if not self._drawn:
+            eng.inner_step()  # draws the graph (deterministic) into slot 0
+            self._drawn = True
+        else:
+            eng.inner_step(presampled=True)
+        eng.detach()
+
+    def _evaluate(self):
+        """evaluate() launches: eval-mode forward on the fixed graph, NLL /
+        correct sums of the val and test rows, and the train step's metrics,
+        into self._res (6 floats on device)."""
+        import torch
+
+        from . import _native as nat
+        eng, ev = self.eng, self._ev
+        ev.g = eng.slots[0].g  # the fixed graph
+        st, n, c = eng._stream(), eng.n, eng.c
+        eng._forward(ev, eng.w[0], self.vm, self.inv_v, 0, 0)  # eval mode: val rows -> ev.lossrow / corrrow
+        g = ev.g
+        nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n,
+                 nat.ptr(ev.h2), 0, 0, 0, nat.ptr(eng.label), nat.ptr(self.tm), self.inv_t,
+                 nat.ptr(self._test_rows[0]), nat.ptr(self._test_rows[1]), c, 0, eng.bt, st)
+        r = self._res
+        r[0:2].copy_(eng.metrics[0][0])
+        for i, t in enumerate((ev.lossrow[0], ev.corrrow[0], self._test_rows[0], self._test_rows[1])):
+            torch.sum(t, dim=0, keepdim=True, out=r[2 + i:3 + i])
+
+    def epoch(self):
+        """train step + evaluate(); returns (train loss, train acc, val loss,
+        val acc, test loss, test acc) of the epoch (one host sync).  With
+        graphs, from the second epoch on both run as one HIP graph replay."""
+        import torch
+        eng = self.eng
+        if getattr(self, "_res", None) is None:
+            self._res = torch.zeros(6, dtype=torch.float32, device=eng.dev)
+        if not self.use_graphs or not self._drawn:
+            self._train_step()
+            self._evaluate()
+        else:
+            if self._graph is None:
+                s = torch.cuda.Stream(eng.dev)
+                s.wait_stream(torch.cuda.current_stream(eng.dev))
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s):
+                        self._train_step()
+                        self._evaluate()
+                torch.cuda.current_stream(eng.dev).wait_stream(s)
+                self._graph = g
+            self._graph.replay()
+        host = self._res.double().cpu().numpy()
+        return (float(host[0] * eng.inv_train), float(host[1] * eng.inv_train), float(host[2] * self.inv_v),
+                float(host[3] * self.inv_v), float(host[4] * self.inv_t), float(host[5] * self.inv_t))
+
+    def params(self):
+        """Current weights in the reference layout (layer_in.fc.weight, ...)."""
+        return self.eng.get_params()
+
+    def sync_generator(self):
+        self.eng.sync_generator()

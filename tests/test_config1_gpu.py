@@ -105,3 +105,39 @@ def test_config1_gcn_training_matches_reference_golden():
     pf = np.concatenate([p.detach().cpu().numpy().ravel() for p in gcn.parameters()])
     assert np.allclose(pf, g["params_final"], rtol=1e-4, atol=1e-5)
     assert ldsgnn.rng.default_generator.forward_counter == int(g["forward_draws"])
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_config1_fused_engine_matches_reference_golden(graphs):
+    """BASELINE config 1 on the fused engine (ldsgnn.fused.FixedGraphGcn: the
+    given graph as a 0/1 θ, no hyper steps; train steps eager or replayed
+    from a HIP graph) against the golden the reference's own loop made
+    (src/scripts/gcn.py:56-99): every epoch's train / val / test loss at 1e-5
+    and accuracy exactly, the same early-stopping epoch, final weights, and
+    the forward counters the dropout draws took."""
+    from ldsgnn.fused import FixedGraphGcn
+    g = np.load(f"{GOLDEN}/gcn_fixed_cora.npz")
+    seed = int(g["seed"])
+    data = load_workload("cora-given", device=DEV)
+    ldsgnn.rng.manual_seed(seed, 0)
+    torch.manual_seed(seed)
+    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(DEV)
+    run = FixedGraphGcn(gcn, data, lr=0.01, weight_decay=5e-4, graphs=graphs)
+    stopper = EarlyStopping(10)
+    rows = []
+    for _ in range(200):
+        tl, ta, vl, va, sl, sa = run.epoch()
+        rows.append([tl, ta, vl, va, sl, sa])
+        stopper.update(vl, model=gcn)
+        if stopper.abort:
+            break
+    rows, ref = np.array(rows), g["rows"]
+    assert rows.shape == ref.shape  # same early-stopping epoch
+    for c in (0, 2, 4):  # losses
+        assert np.allclose(rows[:, c], ref[:, c], rtol=1e-5, atol=1e-6), (c, np.abs(rows[:, c] - ref[:, c]).max())
+    for c in (1, 3, 5):  # accuracies: identical counts
+        assert np.allclose(rows[:, c], ref[:, c], atol=1e-6), c
+    pf = np.concatenate([v.detach().cpu().numpy().ravel() for v in run.params().values()])
+    assert np.allclose(pf, g["params_final"], rtol=1e-4, atol=1e-5)
+    run.sync_generator()
+    assert ldsgnn.rng.default_generator.forward_counter == int(g["forward_draws"])
