@@ -10,6 +10,8 @@
   cora-synthetic a synthetic Cora-shaped problem with a torch kNN θ₀ (round-1 bench)
   synthetic20k   config 5: N = 20 000, F_in 128, X ~ U[0,1) row-normalised,
                  θ_ij ~ U(0, 1) i.i.d. (seed 20000), drawn on `device`
+  synthetic20k-sparse  config 5's optional sparse variant: the same X, θ_ij ~
+                 U(0, 0.01) (≈ 2·10⁶ sampled entries per graph: short rows)
 
 Every workload returns a DenseData whose dense_adj is θ₀ (the
 BernoulliGraphModel init matrix, src/models/factory.py:60-62).
@@ -25,7 +27,7 @@ from ..utils.graph import DenseData
 from .planetoid import FIXTURE_DIR, load_planetoid_npz
 from .synthetic import knn_init, make_dataset
 
-WORKLOADS = ("cora", "cora-given", "citeseer", "cora-synthetic", "synthetic20k")
+WORKLOADS = ("cora", "cora-given", "citeseer", "cora-synthetic", "synthetic20k", "synthetic20k-sparse")
 
 
 def knn_theta0(n: int, path: str = None) -> torch.Tensor:
@@ -52,12 +54,16 @@ def load_workload(name: str, seed: int = 0, device="cpu") -> DenseData:
     elif name == "cora-synthetic":
         data = knn_init(make_dataset("cora", seed=seed), k=10)
         data.name = "synthetic cora-shaped, torch kNN theta0"
-    elif name == "synthetic20k":
+    elif name in ("synthetic20k", "synthetic20k-sparse"):
         data = make_dataset("synthetic20k", seed=seed)
         data = data.to(device)
         g = torch.Generator(device=data.x.device).manual_seed(20000)
         data.dense_adj = torch.rand((data.num_nodes, data.num_nodes), generator=g, device=data.x.device)
-        data.name = "synthetic N=20000, theta ~ U(0,1) i.i.d. (seed 20000)"
+        if name == "synthetic20k-sparse":
+            data.dense_adj.mul_(0.01)
+            data.name = "synthetic N=20000, theta ~ U(0,0.01) i.i.d. (seed 20000)"
+        else:
+            data.name = "synthetic N=20000, theta ~ U(0,1) i.i.d. (seed 20000)"
         return data
     else:
         raise ValueError(f"unknown workload {name!r}: one of {WORKLOADS}")

@@ -317,7 +317,8 @@ class LdsEngine:
 
     def _row_plan(self):
         """The aggregating kernels' row plan (include/ldsgnn.h LdsBatch): rows
-        whose expected degree 1 + Σ_j clamp(θ_ij, 0, 1) exceeds HEAVY_DEGREE,
+        whose expected degree 1 + Σ_j clamp(θ_ij, 0, 1) exceeds HEAVY_DEGREE
+        (and 4 × the median degree),
         or whose expected count of train (or opt) neighbours, self included,
         exceeds HEAVY_MASKED, run on a block of their own.  Decided once from θ
         at construction: it changes speed only (a row of any degree is
@@ -343,7 +344,12 @@ class LdsEngine:
             p = self.theta[lo:hi].clamp(0.0, 1.0) * (rows != cols)
             deg.index_add_(0, rows, p).index_add_(0, cols, p)
             et.index_add_(0, rows, p * mt[cols]).index_add_(0, cols, p * mt[rows])
-        heavy = deg > self.HEAVY_DEGREE
+        # a block per row pays off for the few hubs of a skewed graph; when
+        # the typical row is long (config 5's sparse variant: every row ~100)
+        # a wave per row walks it and the per-row blocks would only multiply
+        # the fused reductions' partials (20 000 → 1 final block summing 21 k)
+        thr = max(float(self.HEAVY_DEGREE), 4.0 * float(deg.median()))
+        heavy = deg > thr
         # the two-hop kernels' own plan (their LdsBatch, bt2): also rows with
         # many train neighbours (no block reductions there, so nred is unaffected)
         heavy2 = heavy | (et > self.HEAVY_MASKED)
