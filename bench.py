@@ -60,8 +60,11 @@ def world_info():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def build(args, rank, device, samples=None):
-    """The drop-in trainers of the workload (src/scripts/bilevel.py:74-99)."""
+def build(args, rank, device, samples=None, exchange=None):
+    """The drop-in trainers of the workload (src/scripts/bilevel.py:74-99).
+    exchange: give the outer trainer the all-reduce reducer (default: when a
+    process group of more than one rank is up); False for a run on this rank
+    alone inside a multi-rank job (the strong-scaling leg's T1)."""
     import ldsgnn
     from ldsgnn.data.workloads import load_workload
     from ldsgnn.models.gcn import MetaDenseGCN
@@ -92,6 +95,8 @@ def build(args, rank, device, samples=None):
         gm = fac.create(args.graph_model)
         opt = fac.optimizer(gm)
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if exchange is not None:
+        multi = multi and bool(exchange)
     outer = OuterProblemTrainer(opt, data, opt_mask, gm, lr_decay=0.99,
                                 grad_reducer=allreduce_mean if multi else None)
     return data, BilevelProblemRunner(inner, outer, data), opt_mask
@@ -377,7 +382,10 @@ def strong_scaling_leg(args, world, rank, device, barrier_sync):
     windows = max(1, args.strong_steps // args.tau)
 
     def timed(S, reducer_world):
-        data, runner, _ = build(args, rank, device, samples=S)
+        # the single-GPU reference time runs on rank 0 alone: no exchange in
+        # its engine (capture_window / hyper_step fall back to the engine's
+        # own reducer, which would all-reduce with ranks waiting at a barrier)
+        data, runner, _ = build(args, rank, device, samples=S, exchange=reducer_world > 1)
         eng, reducer = make_engine(runner, args.tau, reducer_world, S)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
