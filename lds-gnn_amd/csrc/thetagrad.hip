@@ -704,6 +704,73 @@ __device__ __forceinline__ int64_t tri_at_t(int i, int j, int64_t n) {
     }
 }
 
+// Epilogue of the 128-tile kernels (wave (wr, wc) owns outputs wr·64 … + 63 ×
+// wc·64 … + 63 of the tile): dθ = gscale·(acc + R_i + R_j) on the strict upper
+// triangle, clamp-backward mask, then the mode's stores.
+template <bool SMALL>
+__device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const float* Ri, const float* Rj,
+                                              float* __restrict__ theta, float* __restrict__ grad, int n,
+                                              int mode, const double* __restrict__ lr_dev, float gscale,
+                                              int i0, int j0, int wr, int wc, int lane) {
+    const int64_t nn = n;
+    auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
+    // Epilogue: every θ (and partial-grad) operand of the wave's 64 outputs is
+    // loaded before the first store — a load after a store to the same array
+    // cannot be hoisted above it, and per-element load → store chains cost one
+    // memory latency each (1.1 ms of 2.5 at n = 20 000 before this).
+    const bool need_part = mode == 1 || mode == 3;
+    float th[2][2][16], part[2][2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = j0 + wc * 64 + q * 32 + (lane & 31);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int i = i0 + wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const bool in = i < n && j < n && j >= i;
+                const int64_t id = in ? tri_at(i, j, nn) : 0;
+                th[m][q][e] = (in && theta != nullptr) ? theta[id] : 0.f;
+                part[m][q][e] = (in && need_part) ? grad[id] : 0.f;
+            }
+        }
+    __syncthreads();  // Ri / Rj written by other waves
+
+    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int lj = wc * 64 + q * 32 + (lane & 31);
+            const int j = j0 + lj;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                const int i = i0 + li;
+                if (i >= n || j >= n || j < i) continue;
+                const int64_t id = tri_at(i, j, nn);
+                const float t0 = th[m][q][e];
+                float g = 0.f;
+                if (j > i) {
+                    const float gs = gscale * (acc[m][q][e] + Ri[li] + Rj[lj]);
+                    g = mode == 3 ? part[m][q][e] + gs : gs;
+                    if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+                }
+                if (mode == 3) {
+                    grad[id] = g;
+                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                } else if (mode == 2) {
+                    if (grad != nullptr) grad[id] = g;
+                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                } else if (mode == 1) {
+                    grad[id] = part[m][q][e] + g;
+                } else {
+                    grad[id] = g;
+                }
+            }
+        }
+}
+
 template <bool VEC, bool SMALL = false, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
@@ -731,8 +798,6 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int64_t nn = n;
-    auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
 
     // staging: thread t owns row t >> 1 of both blocks, k = 8·(t & 1) … + 7 of the chunk
     const int srow = t >> 1, sk = (t & 1) * 8;
@@ -858,68 +923,164 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
         }
         compute();
     }
-    // Epilogue: every θ (and partial-grad) operand of the wave's 64 outputs is
-    // loaded before the first store — a load after a store to the same array
-    // cannot be hoisted above it, and per-element load → store chains cost one
-    // memory latency each (1.1 ms of 2.5 at n = 20 000 before this).
-    const bool need_part = mode == 1 || mode == 3;
-    float th[2][2][16], part[2][2][16];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int j = j0 + wc * 64 + q * 32 + (lane & 31);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int i = i0 + wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                const bool in = i < n && j < n && j >= i;
-                const int64_t id = in ? tri_at(i, j, nn) : 0;
-                th[m][q][e] = (in && theta != nullptr) ? theta[id] : 0.f;
-                part[m][q][e] = (in && need_part) ? grad[id] : 0.f;
-            }
-        }
-    __syncthreads();  // Ri / Rj written by other waves
+    t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
+}
 
-    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+// ---------------------------------------------------------------------------
+// Software-pipelined 128 × 128 form (form 8).  Ablations of the 64-tile
+// kernel at Cora S = 16 (k = 4224) put half its time in the staging phase: with
+// the LDS stores skipped 546 -> 281 µs, with the bf16 split skipped (stores
+// kept) 509 µs, with the MFMAs skipped 396 µs.  Between its two barriers a
+// chunk's split + LDS stores run while no MFMA of the block can issue, and the
+// resident blocks reach those phases together.  Here the LDS stage is double
+// buffered (2 × 48 KB, dynamic LDS, one block per CU): while a wave reads
+// buffer c & 1 and runs chunk c's 48 MFMAs, it splits chunk c + 1 (loaded two
+// chunks earlier) and stores it into the other buffer; one barrier per chunk.
+// Chunk c + 3's loads are issued after that store, into the registers it
+// freed.  Same chunks, same LDS rows, same MFMA order as form 5: identical bits.
+// ---------------------------------------------------------------------------
+constexpr int kPipeLds = 2 * 12 * kPL2 * 4;  // bytes of the two stage buffers
+
+template <bool SMALL>
+__global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
+    float gscale, int group, int per_xcd) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+    __shared__ float Ri[kT2], Rj[kT2];
+
+    const int nb = (n + kT2 - 1) / kT2;
+    const int ntiles = nb * (nb + 1) / 2;
+    int bi, bj;
+    {
+        const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+        if (L >= ntiles) return;  // whole block: no barrier reached
+        grouped_tile(L, nb, group, bi, bj);
+    }
+    const int i0 = bi * kT2, j0 = bj * kT2;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+
+    // staging: thread t owns row t >> 1 of both blocks, k = 8·(t & 1) … + 7 of
+    // the chunk; branch-free loads (rows past n and k past the end read zeros)
+    const int srow = t >> 1, sk = (t & 1) * 8;
+    const int gi = i0 + srow, gj = j0 + srow;
+    const float* src[4] = {u + (int64_t)gi * ld, v + (int64_t)gi * ld, u + (int64_t)gj * ld,
+                           v + (int64_t)gj * ld};
+    const bool rowok[4] = {gi < n, gi < n, gj < n, gj < n};
+    auto load = [&](float (&x)[4][8], int k0) {
+        const int gk = k0 + sk;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const float* p = (rowok[a] && gk < k) ? src[a] + gk : g_zero8;
+            const float4 f0 = *reinterpret_cast<const float4*>(p);
+            const float4 f1 = *reinterpret_cast<const float4*>(p + 4);
+            x[a][0] = f0.x; x[a][1] = f0.y; x[a][2] = f0.z; x[a][3] = f0.w;
+            x[a][4] = f1.x; x[a][5] = f1.y; x[a][6] = f1.z; x[a][7] = f1.w;
+        }
+    };
+    const int soff = srow * kS2 + 4 * ((t & 1) ^ swz16(srow));
+    auto stage = [&](uint32_t* buf, const float (&x)[4][8]) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            uint32_t h[4], m[4], l[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) split3_pair(x[a][2 * q], x[a][2 * q + 1], h[q], m[q], l[q]);
+            *reinterpret_cast<u32x4*>(buf + (3 * a + 0) * kPL2 + soff) = u32x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u32x4*>(buf + (3 * a + 1) * kPL2 + soff) = u32x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u32x4*>(buf + (3 * a + 2) * kPL2 + soff) = u32x4{l[0], l[1], l[2], l[3]};
+        }
+    };
+    const int fo = 4 * ((lane >> 5) ^ ((lane >> 3) & 1));
+    const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
+    const int rb0 = (wc * 64 + (lane & 31)) * kS2 + fo, rb1 = rb0 + 32 * kS2;
+    f32x16 acc[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int lj = wc * 64 + q * 32 + (lane & 31);
-            const int j = j0 + lj;
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                const int i = i0 + li;
-                if (i >= n || j >= n || j < i) continue;
-                const int64_t id = tri_at(i, j, nn);
-                const float t0 = th[m][q][e];
-                float g = 0.f;
-                if (j > i) {
-                    const float gs = gscale * (acc[m][q][e] + Ri[li] + Rj[lj]);
-                    g = mode == 3 ? part[m][q][e] + gs : gs;
-                    if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
-                }
-                if (mode == 3) {
-                    grad[id] = g;
-                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                } else if (mode == 2) {
-                    if (grad != nullptr) grad[id] = g;
-                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                } else if (mode == 1) {
-                    grad[id] = part[m][q][e] + g;
-                } else {
-                    grad[id] = g;
-                }
+            for (int e = 0; e < 16; ++e) acc[m][q][e] = 0.f;
+    // chunk c from `cur`, overlapped with the stage of the next chunk into `nxt`
+    auto step = [&](const uint32_t* cur, uint32_t* nxt, const float (&x)[4][8]) {
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {  // pr 0: U_I × V_J (planes 0-2, 9-11); pr 1: V_I × U_J (3-5, 6-8)
+            const int pa = pr == 0 ? 0 : 3, pb = pr == 0 ? 9 : 6;
+            bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                fa[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra0));
+                fa[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra1));
+                fb[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pb + s) * kPL2 + rb0));
+                fb[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pb + s) * kPL2 + rb1));
             }
+            // half of the next chunk's stage (operands 2pr, 2pr + 1) beside these MFMAs
+#pragma unroll
+            for (int a = 2 * pr; a < 2 * pr + 2; ++a) {
+                uint32_t h[4], m[4], l[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) split3_pair(x[a][2 * q], x[a][2 * q + 1], h[q], m[q], l[q]);
+                *reinterpret_cast<u32x4*>(nxt + (3 * a + 0) * kPL2 + soff) = u32x4{h[0], h[1], h[2], h[3]};
+                *reinterpret_cast<u32x4*>(nxt + (3 * a + 1) * kPL2 + soff) = u32x4{m[0], m[1], m[2], m[3]};
+                *reinterpret_cast<u32x4*>(nxt + (3 * a + 2) * kPL2 + soff) = u32x4{l[0], l[1], l[2], l[3]};
+            }
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    f32x16 c = acc[m][q];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][1], fb[q][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[q][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][2], fb[q][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[q][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][1], fb[q][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[q][0], c, 0, 0, 0);
+                    acc[m][q] = c;
+                }
         }
+    };
+
+    uint32_t* const b0 = lds_dyn;
+    uint32_t* const b1 = lds_dyn + 12 * kPL2;
+    float xa[4][8], xb[4][8];
+    const int nch = (k + 15) / 16;
+    if (nch > 0) {
+        load(xa, 0);
+        load(xb, 16);
+    }
+    if (t < 2 * kT2) {
+        const int rr = t & (kT2 - 1);
+        const int row = (t < kT2 ? i0 : j0) + rr;
+        float racc = 0.f;
+        if (row < n) racc = row_r_sum(r, (int64_t)row * ldr, ldrc, nr);
+        (t < kT2 ? Ri : Rj)[rr] = racc;
+    }
+    if (nch > 0) {
+        stage(b0, xa);
+        load(xa, 32);
+    }
+    __syncthreads();
+    // chunk c: buffer c & 1 holds it; registers xb (c even) / xa (c odd) hold c + 1
+    for (int c = 0; c < nch; c += 2) {
+        step(b0, b1, xb);
+        load(xb, 16 * (c + 3));
+        __syncthreads();
+        if (c + 1 >= nch) break;
+        step(b1, b0, xa);
+        load(xa, 16 * (c + 4));
+        __syncthreads();
+    }
+    t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
 }
 
 // Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
 // shape (below), 2 = 64-tile with 16-wide k chunks, 3 = 64-tile with 32-wide
 // k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
 // order, 6 = form 2 in XCD-grouped order, 7 = form 5 with 64-bit index
-// arithmetic at every n (the n > 46 340 path; for testing).  Read at launch (a captured HIP graph keeps the form it was
+// arithmetic at every n (the n > 46 340 path; for testing), 8 = the
+// software-pipelined 128-tile (double-buffered stage, XCD-grouped order).  Read at launch (a captured HIP graph keeps the form it was
 // captured with).
 static int g_theta_form = 1;
 constexpr int kGroup = 8;
@@ -938,10 +1099,35 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
     // S = 1: 44.7 vs 65 µs; 46.8 in plain order);
     // 128-tiles in XCD-grouped order for long k (Cora / Citeseer S = 16:
     // 577 / 695 vs 604 / 895 µs) or large n (n = 20 000: 2.01 vs 2.27 ms)
-    if (form == 1) form = (nt2 >= 1024 || k >= 1024) ? 5 : 6;
+    // and the pipelined 128-tile (form 8) where its one block per CU still runs
+    // every tile in one round and k is long (Cora S = 16: 494 vs 546 µs; at
+    // Citeseer S = 16, 351 tiles, 847 vs 674; at n = 20 000, 2.29 vs 1.93 ms)
+    if (form == 1) form = (nt2 <= 256 && k >= 1024) ? 8 : (nt2 >= 1024 || k >= 1024) ? 5 : 6;
     // the branch-free staging needs whole 8-wide k groups in 16-byte aligned rows
     const bool fast = vec4 && (k & 7) == 0;
 #define LDS_TG_ARGS u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, vec4, ldrc, gscale
+    if (form == 8 && !pre && fast) {
+        const int per = (nt2 + 7) / 8;
+        const bool small = n <= 46340;
+        static bool attr_set[2] = {false, false};
+        if (!attr_set[small]) {  // > 64 KB of dynamic LDS must be enabled per kernel
+            if (small)
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_bf3_pipe_kernel<true>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kPipeLds);
+            else
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_bf3_pipe_kernel<false>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, kPipeLds);
+            attr_set[small] = true;
+        }
+        if (small)
+            hipLaunchKernelGGL((theta_grad_bf3_pipe_kernel<true>), dim3(8 * per), dim3(256), kPipeLds, st, u, v, ld, k,
+                               r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, kGroup, per);
+        else
+            hipLaunchKernelGGL((theta_grad_bf3_pipe_kernel<false>), dim3(8 * per), dim3(256), kPipeLds, st, u, v, ld,
+                               k, r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, kGroup, per);
+        return;
+    }
+    if (form == 8) form = 5;  // pre-split operands or unaligned rows: the plain 128-tile form
     if (form == 4 || form == 5 || form == 7) {
         const int per = (nt2 + 7) / 8;
         const int grid = form != 4 ? 8 * per : nt2;
@@ -1178,7 +1364,7 @@ extern "C" int lds_split_planes(const float* x, int rows, int ld, int k, uint16_
 }
 
 extern "C" int lds_theta_grad_set_form(int form, int* prev) {
-    LDS_CHECK_ARG(form >= -1 && form <= 7);
+    LDS_CHECK_ARG(form >= -1 && form <= 8);
     if (prev != nullptr) *prev = g_theta_form;
     if (form >= 0) g_theta_form = form;
     return 0;

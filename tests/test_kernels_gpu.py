@@ -447,7 +447,7 @@ def test_fused_sampler_csr_equals_staged_path(device, n, count, samples, dense):
 
 
 @pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16", "bf16x3-t64k16-grouped", "bf16x3-t64k32",
-                                  "bf16x3-t128", "bf16x3-t128-grouped", "fp32"])
+                                  "bf16x3-t128", "bf16x3-t128-grouped", "bf16x3-t128-pipe", "fp32"])
 @pytest.mark.parametrize("n,k,ld,mode", [(1, 4, 4, 0), (65, 17, 17, 0), (130, 33, 35, 1), (200, 0, 4, 0),
                                          (257, 48, 48, 2), (300, 264, 264, 3), (129, 1030, 1032, 0),
                                          (1100, 40, 40, 3)])
@@ -543,4 +543,38 @@ def test_theta_grad_planes_bit_exact_vs_fp32_operands(device, form, n, k, mode):
 def test_theta_grad_form_default_and_errors(device):
     assert ops.theta_grad_form() == "bf16x3"
     with pytest.raises(nat.NativeError):
-        nat.call("lds_theta_grad_set_form", 8, 0)
+        nat.call("lds_theta_grad_set_form", 9, 0)
+
+
+@pytest.mark.parametrize("n,k,mode", [(2708, 264, 2), (2708, 264, 3), (700, 40, 0), (130, 8, 1), (300, 24, 2),
+                                      (257, 48, 1), (3327, 1056, 0)])
+def test_theta_grad_pipe_bit_exact(device, n, k, mode):
+    """Form 8 (the double-buffered 128-tile) stages the same chunks into the
+    same LDS rows and runs the same MFMA order as form 5: identical bits, for
+    odd and even chunk counts (k = 264: 17 chunks; 24: 2; 8: 1) and partial
+    tiles, in every mode."""
+    g = torch.Generator().manual_seed(5 * n + k + mode)
+    ld = k + 8
+    u = torch.randn(n, ld, generator=g).to(device)
+    v = (torch.randn(n, ld, generator=g) * 0.3).to(device)
+    r = torch.randn(2, n, generator=g).to(device)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    theta[::9] = -0.5
+    base = torch.randn(n * (n + 1) // 2, generator=g)
+    scal = torch.zeros(32, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(0.05)
+    st = nat.stream_of(torch.device(device))
+    outs = []
+    for form in ("bf16x3-t128-grouped", "bf16x3-t128-pipe"):
+        prev = ops.theta_grad_form(form)
+        try:
+            th = theta.clone().to(device)
+            grad = base.clone().to(device)
+            nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
+                     nat.ptr(grad), mode, nat.ptr(scal), 1.0, st)
+            torch.cuda.synchronize()
+            outs.append((th.cpu(), grad.cpu()))
+        finally:
+            ops.theta_grad_form(prev)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
