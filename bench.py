@@ -389,7 +389,8 @@ def strong_scaling_leg(args, world, rank, device, barrier_sync):
         eng, reducer = make_engine(runner, args.tau, reducer_world, S)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
-        eng.capture_window(args.tau, grad_reducer=reducer)
+        # T1 replays whole groups of windows per graph as the N = 1 line does
+        eng.capture_window(args.tau, grad_reducer=reducer, windows=args.graph_windows if reducer is None else 1)
         eng.replay(1)
         if reducer_world > 1:
             barrier_sync()
@@ -495,6 +496,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--tau", type=int, default=5)
+    ap.add_argument("--graph-windows", type=int, default=4,
+                    help="τ-windows per captured HIP graph (N=1, engine path): replays run whole groups, "
+                         "the remainder one window at a time")
     ap.add_argument("--model", default="lds", choices=["lds", "gcn"],
                     help="lds: the LDS bilevel hot path (configs 2-5); gcn: config 1, fixed-graph GCN training")
     ap.add_argument("--dataset", default="cora", help="ldsgnn.data.workloads: cora (config 2, default), "
@@ -575,7 +579,8 @@ def main():
             reducer = eng.outer_update
         use_graph = not args.eager and eng.theta_fn is None  # per-draw θ (GAE proposal dropout): eager windows
         if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
-            eng.capture_window(args.tau, grad_reducer=reducer)
+            eng.capture_window(args.tau, grad_reducer=reducer,
+                               windows=args.graph_windows if reducer is None else 1)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)
     else:
         step = run_steps(runner, 0, args.warmup, args.tau)
@@ -665,7 +670,9 @@ def main():
                        "nodes": n, "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
                        "theta_grad_form": ldsops.theta_grad_form(), "sampled_nnz": nnz,
-                       "replicas_in_sync": in_sync, "graph_model": args.graph_model},
+                       "replicas_in_sync": in_sync, "graph_model": args.graph_model,
+                       "windows_per_graph": (args.graph_windows if reducer is None else 1)
+                       if use_engine and use_graph else None},
             "steady_state": steady,
             "strong_scaling": strong,
             "window": window,

@@ -1096,33 +1096,42 @@ class LdsEngine:
             self.inner_step(presampled=batch)
         return self.hyper_step(grad_reducer=grad_reducer, presampled=batch)
 
-    def capture_window(self, tau: int, grad_reducer=None):
+    def capture_window(self, tau: int, grad_reducer=None, windows: int = 1):
         """Record run_window(tau) as HIP graphs (state must be at a window
         start).  Replays advance RNG counters, Adam step and lr on device.
 
         Without a reducer the window is ONE graph (dθ assembly fused with the
-        SGD step).  With a reducer (replicas over RCCL) the window is split at
-        the exchange: graph A runs up to dθ, `grad_reducer(grad)` runs eagerly
-        between the replays (the collective stays outside the captured work),
-        graph B applies SGD + clamp and the detach."""
+        SGD step); `windows` > 1 also records that many consecutive windows as
+        one graph, which replay() uses for whole groups (the launches of every
+        window are the same, so no boundary between two graph launches falls
+        inside a group).  With a reducer (replicas over RCCL) the window is
+        split at the exchange: graph A runs up to dθ, `grad_reducer(grad)`
+        runs eagerly between the replays (the collective stays outside the
+        captured work), graph B applies SGD + clamp and the detach."""
         assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
         if self.theta_fn is not None:
             raise NotImplementedError("per-draw θ (GAE proposal dropout) computes θ of each draw on the host "
                                       "side's counters: run windows eagerly")
         if tau != self.tau:
             raise ValueError(f"engine was built for tau={self.tau}; capture that window length")
+        if windows < 1:
+            raise ValueError("windows >= 1")
         if grad_reducer is None:
             grad_reducer = self.grad_reducer
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(graph, stream=s):
-                    self.run_window(tau)
+            graphs = []
+            for w in sorted({1, windows}):
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(graph, stream=s):
+                        for _ in range(w):
+                            self.run_window(tau)
+                graphs.append((w, graph))
             torch.cuda.current_stream(self.dev).wait_stream(s)
-            self._graph_capture = ((graph,), tau, None)
-            return graph
+            self._graph_capture = (tuple(graphs), tau, None)
+            return graphs[0][1]
         head, tail = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         pool = torch.cuda.graph_pool_handle()
 
@@ -1143,8 +1152,11 @@ class LdsEngine:
     def replay(self, windows: int = 1):
         graphs, _, reducer = self._graph_capture
         if reducer is None:
-            for _ in range(windows):
-                graphs[0].replay()
+            (_, one), (group, multi) = graphs[0], graphs[-1]
+            for _ in range(windows // group):
+                multi.replay()
+            for _ in range(windows % group):
+                one.replay()
             return
         head, tail = graphs
         for _ in range(windows):

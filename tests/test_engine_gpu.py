@@ -28,14 +28,16 @@ def test_engine_dense_theta_seven_classes():
     assert res["max_theta_err"] < TOL, res
 
 
-def test_graph_replay_equals_eager():
+@pytest.mark.parametrize("group,windows", [(1, 3), (2, 5), (4, 3)])
+def test_graph_replay_equals_eager(group, windows):
     """A captured τ-window replays exactly like eager windows (same RNG draws,
-    Adam steps, lr decay): bitwise-identical θ and weights."""
+    Adam steps, lr decay): bitwise-identical θ and weights — also from a graph
+    of `group` consecutive windows, the remainder from the one-window graph."""
     a = run_engine_and_oracle(n=130, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
     b = run_engine_and_oracle(n=130, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
-    a.capture_window(5)
-    a.replay(3)
-    for _ in range(3):
+    a.capture_window(5, windows=group)
+    a.replay(windows)
+    for _ in range(windows):
         b.run_window(5)
     torch.cuda.synchronize()
     assert torch.equal(a.theta, b.theta)
