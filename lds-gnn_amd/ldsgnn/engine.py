@@ -637,10 +637,12 @@ class LdsEngine:
         than 128 entries first (a 1024-thread block each), then the rest (one
         wave each); with split products (xt_splits > 1) no heavy columns."""
         lens = (self.xcp[1:] - self.xcp[:-1]).long()
-        # batched samples keep every column one wave: the 1024-thread heavy
-        # blocks then only fragment the CU (measured 59.6 vs 73.4 µs per call,
-        # Citeseer S = 16); with one sample the long columns set the time
-        heavy = (lens > 128) if self.xt_splits <= 1 and self.S == 1 else torch.zeros_like(lens, dtype=torch.bool)
+        # up to 8 batched samples the long columns still set the time (Cora,
+        # per call: S = 4 9.9 vs 12.5 µs, S = 8 16.1 vs 16.6 with heavy
+        # blocks); from 16 on every column stays one wave, where the
+        # 1024-thread heavy blocks only fragment the CU (Cora S = 16 31.0 vs
+        # 30.9; Citeseer S = 16 73.4 vs 59.6 µs)
+        heavy = (lens > 128) if self.xt_splits <= 1 and self.S <= 8 else torch.zeros_like(lens, dtype=torch.bool)
         idx = torch.arange(self.fin, device=self.dev)
         self.xt_order = torch.cat([idx[heavy], idx[~heavy]]).to(torch.int32).contiguous()
         self.xt_heavy = int(heavy.sum())
