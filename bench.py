@@ -147,7 +147,8 @@ def algo_cost(name, eng, n_calls_per_window):
     graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)  # row_ptr, col, s, ELL head
     tri = n * (n + 1) // 2
     P = eng.np
-    if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex"):
+    if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex", "lds_theta_grad_sgd_draw"):
+        # (_draw: the next window's graph draw rides in the epilogue; priced on the θ-grad's flops)
         k = eng.S * eng.ldk if eng.S > 1 else eng.window_columns(eng.tau, eng.c)
         return "mfma", 6.0 * 4.0 * k * tri   # split bf16: six bf16 MFMA products per fp32 product
     if name == "lds_sample_graphs_multi":
@@ -155,6 +156,10 @@ def algo_cost(name, eng, n_calls_per_window):
         words = nat.lib.lds_bitmask_words(n)
         per = S * (3 * 8 * n * words + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)  # bits w/r/r, CSR, s, ELL
         return "hbm", 4 * tri + g * per      # θ read once per window
+    if name == "lds_sample_fill_csr":  # the fill alone: bits read, CSR / s / ELL written
+        g = eng.tau + 1
+        words = nat.lib.lds_bitmask_words(n)
+        return "hbm", g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)
     if name == "lds_engine_x_linear":
         return "hbm", S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act
     if name == "lds_engine_xt_adam":
@@ -247,7 +252,8 @@ def window_breakdown(eng, reducer, args, device, k=20):
     real = nat.call
 
     def rec(name, *a):
-        calls.append((name, a))
+        if name != "lds_theta_grad_set_form":  # a host-side query (the engine reads the θ-grad form), no launch
+            calls.append((name, a))
         real(name, *a)
 
     nat.call = rec
@@ -304,6 +310,8 @@ def roofline_of(row, args):
                 "frac": achieved / HBM_PEAK_GBS}
     roof.update(kernel=row["entry"], avg_us=row["avg_us"], launches_per_window=row["launches_per_window"],
                 share_of_window=None)
+    if row["entry"] == "lds_theta_grad_sgd_draw":  # priced on the assembly's flops alone
+        roof["includes"] = "the next window's graph draw (tau+1 graphs, Philox VALU) in the epilogue"
     roof["traffic"], roof["traffic_source"] = pmc_traffic(row["entry"], args)
     return roof
 
@@ -499,6 +507,9 @@ def main():
     ap.add_argument("--graph-windows", type=int, default=4,
                     help="τ-windows per captured HIP graph (N=1, engine path): replays run whole groups, "
                          "the remainder one window at a time")
+    ap.add_argument("--no-prefetch-draw", action="store_true",
+                    help="N=1 engine: each window draws its own graphs (default: the hyper step's θ-grad kernel "
+                         "draws the next window's, lds_theta_grad_sgd_draw)")
     ap.add_argument("--model", default="lds", choices=["lds", "gcn"],
                     help="lds: the LDS bilevel hot path (configs 2-5); gcn: config 1, fixed-graph GCN training")
     ap.add_argument("--dataset", default="cora", help="ldsgnn.data.workloads: cora (config 2, default), "
@@ -580,7 +591,8 @@ def main():
         use_graph = not args.eager and eng.theta_fn is None  # per-draw θ (GAE proposal dropout): eager windows
         if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
             eng.capture_window(args.tau, grad_reducer=reducer,
-                               windows=args.graph_windows if reducer is None else 1)
+                               windows=args.graph_windows if reducer is None else 1,
+                               prefetch=not args.no_prefetch_draw)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)
     else:
         step = run_steps(runner, 0, args.warmup, args.tau)
@@ -672,7 +684,8 @@ def main():
                        "theta_grad_form": ldsops.theta_grad_form(), "sampled_nnz": nnz,
                        "replicas_in_sync": in_sync, "graph_model": args.graph_model,
                        "windows_per_graph": (args.graph_windows if reducer is None else 1)
-                       if use_engine and use_graph else None},
+                       if use_engine and use_graph else None,
+                       "prefetched_draw": bool(use_engine and eng.prefetch_draw)},
             "steady_state": steady,
             "strong_scaling": strong,
             "window": window,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 8
+#define LDS_ABI_VERSION 9
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -114,6 +114,13 @@ int lds_sample_ws_ints(int n);
  * 0: one block per (tile, graph) unless θ exceeds 64 MB; -1: query.  Returns
  * the previous setting.  Process-wide, host-only. */
 int lds_sample_loop_graphs(int on);
+
+/* The fill launch of lds_sample_graphs_multi alone (CSR, s, ELL head of
+ * `graphs` graphs whose bits and degree counts are already drawn, e.g. by
+ * lds_theta_grad_sgd_draw); deg_ws as lds_sample_graphs_multi's. */
+int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_ws, int graphs,
+                        int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
+                        const uint8_t* node_flags, void* stream);
 
 /* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
  * b < samples, is draw counter *counter_base + counter_offset + g with tag
@@ -236,6 +243,20 @@ int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
 int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k,
                              const float* r, int ldr, int nr, float* theta, int n,
                              float* grad, const void* scalars, void* stream);
+
+/* lds_theta_grad_sgd (64-tile split-bf16 form, grouped order) that also draws
+ * the NEXT window's `graphs` graphs from the θ it writes: graph g takes draw
+ * counter counter_offset + g (+ *counter_base when non-NULL), bits and degree
+ * accumulators as lds_sample_graphs_multi's tile kernel (deg_ws zero on
+ * entry, lds_sample_ws_ints(n) ints per graph); the CSR fill is left to the
+ * caller.  Requires ld % 4 == 0, k % 8 == 0 and 16-byte aligned u, v.
+ * Replaces, fused: src/trainers/outer.py:77-81 (backward + SGD + clamp) and the
+ * next window's src/models/sampling.py:68 draws. */
+int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, int k,
+                            const float* r, int ldr, int nr, float* theta, int n,
+                            float* grad, const void* scalars, uint64_t seed, uint32_t tag,
+                            const uint32_t* counter_base, uint32_t counter_offset, int graphs,
+                            uint64_t* bits, int words, int* deg_ws, void* stream);
 
 /* General form of the assembly, for S replica samples per GPU (their factor
  * blocks side by side in U, V: k = S·ldk columns):
@@ -592,7 +613,7 @@ int lds_engine_xt_partials(const int* xcp, const int* xrow, const float* xval, i
 int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT,
                           float* w0, float* m0, float* v0, void* scalars, int graphs,
                           int forwards, int adam_steps, int hypers, const double* betas_dev,
-                          float* adam_tab, int tab_count, int* ws, int64_t ws_count,
+                          float* adam_tab, int tab_count, int* ws, int* ws_src, int64_t ws_count,
                           const LdsBatch* batch, void* stream);
 /* Adam table for the current scalars->adam_step (betas_dev = {β1, β2, lr}
  * doubles): entry k = {lr/(1-β1^(s+1+k)), sqrt(1-β2^(s+1+k))}, k < tab_count

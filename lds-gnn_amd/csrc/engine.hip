@@ -2009,12 +2009,21 @@ __global__ __launch_bounds__(256) void end_window_kernel(int np, const float* __
                                                          int graphs, int forwards, int adam_steps,
                                                          int hypers, const double* __restrict__ betas,
                                                          float* __restrict__ tab, int tab_count, int64_t par,
-                                                         int* __restrict__ ws, int64_t ws_count) {
+                                                         int* __restrict__ ws, int* __restrict__ ws_src,
+                                                         int64_t ws_count) {
     const int e = blockIdx.x * 256 + threadIdx.x;
     if (ws != nullptr) {  // the next window's sampler workspace (lds_sample_graphs_multi, ws_zeroed)
         const int64_t stride = (int64_t)gridDim.x * gridDim.y * 256;
-        for (int64_t k = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; k < ws_count; k += stride)
-            ws[k] = 0;
+        // ws_src (a prefetched draw's degrees, lds_theta_grad_sgd_draw): moved
+        // into ws for the next window's fill, and cleared for the next draw
+        for (int64_t k = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x; k < ws_count; k += stride) {
+            if (ws_src != nullptr) {
+                ws[k] = ws_src[k];
+                ws_src[k] = 0;
+            } else {
+                ws[k] = 0;
+            }
+        }
     }
     if (wT != nullptr && e < np) {
         const int64_t o = (int64_t)blockIdx.y * par;
@@ -2501,16 +2510,16 @@ extern "C" int lds_engine_xt_partials(const int* xcp, const int* xrow, const flo
 extern "C" int lds_engine_end_window(int np, const float* wT, const float* mT, const float* vT, float* w0,
                                      float* m0, float* v0, void* scalars, int graphs, int forwards,
                                      int adam_steps, int hypers, const double* betas_dev, float* adam_tab,
-                                     int tab_count, int* ws, int64_t ws_count, const LdsBatch* batch,
-                                     void* stream) {
+                                     int tab_count, int* ws, int* ws_src, int64_t ws_count,
+                                     const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(scalars && np > 0 && (wT == nullptr || (mT && vT && w0 && m0 && v0)) && batch_ok(batch));
-    LDS_CHECK_ARG(ws_count >= 0 && (ws != nullptr || ws_count == 0));
+    LDS_CHECK_ARG(ws_count >= 0 && (ws != nullptr || ws_count == 0) && (ws_src == nullptr || ws != nullptr));
     LDS_CHECK_ARG(adam_tab == nullptr || (betas_dev && tab_count > 0 && tab_count <= kAdamTabMax));
     Batch bt;
     const int ns = mk_batch(batch, bt);
     hipLaunchKernelGGL(end_window_kernel, dim3((np + 255) / 256, ns), dim3(256), 0, (hipStream_t)stream, np, wT,
                        mT, vT, w0, m0, v0, (EngineScalars*)scalars, graphs, forwards, adam_steps, hypers,
-                       betas_dev, adam_tab, tab_count, bt.par, ws, ws_count);
+                       betas_dev, adam_tab, tab_count, bt.par, ws, ws_src, ws_count);
     LDS_RETURN_LAST_ERROR();
 }
 

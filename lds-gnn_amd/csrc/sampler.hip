@@ -595,6 +595,18 @@ extern "C" int lds_sample_loop_graphs(int on) {
     return prev;
 }
 
+// The fill launch of lds_sample_graphs_multi alone, for graphs whose bits and
+// degree counts were drawn elsewhere (lds_theta_grad_sgd_draw).
+extern "C" int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_ws, int graphs,
+                                   int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
+                                   const uint8_t* node_flags, void* stream) {
+    LDS_CHECK_ARG(bits && deg_ws && row_ptr && col && s && n > 0 && n <= kEllIndex + 1 && col_stride > 0);
+    LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64);
+    hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 15) / 16, graphs), dim3(256), 0, (hipStream_t)stream, bits,
+                       n, words, deg_ws, lds_sample_ws_ints(n), row_ptr, col, col_stride, s, (int2*)ell, node_flags);
+    LDS_RETURN_LAST_ERROR();
+}
+
 extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                                        uint32_t tag_step, const uint32_t* counter_base,
                                        uint32_t counter_offset, int count, int samples, uint64_t* bits,

@@ -515,12 +515,28 @@ __device__ __forceinline__ void grouped_tile(int L, int nb, int G, int& bi, int&
     bj = i + rem;
 }
 
-template <int KC, bool VEC, bool PRE = false, bool PART = true>
+// The next window's graph draw, fused into the θ-grad epilogue (form 6, mode
+// 2): each block draws `graphs` Bernoulli graphs from the θ values its tile
+// just wrote (still in registers) — the sampler's tile draw (sampler.hip
+// sample_tiles_kernel<false, true, true>) with the same Philox words per
+// (row quad, column), the same bit rows / columns and degree atomics, so the
+// bits are identical to lds_sample_graphs_multi on the updated θ.
+struct DrawArgs {
+    uint64_t* bits;   // [graphs][n][words]
+    int words;
+    int* dacc;        // degree accumulators, wsi ints per graph, zero on entry
+    int wsi;
+    uint32_t k0, k1, tag, counter;
+    const uint32_t* counter_base;  // device draw counter (EngineScalars) or NULL
+    int graphs;
+};
+
+template <int KC, bool VEC, bool PRE = false, bool PART = true, bool DRAW = false>
 __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
-    float gscale, int group, int per_xcd, Planes pl) {
+    float gscale, int group, int per_xcd, Planes pl, DrawArgs dr = DrawArgs{}) {
     // (pre-split copies: planes 4 dwords past a multiple of 64 banks, ci_store)
     constexpr int S = Bf3Stage<KC>::kStr, PL = Bf3Stage<KC>::kPlane + (PRE ? 4 : 0);
     __shared__ __attribute__((aligned(16))) uint32_t lds[12 * PL];
@@ -645,10 +661,12 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     __syncthreads();
 
     const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+    uint32_t thr[16];  // DRAW: the next draw's integer thresholds (sampler.hip)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int li = wr * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
         const int i = i0 + li;
+        thr[e] = 0u;
         if (i >= n || j >= n || j < i) continue;
         const int64_t idx = tri_index(i, i, nn) + (j - i);
         float g = 0.f;
@@ -662,11 +680,74 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
             theta[idx] = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
         } else if (mode == 2) {
             if (grad != nullptr) grad[idx] = g;
-            theta[idx] = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
+            const float tn = fminf(fmaxf(fmaf(-lr, g, th[e]), 0.f), 1.f);
+            theta[idx] = tn;
+            if (DRAW && j > i) thr[e] = (uint32_t)ceilf(tn * 16777216.0f);
         } else if (mode == 1) {
             grad[idx] = part[e] + g;
         } else {
             grad[idx] = g;
+        }
+    }
+    if constexpr (DRAW) {
+        // rows of this lane: quad m = e >> 2 covers rows r4(m) .. r4(m) + 3 of column j
+        __shared__ uint32_t rw[64][2];   // row words: [row][column half]
+        __shared__ uint64_t cwp[2][64];  // column words: [wave row half][column]
+        const bool diag = i0 == j0;
+        const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
+        const int rq0 = (i0 + wr * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
+#pragma unroll 1
+        for (int gph = 0; gph < dr.graphs; ++gph) {
+            const uint32_t ctr = dr.counter + cb + (uint32_t)gph;
+            uint64_t* __restrict__ gb = dr.bits + (int64_t)gph * n * dr.words;
+            int* __restrict__ da = dr.dacc + (int64_t)gph * dr.wsi;
+            uint32_t x[16];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * m), dr.tag, ctr}, dr.k0, dr.k1);
+                x[4 * m] = o.x;
+                x[4 * m + 1] = o.y;
+                x[4 * m + 2] = o.z;
+                x[4 * m + 3] = o.w;
+            }
+            uint64_t colw = 0;
+            uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const bool bit = (x[e] >> 8) < thr[e];
+                const uint64_t w = __ballot(bit);
+                mylo = lane == e ? (uint32_t)w : mylo;
+                myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                colw |= (uint64_t)bit << ((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5) + wr * 32);
+            }
+            colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+            if (lane < 16) {  // element e = lane: rows r (h = 0) and r + 4 (h = 1), columns wc·32 …
+                const int r = wr * 32 + (lane & 3) + 8 * (lane >> 2);
+                rw[r][wc] = mylo;
+                rw[r + 4][wc] = myhi;
+            }
+            if (lane < 32) cwp[wr][wc * 32 + lane] = colw;
+            __syncthreads();
+            if (t < 64) {
+                const uint64_t roww = (uint64_t)rw[t][0] | ((uint64_t)rw[t][1] << 32);
+                const int jj = j0 + t, ii = i0 + t;
+                uint64_t out = cwp[0][t] | cwp[1][t];
+                if (!diag) {
+                    if (ii < n) {
+                        gb[(int64_t)ii * dr.words + (j0 >> 6)] = roww;
+                        const int pc = __popcll(roww);
+                        if (pc != 0) atomicAdd(&da[ii], pc);
+                    }
+                } else {
+                    out |= roww | (1ull << t);  // self-loop: diagonal set to 1
+                }
+                if (jj < n) {
+                    gb[(int64_t)jj * dr.words + (i0 >> 6)] = out;
+                    const int pc = __popcll(out);
+                    if (pc != 0) atomicAdd(&da[jj], pc);
+                }
+            }
+            if (gph + 1 < dr.graphs) __syncthreads();  // rw / cwp reused by the next graph
         }
     }
 }
@@ -1360,6 +1441,27 @@ extern "C" int lds_split_planes(const float* x, int rows, int ld, int k, uint16_
     const int64_t tot = (int64_t)rows * k;
     hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
                        rows, ld, k, planes);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, int k, const float* r,
+                                       int ldr, int nr, float* theta, int n, float* grad, const void* scalars,
+                                       uint64_t seed, uint32_t tag, const uint32_t* counter_base,
+                                       uint32_t counter_offset, int graphs, uint64_t* bits, int words,
+                                       int* deg_ws, void* stream) {
+    LDS_CHECK_ARG(u && v && theta && scalars && bits && deg_ws && n > 0 && k >= 0 && ld >= k);
+    LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64 && nr >= 0);
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
+    LDS_CHECK_ARG((ld & 3) == 0 && (k & 7) == 0 && ((uintptr_t)u & 15) == 0 && ((uintptr_t)v & 15) == 0);
+    const int nb = (n + kTile - 1) / kTile;
+    const int ntiles = nb * (nb + 1) / 2;
+    const int per = (ntiles + 7) / 8;
+    const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
+    DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                counter_offset, counter_base, graphs};
+    hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, false, true, true>), dim3(8 * per), dim3(256), 0,
+                       (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup, per,
+                       Planes{nullptr, nullptr}, dr);
     LDS_RETURN_LAST_ERROR();
 }
 

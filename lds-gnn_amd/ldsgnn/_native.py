@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -36,6 +36,7 @@ SIGNATURES = {
     "lds_sample_graphs_multi": [P, c_int, c_uint64, c_uint32, c_uint32, P, c_uint32, c_int, c_int, P, c_int, P,
                                 P, P, c_int64, P, P, P, c_int, P],
     "lds_sample_ws_ints": [c_int],
+    "lds_sample_fill_csr": [P, c_int, c_int, P, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_loop_graphs": [c_int],
     "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
     "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
@@ -54,6 +55,8 @@ SIGNATURES = {
     "lds_theta_grad_set_form": [c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
     "lds_theta_grad_sgd_accum": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
+    "lds_theta_grad_sgd_draw": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_uint64, c_uint32, P,
+                                c_uint32, c_int, P, c_int, P, P],
     "lds_slot_factors": [P, c_int, P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, P, c_int, P,
                          c_int, P, c_int, P],
     "lds_sgd_clamp": [P, P, c_float, c_int64, P],
@@ -102,7 +105,7 @@ SIGNATURES = {
                              c_int, P, P, P],
     "lds_engine_rev_bc": [P, P, P, P, c_int, P, c_int, P, P, P, P, P, P, c_float, c_int, P, P, P, P, P, c_uint64,
                           c_uint32, P, c_int, c_int, c_float, c_float, P, P, c_int, P, c_int, c_int, c_int, P, P, P],
-    "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int64,
+    "lds_engine_end_window": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, P, P, c_int64,
                               P, P],
     "lds_engine_adam_table": [P, P, P, c_int, P],
 }

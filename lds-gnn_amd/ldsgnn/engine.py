@@ -231,6 +231,13 @@ class LdsEngine:
         S = self.S
         self.deg = torch.empty((S, int(nat.lib.lds_sample_ws_ints(n))), dtype=torch.int32, device=dev)
         self._ws_clean = True  # gbatch.deg is zero (fresh, or cleared by the last end_window)
+        # prefetched draws (capture_window(prefetch=True)): the hyper step's
+        # θ-grad kernel also draws the NEXT window's graphs from the θ it writes
+        # (lds_theta_grad_sgd_draw, degrees into deg_next, moved to gbatch.deg
+        # by end_window), and the next window only fills CSR / s / ELL
+        self.prefetch_draw = False
+        self._prefetched = False
+        self._deg_next = None
 
         # tape
         self.tau = max(1, int(tau))
@@ -416,6 +423,7 @@ class LdsEngine:
     def set_params(self, params):
         """Load reference-layout params (layer_in.fc.weight [16, fin], ...)
         into every replica sample (all chains start from the same GCN)."""
+        self._drop_prefetch()
         for b in range(self.S):
             self._write_params(self.w[0][b], params)
         self.t = 0
@@ -440,6 +448,7 @@ class LdsEngine:
         the reference's samples take RNG draws), eval-mode forward with the
         flat parameters, NLL / accuracy on the validation and test masks,
         averaged over samples; one host sync.  Single-sample engines."""
+        self._drop_prefetch()
         if self.S != 1:
             raise NotImplementedError("empirical_mean runs on single-sample engines")
         if not self.long_rows:
@@ -567,6 +576,7 @@ class LdsEngine:
     def _sample(self, g: _Graph, theta: torch.Tensor = None):
         """Draw the next graph of every replica sample into `g` (from `theta`,
         default self.theta)."""
+        self._drop_prefetch()
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta if theta is None else theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(g.bits), self.words,
                  nat.ptr(self.deg), nat.ptr(g.row_ptr), self._col_arg(g.col), self.cap, nat.ptr(g.s),
@@ -750,12 +760,41 @@ class LdsEngine:
         takes draw counter (pending + g), exactly the counter the step-by-step
         path would give it."""
         gb = self.gbatch
-        nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
-                 nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
-                 nat.ptr(gb.deg), nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s),
-                 nat.ptr(gb.ell), nat.ptr(self.nflag), 1 if self._ws_clean else 0, self._stream())
+        if self._prefetched:  # bits + degrees drawn by the last hyper step (lds_theta_grad_sgd_draw)
+            nat.call("lds_sample_fill_csr", nat.ptr(gb.bits), self.n, self.words, nat.ptr(gb.deg), count * self.S,
+                     nat.ptr(gb.row_ptr), nat.ptr(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell),
+                     nat.ptr(self.nflag), self._stream())
+            self._prefetched = False
+        else:
+            nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
+                     nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
+                     nat.ptr(gb.deg), nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s),
+                     nat.ptr(gb.ell), nat.ptr(self.nflag), 1 if self._ws_clean else 0, self._stream())
         self._ws_clean = False
         self._block_ptrs(gb.graphs[:count])
+
+    def _drop_prefetch(self):
+        """A draw or counter use outside a window replay: the prefetched
+        graphs are discarded (the next window draws its own with the counters
+        it then finds); gbatch.deg holds their degrees, so it is cleared first."""
+        if self._prefetched:
+            self._prefetched = False
+            self._ws_clean = False
+
+    def _prefetch_ok(self, T: int, k0: int) -> bool:
+        """The next window's draw can ride in this hyper step's θ-grad kernel:
+        single sample, plain LDS θ, a full window, CSR graphs, and the 64-tile
+        split-bf16 form with aligned operands (lds_theta_grad_sgd_draw)."""
+        from .ops import theta_grad_form
+        if not (self.prefetch_draw and self.S == 1 and self.theta_fn is None and self.outer_update is None
+                and not self.bitmask_agg and T == self.tau and self.gbatch.count == self.tau + 1):
+            return False
+        form = theta_grad_form()
+        nb2 = (self.n + 127) // 128
+        by_shape_64 = form == "bf16x3" and nb2 * (nb2 + 1) // 2 < 1024 and k0 < 1024
+        if not (by_shape_64 or form == "bf16x3-t64k16-grouped"):
+            return False
+        return self.ldk % 4 == 0 and k0 % 8 == 0 and nat.ptr(self.U) % 16 == 0 and nat.ptr(self.V) % 16 == 0
 
     def inner_step(self, presampled: bool = False):
         """One InnerProblemTrainer.train_step (sample + forward + backward +
@@ -791,6 +830,9 @@ class LdsEngine:
         """OuterProblemTrainer.train_step + both detaches.  Returns the device
         metrics row [Σ NLL over opt rows, #correct]."""
         st, n, c = self._stream(), self.n, self.c
+        drew = False
+        if not presampled:
+            self._drop_prefetch()
         if self.outer_update is not None:
             if self.S > 1:
                 raise NotImplementedError("outer_update (θ as a function of model parameters) is single-sample")
@@ -840,6 +882,15 @@ class LdsEngine:
             if split:
                 nat.call("lds_theta_grad_sgd_accum", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0,
                          nat.ptr(self.R), 1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad), nat.ptr(self.scalars), st)
+            elif presampled and self._prefetch_ok(T, k0):  # + the next window's draw, from the θ written here
+                if self._deg_next is None:
+                    self._deg_next = torch.zeros_like(self.gbatch.deg)
+                gb = self.gbatch
+                nat.call("lds_theta_grad_sgd_draw", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R),
+                         1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
+                         nat.ptr(self.scalars), self.seed, self.tag_graph, nat.ptr(self.scalars), self.pending_graph,
+                         gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next), st)
+                drew = True
             else:
                 nat.call("lds_theta_grad_sgd", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1,
                          1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
@@ -852,12 +903,15 @@ class LdsEngine:
                 nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
                          nat.ptr(self.scalars), st)
         # detach: the window restarts from the latest weights / Adam state
+        # (a prefetched draw's degrees move into gbatch.deg for the next fill)
         P = nat.ptr
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
         nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
                  P(self.scalars), self.pending_graph, self.pending_fwd, T, 1, P(self.betas_dev), P(self.adam_tab),
-                 self._tab_count(), P(self.gbatch.deg), self.gbatch.deg.numel(), self.bt, st)
-        self._ws_clean = True
+                 self._tab_count(), P(self.gbatch.deg), P(self._deg_next) if drew else 0, self.gbatch.deg.numel(),
+                 self.bt, st)
+        self._prefetched = drew
+        self._ws_clean = not drew
         self.pending_graph = 0
         self.pending_fwd = 0
         self.t = 0
@@ -903,6 +957,7 @@ class LdsEngine:
         own R row) and hands the stack [T + 1, n(n+1)/2] to the reducer
         (outer_update), which takes each through its own P_t.  Single sample,
         eager windows."""
+        self._drop_prefetch()
         if self.S != 1:
             raise NotImplementedError("per-draw θ is single-sample")
         self.theta_fn = fn
@@ -914,11 +969,12 @@ class LdsEngine:
         of the current step become slot 0, the pending draw counters and Adam
         steps are applied on device (lds_engine_end_window with no hyper step:
         no learning-rate decay)."""
+        self._drop_prefetch()
         T, P, st = self.t, nat.ptr, self._stream()
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
         nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
                  P(self.scalars), self.pending_graph, self.pending_fwd, T, 0, P(self.betas_dev), P(self.adam_tab),
-                 self._tab_count(), P(self.gbatch.deg), self.gbatch.deg.numel(), self.bt, st)
+                 self._tab_count(), P(self.gbatch.deg), 0, self.gbatch.deg.numel(), self.bt, st)
         self._ws_clean = True
         self.pending_graph = 0
         self.pending_fwd = 0
@@ -941,6 +997,7 @@ class LdsEngine:
     def _sample_per_draw(self, g: _Graph, slot: int):
         """θ_slot = theta_fn(absolute forward counter), then the draw from it;
         the model's forward takes that counter (pending_fwd += 1)."""
+        self._drop_prefetch()
         self._per_draw_bufs(max(slot + 1, self.tau + 1))
         c = int(self._i32[1].item()) + self.pending_fwd  # device counter + this window's pending forwards
         self.theta_g[slot].copy_(self.theta_fn(c))
@@ -973,7 +1030,7 @@ class LdsEngine:
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
         nat.call("lds_engine_end_window", self.np, *wmv, P(self.w[0]), P(self.m[0]), P(self.v[0]),
                  P(self.scalars), self.pending_graph, self.pending_fwd, T, 1, P(self.betas_dev), P(self.adam_tab),
-                 self._tab_count(), P(self.gbatch.deg), self.gbatch.deg.numel(), self.bt, st)
+                 self._tab_count(), P(self.gbatch.deg), 0, self.gbatch.deg.numel(), self.bt, st)
         self._ws_clean = True
         self.pending_graph = 0
         self.pending_fwd = 0
@@ -1098,7 +1155,7 @@ class LdsEngine:
             self.inner_step(presampled=batch)
         return self.hyper_step(grad_reducer=grad_reducer, presampled=batch)
 
-    def capture_window(self, tau: int, grad_reducer=None, windows: int = 1):
+    def capture_window(self, tau: int, grad_reducer=None, windows: int = 1, prefetch: bool = False):
         """Record run_window(tau) as HIP graphs (state must be at a window
         start).  Replays advance RNG counters, Adam step and lr on device.
 
@@ -1106,7 +1163,13 @@ class LdsEngine:
         SGD step); `windows` > 1 also records that many consecutive windows as
         one graph, which replay() uses for whole groups (the launches of every
         window are the same, so no boundary between two graph launches falls
-        inside a group).  With a reducer (replicas over RCCL) the window is
+        inside a group).  `prefetch` (single sample, 64-tile θ-grad shapes;
+        ignored elsewhere): each window's hyper step also draws the next
+        window's graphs from the θ it writes (lds_theta_grad_sgd_draw), so a
+        window starts with the CSR fill only; the graphs of the first replayed
+        window are drawn here, eagerly.  Same draws, same counters, same
+        results as windows that draw their own graphs.  With a reducer
+        (replicas over RCCL) the window is
         split at the exchange: graph A runs up to dθ, `grad_reducer(grad)`
         runs eagerly between the replays (the collective stays outside the
         captured work), graph B applies SGD + clamp and the detach."""
@@ -1123,6 +1186,15 @@ class LdsEngine:
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
+            if prefetch:
+                self.prefetch_draw = True
+                if not self._prefetch_ok(tau, tau * self.kg + HID + self.cw):
+                    self.prefetch_draw = False
+                elif not self._prefetched:
+                    if self._deg_next is None:
+                        self._deg_next = torch.zeros_like(self.gbatch.deg)
+                    self._sample_batch(tau + 1)  # the first replayed window's graphs, drawn now
+                    self._prefetched = True
             graphs = []
             for w in sorted({1, windows}):
                 graph = torch.cuda.CUDAGraph()

@@ -419,3 +419,36 @@ def test_runner_control_loop_kats(fused):
                      outer_loop_max_epochs=outer_max, sacred_runner=lambda n, v, s=None: rec.append(n))
         assert rec.count("loss.train") == want_inner
         assert rec.count("loss.outer") == want_hyper
+
+
+@pytest.mark.parametrize("group,windows", [(1, 3), (2, 5)])
+def test_prefetched_draw_replay_equals_eager(group, windows):
+    """capture_window(prefetch=True): every hyper step's θ-grad kernel draws
+    the next window's graphs from the θ it writes and the window only fills
+    CSR / s / ELL (lds_theta_grad_sgd_draw + lds_sample_fill_csr).  Same
+    counters, same draws: bitwise-identical θ, weights and device scalars to
+    windows that draw their own graphs, also after leaving prefetch mode for
+    eager windows (the prefetched graphs are dropped and redrawn)."""
+    a = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    b = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    a.capture_window(5, windows=group, prefetch=True)
+    assert a.prefetch_draw and a._prefetched
+    a.replay(windows)
+    for _ in range(windows):
+        b.run_window(5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+    assert a.scalars_host() == b.scalars_host()
+    # an out-of-window draw drops the prefetch; eager windows continue identically
+    a.inner_step()
+    b.inner_step()
+    a.hyper_step()
+    b.hyper_step()
+    a.run_window(5)
+    b.run_window(5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k

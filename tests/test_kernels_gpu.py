@@ -578,3 +578,51 @@ def test_theta_grad_pipe_bit_exact(device, n, k, mode):
             ops.theta_grad_form(prev)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,k,graphs", [(2708, 264, 6), (300, 40, 3), (130, 8, 1), (700, 24, 2)])
+def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs):
+    """lds_theta_grad_sgd_draw (the 64-tile θ-grad with SGD + clamp, drawing
+    the next window's graphs from the θ it writes) against lds_theta_grad_sgd
+    followed by single lds_sample_bitmask draws of the updated θ: identical θ,
+    identical bit rows (graph g draws counter base + offset + g) and degree
+    counts equal to the rows' popcounts."""
+    g = torch.Generator().manual_seed(n + k + graphs)
+    ld = k + 8
+    u = torch.randn(n, ld, generator=g).to(device)
+    v = (torch.randn(n, ld, generator=g) * 0.3).to(device)
+    r = torch.randn(n, generator=g).to(device)
+    theta = (torch.rand(n * (n + 1) // 2, generator=g) * 0.4).to(device)
+    scal = torch.zeros(64, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(0.05)
+    st = nat.stream_of(torch.device(device))
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    base = torch.tensor([11, 0, 0, 0], dtype=torch.int32, device=device)
+    seed, tag, off = 4321, tag_for(TAG_GRAPH, 3), 6
+    prev = ops.theta_grad_form("bf16x3-t64k16-grouped")
+    try:
+        th1 = theta.clone()
+        nat.call("lds_theta_grad_sgd", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th1), n, 0,
+                 nat.ptr(scal), st)
+    finally:
+        ops.theta_grad_form(prev)
+    th2 = theta.clone()
+    bits = torch.zeros((graphs, n, words), dtype=torch.int64, device=device)
+    deg = torch.zeros((graphs, wsi), dtype=torch.int32, device=device)
+    nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th2), n, 0,
+             nat.ptr(scal), seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg), st)
+    torch.cuda.synchronize()
+    assert torch.equal(th1, th2)
+    one = torch.empty((n, words), dtype=torch.int64, device=device)
+    nb = (n + 63) // 64
+    for gi in range(graphs):
+        nat.call("lds_sample_bitmask", nat.ptr(th1), n, seed, tag, 11 + off + gi, 0, nat.ptr(one), words, st)
+        torch.cuda.synchronize()
+        assert torch.equal(bits[gi, :, :nb], one[:, :nb]), gi
+        pc = torch.zeros(n, dtype=torch.int64, device=device)
+        for w in range(nb):
+            x = one[:, w]
+            for b in range(64):
+                pc += (x >> b) & 1
+        assert torch.equal(deg[gi, :n].long(), pc), gi

@@ -24,7 +24,11 @@ ENTRY_KERNELS = {
     # the window's batched draw: graphs looped in the tile kernel (kLoop, kDeg) + the fused fill
     # (the single-graph <false, false, true> draws of the step-0 window are not this entry's launches)
     "lds_sample_graphs_multi": ["lds::sample_tiles_kernel<false, true, true>", "lds::fill_csr_fused_kernel"],
-    "lds_theta_grad_sgd": ["theta_grad"],
+    "lds_sample_fill_csr": ["lds::fill_csr_fused_kernel"],
+    # θ-grad + SGD; with the next window's draw fused in: the DRAW = true instance
+    "lds_theta_grad_sgd": ["theta_grad_bf3_kernel<16, true, false, true, false>", "theta_grad_bf3_t128",
+                           "theta_grad_bf3_pipe", "theta_grad_mfma"],
+    "lds_theta_grad_sgd_draw": ["theta_grad_bf3_kernel<16, true, false, true, true>"],
     "lds_engine_x_linear": ["x_linear_kernel"],
     "lds_engine_fwd_layer1": ["fwd_layer1_kernel"],
     "lds_engine_fwd_layer2": ["fwd_layer2_kernel"],
