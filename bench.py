@@ -661,6 +661,7 @@ def main():
             window["bitmask_aggregation"] = roofline_of(agg_rows[0], args)
             window["bitmask_aggregation"]["share_of_window"] = agg_rows[0]["us_per_window"] / total
 
+    prefetched = bool(use_engine and eng.prefetch_draw)  # (the strong leg below frees the engine)
     strong = None
     if use_engine and args.strong_total and not param_theta:
         del eng
@@ -685,7 +686,7 @@ def main():
                        "replicas_in_sync": in_sync, "graph_model": args.graph_model,
                        "windows_per_graph": (args.graph_windows if reducer is None else 1)
                        if use_engine and use_graph else None,
-                       "prefetched_draw": bool(use_engine and eng.prefetch_draw)},
+                       "prefetched_draw": prefetched},
             "steady_state": steady,
             "strong_scaling": strong,
             "window": window,
