@@ -115,6 +115,17 @@ int lds_sample_ws_ints(int n);
  * the previous setting.  Process-wide, host-only. */
 int lds_sample_loop_graphs(int on);
 
+/* The outer SGD step + clamp of lds_engine_sgd_clamp fused with the NEXT
+ * window's draw from the θ it writes (`count` graphs × `samples` replicas,
+ * counters / tags as lds_sample_graphs_multi, the graph counter and the f64
+ * lr read from the engine's `scalars`); bits and degree counts as
+ * lds_sample_graphs_multi's tile kernel (deg_ws zero on entry), no fill.
+ * Replaces, fused: src/trainers/outer.py:78-81 (SGD + clamp after the
+ * all-reduce) and the next window's src/models/sampling.py:68 draws. */
+int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, int n, uint64_t seed,
+                          uint32_t tag, uint32_t tag_step, uint32_t counter_offset, int count,
+                          int samples, uint64_t* bits, int words, int* deg_ws, void* stream);
+
 /* The fill launch of lds_sample_graphs_multi alone (CSR, s, ELL head of
  * `graphs` graphs whose bits and degree counts are already drawn, e.g. by
  * lds_theta_grad_sgd_draw); deg_ws as lds_sample_graphs_multi's. */

@@ -39,12 +39,17 @@ namespace lds {
 // on entry.  (Per-64-row-block totals kept the same way cost 2x the kernel's
 // time: ~10^4 atomics per graph on three cache lines serialise at the memory
 // side.)
-template <bool kInj, bool kLoop, bool kDeg>
+// kSgd (lds_sgd_sample_graphs, one block per tile, kLoop): the tile first
+// applies the outer SGD step θ <- clamp(θ - lr·g, 0, 1) (lr = the engine's
+// device f64 at lr_dev; the arithmetic of lds_engine_sgd_clamp) to every
+// packed entry it owns (i <= j) and writes it back, then draws from the new θ.
+template <bool kInj, bool kLoop, bool kDeg, bool kSgd = false>
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
     uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs,
-    int* __restrict__ dacc, int wsi) {
+    int* __restrict__ dacc, int wsi, float* __restrict__ theta_w = nullptr,
+    const float* __restrict__ grad = nullptr, const double* __restrict__ lr_dev = nullptr) {
     __shared__ uint32_t colpart[4][64];  // wave w's column bits (rows 16w .. 16w+15 of the tile)
     __shared__ uint64_t rowword[64];
     const int tile = blockIdx.x;
@@ -67,10 +72,25 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const int r0 = bi * 64 + wave * 16;  // first row of this wave
 
     float th[16];
+    if constexpr (kSgd) {
+        const float lr = (float)*lr_dev;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int i = r0 + r;
-        th[r] = (i < j && j < n) ? theta[tri_index(i, j, nn)] : -1.0f;  // i < n follows
+        for (int r = 0; r < 16; ++r) {
+            const int i = r0 + r;
+            th[r] = -1.0f;
+            if (i <= j && j < n) {
+                const int64_t idx = tri_index(i, j, nn);
+                const float t = fminf(fmaxf(fmaf(-lr, grad[idx], theta_w[idx]), 0.f), 1.f);  // θ via theta_w only
+                theta_w[idx] = t;
+                if (i < j) th[r] = t;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int i = r0 + r;
+            th[r] = (i < j && j < n) ? theta[tri_index(i, j, nn)] : -1.0f;  // i < n follows
+        }
     }
     // Edge (i, j) iff u < clamp(θ, 0, 1) (triu_values_to_symmetric_matrix,
     // src/utils/graph.py:180; θ = -1 marks pairs outside the strict upper
@@ -593,6 +613,28 @@ extern "C" int lds_sample_loop_graphs(int on) {
     const int prev = g_sample_loop_graphs;
     if (on >= 0) g_sample_loop_graphs = on ? 1 : 0;
     return prev;
+}
+
+// The outer SGD step + clamp (lds_engine_sgd_clamp) and the NEXT window's
+// draw of `count` graphs × `samples` replicas from the θ it writes, in one
+// pass over the triangle: graph g, sample b takes counter counter_offset + g
+// + the scalars' graph counter and tag + b·tag_step, as lds_sample_graphs_multi;
+// bits and degree counts as its tile kernel (deg_ws zero on entry); the fill
+// is left to the caller (lds_sample_fill_csr).  `scalars`: the engine's
+// EngineScalars (graph counter at byte 0, f64 lr at byte 16).
+extern "C" int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, int n, uint64_t seed,
+                                     uint32_t tag, uint32_t tag_step, uint32_t counter_offset, int count,
+                                     int samples, uint64_t* bits, int words, int* deg_ws, void* stream) {
+    LDS_CHECK_ARG(theta && grad && scalars && bits && deg_ws && n > 0 && n <= (1 << 20));
+    LDS_CHECK_ARG(count > 0 && samples > 0 && (int64_t)count * samples <= 65535 && words >= (n + 63) / 64);
+    const int nb = (n + 63) / 64;
+    const int ntiles = nb * (nb + 1) / 2;
+    const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true, true>), dim3(ntiles, 1, 1), dim3(256),
+                       0, (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
+                       (const uint32_t*)scalars, (const float*)nullptr, bits, words, ntiles, tag_step, samples, count,
+                       deg_ws, lds_sample_ws_ints(n), theta, grad, lr);
+    LDS_RETURN_LAST_ERROR();
 }
 
 // The fill launch of lds_sample_graphs_multi alone, for graphs whose bits and

@@ -781,13 +781,19 @@ class LdsEngine:
             self._prefetched = False
             self._ws_clean = False
 
-    def _prefetch_ok(self, T: int, k0: int) -> bool:
-        """The next window's draw can ride in this hyper step's θ-grad kernel:
-        single sample, plain LDS θ, a full window, CSR graphs, and the 64-tile
-        split-bf16 form with aligned operands (lds_theta_grad_sgd_draw)."""
+    def _prefetch_ok(self, T: int, k0: int, exchange: bool = False) -> bool:
+        """The next window's draw can ride in this hyper step: plain LDS θ, a
+        full window, CSR graphs; with an exchange (dθ all-reduced before the
+        SGD step) in the SGD + clamp pass (lds_sgd_sample_graphs, any S),
+        else in the θ-grad kernel: single sample, the 64-tile split-bf16 form
+        with aligned operands (lds_theta_grad_sgd_draw)."""
         from .ops import theta_grad_form
-        if not (self.prefetch_draw and self.S == 1 and self.theta_fn is None and self.outer_update is None
+        if not (self.prefetch_draw and self.theta_fn is None and self.outer_update is None
                 and not self.bitmask_agg and T == self.tau and self.gbatch.count == self.tau + 1):
+            return False
+        if exchange:
+            return True
+        if self.S != 1:
             return False
         form = theta_grad_form()
         nb2 = (self.n + 127) // 128
@@ -877,7 +883,7 @@ class LdsEngine:
         else:
             k0 = T * self.kg + HID + self.cw
         if self.S > 1:
-            self._assemble_samples(k0, grad_reducer)
+            drew = self._assemble_samples(k0, grad_reducer, presampled)
         elif grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
             if split:
                 nat.call("lds_theta_grad_sgd_accum", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0,
@@ -900,8 +906,7 @@ class LdsEngine:
                      nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, st)
             grad_reducer(self.grad)  # with outer_update: the model's optimizer step, which rewrites θ
             if self.outer_update is None:
-                nat.call("lds_engine_sgd_clamp", nat.ptr(self.theta), nat.ptr(self.grad), self.theta.numel(),
-                         nat.ptr(self.scalars), st)
+                drew = self._sgd_step(T, k0, presampled)
         # detach: the window restarts from the latest weights / Adam state
         # (a prefetched draw's degrees move into gbatch.deg for the next fill)
         P = nat.ptr
@@ -917,7 +922,22 @@ class LdsEngine:
         self.t = 0
         return self.metrics[self.tau]
 
-    def _assemble_samples(self, k0: int, grad_reducer):
+    def _sgd_step(self, T: int, k0: int, presampled: bool) -> bool:
+        """SGD + clamp of θ after the exchange; with prefetched draws fused
+        with the next window's draw (lds_sgd_sample_graphs).  True if it drew."""
+        st, P = self._stream(), nat.ptr
+        if presampled and self._prefetch_ok(T, k0, exchange=True):
+            if self._deg_next is None:
+                self._deg_next = torch.zeros_like(self.gbatch.deg)
+            gb = self.gbatch
+            nat.call("lds_sgd_sample_graphs", P(self.theta), P(self.grad), P(self.scalars), self.n, self.seed,
+                     self.tag_graph, 1, self.pending_graph, gb.count, self.S, P(gb.bits), self.words,
+                     P(self._deg_next), st)
+            return True
+        nat.call("lds_engine_sgd_clamp", P(self.theta), P(self.grad), self.theta.numel(), P(self.scalars), st)
+        return False
+
+    def _assemble_samples(self, k0: int, grad_reducer, presampled: bool = False) -> bool:
         """Mean hypergradient of the S replica samples: one rank-(S·ldk)
         update over the side-by-side factor blocks (columns past k0 of each
         block zeroed first), R summed over the S stacked rows, gscale = 1/S;
@@ -935,7 +955,8 @@ class LdsEngine:
             nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
                      P(self.theta), n, P(self.grad), 0, 0, gs, st)
             grad_reducer(self.grad)
-            nat.call("lds_engine_sgd_clamp", P(self.theta), P(self.grad), self.theta.numel(), P(self.scalars), st)
+            return self._sgd_step(self.tau if presampled else -1, k0, presampled)
+        return False
 
     def _theta_chunk(self, col0: int, k: int, accumulate: int):
         """grad (=|+=) U[:, col0:col0+k] V[...]ᵀ + V U ᵀ on the side stream, after
@@ -1183,18 +1204,18 @@ class LdsEngine:
             raise ValueError("windows >= 1")
         if grad_reducer is None:
             grad_reducer = self.grad_reducer
+        if prefetch:
+            self.prefetch_draw = True
+            if not self._prefetch_ok(tau, tau * self.kg + HID + self.cw, exchange=grad_reducer is not None):
+                self.prefetch_draw = False
+            elif not self._prefetched:
+                if self._deg_next is None:
+                    self._deg_next = torch.zeros_like(self.gbatch.deg)
+                self._sample_batch(tau + 1)  # the first replayed window's graphs, drawn now
+                self._prefetched = True
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
-            if prefetch:
-                self.prefetch_draw = True
-                if not self._prefetch_ok(tau, tau * self.kg + HID + self.cw):
-                    self.prefetch_draw = False
-                elif not self._prefetched:
-                    if self._deg_next is None:
-                        self._deg_next = torch.zeros_like(self.gbatch.deg)
-                    self._sample_batch(tau + 1)  # the first replayed window's graphs, drawn now
-                    self._prefetched = True
             graphs = []
             for w in sorted({1, windows}):
                 graph = torch.cuda.CUDAGraph()

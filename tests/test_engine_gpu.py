@@ -452,3 +452,34 @@ def test_prefetched_draw_replay_equals_eager(group, windows):
     assert torch.equal(a.theta, b.theta)
     for k, v in a.get_params().items():
         assert torch.equal(v, b.get_params()[k]), k
+
+
+@pytest.mark.parametrize("samples", [1, 3])
+def test_prefetched_draw_with_exchange_equals_eager(samples):
+    """With an exchange between dθ and the SGD step (the N > 1 path: graph A,
+    the reducer, graph B), capture_window(prefetch=True) fuses the SGD + clamp
+    with the next window's draw (lds_sgd_sample_graphs).  Against eager
+    windows with the same reducer (here: dθ halved, a stand-in for the
+    all-reduce mean): bitwise-identical θ, weights and device scalars."""
+    from tests.parity_harness import run_engine_samples_and_oracle
+
+    def half(grad):
+        grad.mul_(0.5)
+
+    def mk():
+        if samples == 1:
+            return run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+        return run_engine_samples_and_oracle(samples=samples, n=150, f_in=26, classes=5, steps=1, tau=5,
+                                             dropout=0.5, seed=7, replica0=2)["engine"]
+    a, b = mk(), mk()
+    a.capture_window(5, grad_reducer=half, prefetch=True)
+    assert a.prefetch_draw and a._prefetched
+    a.replay(3)
+    for _ in range(3):
+        b.run_window(5, grad_reducer=half)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for s in range(samples):
+        for k, v in a.get_params(s).items():
+            assert torch.equal(v, b.get_params(s)[k]), (s, k)
+    assert a.scalars_host() == b.scalars_host()
