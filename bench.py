@@ -398,7 +398,8 @@ def strong_scaling_leg(args, world, rank, device, barrier_sync):
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
         # T1 replays whole groups of windows per graph as the N = 1 line does
-        eng.capture_window(args.tau, grad_reducer=reducer, windows=args.graph_windows if reducer is None else 1)
+        eng.capture_window(args.tau, grad_reducer=reducer, windows=args.graph_windows if reducer is None else 1,
+                           prefetch=not args.no_prefetch_draw)  # (T1, S_total samples, no exchange: not eligible)
         eng.replay(1)
         if reducer_world > 1:
             barrier_sync()
