@@ -773,6 +773,11 @@ class LdsEngine:
         self._ws_clean = False
         self._block_ptrs(gb.graphs[:count])
 
+    def discard_prefetched_draws(self):
+        """Forget graphs a hyper step drew for the next window (θ about to be
+        rewritten from outside the engine); the next window draws its own."""
+        self._drop_prefetch()
+
     def _drop_prefetch(self):
         """A draw or counter use outside a window replay: the prefetched
         graphs are discarded (the next window draws its own with the counters
@@ -1184,12 +1189,17 @@ class LdsEngine:
         SGD step); `windows` > 1 also records that many consecutive windows as
         one graph, which replay() uses for whole groups (the launches of every
         window are the same, so no boundary between two graph launches falls
-        inside a group).  `prefetch` (single sample, 64-tile θ-grad shapes;
-        ignored elsewhere): each window's hyper step also draws the next
-        window's graphs from the θ it writes (lds_theta_grad_sgd_draw), so a
-        window starts with the CSR fill only; the graphs of the first replayed
-        window are drawn here, eagerly.  Same draws, same counters, same
-        results as windows that draw their own graphs.  With a reducer
+        inside a group).  `prefetch`: each window's hyper step also draws
+        the next window's graphs from the θ it writes — in the θ-grad kernel
+        (lds_theta_grad_sgd_draw; single sample, 64-tile shapes) or, with a
+        reducer, in the SGD + clamp pass after the exchange
+        (lds_sgd_sample_graphs; any S) — so a window starts with the CSR fill
+        only; the graphs of the first replayed window are drawn here,
+        eagerly; ignored where neither applies.  Same draws, same counters,
+        same results as windows that draw their own graphs.  The engine's
+        own out-of-window draws and parameter changes discard the prefetched
+        graphs; a caller that rewrites θ in place between windows calls
+        discard_prefetched_draws() first.  With a reducer
         (replicas over RCCL) the window is
         split at the exchange: graph A runs up to dθ, `grad_reducer(grad)`
         runs eagerly between the replays (the collective stays outside the
