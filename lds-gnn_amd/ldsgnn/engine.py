@@ -802,6 +802,9 @@ class LdsEngine:
             return False
         form = theta_grad_form()
         nb2 = (self.n + 127) // 128
+        # the by-shape rule of csrc/thetagrad.hip launch_theta_grad (form 1 -> 6
+        # unless 128-tiles: nt128 >= 1024, or k >= 1024), so the fused kernel
+        # replaces exactly the launch the plain hyper step would make
         by_shape_64 = form == "bf16x3" and nb2 * (nb2 + 1) // 2 < 1024 and k0 < 1024
         if not (by_shape_64 or form == "bf16x3-t64k16-grouped"):
             return False
