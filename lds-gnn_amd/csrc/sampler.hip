@@ -50,8 +50,12 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs,
     int* __restrict__ dacc, int wsi, float* __restrict__ theta_w = nullptr,
     const float* __restrict__ grad = nullptr, const double* __restrict__ lr_dev = nullptr) {
-    __shared__ uint32_t colpart[4][64];  // wave w's column bits (rows 16w .. 16w+15 of the tile)
-    __shared__ uint64_t rowword[64];
+    // items are drawn in groups of kGrp: per item wave w leaves its column bits
+    // (rows 16w .. 16w+15 of the tile) here, then wave q assembles item q's
+    // column words — one barrier pair per group instead of per item
+    constexpr int kGrp = 4;
+    __shared__ uint32_t colpart[kGrp][4][64];
+    __shared__ uint64_t rowword[kGrp][64];
     const int tile = blockIdx.x;
     // batched launches: graph blockIdx.y draws counter + blockIdx.y; replica
     // samples either come from grid.z (one per block) or, with `samples` > 1,
@@ -106,66 +110,80 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const int z0 = kLoop ? 0 : (int)blockIdx.z;
     const int z1 = kLoop ? samples * graphs : z0 + 1;
     const bool rvalid = lane < 16 && r0 + lane < n;  // lane r stores row r0 + r's word
-#pragma unroll 1
-    for (int it = z0; it < z1; ++it) {
+    // item -> (graph index, sample, counter, tag, its bits / degree slices)
+    auto item = [&](int it, int& gidx, int& z) {
         const int gl = kLoop ? it / samples : 0;
-        const int z = kLoop ? it - gl * samples : it;
-        const int gidx = (int)blockIdx.y + gl;
-        const uint32_t ctr = counter + (uint32_t)gl;
-        const uint32_t tg = tag + (uint32_t)z * tag_step;
-        uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
-        int* __restrict__ da = kDeg ? dacc + ((int64_t)gidx * nsamp + z) * wsi : nullptr;
-        // the draws of all 16 rows first: four independent Philox chains per lane
-        bool e[16];
-        if constexpr (kInj) {
+        z = kLoop ? it - gl * samples : it;
+        gidx = (int)blockIdx.y + gl;
+        return gl;
+    };
+#pragma unroll 1
+    for (int base = z0; base < z1; base += kGrp) {
+        const int gn = min(kGrp, z1 - base);
+#pragma unroll 1
+        for (int q = 0; q < gn; ++q) {
+            int gidx, z;
+            const int gl = item(base + q, gidx, z);
+            const uint32_t ctr = counter + (uint32_t)gl;
+            const uint32_t tg = tag + (uint32_t)z * tag_step;
+            uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
+            int* __restrict__ da = kDeg ? dacc + ((int64_t)gidx * nsamp + z) * wsi : nullptr;
+            // the draws of all 16 rows first: four independent Philox chains per lane
+            bool e[16];
+            if constexpr (kInj) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = r0 + r;
+                    const float u = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
+                    e[r] = th[r] >= 0.0f && u < fminf(th[r], 1.0f);
+                }
+            } else {
+                uint32_t x[16];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)((r0 >> 2) + m), tg, ctr}, k0, k1);
+                    x[4 * m] = o.x;
+                    x[4 * m + 1] = o.y;
+                    x[4 * m + 2] = o.z;
+                    x[4 * m + 3] = o.w;
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) e[r] = (x[r] >> 8) < thr[r];
+            }
+            // row words out of ballots (lane r keeps row r's), column bits per lane
+            uint32_t row_lo = 0, row_hi = 0, cw = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int i = r0 + r;
-                const float u = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
-                e[r] = th[r] >= 0.0f && u < fminf(th[r], 1.0f);
+                const uint64_t w = __ballot(e[r]);
+                row_lo = lane == r ? (uint32_t)w : row_lo;
+                row_hi = lane == r ? (uint32_t)(w >> 32) : row_hi;
+                cw |= (uint32_t)e[r] << r;
             }
-        } else {
-            uint32_t x[16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)((r0 >> 2) + q), tg, ctr}, k0, k1);
-                x[4 * q] = o.x;
-                x[4 * q + 1] = o.y;
-                x[4 * q + 2] = o.z;
-                x[4 * q + 3] = o.w;
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) e[r] = (x[r] >> 8) < thr[r];
-        }
-        // row words out of ballots (lane r keeps row r's), column bits per lane
-        uint32_t row_lo = 0, row_hi = 0, cw = 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint64_t w = __ballot(e[r]);
-            row_lo = lane == r ? (uint32_t)w : row_lo;
-            row_hi = lane == r ? (uint32_t)(w >> 32) : row_hi;
-            cw |= (uint32_t)e[r] << r;
-        }
-        const uint64_t myrow = ((uint64_t)row_hi << 32) | row_lo;
-        if (!diag_tile) {
-            if (rvalid) {
-                gb[(int64_t)(r0 + lane) * words + bj] = myrow;
-                if constexpr (kDeg) {  // row part of an off-diagonal tile (diagonal tiles: column part only)
-                    const int pc = __popcll(myrow);
-                    if (pc != 0) atomicAdd(&da[r0 + lane], pc);
+            const uint64_t myrow = ((uint64_t)row_hi << 32) | row_lo;
+            if (!diag_tile) {
+                if (rvalid) {
+                    gb[(int64_t)(r0 + lane) * words + bj] = myrow;
+                    if constexpr (kDeg) {  // row part of an off-diagonal tile (diagonal tiles: column part only)
+                        const int pc = __popcll(myrow);
+                        if (pc != 0) atomicAdd(&da[r0 + lane], pc);
+                    }
                 }
+            } else if (rvalid) {
+                rowword[q][wave * 16 + lane] = myrow;
             }
-        } else if (rvalid) {
-            rowword[wave * 16 + lane] = myrow;
+            colpart[q][wave][lane] = cw;
         }
-        colpart[wave][lane] = cw;
         __syncthreads();
-        if (wave == 0) {
+        if (wave < gn) {  // wave q: the column words of item base + q
+            int gidx, z;
+            item(base + wave, gidx, z);
+            uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
+            int* __restrict__ da = kDeg ? dacc + ((int64_t)gidx * nsamp + z) * wsi : nullptr;
             int pc = 0;
             if (j < n) {
-                uint64_t out = (uint64_t)colpart[0][lane] | ((uint64_t)colpart[1][lane] << 16) |
-                               ((uint64_t)colpart[2][lane] << 32) | ((uint64_t)colpart[3][lane] << 48);
-                if (diag_tile) out |= rowword[lane] | (1ull << lane);  // self-loop: diagonal set to 1
+                uint64_t out = (uint64_t)colpart[wave][0][lane] | ((uint64_t)colpart[wave][1][lane] << 16) |
+                               ((uint64_t)colpart[wave][2][lane] << 32) | ((uint64_t)colpart[wave][3][lane] << 48);
+                if (diag_tile) out |= rowword[wave][lane] | (1ull << lane);  // self-loop: diagonal set to 1
                 gb[(int64_t)j * words + bi] = out;
                 pc = __popcll(out);
             }
@@ -173,7 +191,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                 if (pc != 0) atomicAdd(&da[j], pc);
             }
         }
-        if (it + 1 < z1) __syncthreads();  // colpart / rowword are reused by the next item
+        if (base + kGrp < z1) __syncthreads();  // colpart / rowword are reused by the next group
     }
 }
 
