@@ -691,47 +691,57 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     }
     if constexpr (DRAW) {
         // rows of this lane: quad m = e >> 2 covers rows r4(m) .. r4(m) + 3 of column j
-        __shared__ uint32_t rw[64][2];   // row words: [row][column half]
-        __shared__ uint64_t cwp[2][64];  // column words: [wave row half][column]
+        // graphs in groups of four: each leaves its row words / column words
+        // in LDS, then threads 64q .. 64q + 63 store graph q's (one barrier
+        // pair per group)
+        constexpr int kGrp = 4;
+        __shared__ uint32_t rw[kGrp][64][2];   // row words: [graph][row][column half]
+        __shared__ uint64_t cwp[kGrp][2][64];  // column words: [graph][wave row half][column]
         const bool diag = i0 == j0;
         const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
         const int rq0 = (i0 + wr * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
 #pragma unroll 1
-        for (int gph = 0; gph < dr.graphs; ++gph) {
-            const uint32_t ctr = dr.counter + cb + (uint32_t)gph;
-            uint64_t* __restrict__ gb = dr.bits + (int64_t)gph * n * dr.words;
-            int* __restrict__ da = dr.dacc + (int64_t)gph * dr.wsi;
-            uint32_t x[16];
+        for (int base = 0; base < dr.graphs; base += kGrp) {
+            const int gn = min(kGrp, dr.graphs - base);
+#pragma unroll 1
+            for (int q = 0; q < gn; ++q) {
+                const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
+                uint32_t x[16];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * m), dr.tag, ctr}, dr.k0, dr.k1);
-                x[4 * m] = o.x;
-                x[4 * m + 1] = o.y;
-                x[4 * m + 2] = o.z;
-                x[4 * m + 3] = o.w;
-            }
-            uint64_t colw = 0;
-            uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+                for (int m = 0; m < 4; ++m) {
+                    const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * m), dr.tag, ctr}, dr.k0,
+                                                  dr.k1);
+                    x[4 * m] = o.x;
+                    x[4 * m + 1] = o.y;
+                    x[4 * m + 2] = o.z;
+                    x[4 * m + 3] = o.w;
+                }
+                uint64_t colw = 0;
+                uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const bool bit = (x[e] >> 8) < thr[e];
-                const uint64_t w = __ballot(bit);
-                mylo = lane == e ? (uint32_t)w : mylo;
-                myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
-                colw |= (uint64_t)bit << ((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5) + wr * 32);
+                for (int e = 0; e < 16; ++e) {
+                    const bool bit = (x[e] >> 8) < thr[e];
+                    const uint64_t w = __ballot(bit);
+                    mylo = lane == e ? (uint32_t)w : mylo;
+                    myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                    colw |= (uint64_t)bit << ((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5) + wr * 32);
+                }
+                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+                if (lane < 16) {  // element e = lane: rows r (h = 0) and r + 4 (h = 1), columns wc·32 …
+                    const int r = wr * 32 + (lane & 3) + 8 * (lane >> 2);
+                    rw[q][r][wc] = mylo;
+                    rw[q][r + 4][wc] = myhi;
+                }
+                if (lane < 32) cwp[q][wr][wc * 32 + lane] = colw;
             }
-            colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
-            if (lane < 16) {  // element e = lane: rows r (h = 0) and r + 4 (h = 1), columns wc·32 …
-                const int r = wr * 32 + (lane & 3) + 8 * (lane >> 2);
-                rw[r][wc] = mylo;
-                rw[r + 4][wc] = myhi;
-            }
-            if (lane < 32) cwp[wr][wc * 32 + lane] = colw;
             __syncthreads();
-            if (t < 64) {
-                const uint64_t roww = (uint64_t)rw[t][0] | ((uint64_t)rw[t][1] << 32);
-                const int jj = j0 + t, ii = i0 + t;
-                uint64_t out = cwp[0][t] | cwp[1][t];
+            const int q = t >> 6, tt = t & 63;
+            if (q < gn) {
+                uint64_t* __restrict__ gb = dr.bits + (int64_t)(base + q) * n * dr.words;
+                int* __restrict__ da = dr.dacc + (int64_t)(base + q) * dr.wsi;
+                const uint64_t roww = (uint64_t)rw[q][tt][0] | ((uint64_t)rw[q][tt][1] << 32);
+                const int jj = j0 + tt, ii = i0 + tt;
+                uint64_t out = cwp[q][0][tt] | cwp[q][1][tt];
                 if (!diag) {
                     if (ii < n) {
                         gb[(int64_t)ii * dr.words + (j0 >> 6)] = roww;
@@ -739,7 +749,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
                         if (pc != 0) atomicAdd(&da[ii], pc);
                     }
                 } else {
-                    out |= roww | (1ull << t);  // self-loop: diagonal set to 1
+                    out |= roww | (1ull << tt);  // self-loop: diagonal set to 1
                 }
                 if (jj < n) {
                     gb[(int64_t)jj * dr.words + (i0 >> 6)] = out;
@@ -747,7 +757,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
                     if (pc != 0) atomicAdd(&da[jj], pc);
                 }
             }
-            if (gph + 1 < dr.graphs) __syncthreads();  // rw / cwp reused by the next graph
+            if (base + kGrp < dr.graphs) __syncthreads();  // rw / cwp reused by the next group
         }
     }
 }
