@@ -621,6 +621,14 @@ extern "C" int lds_csr_degree_scale(const int* row_ptr, int n, int* deg, float* 
 
 extern "C" int lds_sample_ws_ints(int n) { return n; }
 
+// Clears the degree workspace of a draw that does not find it zeroed.  A
+// kernel rather than hipMemsetAsync, so that a captured step holds kernel
+// nodes only (the per-step graphs of the fused runner replay this call).
+__global__ void __launch_bounds__(256) zero_ints_kernel(int* __restrict__ p, int64_t count) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) p[i] = 0;
+}
+
 // 1 (default): the window's graphs loop inside the tile block over one θ
 // load; 0: one block per (tile, graph) unless θ is past the MALL.  Measured at
 // Cora (6 graphs per window): 31.0 µs / 21.9 MB fetched per launch looping
@@ -690,7 +698,10 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
     hipStream_t st = (hipStream_t)stream;
     const bool fused = col != nullptr;  // degrees counted by the tiles, scan folded into the fill
     if (fused && !ws_zeroed) {
-        const hipError_t e = hipMemsetAsync(deg_ws, 0, (size_t)graphs * wsi * sizeof(int), st);
+        const int64_t cnt = (int64_t)graphs * wsi;
+        const int blocks = (int)std::min<int64_t>((cnt + 255) / 256, 1024);
+        hipLaunchKernelGGL(zero_ints_kernel, dim3(blocks), dim3(256), 0, st, deg_ws, cnt);
+        const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
     int* dacc = fused ? deg_ws : nullptr;

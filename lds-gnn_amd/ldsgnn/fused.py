@@ -149,16 +149,15 @@ class FusedBilevelRunner:
     (MetaDenseGCN.reset_weights consumes the torch RNG exactly as there); the
     per-step train loss is read back for the inner early stopping (one sync per
     inner step, as the reference's `.item()`), so the unit of replay is the
-    step.  Steps launch eagerly by default.  `step_graphs=True` captures every
-    inner step position and hyper step length as a HIP graph at its second use
-    and replays it after that (LdsEngine.inner_step_graphed /
-    hyper_step_graphed); it matches the eager loop on the tests' problems, but
-    a full Cora run (τ = 20, pre-trained θ) faulted on the first replay of the
-    step-0 graph after a 20-step window, while the same run with eager steps
-    completes — so it is opt-in until that is found."""
+    step.  With `step_graphs` (default) every inner step position and hyper
+    step length is captured as a HIP graph at its second use and replayed
+    after that (LdsEngine.inner_step_graphed / hyper_step_graphed), with
+    results identical to eager steps (`step_graphs=False`).  A captured step
+    holds kernel nodes only: a memset node in the per-step draw faulted on
+    its replay after a τ = 20 window."""
 
     def __init__(self, inner_trainer, outer_trainer, data, n_samples_empirical_mean: int = 16,
-                 generator: "_rng.Generator" = None, step_graphs: bool = False):
+                 generator: "_rng.Generator" = None, step_graphs: bool = True):
         self.inner_trainer = inner_trainer
         self.outer_trainer = outer_trainer
         self.data = data

@@ -285,6 +285,50 @@ def test_fused_runner_matches_dropin_runner(step_graphs):
         assert abs(a[k] - b[k]) < 1e-4, (k, a[k], b[k])
 
 
+def test_fused_runner_step_graphs_cora_tau20_equal_eager():
+    """Per-step graphs replayed across τ = 20 windows on the real Cora split
+    (the configuration whose step-0 replay faulted while a captured draw held
+    a memset node): identical weights, θ and metrics to eager
+    steps after 45 inner steps (two replays of the step-0 graph)."""
+    import numpy as np
+
+    import ldsgnn
+    from ldsgnn.data.planetoid import load_planetoid_npz
+    from ldsgnn.fused import FusedBilevelRunner
+    from ldsgnn.models.gcn import MetaDenseGCN
+    from ldsgnn.models.graph import BernoulliGraphModel
+    from ldsgnn.trainers.inner import InnerProblemTrainer
+    from ldsgnn.trainers.outer import OuterProblemTrainer
+    from ldsgnn.utils.graph import split_mask
+    dev = torch.device("cuda:0")
+
+    def run(step_graphs):
+        torch.manual_seed(5)
+        np.random.seed(5)
+        ldsgnn.rng.manual_seed(5, 0)
+        data = load_planetoid_npz("cora").to(dev)
+        data.val_mask, opt_mask = split_mask(data.val_mask, 0.5, shuffle=True)
+        data.val_mask, opt_mask = data.val_mask.to(dev), opt_mask.to(dev)
+        gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(dev)
+        inner = InnerProblemTrainer(gcn, data, lr=0.01, weight_decay=5e-4)
+        gm = BernoulliGraphModel(data.dense_adj)
+        outer = OuterProblemTrainer(torch.optim.SGD(gm.parameters(), lr=0.1), data, opt_mask, gm, lr_decay=0.99,
+                                    pretrain=False)
+        runner = FusedBilevelRunner(inner, outer, data, n_samples_empirical_mean=16, step_graphs=step_graphs)
+        rec = []
+        runner.train(patience=100, hyper_gradient_interval=20, inner_loop_max_epochs=45, outer_loop_max_epochs=1,
+                     sacred_runner=lambda name, value, step=None: rec.append((name, step, value)))
+        torch.cuda.synchronize()
+        return rec, runner.engine.theta.clone(), runner.evaluate()
+
+    ra, ta, ea = run(False)
+    rb, tb, eb = run(True)
+    assert sum(1 for r in ra if r[0] == "loss.train") >= 45  # EarlyStopping counts max_epochs inclusively
+    assert ra == rb
+    assert torch.equal(ta, tb)
+    assert ea == eb
+
+
 def test_fused_runner_embedding_model_matches_dropin():
     """The embedding graph model (P = σ(E·Eᵀ)) on the fused engine — inner
     steps and dθ in HIP, the outer SGD on E by autograd through P's upper
