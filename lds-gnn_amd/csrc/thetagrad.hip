@@ -1166,6 +1166,285 @@ __global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
     t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Eight-wave pipelined 128 × 128 form (form 9).  Form 8 runs one wave per
+// SIMD: its 176 split VALU, 12 ds_write and 24 ds_read_b128 per chunk issue
+// from the same single instruction stream as its 48 MFMAs, and every LDS read
+// latency and load wait is exposed (1.87 µs per chunk against a 0.64 µs MFMA
+// floor at Cora S = 16).  Here a 512-thread block owns the 128 × 128 tile:
+// wave (wr, wc) = (w >> 2, w & 3) a 64 × 32 sub-tile (two 32 × 32
+// accumulators sharing each staged V_J / U_J fragment), two waves per SIMD, so
+// one wave's staging and reads issue beside its partner's MFMAs.  Per chunk a
+// wave reads 18 fragments for 24 MFMAs (0.75 KB per MFMA; the 64-tile form
+// reads 1 KB and writes 0.5 KB more per MFMA) and stages a quarter row of
+// each of the four operands; the stage is double-buffered (2 × 48 KB dynamic
+// LDS, one barrier per chunk) as in form 8.  Same chunks, same LDS rows, same
+// MFMA sequence per accumulator as forms 2-8: identical bits.
+//
+// DRAW (mode 2): the next window's graphs are drawn from the θ the epilogue
+// writes, as in the 64-tile lds_theta_grad_sgd_draw: each lane's 2 × 16
+// outputs are 2 × 4 row quads of one column, exactly the Philox counters of
+// the sampler's tile draw (sampler.hip).  Bit rows come from ballots (row
+// segments of 32 columns, joined across the wc pairs in LDS) and column words
+// from each lane's own bits; the dead stage buffers hold them, and a second
+// pass stores each (row, 2-word) pair once with 16-byte stores and one degree
+// atomic per row and graph (half the 64-tile form's atomics).  All eight waves
+// run the Philox work, two per SIMD: the VALU issues at its full rate.
+// ---------------------------------------------------------------------------
+constexpr int kW8Lds = 2 * 12 * kPL2 * 4;  // bytes of the two stage buffers (96 KB)
+constexpr int kW8Grp = 8;                  // graphs per draw group (4 KB of LDS each)
+
+template <bool SMALL, bool PART, bool DRAW>
+__global__ __launch_bounds__(512, 2) void theta_grad_w8_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
+    float gscale, int group, int per_xcd, DrawArgs dr) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+    __shared__ float Ri[kT2], Rj[kT2];
+
+    const int nb = (n + kT2 - 1) / kT2;
+    const int ntiles = nb * (nb + 1) / 2;
+    int bi, bj;
+    {
+        const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+        if (L >= ntiles) return;  // whole block: no barrier reached
+        grouped_tile(L, nb, group, bi, bj);
+    }
+    const int i0 = bi * kT2, j0 = bj * kT2;
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    const int64_t nn = n;
+
+    // staging: thread t owns row t >> 2 of both blocks, k = 4·(t & 3) … + 3 of
+    // the chunk; branch-free loads (rows past n and k past the end read zeros)
+    const int srow = t >> 2, kq = t & 3;
+    const int gi = i0 + srow, gj = j0 + srow;
+    const float* src[4] = {u + (int64_t)gi * ld, v + (int64_t)gi * ld, u + (int64_t)gj * ld,
+                           v + (int64_t)gj * ld};
+    const bool rowok[4] = {gi < n, gi < n, gj < n, gj < n};
+    auto load = [&](float (&x)[4][4], int k0) {
+        const int gk = k0 + 4 * kq;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const float* p = (rowok[a] && gk < k) ? src[a] + gk : g_zero8;
+            const float4 f = *reinterpret_cast<const float4*>(p);
+            x[a][0] = f.x; x[a][1] = f.y; x[a][2] = f.z; x[a][3] = f.w;
+        }
+    };
+    // the 16-wide-chunk LDS rows of forms 2-8: 8 dwords, 16-byte halves
+    // swapped by row bit 3; this thread's quarter is dwords 2·(kq & 1) … + 1
+    // of half kq >> 1 (ds_write_b64 lane groups: 4 rows × 4 quarters, 32
+    // distinct banks)
+    const int soff = srow * kS2 + 4 * ((kq >> 1) ^ swz16(srow)) + 2 * (kq & 1);
+    auto stage_arr = [&](uint32_t* buf, const float (&x)[4], int a) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3_pair(x[0], x[1], h0, m0, l0);
+        split3_pair(x[2], x[3], h1, m1, l1);
+        *reinterpret_cast<uint2*>(buf + (3 * a + 0) * kPL2 + soff) = uint2{h0, h1};
+        *reinterpret_cast<uint2*>(buf + (3 * a + 1) * kPL2 + soff) = uint2{m0, m1};
+        *reinterpret_cast<uint2*>(buf + (3 * a + 2) * kPL2 + soff) = uint2{l0, l1};
+    };
+
+    // the epilogue's θ (and partial-grad) operands, issued before the k loop
+    const int jl = wc * 32 + (lane & 31);
+    const int j = j0 + jl;
+    auto row_of = [&](int m, int e) { return wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); };
+    float th[2][16], part[2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = i0 + row_of(m, e);
+            const bool in = i < n && j < n && j >= i;
+            const int64_t id = in ? tri_at_t<SMALL>(i, j, nn) : 0;
+            th[m][e] = (in && theta != nullptr) ? theta[id] : 0.f;
+            part[m][e] = (PART && in) ? grad[id] : 0.f;
+        }
+
+    if (t < 2 * kT2) {
+        const int rr = t & (kT2 - 1);
+        const int row = (t < kT2 ? i0 : j0) + rr;
+        float racc = 0.f;
+        if (row < n) racc = row_r_sum(r, (int64_t)row * ldr, ldrc, nr);
+        (t < kT2 ? Ri : Rj)[rr] = racc;
+    }
+
+    const int fo = 4 * ((lane >> 5) ^ ((lane >> 3) & 1));  // fragment rows: bit 3 = lane bit 3
+    const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
+    const int rb = (wc * 32 + (lane & 31)) * kS2 + fo;
+    f32x16 acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+    // chunk c from `cur`, beside the stage of the next chunk into `nxt`
+    auto step = [&](const uint32_t* cur, uint32_t* nxt, const float (&x)[4][4]) {
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {  // pr 0: U_I × V_J (planes 0-2, 9-11); pr 1: V_I × U_J (3-5, 6-8)
+            const int pa = pr == 0 ? 0 : 3, pb = pr == 0 ? 9 : 6;
+            bf16x8 fa[2][3], fb[3];
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                fa[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra0));
+                fa[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra1));
+                fb[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pb + s) * kPL2 + rb));
+            }
+            stage_arr(nxt, x[2 * pr], 2 * pr);
+            stage_arr(nxt, x[2 * pr + 1], 2 * pr + 1);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                f32x16 c = acc[m];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][1], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][2], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][1], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][0], fb[0], c, 0, 0, 0);
+                acc[m] = c;
+            }
+        }
+    };
+
+    uint32_t* const b0 = lds_dyn;
+    uint32_t* const b1 = lds_dyn + 12 * kPL2;
+    float xa[4][4], xb[4][4];
+    const int nch = (k + 15) / 16;
+    if (nch > 0) {
+        load(xa, 0);
+        load(xb, 16);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) stage_arr(b0, xa[a], a);
+        load(xa, 32);
+    }
+    __syncthreads();
+    // chunk c: buffer c & 1 holds it; registers xb (c even) / xa (c odd) hold c + 1
+    for (int c = 0; c < nch; c += 2) {
+        step(b0, b1, xb);
+        load(xb, 16 * (c + 3));
+        __syncthreads();
+        if (c + 1 >= nch) break;
+        step(b1, b0, xa);
+        load(xa, 16 * (c + 4));
+        __syncthreads();
+    }
+
+    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+    uint32_t thr[2][16];  // DRAW: the next draw's integer thresholds (sampler.hip)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int li = row_of(m, e);
+            const int i = i0 + li;
+            thr[m][e] = 0u;
+            if (i >= n || j >= n || j < i) continue;
+            const int64_t id = tri_at_t<SMALL>(i, j, nn);
+            const float t0 = th[m][e];
+            float g = 0.f;
+            if (j > i) {
+                const float gs = gscale * (acc[m][e] + Ri[li] + Rj[jl]);
+                g = mode == 3 ? part[m][e] + gs : gs;
+                if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+            }
+            if (mode == 3) {
+                grad[id] = g;
+                theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+            } else if (mode == 2) {
+                if (grad != nullptr) grad[id] = g;
+                const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                theta[id] = tn;
+                if (DRAW && j > i) thr[m][e] = (uint32_t)ceilf(tn * 16777216.0f);
+            } else if (mode == 1) {
+                grad[id] = part[m][e] + g;
+            } else {
+                grad[id] = g;
+            }
+        }
+    if constexpr (DRAW) {
+        // LDS (the dead stage buffers): per graph of a group, row segments
+        // rw[row][wc] (uint32: 32 columns) and column words cw[h][col] (uint64:
+        // 64 rows of half h)
+        uint32_t* const rwb = lds_dyn;                                              // kW8Grp × 128 × 4
+        uint64_t* const cwb = reinterpret_cast<uint64_t*>(lds_dyn + kW8Grp * 512);  // kW8Grp × 2 × 128
+        const bool diag = i0 == j0;
+        const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
+#pragma unroll 1
+        for (int base = 0; base < dr.graphs; base += kW8Grp) {
+            const int gn = min(kW8Grp, dr.graphs - base);
+            __syncthreads();  // the stage buffers (first group) / the previous group's words are consumed
+#pragma unroll 1
+            for (int q = 0; q < gn; ++q) {
+                const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
+                uint64_t colw = 0;
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
+                    uint32_t x[16];
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr},
+                                                      dr.k0, dr.k1);
+                        x[4 * qd] = o.x;
+                        x[4 * qd + 1] = o.y;
+                        x[4 * qd + 2] = o.z;
+                        x[4 * qd + 3] = o.w;
+                    }
+                    uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const bool bit = (x[e] >> 8) < thr[m][e];
+                        const uint64_t w = __ballot(bit);
+                        mylo = lane == e ? (uint32_t)w : mylo;
+                        myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                        colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                    }
+                    if (lane < 16) {  // element e = lane: rows rr and rr + 4 of columns wc·32 …
+                        const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
+                        rwb[(q * 128 + rr) * 4 + wc] = mylo;
+                        rwb[(q * 128 + rr + 4) * 4 + wc] = myhi;
+                    }
+                }
+                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+                if (lane < 32) cwb[(q * 2 + wr) * 128 + wc * 32 + lane] = colw;
+            }
+            __syncthreads();
+            // one (row, two words) pair per work item: rows of I (part 0), rows of J (part 1)
+            for (int it = t; it < gn * 256; it += 512) {
+                const int q = it >> 8, part1 = (it >> 7) & 1, x = it & 127;
+                if (diag && part1) continue;
+                const int row = (part1 ? j0 : i0) + x;
+                if (row >= n) continue;
+                uint64_t* __restrict__ gb = dr.bits + (int64_t)(base + q) * n * dr.words;
+                int* __restrict__ da = dr.dacc + (int64_t)(base + q) * dr.wsi;
+                const uint32_t* rws = rwb + (q * 128 + x) * 4;
+                uint64_t w0, w1;
+                int wbase;
+                if (part1) {  // column x of J: its rows of I (the mirrored entries)
+                    w0 = cwb[(q * 2 + 0) * 128 + x];
+                    w1 = cwb[(q * 2 + 1) * 128 + x];
+                    wbase = i0 >> 6;
+                } else {
+                    w0 = (uint64_t)rws[0] | ((uint64_t)rws[1] << 32);
+                    w1 = (uint64_t)rws[2] | ((uint64_t)rws[3] << 32);
+                    wbase = j0 >> 6;
+                    if (diag) {  // strict upper (row words) | strict lower (column words) | self-loop
+                        w0 |= cwb[(q * 2 + 0) * 128 + x];
+                        w1 |= cwb[(q * 2 + 1) * 128 + x];
+                        if (x < 64) w0 |= 1ull << x;
+                        else w1 |= 1ull << (x - 64);
+                    }
+                }
+                *reinterpret_cast<ulonglong2*>(gb + (int64_t)row * dr.words + wbase) = ulonglong2{w0, w1};
+                const int pc = __popcll(w0) + __popcll(w1);
+                if (pc != 0) atomicAdd(&da[row], pc);
+            }
+        }
+    }
+}
+
 // Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
 // shape (below), 2 = 64-tile with 16-wide k chunks, 3 = 64-tile with 32-wide
 // k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
@@ -1175,6 +1454,44 @@ __global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
 // captured with).
 static int g_theta_form = 1;
 constexpr int kGroup = 8;
+
+template <bool SMALL, bool PART, bool DRAW>
+static void launch_w8_inst(int grid, hipStream_t st, const float* u, const float* v, int ld, int k, const float* r,
+                           int ldr, int nr, float* theta, int n, float* grad, int mode, const double* lr, int ldrc,
+                           float gscale, int per, const DrawArgs& dr) {
+    static bool attr_set = false;  // > 64 KB of dynamic LDS must be enabled per kernel
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_w8_kernel<SMALL, PART, DRAW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kW8Lds);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((theta_grad_w8_kernel<SMALL, PART, DRAW>), dim3(grid), dim3(512), kW8Lds, st, u, v, ld, k, r,
+                       ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, kGroup, per, dr);
+}
+
+// Form 9 (needs 16-byte aligned rows and k % 8 == 0, the `fast` condition).
+static void launch_w8(hipStream_t st, const float* u, const float* v, int ld, int k, const float* r, int ldr, int nr,
+                      float* theta, int n, float* grad, int mode, const double* lr, int ldrc, float gscale,
+                      const DrawArgs* dr) {
+    const int nb2 = (n + kT2 - 1) / kT2;
+    const int nt2 = nb2 * (nb2 + 1) / 2;
+    const int per = (nt2 + 7) / 8;
+    const int grid = 8 * per;
+    const bool small = n <= 46340;
+    const bool part = mode == 1 || mode == 3;
+#define LDS_W8_ARGS grid, st, u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, per
+    if (dr != nullptr) {  // mode 2 only (checked by the caller)
+        if (small) launch_w8_inst<true, false, true>(LDS_W8_ARGS, *dr);
+        else launch_w8_inst<false, false, true>(LDS_W8_ARGS, *dr);
+        return;
+    }
+    const DrawArgs none{};
+    if (small && part) launch_w8_inst<true, true, false>(LDS_W8_ARGS, none);
+    else if (small) launch_w8_inst<true, false, false>(LDS_W8_ARGS, none);
+    else if (part) launch_w8_inst<false, true, false>(LDS_W8_ARGS, none);
+    else launch_w8_inst<false, false, false>(LDS_W8_ARGS, none);
+#undef LDS_W8_ARGS
+}
 
 static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const float* v, int ld, int k,
                               const float* r, int ldr, int nr, float* theta, int n, float* grad, int mode,
@@ -1196,6 +1513,11 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
     if (form == 1) form = (nt2 <= 256 && k >= 1024) ? 8 : (nt2 >= 1024 || k >= 1024) ? 5 : 6;
     // the branch-free staging needs whole 8-wide k groups in 16-byte aligned rows
     const bool fast = vec4 && (k & 7) == 0;
+    if (form == 9 && !pre && fast) {
+        launch_w8(st, u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, nullptr);
+        return;
+    }
+    if (form == 9) form = 5;  // pre-split operands or unaligned rows: the plain 128-tile form
 #define LDS_TG_ARGS u, v, ld, k, r, ldr, nr, theta, n, grad, mode, lr, vec4, ldrc, gscale
     if (form == 8 && !pre && fast) {
         const int per = (nt2 + 7) / 8;
@@ -1469,14 +1791,20 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
     const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
     DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                 counter_offset, counter_base, graphs};
-    hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, false, true, true>), dim3(8 * per), dim3(256), 0,
-                       (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup, per,
-                       Planes{nullptr, nullptr}, dr);
+    // the eight-wave 128-tile form (form 9) by default; the 64-tile form when
+    // pinned (forms 2 / 6, for A/B timing).  Both give identical θ, bits and degrees.
+    if (g_theta_form == 2 || g_theta_form == 6) {
+        hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, false, true, true>), dim3(8 * per), dim3(256), 0,
+                           (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup,
+                           per, Planes{nullptr, nullptr}, dr);
+    } else {
+        launch_w8((hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1.0f, &dr);
+    }
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_theta_grad_set_form(int form, int* prev) {
-    LDS_CHECK_ARG(form >= -1 && form <= 8);
+    LDS_CHECK_ARG(form >= -1 && form <= 9);
     if (prev != nullptr) *prev = g_theta_form;
     if (form >= 0) g_theta_form = form;
     return 0;

@@ -426,7 +426,7 @@ def theta_grad(u: torch.Tensor, v: torch.Tensor, r: torch.Tensor, n: int,
 
 THETA_GRAD_FORMS = {"fp32": 0, "bf16x3": 1, "bf16x3-t64k16": 2, "bf16x3-t64k32": 3, "bf16x3-t128": 4,
                     "bf16x3-t128-grouped": 5, "bf16x3-t64k16-grouped": 6, "bf16x3-t128-grouped-i64": 7,
-                    "bf16x3-t128-pipe": 8}
+                    "bf16x3-t128-pipe": 8, "bf16x3-t128-w8": 9}
 
 
 def theta_grad_form(form: Optional[str] = None) -> str:

@@ -447,7 +447,8 @@ def test_fused_sampler_csr_equals_staged_path(device, n, count, samples, dense):
 
 
 @pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t64k16", "bf16x3-t64k16-grouped", "bf16x3-t64k32",
-                                  "bf16x3-t128", "bf16x3-t128-grouped", "bf16x3-t128-pipe", "fp32"])
+                                  "bf16x3-t128", "bf16x3-t128-grouped", "bf16x3-t128-pipe", "bf16x3-t128-w8",
+                                  "fp32"])
 @pytest.mark.parametrize("n,k,ld,mode", [(1, 4, 4, 0), (65, 17, 17, 0), (130, 33, 35, 1), (200, 0, 4, 0),
                                          (257, 48, 48, 2), (300, 264, 264, 3), (129, 1030, 1032, 0),
                                          (1100, 40, 40, 3)])
@@ -543,7 +544,7 @@ def test_theta_grad_planes_bit_exact_vs_fp32_operands(device, form, n, k, mode):
 def test_theta_grad_form_default_and_errors(device):
     assert ops.theta_grad_form() == "bf16x3"
     with pytest.raises(nat.NativeError):
-        nat.call("lds_theta_grad_set_form", 9, 0)
+        nat.call("lds_theta_grad_set_form", 10, 0)
 
 
 @pytest.mark.parametrize("n,k,mode", [(2708, 264, 2), (2708, 264, 3), (700, 40, 0), (130, 8, 1), (300, 24, 2),
@@ -565,7 +566,7 @@ def test_theta_grad_pipe_bit_exact(device, n, k, mode):
     scal[16:24].view(torch.float64).fill_(0.05)
     st = nat.stream_of(torch.device(device))
     outs = []
-    for form in ("bf16x3-t128-grouped", "bf16x3-t128-pipe"):
+    for form in ("bf16x3-t128-grouped", "bf16x3-t128-pipe", "bf16x3-t128-w8"):
         prev = ops.theta_grad_form(form)
         try:
             th = theta.clone().to(device)
@@ -576,14 +577,18 @@ def test_theta_grad_pipe_bit_exact(device, n, k, mode):
             outs.append((th.cpu(), grad.cpu()))
         finally:
             ops.theta_grad_form(prev)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert torch.equal(outs[0][1], o[1])
 
 
-@pytest.mark.parametrize("n,k,graphs", [(2708, 264, 6), (300, 40, 3), (130, 8, 1), (700, 24, 2)])
-def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs):
-    """lds_theta_grad_sgd_draw (the 64-tile θ-grad with SGD + clamp, drawing
-    the next window's graphs from the θ it writes) against lds_theta_grad_sgd
+@pytest.mark.parametrize("draw_form", ["bf16x3", "bf16x3-t64k16-grouped"])
+@pytest.mark.parametrize("n,k,graphs", [(2708, 264, 6), (300, 40, 3), (130, 8, 1), (700, 24, 2), (1000, 16, 21),
+                                        (64, 8, 2), (129, 24, 9)])
+def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs, draw_form):
+    """lds_theta_grad_sgd_draw (the θ-grad with SGD + clamp, drawing the next
+    window's graphs from the θ it writes; the eight-wave 128-tile form by
+    default, the 64-tile form when pinned) against lds_theta_grad_sgd
     followed by single lds_sample_bitmask draws of the updated θ: identical θ,
     identical bit rows (graph g draws counter base + offset + g) and degree
     counts equal to the rows' popcounts."""
@@ -610,9 +615,13 @@ def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs):
     th2 = theta.clone()
     bits = torch.zeros((graphs, n, words), dtype=torch.int64, device=device)
     deg = torch.zeros((graphs, wsi), dtype=torch.int32, device=device)
-    nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th2), n, 0,
-             nat.ptr(scal), seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg), st)
-    torch.cuda.synchronize()
+    prev = ops.theta_grad_form(draw_form)  # the eight-wave 128-tile draw (default) or the 64-tile one
+    try:
+        nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th2), n, 0,
+                 nat.ptr(scal), seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg), st)
+        torch.cuda.synchronize()
+    finally:
+        ops.theta_grad_form(prev)
     assert torch.equal(th1, th2)
     one = torch.empty((n, words), dtype=torch.int64, device=device)
     nb = (n + 63) // 64
