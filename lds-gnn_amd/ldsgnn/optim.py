@@ -66,6 +66,19 @@ class DifferentiableOptimizer:
     def _update(self, grouped_grads):
         raise NotImplementedError
 
+    def truncate(self) -> None:
+        """Cut the autograd history held by the optimizer, in place: every
+        tensor in the state (m, v) and among the group hyper-parameters
+        becomes a leaf that requires grad.  Plain numbers (step, lr) and the
+        group's params list are left alone.  This is what the reference's
+        InnerProblemTrainer.detach_optimizer does to higher's state
+        (src/trainers/inner.py:110-125)."""
+        tensors = [value for group in self.param_groups for value in group.values()]
+        tensors += [value for per_group in self.state for slot in per_group.values() for value in slot.values()]
+        for t in tensors:
+            if isinstance(t, torch.Tensor):
+                t.detach_().requires_grad_()
+
 
 def _maybe_mask(tensor: torch.Tensor, mask: torch.Tensor) -> None:
     if isinstance(tensor, torch.Tensor) and tensor.requires_grad:
