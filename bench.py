@@ -48,6 +48,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md)
+ELL_W = 64              # ELL head width, neighbours per row (csrc/common.hpp kEllWidth)
 FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
@@ -144,7 +145,7 @@ def algo_cost(name, eng, n_calls_per_window):
     nnz = eng.sampled_nnz_mean()
     xnnz = int(eng.xcol.numel())
     act = 4 * 16 * n * S                      # one n × 16 fp32 activation array (all samples)
-    graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)  # row_ptr, col, s, ELL head
+    graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)  # row_ptr, col, s, ELL head
     tri = n * (n + 1) // 2
     P = eng.np
     if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex", "lds_theta_grad_sgd_draw"):
@@ -154,12 +155,12 @@ def algo_cost(name, eng, n_calls_per_window):
     if name == "lds_sample_graphs_multi":
         g = eng.tau + 1
         words = nat.lib.lds_bitmask_words(n)
-        per = S * (3 * 8 * n * words + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)  # bits w/r/r, CSR, s, ELL
+        per = S * (3 * 8 * n * words + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)  # bits w/r/r, CSR, s, ELL
         return "hbm", 4 * tri + g * per      # θ read once per window
     if name == "lds_sample_fill_csr":  # the fill alone: bits read, CSR / s / ELL written
         g = eng.tau + 1
         words = nat.lib.lds_bitmask_words(n)
-        return "hbm", g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n)
+        return "hbm", g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)
     if name == "lds_engine_x_linear":
         return "hbm", S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act
     if name == "lds_engine_xt_adam":
@@ -180,7 +181,7 @@ def algo_cost(name, eng, n_calls_per_window):
         chunks = (n + 511) // 512
         return "mfma_i8", 2.0 * n * chunks * 512 * 16 * 4
     if name == "lds_spmm_norm_blocked":
-        return "hbm", 4 * (n + 1) + 4 * nnz + 4 * n + 8 * 16 * n
+        return "hbm", 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n
     if name == "lds_engine_xt_partials":
         return "hbm", 8 * xnnz + act
     return "hbm", 0
@@ -252,8 +253,7 @@ def window_breakdown(eng, reducer, args, device, k=20):
     real = nat.call
 
     def rec(name, *a):
-        if name != "lds_theta_grad_set_form":  # a host-side query (the engine reads the θ-grad form), no launch
-            calls.append((name, a))
+        calls.append((name, a))
         real(name, *a)
 
     nat.call = rec
@@ -521,8 +521,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--theta-form", default=None, help="θ-grad assembly form (ldsgnn.ops.THETA_GRAD_FORMS; "
                     "default: bf16x3, the split-bf16 MFMA form picked by shape)")
-    ap.add_argument("--sample-loop", type=int, default=None, help="1: the window's graphs loop inside each sampler "
-                    "tile block over one θ load (lds_sample_loop_graphs); 0: one block per (tile, graph)")
     ap.add_argument("--samples", type=int, default=1, help="Monte-Carlo replica samples per GPU, batched in "
                     "every launch (BASELINE configs 3/4); value is then sample-steps/s")
     ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
@@ -562,9 +560,6 @@ def main():
     from ldsgnn import ops as ldsops
     if args.theta_form is not None:
         ldsops.theta_grad_form(args.theta_form)
-    if args.sample_loop is not None:
-        from ldsgnn import _native as nat
-        nat.lib.lds_sample_loop_graphs(int(args.sample_loop))
     if args.model == "gcn":
         bench_gcn(args, world, rank, device, barrier_sync)
         if world > 1:
@@ -663,6 +658,7 @@ def main():
             window["bitmask_aggregation"]["share_of_window"] = agg_rows[0]["us_per_window"] / total
 
     prefetched = bool(use_engine and eng.prefetch_draw)  # (the strong leg below frees the engine)
+    form_name = eng._form_name() if use_engine else ldsops.theta_grad_form()
     strong = None
     if use_engine and args.strong_total and not param_theta:
         del eng
@@ -683,7 +679,7 @@ def main():
             "config": {"workload": f"{args.dataset}-lds-S{args.samples}-tau{args.tau}", "path": args.path,
                        "nodes": n, "features": data.num_features, "classes": data.num_classes, "hidden": 16,
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
-                       "theta_grad_form": ldsops.theta_grad_form(), "sampled_nnz": nnz,
+                       "theta_grad_form": form_name, "sampled_nnz": nnz,
                        "replicas_in_sync": in_sync, "graph_model": args.graph_model,
                        "windows_per_graph": (args.graph_windows if reducer is None else 1)
                        if use_engine and use_graph else None,

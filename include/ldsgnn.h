@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 9
+#define LDS_ABI_VERSION 10
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -109,12 +109,6 @@ int lds_bitmask_fill_csr_ell(const uint64_t* bits, int n, int words,
 
 /* Workspace ints per graph of lds_sample_graphs_multi (the row degrees). */
 int lds_sample_ws_ints(int n);
-/* on = 1 (default): lds_sample_graphs_multi draws all `count` graphs of a
- * call from one θ tile load per block (a loop over graphs in the block);
- * 0: one block per (tile, graph) unless θ exceeds 64 MB; -1: query.  Returns
- * the previous setting.  Process-wide, host-only. */
-int lds_sample_loop_graphs(int on);
-
 /* The outer SGD step + clamp of lds_engine_sgd_clamp fused with the NEXT
  * window's draw from the θ it writes (`count` graphs × `samples` replicas,
  * counters / tags as lds_sample_graphs_multi, the graph counter and the f64
@@ -229,7 +223,7 @@ int lds_aggregate_bitmask(const uint64_t* bits, int words, const float* s, int n
  * ------------------------------------------------------------------------- */
 int lds_theta_grad(const float* u, const float* v, int ld, int k,
                    const float* r, int ldr, int nr, const float* theta, int n,
-                   float* grad, int accumulate, void* stream);
+                   float* grad, int accumulate, int form, void* stream);
 
 /* The same update on the fp32 VALU (the MFMA form above is the default);
  * kept for A/B timing. */
@@ -244,7 +238,7 @@ int lds_theta_grad_valu(const float* u, const float* v, int ld, int k,
  * (src/trainers/outer.py:77-83) for one hyper step. */
 int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
                        const float* r, int ldr, int nr, float* theta, int n,
-                       float* grad, const void* scalars, void* stream);
+                       float* grad, const void* scalars, int form, void* stream);
 
 /* lds_theta_grad_sgd for the last column chunk of a split assembly: grad
  * holds the sum of the earlier chunks (lds_theta_grad with accumulate, no R,
@@ -253,9 +247,9 @@ int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
  * stream while the reverse pass continues. */
 int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k,
                              const float* r, int ldr, int nr, float* theta, int n,
-                             float* grad, const void* scalars, void* stream);
+                             float* grad, const void* scalars, int form, void* stream);
 
-/* lds_theta_grad_sgd (64-tile split-bf16 form, grouped order) that also draws
+/* lds_theta_grad_sgd (split-bf16; see `form` below) that also draws
  * the NEXT window's `graphs` graphs from the θ it writes: graph g takes draw
  * counter counter_offset + g (+ *counter_base when non-NULL), bits and degree
  * accumulators as lds_sample_graphs_multi's tile kernel (deg_ws zero on
@@ -267,7 +261,7 @@ int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, int k,
                             const float* r, int ldr, int nr, float* theta, int n,
                             float* grad, const void* scalars, uint64_t seed, uint32_t tag,
                             const uint32_t* counter_base, uint32_t counter_offset, int graphs,
-                            uint64_t* bits, int words, int* deg_ws, void* stream);
+                            uint64_t* bits, int words, int* deg_ws, int form, void* stream);
 
 /* General form of the assembly, for S replica samples per GPU (their factor
  * blocks side by side in U, V: k = S·ldk columns):
@@ -279,7 +273,7 @@ int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, int k,
  * grad != NULL); 3 as 2 with g += grad first.  lr from `scalars` (modes 2, 3). */
 int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                       int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
-                      int mode, const void* scalars, float gscale, void* stream);
+                      int mode, const void* scalars, float gscale, int form, void* stream);
 /* lds_theta_grad_ex on pre-split operands: every fp32 value x of U and V as
  * its three truncation-split bf16 words x = hi + mid + lo (lds_split_planes
  * makes them from fp32; the engine's factor producers write them directly),
@@ -290,23 +284,26 @@ int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float
  * bounds the chunks, up / vp 16-byte aligned. */
 int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k, const float* r,
                           int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad, int mode,
-                          const void* scalars, float gscale, void* stream);
+                          const void* scalars, float gscale, int form, void* stream);
 /* The chunk-major split words of the first k columns of x (rows × ld fp32)
  * into planes (ceil(k/16) chunks of rows × 48 uint16). */
 int lds_split_planes(const float* x, int rows, int ld, int k, uint16_t* planes, void* stream);
-/* Arithmetic form of every θ-gradient assembly above (process-wide; a
- * captured HIP graph keeps the form it was captured with):
+/* `form`: the arithmetic form of every θ-gradient assembly above, chosen per
+ * call (no process-wide state; a captured HIP graph holds the form it was
+ * captured with in its launch):
  *   0 fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chains);
- *   1 split-bf16 MFMA (default), tile shape by problem size: each fp32
+ *   1 split-bf16 MFMA, tile shape by problem size (the default): each fp32
  *     operand as three bf16 words, six v_mfma_f32_32x32x16_bf16 per product
  *     (fp32 accuracy, |error| <= ~2^-22 |U||V| per term, fp32 accumulation);
  *   2 split-bf16, 64 × 64 tiles, 16-wide k chunks;  3 the same, 32-wide;
  *   4 split-bf16, 128 × 128 tiles;  5 the same in XCD-grouped tile order;
- *   6 form 2 in XCD-grouped tile order,
+ *   6 form 2 in XCD-grouped tile order;
  *   7 form 5 with 64-bit packed-index arithmetic at every n (the path n > 46 340
- *     takes; for testing).
- * form = -1 only reads the current form into *prev (prev may be NULL). */
-int lds_theta_grad_set_form(int form, int* prev);
+ *     takes; for testing);
+ *   8 the software-pipelined 128 × 128 form (double-buffered stage);
+ *   9 the eight-wave pipelined 128 × 128 form (64 × 32 wave tiles).
+ * Every split-bf16 form gives bit-identical results.  lds_theta_grad_sgd_draw
+ * runs form 9 when asked for it and the 64-tile form (6) otherwise. */
 
 /* Slot factors for lds_theta_grad from one aggregation Y = ÂZ and its
  * cotangent G (dZ = ÂG):  U = s⊙G, V = s⊙Z, r = -½ s² (G·Y + Z·dZ) rowwise.
@@ -631,6 +628,16 @@ int lds_engine_end_window(int np, const float* wT, const float* mT, const float*
  * <= 256; the constants of torch/higher's Adam, computed in double. */
 int lds_engine_adam_table(const void* scalars, const double* betas_dev, float* adam_tab,
                           int tab_count, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Captured-graph check (host only).  counts[t] = the number of nodes of HIP
+ * graph type t (hipGraphNodeType: 0 kernel, 1 memcpy, 2 memset, 5 empty, …)
+ * in `graph` (a hipGraph_t, e.g. torch.cuda.CUDAGraph(keep_graph=True)
+ * .raw_cuda_graph()), t < ncounts - 1; the last slot counts the types past
+ * the array.  The engine refuses a captured step or window that holds
+ * anything but kernel and empty nodes.
+ * ------------------------------------------------------------------------- */
+int lds_graph_node_census(void* graph, int* counts, int ncounts);
 
 #ifdef __cplusplus
 }

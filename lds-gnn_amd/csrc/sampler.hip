@@ -26,7 +26,7 @@ namespace lds {
 // Batched launches: grid.y = graph (counter + y), grid.z = replica sample (tag +
 // z·tag_step); bit matrix (y·samples + z) of the batch.  kLoop: the block loops
 // over the (graph, sample) items of the launch on ONE θ tile load (θ read once
-// per window instead of once per graph; lds_sample_loop_graphs).  r01's form
+// per window instead of once per graph; always on since round 3).  r01's form
 // of that loop took 157 VGPRs and lost to one block per graph; with the
 // integer-threshold compare and the single row-word store below it takes 69
 // and the loop is the faster form (31.0 µs, 21.9 MB fetched per Cora window of
@@ -634,12 +634,6 @@ __global__ void __launch_bounds__(256) zero_ints_kernel(int* __restrict__ p, int
 // Cora (6 graphs per window): 31.0 µs / 21.9 MB fetched per launch looping
 // against 30.8 µs / 113.9 MB, bench 12.64k vs 12.60k steps/s.  Returns the
 // previous setting.
-static int g_sample_loop_graphs = 1;
-extern "C" int lds_sample_loop_graphs(int on) {
-    const int prev = g_sample_loop_graphs;
-    if (on >= 0) g_sample_loop_graphs = on ? 1 : 0;
-    return prev;
-}
 
 // The outer SGD step + clamp (lds_engine_sgd_clamp) and the NEXT window's
 // draw of `count` graphs × `samples` replicas from the θ it writes, in one
@@ -705,10 +699,9 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
         if (e != hipSuccess) return (int)e;
     }
     int* dacc = fused ? deg_ws : nullptr;
-    // replica samples loop inside the block over one θ tile load; past the
-    // MALL (θ > ~64 MB) the window's graphs join that loop too
-    const bool big = (int64_t)n * (n + 1) / 2 * 4 > ((int64_t)64 << 20);
-    const int loop_graphs = (big || g_sample_loop_graphs) ? count : 1;
+    // replica samples and the window's graphs loop inside the block over one
+    // θ tile load (θ read once per window)
+    const int loop_graphs = count;
     if (samples > 1 || (loop_graphs > 1 && count > 1)) {
         if (fused)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true>), dim3(ntiles, count / loop_graphs, 1),

@@ -1450,9 +1450,9 @@ __global__ __launch_bounds__(512, 2) void theta_grad_w8_kernel(
 // k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
 // order, 6 = form 2 in XCD-grouped order, 7 = form 5 with 64-bit index
 // arithmetic at every n (the n > 46 340 path; for testing), 8 = the
-// software-pipelined 128-tile (double-buffered stage, XCD-grouped order).  Read at launch (a captured HIP graph keeps the form it was
-// captured with).
-static int g_theta_form = 1;
+// software-pipelined 128-tile (double-buffered stage, XCD-grouped order),
+// 9 = the eight-wave pipelined 128-tile.  Chosen per call (the `form`
+// argument of every entry point).
 constexpr int kGroup = 8;
 
 template <bool SMALL, bool PART, bool DRAW>
@@ -1495,9 +1495,8 @@ static void launch_w8(hipStream_t st, const float* u, const float* v, int ld, in
 
 static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const float* v, int ld, int k,
                               const float* r, int ldr, int nr, float* theta, int n, float* grad, int mode,
-                              const double* lr, int vec4, int ldrc, float gscale,
+                              const double* lr, int vec4, int ldrc, float gscale, int form,
                               Planes pl = Planes{nullptr, nullptr}) {
-    int form = g_theta_form;
     const bool pre = pl.u != nullptr;
     if (pre && (form == 0 || form == 3)) form = 6;  // pre-split: the 16-wide-chunk 64-tile or the 128-tile forms
     const int nb2 = (n + kT2 - 1) / kT2;
@@ -1660,14 +1659,15 @@ using namespace lds;
 
 extern "C" int lds_theta_grad(const float* u, const float* v, int ld, int k, const float* r,
                               int ldr, int nr, const float* theta, int n, float* grad,
-                              int accumulate, void* stream) {
+                              int accumulate, int form, void* stream) {
+    LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(grad != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
     const int nb = (n + kTile - 1) / kTile;
     const int ntiles = nb * (nb + 1) / 2;
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
-    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, const_cast<float*>(theta), n, grad, accumulate ? 1 : 0, (const double*)nullptr, vec4, 1, 1.0f);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, const_cast<float*>(theta), n, grad, accumulate ? 1 : 0, (const double*)nullptr, vec4, 1, 1.0f, form);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1687,7 +1687,8 @@ extern "C" int lds_theta_grad_valu(const float* u, const float* v, int ld, int k
 
 extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k, const float* r,
                                   int ldr, int nr, float* theta, int n, float* grad,
-                                  const void* scalars, void* stream) {
+                                  const void* scalars, int form, void* stream) {
+    LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(theta != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
@@ -1696,13 +1697,14 @@ extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     // EngineScalars: f64 outer_lr at byte offset 16
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
-    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4, 1, 1.0f);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, vec4, 1, 1.0f, form);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k, const float* r,
                                         int ldr, int nr, float* theta, int n, float* grad,
-                                        const void* scalars, void* stream) {
+                                        const void* scalars, int form, void* stream) {
+    LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(theta != nullptr && grad != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
@@ -1710,13 +1712,14 @@ extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, 
     const int ntiles = nb * (nb + 1) / 2;
     const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
     const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
-    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4, 1, 1.0f);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 3, lr, vec4, 1, 1.0f, form);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                                  int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
-                                 int mode, const void* scalars, float gscale, void* stream) {
+                                 int mode, const void* scalars, float gscale, int form, void* stream) {
+    LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
@@ -1731,13 +1734,14 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
     //  4-wave block per CU; at n = 20 000 (12 k tiles) 3.12 ms against 2.27 ms,
     //  196 VGPRs and 66 KB LDS leave 2 waves per SIMD.  MFMA busy of this form
     //  at S = 16 is 63 % of the cycles at a 2.26 GHz DVFS clock, r01 PMC)
-    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale);
+    launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale, form);
     LDS_RETURN_LAST_ERROR();
 }
 
 extern "C" int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k, const float* r,
                                      int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad, int mode,
-                                     const void* scalars, float gscale, void* stream) {
+                                     const void* scalars, float gscale, int form, void* stream) {
+    LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
     LDS_CHECK_ARG(k == 0 || (up != nullptr && vp != nullptr && ld >= k));
     LDS_CHECK_ARG((k & 7) == 0);
@@ -1749,7 +1753,7 @@ extern "C" int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int
     const int ntiles = nb * (nb + 1) / 2;
     const double* lr = mode >= 2 ? reinterpret_cast<const double*>((const char*)scalars + 16) : nullptr;
     launch_theta_grad(ntiles, (hipStream_t)stream, nullptr, nullptr, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr,
-                      1, ldr_col, gscale, Planes{up, vp});
+                      1, ldr_col, gscale, form, Planes{up, vp});
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -1780,7 +1784,8 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
                                        int ldr, int nr, float* theta, int n, float* grad, const void* scalars,
                                        uint64_t seed, uint32_t tag, const uint32_t* counter_base,
                                        uint32_t counter_offset, int graphs, uint64_t* bits, int words,
-                                       int* deg_ws, void* stream) {
+                                       int* deg_ws, int form, void* stream) {
+    LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(u && v && theta && scalars && bits && deg_ws && n > 0 && k >= 0 && ld >= k);
     LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64 && nr >= 0);
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
@@ -1791,23 +1796,18 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
     const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
     DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                 counter_offset, counter_base, graphs};
-    // the eight-wave 128-tile form (form 9) by default; the 64-tile form when
-    // pinned (forms 2 / 6, for A/B timing).  Both give identical θ, bits and degrees.
-    if (g_theta_form == 2 || g_theta_form == 6) {
+    // the 64-tile form (form 6) unless the eight-wave 128-tile form (9) is
+    // asked for; both give identical θ, bits and degrees.  MI355X (tools/
+    // microbench/tg_draw_ab.py): 61.8 vs 63.6 µs at Cora, 86 vs 114 at
+    // Citeseer, 2.61 vs 2.91 ms at n = 20 000 (six graphs, k = 264).
+    if (form == 9) {
+        launch_w8((hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1.0f, &dr);
+    } else {
         hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, false, true, true>), dim3(8 * per), dim3(256), 0,
                            (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup,
                            per, Planes{nullptr, nullptr}, dr);
-    } else {
-        launch_w8((hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1.0f, &dr);
     }
     LDS_RETURN_LAST_ERROR();
-}
-
-extern "C" int lds_theta_grad_set_form(int form, int* prev) {
-    LDS_CHECK_ARG(form >= -1 && form <= 9);
-    if (prev != nullptr) *prev = g_theta_form;
-    if (form >= 0) g_theta_form = form;
-    return 0;
 }
 
 extern "C" int lds_slot_factors(const float* g, int ldg, const float* z, int ldz, const float* y,

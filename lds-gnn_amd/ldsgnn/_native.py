@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -24,6 +24,7 @@ P = c_void_p  # device pointers travel as integers
 _RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes"}  # byte counts
 SIGNATURES = {
     "lds_abi_version": [],
+    "lds_graph_node_census": [P, P, c_int],
     "lds_bitmask_words": [c_int],
     "lds_philox_uniform": [c_uint64, c_uint32, c_uint32, c_int, c_int, P, P],
     "lds_sample_bitmask": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P],
@@ -39,9 +40,9 @@ SIGNATURES = {
     "lds_sample_fill_csr": [P, c_int, c_int, P, c_int, P, P, c_int64, P, P, P, P],
     "lds_sgd_sample_graphs": [P, P, P, c_int, c_uint64, c_uint32, c_uint32, c_uint32, c_int, c_int, P, c_int, P,
                               P],
-    "lds_sample_loop_graphs": [c_int],
-    "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
-    "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, P],
+    "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int, P],
+    "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int,
+                              P],
     "lds_split_planes": [P, c_int, c_int, c_int, P, P],
     "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
@@ -52,13 +53,12 @@ SIGNATURES = {
     "lds_spmm_norm_blocked": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P],
     "lds_bitmask_agg_ws_bytes": [c_int],
     "lds_aggregate_bitmask": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, P],
-    "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
+    "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
-    "lds_theta_grad_set_form": [c_int, P],
-    "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
-    "lds_theta_grad_sgd_accum": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P],
+    "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_int, P],
+    "lds_theta_grad_sgd_accum": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_int, P],
     "lds_theta_grad_sgd_draw": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_uint64, c_uint32, P,
-                                c_uint32, c_int, P, c_int, P, P],
+                                c_uint32, c_int, P, c_int, P, c_int, P],
     "lds_slot_factors": [P, c_int, P, c_int, P, c_int, P, c_int, P, c_int, c_int, c_int, P, c_int, P,
                          c_int, P, c_int, P],
     "lds_sgd_clamp": [P, P, c_float, c_int64, P],
@@ -195,6 +195,34 @@ def call(name: str, *args) -> None:
         check(err, name)
         return
     check(getattr(lib, name)(*args), name)
+
+
+# hipGraphNodeType values a captured step or window may hold: kernel launches
+# and the empty nodes a capture inserts where streams join
+_GRAPH_NODE_OK = {0: "kernel", 5: "empty"}
+_GRAPH_NODE_NAMES = {1: "memcpy", 2: "memset", 3: "host", 4: "child graph", 6: "event wait", 7: "event record",
+                     10: "mem alloc", 11: "mem free", 12: "memcpy from symbol", 13: "memcpy to symbol"}
+
+
+def new_graph() -> "torch.cuda.CUDAGraph":
+    """A HIP graph whose capture is inspected before instantiation
+    (seal_graph)."""
+    return torch.cuda.CUDAGraph(keep_graph=True)
+
+
+def seal_graph(graph: "torch.cuda.CUDAGraph", what: str) -> "torch.cuda.CUDAGraph":
+    """Refuse a captured graph that holds anything but kernel (and empty)
+    nodes, then instantiate it.  A memset node in a replayed step graph
+    faulted the GPU in round 2; every clear the engine needs is a
+    kernel, and this keeps any other node type from entering a capture: the
+    failure is a host-side error at capture time, never a GPU fault."""
+    counts = (ctypes.c_int * 16)()
+    call("lds_graph_node_census", graph.raw_cuda_graph(), ctypes.addressof(counts), 16)
+    bad = {_GRAPH_NODE_NAMES.get(t, f"type {t}"): c for t, c in enumerate(counts) if c and t not in _GRAPH_NODE_OK}
+    if bad:
+        raise RuntimeError(f"captured {what} holds non-kernel graph nodes {bad}: refusing to replay it")
+    graph.instantiate()
+    return graph
 
 
 class LdsBatch(ctypes.Structure):

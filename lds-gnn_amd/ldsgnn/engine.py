@@ -107,6 +107,22 @@ class _Slot:
         self.corrrow = torch.zeros((S, n), dtype=torch.float32, device=dev)
 
 
+_POP8 = None
+
+
+def _popcount(words: torch.Tensor) -> int:
+    """Set bits in a device bit-row tensor (host sync; reporting only), by a
+    byte table in 64 MB slices."""
+    global _POP8
+    if _POP8 is None or _POP8.device != words.device:
+        _POP8 = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int32, device=words.device)
+    b = words.reshape(-1).view(torch.uint8)
+    tot = 0
+    for i in range(0, b.numel(), 1 << 26):
+        tot += int(_POP8[b[i:i + (1 << 26)].long()].sum().item())
+    return tot
+
+
 def _csr_of(dense: torch.Tensor):
     sp = dense.to_sparse_csr()
     return (sp.crow_indices().to(torch.int32).contiguous(), sp.col_indices().to(torch.int32).contiguous(),
@@ -297,6 +313,9 @@ class LdsEngine:
         # MI355X the replayed graph did not overlap the branches and the
         # chunks' read-modify-write of dθ cost 2.3x the single launch (r01).
         self.split_theta_grad = False
+        # θ-grad assembly form of this engine's launches (ldsgnn.ops.THETA_GRAD_FORMS
+        # name; None: the module default ops.theta_grad_form() at launch time)
+        self.theta_form = None
         self.side = torch.cuda.Stream(dev)
         self.metrics = torch.zeros((self.tau + 1, S, 2), dtype=torch.float32, device=dev)
         self._graph_capture = None
@@ -305,6 +324,15 @@ class LdsEngine:
         self.reset_optimizer()
 
     # ------------------------------------------------------------------ setup
+    def _form_name(self) -> str:
+        from .ops import theta_grad_form
+        return self.theta_form if self.theta_form is not None else theta_grad_form()
+
+    def _form(self) -> int:
+        """The C-ABI `form` argument of this engine's θ-grad launches."""
+        from .ops import form_code
+        return form_code(self._form_name())
+
     def _alloc_factors(self):
         """U, V: n × (S·ldk), sample b in columns [b·ldk, (b+1)·ldk); R: [S, n]."""
         self._layout_version += 1  # captured step graphs are stale
@@ -786,21 +814,20 @@ class LdsEngine:
             self._prefetched = False
             self._ws_clean = False
 
-    def _prefetch_ok(self, T: int, k0: int, exchange: bool = False) -> bool:
+    def _prefetch_ok(self, T: int, k0: int, exchange: bool = False, check_flag: bool = True) -> bool:
         """The next window's draw can ride in this hyper step: plain LDS θ, a
         full window, CSR graphs; with an exchange (dθ all-reduced before the
         SGD step) in the SGD + clamp pass (lds_sgd_sample_graphs, any S),
         else in the θ-grad kernel: single sample, the 64-tile split-bf16 form
         with aligned operands (lds_theta_grad_sgd_draw)."""
-        from .ops import theta_grad_form
-        if not (self.prefetch_draw and self.theta_fn is None and self.outer_update is None
+        if not ((self.prefetch_draw or not check_flag) and self.theta_fn is None and self.outer_update is None
                 and not self.bitmask_agg and T == self.tau and self.gbatch.count == self.tau + 1):
             return False
         if exchange:
             return True
         if self.S != 1:
             return False
-        form = theta_grad_form()
+        form = self._form_name()
         nb2 = (self.n + 127) // 128
         # the by-shape rule of csrc/thetagrad.hip launch_theta_grad (form 1 -> 6
         # unless 128-tiles: nt128 >= 1024, or k >= 1024), so the fused kernel
@@ -895,7 +922,7 @@ class LdsEngine:
         elif grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
             if split:
                 nat.call("lds_theta_grad_sgd_accum", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0,
-                         nat.ptr(self.R), 1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad), nat.ptr(self.scalars), st)
+                         nat.ptr(self.R), 1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad), nat.ptr(self.scalars), self._form(), st)
             elif presampled and self._prefetch_ok(T, k0):  # + the next window's draw, from the θ written here
                 if self._deg_next is None:
                     self._deg_next = torch.zeros_like(self.gbatch.deg)
@@ -903,15 +930,15 @@ class LdsEngine:
                 nat.call("lds_theta_grad_sgd_draw", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R),
                          1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
                          nat.ptr(self.scalars), self.seed, self.tag_graph, nat.ptr(self.scalars), self.pending_graph,
-                         gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next), st)
+                         gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next), self._form(), st)
                 drew = True
             else:
                 nat.call("lds_theta_grad_sgd", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1,
                          1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
-                         nat.ptr(self.scalars), st)
+                         nat.ptr(self.scalars), self._form(), st)
         else:  # replicas: dθ, all-reduce (mean), then the identical update everywhere
             nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
-                     nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, st)
+                     nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, self._form(), st)
             grad_reducer(self.grad)  # with outer_update: the model's optimizer step, which rewrites θ
             if self.outer_update is None:
                 drew = self._sgd_step(T, k0, presampled)
@@ -958,10 +985,10 @@ class LdsEngine:
         gs = float(np.float32(1.0) / np.float32(S))
         if grad_reducer is None:
             nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
-                     P(self.theta), n, P(self.grad) if self.keep_grad else 0, 2, P(self.scalars), gs, st)
+                     P(self.theta), n, P(self.grad) if self.keep_grad else 0, 2, P(self.scalars), gs, self._form(), st)
         else:
             nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
-                     P(self.theta), n, P(self.grad), 0, 0, gs, st)
+                     P(self.theta), n, P(self.grad), 0, 0, gs, self._form(), st)
             grad_reducer(self.grad)
             return self._sgd_step(self.tau if presampled else -1, k0, presampled)
         return False
@@ -974,7 +1001,7 @@ class LdsEngine:
         side.wait_stream(torch.cuda.current_stream(self.dev))
         off = 4 * col0
         nat.call("lds_theta_grad", nat.ptr(self.U) + off, nat.ptr(self.V) + off, self.ldk, k, 0, 0, 0, 0, self.n,
-                 nat.ptr(self.grad), accumulate, side.cuda_stream)
+                 nat.ptr(self.grad), accumulate, self._form(), side.cuda_stream)
 
     # ------------------------------------------------------- per-draw θ
     def set_theta_fn(self, fn):
@@ -1053,7 +1080,7 @@ class LdsEngine:
         for t in range(T + 1):
             k0, k = (t * self.kg, self.kg) if t < T else (T * self.kg, HID + self.cw)
             nat.call("lds_theta_grad", nat.ptr(self.U) + 4 * k0, nat.ptr(self.V) + 4 * k0, self.ldk, k,
-                     nat.ptr(self.Rg[t]), 1, 1, 0, n, nat.ptr(self.grad_g[t]), 0, st)
+                     nat.ptr(self.Rg[t]), 1, 1, 0, n, nat.ptr(self.grad_g[t]), 0, self._form(), st)
         grad_reducer(self.grad_g[:T + 1])
         P = nat.ptr
         wmv = (P(self.w[T]), P(self.m[T]), P(self.v[T])) if T else (0, 0, 0)
@@ -1129,12 +1156,11 @@ class LdsEngine:
         (buffers grow then), is captured and replayed the second time and
         replayed after that; the host-side state the eager call would leave
         (position, pending offsets) is restored from the capture."""
-        from .ops import theta_grad_form
         # everything the captured launches bake in: position, pending counter
-        # offsets, Adam-table length, the θ-grad form (process-wide), whether
-        # dθ is written, and the buffer layout (last)
+        # offsets, Adam-table length, the θ-grad form, whether dθ is written,
+        # and the buffer layout (last)
         key = (kind, self.t, self.pending_graph, self.pending_fwd, self.train_flag, self._tab_count(),
-               theta_grad_form(), self.keep_grad, self._layout_version)
+               self._form_name(), self.keep_grad, self._layout_version)
         cache = self._step_graphs
         stale = [k for k in cache if k[-1] != self._layout_version]
         for k in stale:  # captures over re-laid buffers never replay again: free their pools
@@ -1146,13 +1172,14 @@ class LdsEngine:
                 return fn()
             s = torch.cuda.Stream(self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
-            graph = torch.cuda.CUDAGraph()
+            graph = nat.new_graph()
             with torch.cuda.stream(s):
                 with torch.cuda.graph(graph, stream=s):
                     ret = fn()
             torch.cuda.current_stream(self.dev).wait_stream(s)
             if self._layout_version != key[-1]:  # the call re-laid buffers: never replay it
                 raise RuntimeError("engine buffers were re-allocated during step capture")
+            nat.seal_graph(graph, f"{kind} step")
             hit = cache[key] = (graph, (self.t, self.pending_graph, self.pending_fwd), ret)
         graph, post, ret = hit
         graph.replay()
@@ -1217,30 +1244,27 @@ class LdsEngine:
             raise ValueError("windows >= 1")
         if grad_reducer is None:
             grad_reducer = self.grad_reducer
-        if prefetch:
-            self.prefetch_draw = True
-            if not self._prefetch_ok(tau, tau * self.kg + HID + self.cw, exchange=grad_reducer is not None):
-                self.prefetch_draw = False
-            elif not self._prefetched:
-                if self._deg_next is None:
-                    self._deg_next = torch.zeros_like(self.gbatch.deg)
-                self._sample_batch(tau + 1)  # the first replayed window's graphs, drawn now
-                self._prefetched = True
+        # every capture sets the flag (an earlier prefetching capture must not
+        # leak into this one) and starts from the entry state its graphs
+        # assume: prefetched draws present, or none and a clean degree buffer
+        self.prefetch_draw = bool(prefetch) and \
+            self._prefetch_ok(tau, tau * self.kg + HID + self.cw, exchange=grad_reducer is not None, check_flag=False)
+        self._enter_window_state(self.prefetch_draw, tau)
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
             graphs = []
             for w in sorted({1, windows}):
-                graph = torch.cuda.CUDAGraph()
+                graph = nat.new_graph()
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(graph, stream=s):
                         for _ in range(w):
                             self.run_window(tau)
-                graphs.append((w, graph))
+                graphs.append((w, nat.seal_graph(graph, f"{w}-window group")))
             torch.cuda.current_stream(self.dev).wait_stream(s)
-            self._graph_capture = (tuple(graphs), tau, None)
+            self._graph_capture = (tuple(graphs), tau, None, self.prefetch_draw)
             return graphs[0][1]
-        head, tail = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        head, tail = nat.new_graph(), nat.new_graph()
         pool = torch.cuda.graph_pool_handle()
 
         def switch(_grad):  # the exchange point: close graph A, open graph B
@@ -1254,11 +1278,32 @@ class LdsEngine:
             finally:
                 tail.capture_end()
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        self._graph_capture = ((head, tail), tau, grad_reducer)
+        nat.seal_graph(head, "window (to the exchange)")
+        nat.seal_graph(tail, "window (after the exchange)")
+        self._graph_capture = ((head, tail), tau, grad_reducer, self.prefetch_draw)
         return head, tail
 
+    def _enter_window_state(self, prefetched: bool, tau: int) -> None:
+        """Bring the device to the window-start state a captured window
+        assumes: with prefetch, the window's τ+1 graphs already drawn (bits +
+        degrees; drawn here, eagerly, if a discard, an out-of-window draw or a
+        non-prefetching step dropped them); without, no prefetched graphs and
+        a zeroed degree workspace (the captured draw accumulates into it)."""
+        if prefetched:
+            if not self._prefetched:
+                if self._deg_next is None:
+                    self._deg_next = torch.zeros_like(self.gbatch.deg)
+                self._sample_batch(tau + 1)  # bits + degrees of this window's graphs
+                self._prefetched = True
+        else:
+            if self._prefetched or not self._ws_clean:
+                self.gbatch.deg.zero_()
+            self._prefetched = False
+            self._ws_clean = True
+
     def replay(self, windows: int = 1):
-        graphs, _, reducer = self._graph_capture
+        graphs, tau, reducer, prefetched = self._graph_capture
+        self._enter_window_state(prefetched, tau)
         if reducer is None:
             (_, one), (group, multi) = graphs[0], graphs[-1]
             for _ in range(windows // group):
@@ -1291,18 +1336,18 @@ class LdsEngine:
     def sampled_nnz(self) -> int:
         """Stored entries (self-loops included) of the last window's outer
         graph, sample 0 (host sync)."""
-        if self.bitmask_agg:  # no CSR: the degrees of the popcount pass
-            return int(self.gbatch.deg[self.tau, 0, :self.n].sum().item())
+        if self.bitmask_agg:  # no CSR: count the set bits (end_window clears the degrees)
+            return int(_popcount(self.gbatch.bits[self.tau, 0]))
         return int(self.gbatch.row_ptr[self.tau, 0, self.n].item())
 
     def sampled_nnz_mean(self) -> float:
         """Mean stored entries per sampled graph over the last batched window's
         τ+1 graphs and replica samples (host sync)."""
         if self.bitmask_agg:
-            tot = self.gbatch.deg[:, :, :self.n].double().sum()
+            tot = sum(_popcount(self.gbatch.bits[g, b]) for g in range(self.gbatch.count) for b in range(self.S))
         else:
-            tot = self.gbatch.row_ptr[:, :, self.n].double().sum()
-        return float(tot.item()) / (self.gbatch.count * self.S)
+            tot = float(self.gbatch.row_ptr[:, :, self.n].double().sum().item())
+        return float(tot) / (self.gbatch.count * self.S)
 
     @staticmethod
     def window_columns(tau: int, c: int) -> int:

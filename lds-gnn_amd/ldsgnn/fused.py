@@ -51,7 +51,18 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
     gm.probs.grad = eng.grad
     if outer.grad_reducer is not None:
         reducer, model = outer.grad_reducer, gm
-        eng.grad_reducer = lambda grad: reducer(model)
+
+        def reduce_engine_grad(grad):
+            # re-bind on every call: a zero_grad(set_to_none=True) in between
+            # would otherwise leave θ.grad None, the reducer would skip it and
+            # each rank would apply only its own dθ
+            model.probs.grad = grad
+            reducer(model)
+            if model.probs.grad is not grad:  # a reducer that rebinds .grad
+                grad.copy_(model.probs.grad)
+                model.probs.grad = grad
+
+        eng.grad_reducer = reduce_engine_grad
     return eng
 
 
@@ -312,7 +323,7 @@ class FixedGraphGcn:
                  nat.ptr(ev.h2), 0, 0, 0, nat.ptr(eng.label), nat.ptr(self.tm), self.inv_t,
                  nat.ptr(self._test_rows[0]), nat.ptr(self._test_rows[1]), c, 0, eng.bt, st)
         r = self._res
-        r[0:2].copy_(eng.metrics[0][0])
+        torch.mul(eng.metrics[0][0], 1.0, out=r[0:2])  # a kernel: captured graphs hold kernel nodes only
         for i, t in enumerate((ev.lossrow[0], ev.corrrow[0], self._test_rows[0], self._test_rows[1])):
             torch.sum(t, dim=0, keepdim=True, out=r[2 + i:3 + i])
 
@@ -331,13 +342,13 @@ class FixedGraphGcn:
             if self._graph is None:
                 s = torch.cuda.Stream(eng.dev)
                 s.wait_stream(torch.cuda.current_stream(eng.dev))
-                g = torch.cuda.CUDAGraph()
+                g = nat.new_graph()
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s):
                         self._train_step()
                         self._evaluate()
                 torch.cuda.current_stream(eng.dev).wait_stream(s)
-                self._graph = g
+                self._graph = nat.seal_graph(g, "fixed-graph epoch")
             self._graph.replay()
         host = self._res.double().cpu().numpy()
         return (float(host[0] * eng.inv_train), float(host[1] * eng.inv_train), float(host[2] * self.inv_v),

@@ -302,7 +302,7 @@ class _GraphToken(Function):
         w = ch.width
         base = dtok.data_ptr()
         nat.call("lds_theta_grad", base, base + 4 * ch.kcap, w, ch.kused, base + 8 * ch.kcap, w,
-                 ch.rused, nat.ptr(theta), ch.graph.n, nat.ptr(grad), 0, _stream(theta))
+                 ch.rused, nat.ptr(theta), ch.graph.n, nat.ptr(grad), 0, form_code(), _stream(theta))
         return grad, None
 
 
@@ -420,7 +420,7 @@ def theta_grad(u: torch.Tensor, v: torch.Tensor, r: torch.Tensor, n: int,
     if out is None:
         out = torch.empty(n * (n + 1) // 2, dtype=torch.float32, device=u.device)
     nat.call("lds_theta_grad", nat.ptr(u), nat.ptr(v), u.stride(0), u.size(1), nat.ptr(r),
-             r.stride(0), r.size(1), nat.ptr(theta), n, nat.ptr(out), int(accumulate), _stream(u))
+             r.stride(0), r.size(1), nat.ptr(theta), n, nat.ptr(out), int(accumulate), form_code(), _stream(u))
     return out
 
 
@@ -429,18 +429,31 @@ THETA_GRAD_FORMS = {"fp32": 0, "bf16x3": 1, "bf16x3-t64k16": 2, "bf16x3-t64k32":
                     "bf16x3-t128-pipe": 8, "bf16x3-t128-w8": 9}
 
 
+_theta_form = "bf16x3"
+
+
 def theta_grad_form(form: Optional[str] = None) -> str:
-    """Select the θ-gradient assembly's arithmetic form (lds_theta_grad_set_form):
-    "bf16x3" (default: fp32 operands split into three bf16 words, six bf16
-    MFMAs per product, fp32 accuracy; tile shape chosen by problem size), one
-    pinned split-bf16 variant (64-tiles with 16- or 32-wide k chunks, 128-tiles
-    in plain or XCD-grouped order), or "fp32" (fp32-in MFMA).
-    Returns the previous form.  Process-wide; HIP graphs keep the form they
-    were captured with."""
-    prev = ctypes.c_int(0)
-    code = -1 if form is None else THETA_GRAD_FORMS[form]
-    nat.call("lds_theta_grad_set_form", code, ctypes.addressof(prev))
-    return {v: k for k, v in THETA_GRAD_FORMS.items()}[prev.value]
+    """Select the default arithmetic form of the θ-gradient assembly that this
+    module's callers pass to the C-ABI (every lds_theta_grad* entry point takes
+    the form per call; the library keeps no form state): "bf16x3" (default:
+    fp32 operands split into three bf16 words, six bf16 MFMAs per product,
+    fp32 accuracy; tile shape chosen by problem size), one pinned split-bf16
+    variant (64-tiles with 16- or 32-wide k chunks, 128-tiles in plain or
+    XCD-grouped order, the pipelined 128-tiles), or "fp32" (fp32-in MFMA).
+    Returns the previous default.  An LdsEngine with its own `theta_form`
+    ignores this default; HIP graphs keep the form they were captured with."""
+    global _theta_form
+    prev = _theta_form
+    if form is not None:
+        if form not in THETA_GRAD_FORMS:
+            raise ValueError(f"unknown θ-grad form {form!r}; one of {sorted(THETA_GRAD_FORMS)}")
+        _theta_form = form
+    return prev
+
+
+def form_code(form: Optional[str] = None) -> int:
+    """The C-ABI `form` argument of `form` (default: theta_grad_form())."""
+    return THETA_GRAD_FORMS[_theta_form if form is None else form]
 
 
 def philox_uniform(seed: int, tag: int, counter: int, rows: int, cols: int,
@@ -452,5 +465,5 @@ def philox_uniform(seed: int, tag: int, counter: int, rows: int, cols: int,
 
 __all__ = [
     "CsrGraph", "SampledGraph", "sample_graph_from_triu", "csr_graph_from_dense", "aggregate",
-    "keyed_dropout", "sgd_clamp_", "theta_grad", "theta_grad_form", "philox_uniform", "TAG_DROP_X", "TAG_DROP_H",
+    "keyed_dropout", "sgd_clamp_", "theta_grad", "theta_grad_form", "form_code", "philox_uniform", "TAG_DROP_X", "TAG_DROP_H",
 ]

@@ -44,7 +44,7 @@ def test_theta_grad_n20000_vs_fp64_rows(device, form):
     prev = ops.theta_grad_form(form)
     try:
         nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, S, nat.ptr(theta), n,
-                 nat.ptr(grad), 0, nat.ptr(scal), 1.0, nat.stream_of(device))
+                 nat.ptr(grad), 0, nat.ptr(scal), 1.0, ops.form_code(), nat.stream_of(device))
         torch.cuda.synchronize()
     finally:
         ops.theta_grad_form(prev)

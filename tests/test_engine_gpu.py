@@ -498,6 +498,52 @@ def test_prefetched_draw_replay_equals_eager(group, windows):
         assert torch.equal(v, b.get_params()[k]), k
 
 
+def test_prefetched_replay_after_discard_and_eager_steps():
+    """A prefetching captured window replayed after its prefetched graphs were
+    dropped — by discard_prefetched_draws() and an in-place rewrite of θ, or by
+    a non-prefetching eager hyper step (whose end_window clears the degree
+    workspace) — redraws the window's graphs eagerly before the replay
+    (LdsEngine._enter_window_state): bitwise equal to eager windows.  A later
+    capture without prefetch starts from a clean workspace in every graph."""
+    a = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    b = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+
+    def same():
+        torch.cuda.synchronize()
+        assert torch.equal(a.theta, b.theta)
+        for k, v in a.get_params().items():
+            assert torch.equal(v, b.get_params()[k]), k
+        assert a.scalars_host() == b.scalars_host()
+
+    a.capture_window(5, windows=2, prefetch=True)
+    a.replay(2)
+    for _ in range(2):
+        b.run_window(5)
+    same()
+    for e in (a, b):  # θ rewritten from outside the engine
+        e.discard_prefetched_draws()
+        e.theta.mul_(0.75).add_(0.01)
+    a.replay(3)
+    for _ in range(3):
+        b.run_window(5)
+    same()
+    for e in (a, b):  # eager steps: the hyper step draws nothing and clears the degrees
+        e.inner_step()
+        e.hyper_step()
+    a.replay(1)
+    b.run_window(5)
+    same()
+    # a non-prefetching capture after a prefetching one: both graph sizes start with a full draw
+    a.capture_window(5, windows=2, prefetch=False)
+    assert not a.prefetch_draw
+    b.prefetch_draw = False
+    b._drop_prefetch()
+    a.replay(3)
+    for _ in range(3):
+        b.run_window(5)
+    same()
+
+
 @pytest.mark.parametrize("samples", [1, 3])
 def test_prefetched_draw_with_exchange_equals_eager(samples):
     """With an exchange between dθ and the SGD step (the N > 1 path: graph A,

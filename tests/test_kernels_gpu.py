@@ -210,7 +210,7 @@ def test_theta_grad_mfma_matches_valu_and_sgd_mode(device):
     th2 = theta.clone()
     gout = torch.empty_like(theta)
     nat.call("lds_theta_grad_sgd", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 2, 2, nat.ptr(th2), n, nat.ptr(gout),
-             nat.ptr(sc), nat.stream_of(u.device))
+             nat.ptr(sc), ops.form_code(), nat.stream_of(u.device))
     assert torch.equal(gout, a)
     assert torch.allclose(th2, (theta - 0.3 * a).clamp(0, 1), atol=1e-6)
 
@@ -347,7 +347,7 @@ def test_theta_grad_ex_wide_k(device, n, k, mode):
     scal[16:24].view(torch.float64).fill_(lr)
     ud_, vd_, rd_ = u.to(device), v.to(device), r.to(device)  # keep the device copies alive across the call
     nat.call("lds_theta_grad_ex", nat.ptr(ud_), nat.ptr(vd_), k, k, nat.ptr(rd_), 1, n, S, nat.ptr(th), n,
-             nat.ptr(grad), mode, nat.ptr(scal), gs, nat.stream_of(th.device))
+             nat.ptr(grad), mode, nat.ptr(scal), gs, ops.form_code(), nat.stream_of(th.device))
     torch.cuda.synchronize()
     tol = 1e-5 * float(ref.abs().max())
     if mode == 0:
@@ -481,7 +481,7 @@ def test_theta_grad_forms_vs_dense(device, form, n, k, ld, mode):
     prev = ops.theta_grad_form(form)
     try:
         nat.call("lds_theta_grad_ex", nat.ptr(ub_), nat.ptr(vb_), ld, k, nat.ptr(r_), 1, n, 2, nat.ptr(th), n,
-                 nat.ptr(grad), mode, nat.ptr(scal), 1.0, nat.stream_of(th.device))
+                 nat.ptr(grad), mode, nat.ptr(scal), 1.0, ops.form_code(), nat.stream_of(th.device))
         torch.cuda.synchronize()
     finally:
         assert ops.theta_grad_form(prev) == form
@@ -529,10 +529,10 @@ def test_theta_grad_planes_bit_exact_vs_fp32_operands(device, form, n, k, mode):
             grad = base.clone().to(device)
             if planes:
                 nat.call("lds_theta_grad_planes", nat.ptr(up), nat.ptr(vp), ld, k, nat.ptr(r), 1, n, 2,
-                         nat.ptr(th), n, nat.ptr(grad), mode, nat.ptr(scal), 1.0, st)
+                         nat.ptr(th), n, nat.ptr(grad), mode, nat.ptr(scal), 1.0, ops.form_code(), st)
             else:
                 nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
-                         nat.ptr(grad), mode, nat.ptr(scal), 1.0, st)
+                         nat.ptr(grad), mode, nat.ptr(scal), 1.0, ops.form_code(), st)
             torch.cuda.synchronize()
             outs.append((th.cpu(), grad.cpu()))
     finally:
@@ -543,8 +543,11 @@ def test_theta_grad_planes_bit_exact_vs_fp32_operands(device, form, n, k, mode):
 
 def test_theta_grad_form_default_and_errors(device):
     assert ops.theta_grad_form() == "bf16x3"
+    u = torch.zeros((16, 8), device=device)
+    g = torch.zeros(16 * 17 // 2, device=device)
     with pytest.raises(nat.NativeError):
-        nat.call("lds_theta_grad_set_form", 10, 0)
+        nat.call("lds_theta_grad", nat.ptr(u), nat.ptr(u), 8, 8, 0, 0, 0, 0, 16, nat.ptr(g), 0, 10,
+                 nat.stream_of(torch.device(device)))
 
 
 @pytest.mark.parametrize("n,k,mode", [(2708, 264, 2), (2708, 264, 3), (700, 40, 0), (130, 8, 1), (300, 24, 2),
@@ -572,7 +575,7 @@ def test_theta_grad_pipe_bit_exact(device, n, k, mode):
             th = theta.clone().to(device)
             grad = base.clone().to(device)
             nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
-                     nat.ptr(grad), mode, nat.ptr(scal), 1.0, st)
+                     nat.ptr(grad), mode, nat.ptr(scal), 1.0, ops.form_code(), st)
             torch.cuda.synchronize()
             outs.append((th.cpu(), grad.cpu()))
         finally:
@@ -609,7 +612,7 @@ def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs, draw_for
     try:
         th1 = theta.clone()
         nat.call("lds_theta_grad_sgd", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th1), n, 0,
-                 nat.ptr(scal), st)
+                 nat.ptr(scal), ops.form_code(), st)
     finally:
         ops.theta_grad_form(prev)
     th2 = theta.clone()
@@ -618,7 +621,7 @@ def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs, draw_for
     prev = ops.theta_grad_form(draw_form)  # the eight-wave 128-tile draw (default) or the 64-tile one
     try:
         nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th2), n, 0,
-                 nat.ptr(scal), seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg), st)
+                 nat.ptr(scal), seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg), ops.form_code(), st)
         torch.cuda.synchronize()
     finally:
         ops.theta_grad_form(prev)

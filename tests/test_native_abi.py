@@ -45,7 +45,7 @@ def test_argument_errors_need_no_gpu():
     import ldsgnn._native as nat
     # invalid arguments are rejected before any launch (hipErrorInvalidValue = 1)
     assert nat.lib.lds_spmm_norm(None, None, None, 0, None, 0, 0, None, 0, 0, None) == 1
-    assert nat.lib.lds_theta_grad(None, None, 0, 0, None, 0, 0, None, 0, None, 0, None) == 1
+    assert nat.lib.lds_theta_grad(None, None, 0, 0, None, 0, 0, None, 0, None, 0, 1, None) == 1
 
 
 def test_product_path_refuses_cpu_tensors():
@@ -56,21 +56,32 @@ def test_product_path_refuses_cpu_tensors():
         ops.sample_graph_from_triu(torch.rand(6), 3)
 
 
-def test_theta_grad_form_selection_needs_no_gpu():
-    """The θ-grad assembly form is host-side state (lds_theta_grad_set_form):
-    default split bf16, every named form round-trips, out-of-range codes are
-    rejected."""
-    import ctypes as C
+def test_theta_grad_form_is_a_per_call_argument():
+    """The θ-grad assembly form is an argument of every lds_theta_grad* call
+    (no library state: two engines with different forms in one process do not
+    interfere).  ops.theta_grad_form() is the host-side default its callers
+    pass; every named form round-trips, unknown names raise, and an
+    out-of-range code is rejected by the library before any launch."""
+    import pytest
 
     import ldsgnn._native as nat
     from ldsgnn import ops
-    assert ops.theta_grad_form() == "bf16x3"
+    assert not hasattr(nat.lib, "lds_theta_grad_set_form") or "lds_theta_grad_set_form" not in nat.SIGNATURES
+    assert ops.theta_grad_form() == "bf16x3" and ops.form_code() == 1
     try:
-        for name in ops.THETA_GRAD_FORMS:
+        for name, code in ops.THETA_GRAD_FORMS.items():
             ops.theta_grad_form(name)
-            assert ops.theta_grad_form() == name
+            assert ops.theta_grad_form() == name and ops.form_code() == code
     finally:
         ops.theta_grad_form("bf16x3")
-    prev = C.c_int(-7)
-    assert nat.lib.lds_theta_grad_set_form(len(ops.THETA_GRAD_FORMS), C.byref(prev)) == 1
-    assert nat.lib.lds_theta_grad_set_form(-1, C.byref(prev)) == 0 and prev.value == 1
+    with pytest.raises(ValueError):
+        ops.theta_grad_form("bf16x4")
+    # a valid call shape with form 10: hipErrorInvalidValue from the form check
+    fake = 1 << 20  # never dereferenced: the argument checks run first
+    assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, 10, None) == 1
+    assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, -1, None) == 1
+
+
+def test_graph_census_argument_errors_need_no_gpu():
+    import ldsgnn._native as nat
+    assert nat.lib.lds_graph_node_census(None, None, 0) == 1

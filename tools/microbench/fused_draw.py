@@ -42,20 +42,20 @@ def main():
 
     def separate():
         nat.call("lds_theta_grad_sgd", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, 1, nat.ptr(theta), n, 0,
-                 nat.ptr(scal), nat.stream_of(dev))
+                 nat.ptr(scal), 1, nat.stream_of(dev))
         nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 0, graphs, 1,
                  nat.ptr(bits), words, nat.ptr(deg), nat.ptr(row_ptr), nat.ptr(col), cap, nat.ptr(s), nat.ptr(ell),
                  0, 0, nat.stream_of(dev))
 
     def fused():
         nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, 1, nat.ptr(theta), n, 0,
-                 nat.ptr(scal), seed, tag, nat.ptr(base), 0, graphs, nat.ptr(bits), words, nat.ptr(deg),
+                 nat.ptr(scal), seed, tag, nat.ptr(base), 0, graphs, nat.ptr(bits), words, nat.ptr(deg), 1,
                  nat.stream_of(dev))
         deg.zero_()  # the engine would clear it elsewhere; keeps the atomics bounded here
 
     def plain():
         nat.call("lds_theta_grad_sgd", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, 1, nat.ptr(theta), n, 0,
-                 nat.ptr(scal), nat.stream_of(dev))
+                 nat.ptr(scal), 1, nat.stream_of(dev))
 
     out = {"n": n, "k": k, "graphs": graphs}
     for name, fn in (("separate", separate), ("fused", fused), ("plain_theta_grad", plain)):

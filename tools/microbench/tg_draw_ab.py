@@ -67,7 +67,7 @@ def run(name, n, k, graphs, plain_forms):
     def draw_call():
         nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, 1, nat.ptr(theta), n,
                  nat.ptr(grad), nat.ptr(scal), seed, tag, nat.ptr(base), 0, graphs, nat.ptr(bits), words,
-                 nat.ptr(deg), nat.stream_of(dev))
+                 nat.ptr(deg), ops.form_code(), nat.stream_of(dev))
 
     results = {}
     for form in ("bf16x3-t64k16-grouped", "bf16x3"):
@@ -96,7 +96,7 @@ def run(name, n, k, graphs, plain_forms):
         try:
             def fn():
                 nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, 1, nat.ptr(theta), n,
-                         nat.ptr(grad), 2, nat.ptr(scal), 1.0, st)
+                         nat.ptr(grad), 2, nat.ptr(scal), 1.0, ops.form_code(), st)
             theta.copy_(theta0)
             fn()
             torch.cuda.synchronize()

@@ -34,7 +34,7 @@ def main():
                 for gp in (True, False):
                     gptr = nat.ptr(grad) if gp else 0
                     t = time_it(lambda: nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), kfull, k, nat.ptr(r), 1,
-                                                 n, 1, nat.ptr(theta), n, gptr, 2, nat.ptr(scal), 1.0, st), reps)
+                                                 n, 1, nat.ptr(theta), n, gptr, 2, nat.ptr(scal), 1.0, ops.form_code(), st), reps)
                     res[f"{form}/k{k}/{'grad' if gp else 'nograd'}"] = round(t, 1)
         ops.theta_grad_form("bf16x3")
         res["epilogue_bytes_grad"] = 12 * m

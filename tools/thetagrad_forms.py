@@ -52,7 +52,7 @@ def run(name, n, k, S, reps):
 
     def call(mode):
         nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, S, nat.ptr(theta), n,
-                 nat.ptr(grad), mode, nat.ptr(scal), gs, st)
+                 nat.ptr(grad), mode, nat.ptr(scal), gs, ops.form_code(), st)
 
     rows = torch.randint(0, n, (12,), generator=g, device=dev).tolist()
     ud, vd, rd = u.double(), v.double(), r.double().sum(0)
