@@ -332,6 +332,8 @@ class FixedGraphGcn:
         val acc, test loss, test acc) of the epoch (one host sync).  With
         graphs, from the second epoch on both run as one HIP graph replay."""
         import torch
+
+        from . import _native as nat
         eng = self.eng
         if getattr(self, "_res", None) is None:
             self._res = torch.zeros(6, dtype=torch.float32, device=eng.dev)

@@ -548,6 +548,149 @@ def g_hypergrad_cora_real(out, seed=11):
     out["params_final"] = np.concatenate([params[k].detach().numpy().ravel() for k in params])
 
 
+def g_hypergrad_cora_wellcond(out, seed=11):
+    """Two well-conditioned θ-gradients at BASELINE config 2's size (real
+    Cora, kNN θ₀), where no Adam step sits between θ and the loss, so rounding
+    is not amplified (unlike hypergrad_cora_real's windows):
+      outer: the reference's step-0 window (dropout 0.5), then a hyper step
+             with NO inner step before it — NLL on the opt mask through one
+             sampled outer graph with the weights as leaves
+             (src/trainers/outer.py:57-87 after bilevel.py:109-114's detach);
+      nd:    the same real-Cora run with dropout 0 (every forward
+             deterministic given its graph): the step-0 window, its
+             outer-only hyper step, then a dropout-free τ = 5 window.
+    Stored per gradient: 20 000 picked entries, sum and L2 norm."""
+    data = _planetoid("cora")
+    knn = np.load(os.path.join(HERE, "knn_cora.npz"))
+    adj = _adj_from_edges(data.num_nodes, knn["edges"])
+    val, opt = _opt_split(data, seed)
+    prob = dict(x=data.x, y=data.y, train=data.train_mask, val=val, opt=opt, test=data.test_mask, adj=adj)
+    out["seed"] = np.int64(seed)
+    out["opt_mask"] = opt.numpy()
+    out["val_mask"] = val.numpy()
+    for tag, dropout in (("", 0.5), ("nd_", 0.0)):
+        rnd = KeyedRandomness(seed=seed)
+        patch_reference(rnd)
+        runner = build_reference(prob, seed=seed, dropout=dropout)
+        grads, thetas = [], []
+        _spy_grads(runner, grads)
+        loss0 = runner.inner_opt_step().loss
+        runner.hyper_opt_step(0)
+        thetas.append(runner.outer_trainer.model.probs.detach().clone().numpy())
+        runner.hyper_opt_step(1)  # no inner step in this window: the outer graph's path only
+        thetas.append(runner.outer_trainer.model.probs.detach().clone().numpy())
+        keys = ["grad_step0", "grad_outer"]
+        if dropout == 0.0:  # then a whole τ = 5 window (steps 1-5)
+            losses = [runner.inner_opt_step().loss for _ in range(5)]
+            runner.hyper_opt_step(5)
+            thetas.append(runner.outer_trainer.model.probs.detach().clone().numpy())
+            keys.append("grad_window")
+            out[tag + "window_losses"] = np.array(losses)
+        if "idx" not in out:
+            out["idx"] = np.random.default_rng(seed).choice(grads[0].size, 20000, replace=False).astype(np.int64)
+        pick = out["idx"]
+        out[tag + "inner_loss0"] = np.float64(loss0)
+        for h, key in enumerate(keys):
+            _store_vec(out, tag + key, grads[h], pick)
+            _store_vec(out, tag + key.replace("grad", "theta"), thetas[h], pick)
+        params = runner.inner_trainer.model_params
+        out[tag + "params"] = np.concatenate([params[k].detach().numpy().ravel() for k in params])
+
+
+def g_graph_models(out):
+    """SURVEY §8(f) item 4 by the reference code itself (src/models/graph.py:
+    81-200, src/models/sampling.py:19-85), on the keyed Philox uniforms
+    (stored as `u_*`, injected into the product's sampler):
+      emb_*   PairwiseEmbeddingSampler (n 70, d 8, prob_pow 1 and 2):
+              forward() P, sample() (the sacred default: undirected, NONE,
+              STE) and dE of L = Σ (normalize(A_ste)·Z) ⊙ W;
+      knn_*   sample_graph with KNN sparsification (k 7) on the embeddings,
+              cosine and np.dot (the reference passes np.dot to sklearn as a
+              callable metric, i.e. as a distance), and dE through it;
+      eps_*   sample_graph with EPS (eps 0.5, 1.5) on the draw, and the
+              dense=True EPS rule on the probabilities;
+      gae_*   GraphProposalNetwork.calculate_edges_and_embeddings (n 48,
+              f_in 12, embedding 8, dropout 0; normalised similarities /
+              add_original) with its GCN weights, P and embeddings, and the
+              gradients of L through one STE sample to the GCN weights,
+              probs_factor and probs_bias."""
+    import src.models.sampling as sm
+    from src.models.graph import GraphProposalNetwork, PairwiseEmbeddingSampler
+    from src.utils.graph import normalize_adjacency_matrix
+    rnd = KeyedRandomness(seed=61)
+    patch_reference(rnd)
+
+    def uniforms(n):  # the next Bernoulli draw's uniforms (graph counter rnd.graph_counter)
+        return philox.uniform(rnd.seed, philox.tag_for(TAG_GRAPH, rnd.replica), rnd.graph_counter, n, n)
+
+    def loss_of(a, z, w):
+        return ((normalize_adjacency_matrix(a) @ z) * w).sum()
+
+    g = torch.Generator().manual_seed(3)
+    n, d = 70, 8
+    e0 = torch.rand(n, d, generator=g) * 2 - 1
+    z = torch.randn(n, 16, generator=g)
+    w = torch.randn(n, 16, generator=g)
+    out["emb_e"], out["emb_z"], out["emb_w"] = e0.numpy(), z.numpy(), w.numpy()
+    for pw in (1.0, 2.0):
+        key = f"emb_pow{int(pw)}_"
+        m = PairwiseEmbeddingSampler(n_nodes=n, embedding_dim=d, prob_pow=pw)
+        with torch.no_grad():
+            m.embeddings.copy_(e0)
+        out[key + "p"] = m.forward().detach().numpy()
+        out[key + "u"] = uniforms(n)
+        a = m.sample()
+        out[key + "sample"] = a.detach().numpy()
+        loss_of(a, z, w).backward()
+        out[key + "grad_e"] = m.embeddings.grad.detach().numpy()
+    for metric in ("cosine", "dot"):
+        key = f"knn_{metric}_"
+        e = e0.clone().requires_grad_(True)
+        p = torch.sigmoid(e @ e.t())
+        out[key + "u"] = uniforms(n)
+        a = sm.sample_graph(p, undirected=True, embeddings=e, dense=False, k=7,
+                            sparsification=sm.SPARSIFICATION.KNN, knn_metric=metric)
+        out[key + "sample"] = a.detach().numpy()
+        loss_of(a, z, w).backward()
+        out[key + "grad_e"] = e.grad.detach().numpy()
+    pe = torch.sigmoid(e0[:50] @ e0[:50].t())
+    out["eps_p"] = pe.numpy()
+    for eps in (0.5, 1.5):
+        key = f"eps_{str(eps).replace('.', 'p')}_"
+        out[key + "u"] = uniforms(50)
+        a = sm.sample_graph(pe, undirected=True, dense=False, sparsification=sm.SPARSIFICATION.EPS, eps=eps)
+        out[key + "sample"] = a.detach().numpy()
+    pd = pe.clone().requires_grad_(True)
+    a = sm.sample_graph(pd, undirected=True, dense=True, sparsification=sm.SPARSIFICATION.EPS, eps=0.6)
+    a.sum().backward()
+    out["eps_dense"], out["eps_dense_grad"] = a.detach().numpy(), pd.grad.numpy()
+
+    n, f_in, emb = 48, 12, 8
+    g = torch.Generator().manual_seed(21)
+    x = torch.rand(n, f_in, generator=g)
+    adj = (torch.rand(n, n, generator=g) < 0.1).float()
+    adj = torch.maximum(adj, adj.t())
+    adj.fill_diagonal_(0.0)
+    z = torch.randn(n, 16, generator=g)
+    w = torch.randn(n, 16, generator=g)
+    out["gae_x"], out["gae_adj"], out["gae_z"], out["gae_w"] = x.numpy(), adj.numpy(), z.numpy(), w.numpy()
+    for tag, normalize, add_original in (("cos", True, False), ("dot", False, True)):
+        key = f"gae_{tag}_"
+        torch.manual_seed(4)
+        m = GraphProposalNetwork(x, adj, dropout=0.0, add_original=add_original, embedding_dim=emb,
+                                 probs_bias_init=-0.5, probs_factor_init=2.0, normalize_similarities=normalize)
+        out[key + "params"] = np.concatenate([q.detach().numpy().ravel() for q in m.gcn.parameters()])
+        p, e = m.calculate_edges_and_embeddings()
+        out[key + "p"], out[key + "emb"] = p.detach().numpy(), e.detach().numpy()
+        out[key + "u"] = uniforms(n)
+        a = m.sample()
+        out[key + "sample"] = a.detach().numpy()
+        loss_of(a, z, w).backward()
+        out[key + "grad_params"] = np.concatenate([q.grad.numpy().ravel() for q in m.gcn.parameters()])
+        out[key + "grad_factor"] = np.float64(m.probs_factor.grad)
+        out[key + "grad_bias"] = np.float64(m.probs_bias.grad)
+
+
 class _Fp64Products:
     """The reference's two matrix products — the aggregation torch.mm
     (src/models/layers.py:44) and the linear layers' F.linear (torchmeta
@@ -782,7 +925,8 @@ def main():
             ("hypergrad_cora_real_probe", g_hypergrad_cora_real_probe),
             ("hypergrad_citeseer_s16", g_hypergrad_citeseer_s16),
             ("hypergrad_citeseer_s16_probe", g_hypergrad_citeseer_s16_probe), ("gcn_fixed_cora", g_gcn_fixed_cora),
-            ("pretrainer", g_pretrainer)]
+            ("pretrainer", g_pretrainer), ("hypergrad_cora_wellcond", g_hypergrad_cora_wellcond),
+            ("graph_models", g_graph_models)]
     only = set(sys.argv[1:])
     for name, fn in jobs:
         if only and name not in only:

@@ -199,3 +199,111 @@ def test_factory_builds_every_model(device):
         fac.create("nope")
     # both models sample through the HIP sampler
     assert emb.sample().n == n and gae.sample().n == n
+
+
+# ---------------------------------------------------------------------------
+# against the reference itself (golden graph_models, tests/golden/make_golden.py)
+# ---------------------------------------------------------------------------
+def _golden_models():
+    import numpy as np
+
+    from tests.conftest import GOLDEN
+    return np.load(f"{GOLDEN}/graph_models.npz")
+
+
+def _dense_with_loops(a):
+    a = torch.as_tensor(a).clone()
+    a.fill_diagonal_(1.0)  # normalize_adjacency_matrix sets the diagonal to 1 (self-loops)
+    return a
+
+
+def _rel(got, ref):
+    ref = torch.as_tensor(ref, dtype=torch.float64)
+    return float((got.detach().double().cpu() - ref).abs().max() / ref.abs().max())
+
+
+@pytest.mark.parametrize("pw", [1, 2])
+def test_embedding_sampler_matches_reference_golden(device, pw):
+    """PairwiseEmbeddingSampler (src/models/graph.py:81-112) as the reference
+    computes it: P, the sampled edges for the same uniforms (bit-exact), and
+    dE through one normalised aggregation at the north-star 1e-5."""
+    g = _golden_models()
+    key = f"emb_pow{pw}_"
+    e, z, w = (torch.from_numpy(g[k]) for k in ("emb_e", "emb_z", "emb_w"))
+    n, d = e.shape
+    model = PairwiseEmbeddingSampler(n_nodes=n, embedding_dim=d, prob_pow=float(pw)).to(device)
+    with torch.no_grad():
+        model.embeddings.copy_(e.to(device))
+    p = model.forward()
+    assert _rel(p, g[key + "p"]) <= 1e-6
+    graph = Sampler.sample(p, embeddings=model.embeddings, u_inject=torch.from_numpy(g[key + "u"]).to(device))
+    assert torch.equal(graph.to_dense().cpu(), _dense_with_loops(g[key + "sample"]))
+    (ops.aggregate(z.to(device), graph) * w.to(device)).sum().backward()
+    assert _rel(model.embeddings.grad, g[key + "grad_e"]) <= 1e-5
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_knn_sparsification_matches_reference_golden(device, metric):
+    """sample_graph with KNN sparsification (src/models/sampling.py:19-36,
+    47-79): the reference's sklearn kNN pattern (for "dot" the reference hands
+    np.dot to sklearn as a distance), the sampled edges bit-exact, dE at 1e-5."""
+    g = _golden_models()
+    key = f"knn_{metric}_"
+    e = torch.from_numpy(g["emb_e"]).to(device).requires_grad_(True)
+    z, w = torch.from_numpy(g["emb_z"]).to(device), torch.from_numpy(g["emb_w"]).to(device)
+    p = torch.sigmoid(e @ e.t())
+    graph = Sampler.sample(p, sparsification="KNN", k=7, knn_metric=metric, embeddings=e,
+                           u_inject=torch.from_numpy(g[key + "u"]).to(device))
+    assert torch.equal(graph.to_dense().cpu(), _dense_with_loops(g[key + "sample"]))
+    (ops.aggregate(z, graph) * w).sum().backward()
+    assert _rel(e.grad, g[key + "grad_e"]) <= 1e-5
+
+
+@pytest.mark.parametrize("eps", [0.5, 1.5])
+def test_eps_sparsification_matches_reference_golden(device, eps):
+    g = _golden_models()
+    key = f"eps_{str(eps).replace('.', 'p')}_"
+    p = torch.from_numpy(g["eps_p"]).to(device)
+    graph = Sampler.sample(p, sparsification="EPS", eps=eps, u_inject=torch.from_numpy(g[key + "u"]).to(device))
+    assert torch.equal(graph.to_dense().cpu(), _dense_with_loops(g[key + "sample"]))
+
+
+def test_eps_dense_matches_reference_golden(device):
+    g = _golden_models()
+    p = torch.from_numpy(g["eps_p"]).to(device).requires_grad_(True)
+    out = Sampler.sample(p, sparsification="EPS", eps=0.6, dense=True)
+    assert torch.equal(out.detach().cpu(), torch.from_numpy(g["eps_dense"]))
+    out.sum().backward()
+    assert torch.equal(p.grad.cpu(), torch.from_numpy(g["eps_dense_grad"]))
+
+
+@pytest.mark.parametrize("tag,normalize,add_original", [("cos", True, False), ("dot", False, True)])
+def test_graph_proposal_network_matches_reference_golden(device, tag, normalize, add_original):
+    """GraphProposalNetwork.calculate_edges_and_embeddings (src/models/graph.py:
+    167-180) with the reference's GCN weights: embeddings and P at 1e-5, the
+    sample bit-exact for the same uniforms, and the gradients of one
+    normalised aggregation to the GCN weights, probs_factor and probs_bias."""
+    g = _golden_models()
+    key = f"gae_{tag}_"
+    x, adj = torch.from_numpy(g["gae_x"]).to(device), torch.from_numpy(g["gae_adj"]).to(device)
+    z, w = torch.from_numpy(g["gae_z"]).to(device), torch.from_numpy(g["gae_w"]).to(device)
+    model = GraphProposalNetwork(x, adj, dropout=0.0, add_original=add_original, embedding_dim=8,
+                                 probs_bias_init=-0.5, probs_factor_init=2.0,
+                                 normalize_similarities=normalize).to(device)
+    flat = torch.from_numpy(g[key + "params"]).to(device)
+    off = 0
+    with torch.no_grad():
+        for q in model.gcn.parameters():
+            q.copy_(flat[off:off + q.numel()].view_as(q))
+            off += q.numel()
+    p, emb = model.calculate_edges_and_embeddings()
+    assert _rel(emb, g[key + "emb"]) <= 1e-5
+    assert float((p.detach().double().cpu() - torch.from_numpy(g[key + "p"]).double()).abs().max()) <= 1e-5
+    graph = Sampler.sample(p, embeddings=emb, u_inject=torch.from_numpy(g[key + "u"]).to(device))
+    assert torch.equal(graph.to_dense().cpu(), _dense_with_loops(g[key + "sample"]))
+    (ops.aggregate(z, graph) * w).sum().backward()
+    got = torch.cat([q.grad.reshape(-1) for q in model.gcn.parameters()])
+    assert _rel(got, g[key + "grad_params"]) <= 1e-5
+    for name, ref in (("probs_factor", g[key + "grad_factor"]), ("probs_bias", g[key + "grad_bias"])):
+        v = float(getattr(model, name).grad)
+        assert abs(v - float(ref)) <= 1e-5 * max(1.0, abs(float(ref))), (name, v, float(ref))

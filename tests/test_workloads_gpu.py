@@ -50,14 +50,14 @@ TOL = 1e-5
 GRAD_TOL = 1e-5
 
 
-def _trainers(workload, g, seed, replica=0):
+def _trainers(workload, g, seed, replica=0, dropout=0.5):
     data = load_workload(workload)
     data.val_mask = torch.from_numpy(g["val_mask"])
     opt = torch.from_numpy(g["opt_mask"]).to(DEV)
     data = data.to(DEV)
     ldsgnn.rng.manual_seed(seed, replica)
     torch.manual_seed(seed)
-    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=0.5).to(DEV)
+    gcn = MetaDenseGCN(data.num_features, 16, data.num_classes, dropout=dropout).to(DEV)
     inner = InnerProblemTrainer(gcn, data, lr=0.01, weight_decay=5e-4)
     gm = BernoulliGraphModel(data.dense_adj)
     outer = OuterProblemTrainer(torch.optim.SGD(gm.parameters(), lr=0.1), data, opt, gm, lr_decay=0.99)
@@ -134,6 +134,57 @@ def test_config2_engine_window_matches_reference_golden():
     err = np.abs(flat - g["params_final"])
     assert err.max() <= max(1e-5 * np.abs(g["params_final"]).max(), PROBE_FACTOR * probe_w), (err.max(), probe_w)
     assert (err > 1e-6).sum() <= 10  # only the few ill-conditioned weights move beyond 1e-6
+
+
+def _vec_err(got, g, key):
+    """(max error / max|ref|, L2 relative error) on the golden's picked entries."""
+    got = got.detach().double().cpu().numpy()[g["idx"]]
+    ref = g[key + "_val"].astype(np.float64)
+    err = np.abs(got - ref)
+    return float(err.max() / np.abs(ref).max()), float(np.sqrt((err ** 2).sum() / (ref ** 2).sum()))
+
+
+@pytest.mark.parametrize("dropout", [0.5, 0.0])
+def test_config2_wellconditioned_gradients_at_north_star_tolerance(dropout):
+    """Kernel error separated from conditioning (golden hypergrad_cora_wellcond,
+    made by the reference at config 2's size: real Cora, kNN θ₀): the θ-gradient
+    of a hyper step with NO inner step in its window — NLL on the opt mask
+    through one sampled outer graph, the weights leaves — has no Adam step
+    between θ and the loss to amplify rounding, and the engine holds it (and θ
+    after the SGD step) to the north-star 1e-5: every picked entry within
+    1e-5 × max|dθ|, ‖dθ‖₂ within 1e-5.  The dropout-free run also checks its
+    step-0 window and a whole dropout-free τ = 5 window, whose dθ passes
+    through Adam steps (reported in the assertion message; held to 1e-5 where
+    the conditioning allows, see test_config2_reference_conditioning_probe)."""
+    g = np.load(f"{GOLDEN}/hypergrad_cora_wellcond.npz")
+    tag = "" if dropout else "nd_"
+    seed = int(g["seed"])
+    data, inner, outer, gm = _trainers("cora", g, seed, dropout=dropout)
+    eng = engine_from_trainers(inner, outer, tau=5, generator=ldsgnn.rng.default_generator)
+    eng.inner_step()
+    eng.hyper_step()
+    torch.cuda.synchronize()
+    assert abs(eng.inner_metrics(0)[0] - float(g[tag + "inner_loss0"])) <= TOL * float(g[tag + "inner_loss0"])
+    step0 = _vec_err(eng.grad, g, tag + "grad_step0")
+    _check_vec(eng.theta, g, tag + "theta_step0", TOL)
+    eng.hyper_step()  # a window with no inner step: the outer graph's path only
+    torch.cuda.synchronize()
+    outer_err = _vec_err(eng.grad, g, tag + "grad_outer")
+    _check_vec(eng.grad, g, tag + "grad_outer", GRAD_TOL)
+    _check_vec(eng.theta, g, tag + "theta_outer", TOL)
+    if dropout:
+        return
+    for _ in range(5):
+        eng.inner_step()
+    eng.hyper_step()
+    torch.cuda.synchronize()
+    losses = [eng.inner_metrics(t)[0] for t in range(5)]
+    assert np.allclose(losses, g["nd_window_losses"], rtol=TOL, atol=1e-6), (losses, g["nd_window_losses"])
+    window = _vec_err(eng.grad, g, "nd_grad_window")
+    _check_vec(eng.theta, g, "nd_theta_window", TOL)
+    diag = {"step0": step0, "outer": outer_err, "window": window}
+    print("config2 dropout-free gradient errors (max/max|ref|, L2 rel):", diag)
+    assert window[1] <= 1e-5, diag  # the window's dθ as a whole (L2) at the north-star tolerance
 
 
 def test_config3_citeseer_s16_engine_window_matches_reference_golden():
