@@ -129,7 +129,9 @@ def main():
     pub = PUBLISHED.get((args.model, args.dataset))
     print(json.dumps({"summary": f"{args.model} {args.dataset}", "runs": len(accs), "test_acc_mean": float(np.mean(accs)),
                       "test_acc_std": float(np.std(accs)), "published": pub,
-                      "config": "final LDS (τ=5, patience 20, S_eval 16, θ lr 0.1 decay 0.99, pretrain)"
+                      "config": f"LDS (τ={args.tau}, patience 20, S_eval 16, θ lr 0.1 decay 0.99, "
+                                f"{'no pretrain' if args.no_pretrain else 'pretrain'}, "
+                                f"{'fused engine' if args.fused else 'drop-in autograd'})"
                       if args.model == "lds" else "GCN (Adam 0.01, wd 5e-4, 200 epochs, patience 10)"}), flush=True)
 
 

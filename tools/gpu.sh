@@ -1,0 +1,80 @@
+#!/bin/bash
+# One launcher for every GPU-box step (replaces the round-1/2 per-session
+# tools/gpu_*.sh copies).  Each step runs under its own time limit; the first
+# failing step ends the script (no GPU work after a failure).
+#
+#   tools/gpu.sh TAG STEP [STEP ...]
+#
+# Steps (outputs under gpurun_out/, named with TAG):
+#   tests      the whole -m gpu suite                       tests_TAG.log
+#   smoke      __graft_entry__.smoke()                      smoke_TAG.log
+#   bench      the default bench line (Cora, S = 1)          bench_TAG.json
+#   prof       rocprofv3 kernel-trace summary of the bench   prof_TAG/
+#   pmc        FETCH_SIZE / WRITE_SIZE passes of the bench   pmc_TAG_{fetch,write}/
+#   config5    synthetic N = 20 000 line + its kernel trace c5_bench_TAG.json, c5_prof_TAG/
+#   c5cpu      the config-5 line with its CPU baseline       c5_cpu_TAG.json
+#   samples    Cora S = 8 / 16, Citeseer S = 16 lines        s_<ds>_<S>_TAG.json
+#   scpu       the Citeseer S = 16 line with its CPU baseline s_cpu_TAG.json
+#   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
+set -o pipefail
+tag=${1:?usage: tools/gpu.sh TAG STEP...}
+shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out
+run() {  # seconds, then the command; stdout/stderr redirected by the caller
+    local t=$1
+    shift
+    timeout -k 10 "$t" "$@"
+}
+for step in "$@"; do
+    echo "[gpu.sh] $step $(date +%T)"
+    case $step in
+    tests)
+        run 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+            > $O/tests_$tag.log 2>&1 || exit $? ;;
+    smoke)
+        run 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$tag.log 2>&1 || exit $? ;;
+    bench)
+        run 300 python bench.py > $O/bench_$tag.json 2> $O/bench_$tag.err || exit $? ;;
+    prof)
+        run 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$tag -o run -- \
+            python3 bench.py --no-cpu-baseline --steps 100 > $O/prof_$tag.log 2>&1 || exit $? ;;
+    pmc)
+        for c in FETCH_SIZE WRITE_SIZE; do
+            lc=$(echo $c | cut -d_ -f1 | tr 'A-Z' 'a-z')
+            run 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_${tag}_$lc -o run -- \
+                python3 bench.py --no-cpu-baseline --no-breakdown --steps 50 --warmup 10 \
+                > $O/pmc_${tag}_$lc.log 2>&1 || exit $?
+        done ;;
+    config5)
+        run 400 python -u bench.py --dataset synthetic20k --steps 10 --warmup 5 --no-cpu-baseline \
+            > $O/c5_bench_$tag.json 2> $O/c5_bench_$tag.err || exit $?
+        run 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5_prof_$tag -o run -- \
+            python3 bench.py --dataset synthetic20k --steps 10 --warmup 5 --no-cpu-baseline --no-breakdown \
+            > $O/c5_prof_$tag.log 2>&1 || exit $? ;;
+    c5cpu)
+        run 900 python -u bench.py --dataset synthetic20k --steps 10 --warmup 5 --cpu-steps 1 \
+            > $O/c5_cpu_$tag.json 2> $O/c5_cpu_$tag.err || exit $? ;;
+    samples)
+        for spec in "cora 8" "cora 16" "citeseer 16"; do
+            set -- $spec
+            run 300 python bench.py --dataset $1 --samples $2 --steps 100 --warmup 10 --no-cpu-baseline \
+                > $O/s_${1}_$2_$tag.json 2> $O/s_${1}_$2_$tag.err || exit $?
+        done ;;
+    scpu)
+        run 400 python bench.py --dataset citeseer --samples 16 --steps 100 --warmup 10 \
+            > $O/s_cpu_$tag.json 2> $O/s_cpu_$tag.err || exit $? ;;
+    multirank)
+        run 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29517 bench.py --gpus 2 --backend gloo --steps 50 --warmup 10 --no-cpu-baseline \
+            > $O/bench_2rank_gloo_$tag.log 2>&1 || exit $?
+        run 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29518 bench.py --gpus 2 --backend gloo --samples 8 --steps 50 --warmup 10 \
+            --no-cpu-baseline > $O/bench_2rank_gloo_s8_$tag.log 2>&1 || exit $? ;;
+    *)
+        echo "unknown step $step" >&2
+        exit 2 ;;
+    esac
+done
+echo "[gpu.sh] done $(date +%T)"
