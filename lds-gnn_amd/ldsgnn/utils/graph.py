@@ -133,20 +133,39 @@ def knn_graph_dense(x: torch.Tensor, k: int, loop: bool = True, metric: str = "c
     """src/data/utils.py:165-175: sklearn's kneighbors_graph(mode='connectivity',
     include_self=loop) as a dense 0/1 matrix, directed rows (row i marks its k
     nearest), on x's device.  metric "cosine": distance 1 - cos; "dot" (the
-    reference passes np.dot as a callable metric, sklearn then treats the dot
-    product as a distance): the k smallest dot products.  Ties broken by
-    index.  The query point counts as its own neighbour when loop=True."""
+    reference passes np.dot as a callable metric, so sklearn treats the dot
+    product as a distance): the smallest dot products are the nearest.
+
+    sklearn's rule for the query point itself:
+    - include_self=True: the k nearest of all points — the point itself only
+      if its own distance ranks (for cosine it always does: distance 0);
+    - include_self=False: the k + 1 nearest are taken and the point itself is
+      dropped from them; when it is not among them, the FIRST (nearest)
+      candidate is dropped instead (sklearn.neighbors KNeighborsMixin
+      .kneighbors with X=None).  Under "dot" a point's own distance |x|² is
+      rarely among the smallest, so its nearest neighbour is skipped.
+    Pinned against the reference's own sklearn calls: tests/golden/knn_cora.npz
+    (cosine) and graph_models.npz (cosine and dot)."""
     x = x.detach().float()
     n = x.size(0)
-    if metric == "cosine":   # nearest = largest cosine
+    if metric == "cosine":   # nearest = largest cosine; a point is its own nearest (distance 0)
         xn = x / x.norm(dim=1, keepdim=True).clamp(min=1e-12)
         score = xn @ xn.t()
-    elif metric == "dot":    # nearest = smallest dot product (sklearn reads it as a distance)
+        score.fill_diagonal_(float("inf") if loop else -float("inf"))
+        idx = torch.topk(score, k, dim=1).indices
+    elif metric == "dot":    # nearest = smallest dot product
         score = -(x @ x.t())
+        if loop:
+            idx = torch.topk(score, k, dim=1).indices
+        else:
+            cand = torch.topk(score, k + 1, dim=1).indices            # nearest first
+            rows = torch.arange(n, device=x.device).unsqueeze(1)
+            is_self = cand == rows
+            drop = torch.where(is_self.any(1, keepdim=True), is_self,
+                               torch.arange(k + 1, device=x.device).unsqueeze(0) == 0)
+            idx = cand[~drop].view(n, k)
     else:
         raise NotImplementedError(f"knn metric {metric}")
-    score.fill_diagonal_(float("inf") if loop else -float("inf"))
-    idx = torch.topk(score, k, dim=1).indices
     a = torch.zeros((n, n), dtype=torch.float32, device=x.device)
     a.scatter_(1, idx, 1.0)
     return a

@@ -606,14 +606,17 @@ def g_graph_models(out):
               STE) and dE of L = Σ (normalize(A_ste)·Z) ⊙ W;
       knn_*   sample_graph with KNN sparsification (k 7) on the embeddings,
               cosine and np.dot (the reference passes np.dot to sklearn as a
-              callable metric, i.e. as a distance), and dE through it;
+              callable metric, i.e. as a distance), and dE through it; for
+              np.dot also with sklearn's exact brute-force search (knn_dotbrute:
+              the default BallTree is not exact on a non-metric);
       eps_*   sample_graph with EPS (eps 0.5, 1.5) on the draw, and the
               dense=True EPS rule on the probabilities;
       gae_*   GraphProposalNetwork.calculate_edges_and_embeddings (n 48,
               f_in 12, embedding 8, dropout 0; normalised similarities /
               add_original) with its GCN weights, P and embeddings, and the
               gradients of L through one STE sample to the GCN weights,
-              probs_factor and probs_bias."""
+              probs_factor and probs_bias (plus the fp64 rerun of the same
+              gradient: the reference's own conditioning probe)."""
     import src.models.sampling as sm
     from src.models.graph import GraphProposalNetwork, PairwiseEmbeddingSampler
     from src.utils.graph import normalize_adjacency_matrix
@@ -643,16 +646,31 @@ def g_graph_models(out):
         out[key + "sample"] = a.detach().numpy()
         loss_of(a, z, w).backward()
         out[key + "grad_e"] = m.embeddings.grad.detach().numpy()
-    for metric in ("cosine", "dot"):
+    ref_knn = sm.knn_graph_dense
+
+    def knn_brute(x, k, loop=True, metric="cosine"):
+        # the reference's knn_graph_dense (src/data/utils.py:165-175) with
+        # sklearn's exact brute-force search: with metric=np.dot sklearn's
+        # default picks a BallTree, whose pruning is not exact on a
+        # non-metric (negative "distances")
+        from sklearn.neighbors import NearestNeighbors
+        nn = NearestNeighbors(n_neighbors=k, metric=metric, algorithm="brute").fit(x.numpy())
+        return torch.FloatTensor(nn.kneighbors_graph(None if not loop else x.numpy(), n_neighbors=k,
+                                                     mode="connectivity").toarray())
+
+    for metric, knn in (("cosine", ref_knn), ("dot", ref_knn), ("dotbrute", knn_brute)):
         key = f"knn_{metric}_"
+        sm.knn_graph_dense = knn
         e = e0.clone().requires_grad_(True)
         p = torch.sigmoid(e @ e.t())
         out[key + "u"] = uniforms(n)
         a = sm.sample_graph(p, undirected=True, embeddings=e, dense=False, k=7,
-                            sparsification=sm.SPARSIFICATION.KNN, knn_metric=metric)
+                            sparsification=sm.SPARSIFICATION.KNN, knn_metric=metric[:3] if metric != "cosine"
+                            else metric)
         out[key + "sample"] = a.detach().numpy()
         loss_of(a, z, w).backward()
         out[key + "grad_e"] = e.grad.detach().numpy()
+    sm.knn_graph_dense = ref_knn
     pe = torch.sigmoid(e0[:50] @ e0[:50].t())
     out["eps_p"] = pe.numpy()
     for eps in (0.5, 1.5):
@@ -689,6 +707,19 @@ def g_graph_models(out):
         out[key + "grad_params"] = np.concatenate([q.grad.numpy().ravel() for q in m.gcn.parameters()])
         out[key + "grad_factor"] = np.float64(m.probs_factor.grad)
         out[key + "grad_bias"] = np.float64(m.probs_bias.grad)
+        # conditioning probe: the same reference computation in fp64 (same
+        # weights, same sample).  With normalised similarities near 1 the
+        # reference's own fp32 gradient moves by ~1e-4 of its max under it.
+        m64 = GraphProposalNetwork(x.double(), adj.double(), dropout=0.0, add_original=add_original,
+                                   embedding_dim=emb, probs_bias_init=-0.5, probs_factor_init=2.0,
+                                   normalize_similarities=normalize).double()
+        with torch.no_grad():
+            for q64, q in zip(m64.gcn.parameters(), m.gcn.parameters()):
+                q64.copy_(q.double())
+        p64, _ = m64.calculate_edges_and_embeddings()
+        a64 = (torch.from_numpy(out[key + "sample"]).double() - p64).detach() + p64
+        ((normalize_adjacency_matrix(a64) @ z.double()) * w.double()).sum().backward()
+        out[key + "grad_params_fp64"] = np.concatenate([q.grad.numpy().ravel() for q in m64.gcn.parameters()])
 
 
 class _Fp64Products:
