@@ -10,14 +10,32 @@ from ldsgnn.utils.graph import DenseData, knn_graph_dense
 
 
 def test_knn_dot_metric_is_a_distance():
-    """np.dot passed to sklearn as a metric is read as a distance: the k
-    smallest dot products are the neighbours (src/models/sampling.py:30-32)."""
+    """np.dot passed to sklearn as a metric is read as a distance
+    (src/models/sampling.py:30-32, src/data/utils.py:165-175).  Without
+    include_self sklearn takes the k + 1 nearest and drops the query point —
+    or, when the point is not among them (its own "distance" |x|² is large),
+    the nearest one: row 0's dots with rows 0..3 are 1, 2, -1, 0, so the two
+    nearest are rows 2 and 3, row 0 is not among them, row 2 is dropped."""
     x = torch.tensor([[1.0, 0.0], [2.0, 0.0], [-1.0, 0.0], [0.0, 1.0]])
     a = knn_graph_dense(x, 1, loop=False, metric="dot")
-    # row 0: dots with rows 1..3 = 2, -1, 0 -> nearest is row 2
-    assert torch.equal(a[0], torch.tensor([0.0, 0.0, 1.0, 0.0]))
+    assert torch.equal(a[0], torch.tensor([0.0, 0.0, 0.0, 1.0]))
     c = knn_graph_dense(x, 1, loop=False, metric="cosine")
     assert torch.equal(c[0], torch.tensor([0.0, 1.0, 0.0, 0.0]))
+
+
+@pytest.mark.parametrize("loop", [False, True])
+@pytest.mark.parametrize("metric", ["dot", "cosine"])
+def test_knn_matches_sklearn_brute_force(loop, metric):
+    """The same pattern as sklearn's exact search (algorithm="brute") with the
+    reference's metric arguments, on random embeddings."""
+    import numpy as np
+    from sklearn.neighbors import NearestNeighbors
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(60, 6, generator=g)
+    nn = NearestNeighbors(n_neighbors=5, metric=np.dot if metric == "dot" else metric, algorithm="brute")
+    nn.fit(x.numpy())
+    ref = nn.kneighbors_graph(x.numpy() if loop else None, n_neighbors=5, mode="connectivity").toarray()
+    assert np.array_equal(knn_graph_dense(x, 5, loop=loop, metric=metric).numpy(), ref)
 
 
 def test_knn_loop_includes_self_first():
