@@ -122,7 +122,9 @@ int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, 
 
 /* The fill launch of lds_sample_graphs_multi alone (CSR, s, ELL head of
  * `graphs` graphs whose bits and degree counts are already drawn, e.g. by
- * lds_theta_grad_sgd_draw); deg_ws as lds_sample_graphs_multi's. */
+ * lds_theta_grad_sgd_draw); deg_ws as lds_sample_graphs_multi's.  col == NULL:
+ * s only (graphs aggregated from their bits, lds_aggregate_bitmask; row_ptr
+ * and ell may be NULL). */
 int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_ws, int graphs,
                         int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
                         const uint8_t* node_flags, void* stream);

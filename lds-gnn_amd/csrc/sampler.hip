@@ -657,13 +657,29 @@ extern "C" int lds_sgd_sample_graphs(float* theta, const float* grad, const void
     LDS_RETURN_LAST_ERROR();
 }
 
+// s = deg^-1/2 of `graphs` graphs from their accumulated degree counts (the
+// bitmask form of the fill: dense graphs aggregated from their bits need no CSR).
+__global__ __launch_bounds__(256) void degree_scale_kernel(const int* __restrict__ dacc, int wsi, int n,
+                                                           float* __restrict__ s) {
+    const int row = blockIdx.x * 256 + threadIdx.x;
+    if (row >= n) return;
+    s[(int64_t)blockIdx.y * n + row] = inv_sqrt_degree(dacc[(int64_t)blockIdx.y * wsi + row]);
+}
+
 // The fill launch of lds_sample_graphs_multi alone, for graphs whose bits and
-// degree counts were drawn elsewhere (lds_theta_grad_sgd_draw).
+// degree counts were drawn elsewhere (lds_theta_grad_sgd_draw); col == NULL:
+// s only (row_ptr, ell unused, may be NULL).
 extern "C" int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_ws, int graphs,
                                    int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
                                    const uint8_t* node_flags, void* stream) {
-    LDS_CHECK_ARG(bits && deg_ws && row_ptr && col && s && n > 0 && n <= kEllIndex + 1 && col_stride > 0);
+    LDS_CHECK_ARG(bits && deg_ws && s && n > 0 && n <= kEllIndex + 1);
+    LDS_CHECK_ARG(col == nullptr || (row_ptr != nullptr && col_stride > 0));
     LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64);
+    if (col == nullptr) {
+        hipLaunchKernelGGL(degree_scale_kernel, dim3((n + 255) / 256, graphs), dim3(256), 0, (hipStream_t)stream,
+                           deg_ws, lds_sample_ws_ints(n), n, s);
+        LDS_RETURN_LAST_ERROR();
+    }
     hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 15) / 16, graphs), dim3(256), 0, (hipStream_t)stream, bits,
                        n, words, deg_ws, lds_sample_ws_ints(n), row_ptr, col, col_stride, s, (int2*)ell, node_flags);
     LDS_RETURN_LAST_ERROR();

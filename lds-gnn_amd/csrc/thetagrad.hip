@@ -798,11 +798,12 @@ __device__ __forceinline__ int64_t tri_at_t(int i, int j, int64_t n) {
 // Epilogue of the 128-tile kernels (wave (wr, wc) owns outputs wr·64 … + 63 ×
 // wc·64 … + 63 of the tile): dθ = gscale·(acc + R_i + R_j) on the strict upper
 // triangle, clamp-backward mask, then the mode's stores.
-template <bool SMALL>
+template <bool SMALL, bool DRAW = false>
 __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const float* Ri, const float* Rj,
                                               float* __restrict__ theta, float* __restrict__ grad, int n,
                                               int mode, const double* __restrict__ lr_dev, float gscale,
-                                              int i0, int j0, int wr, int wc, int lane) {
+                                              int i0, int j0, int wr, int wc, int lane,
+                                              uint32_t (*thr)[2][16] = nullptr) {
     const int64_t nn = n;
     auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
     // Epilogue: every θ (and partial-grad) operand of the wave's 64 outputs is
@@ -838,6 +839,7 @@ __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const f
             for (int e = 0; e < 16; ++e) {
                 const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
                 const int i = i0 + li;
+                if constexpr (DRAW) thr[m][q][e] = 0u;
                 if (i >= n || j >= n || j < i) continue;
                 const int64_t id = tri_at(i, j, nn);
                 const float t0 = th[m][q][e];
@@ -852,7 +854,10 @@ __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const f
                     theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
                 } else if (mode == 2) {
                     if (grad != nullptr) grad[id] = g;
-                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                    const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                    theta[id] = tn;
+                    // the next draw's integer threshold (sampler.hip): bit iff (x >> 8) < ceil(θ·2^24)
+                    if constexpr (DRAW) thr[m][q][e] = j > i ? (uint32_t)ceilf(tn * 16777216.0f) : 0u;
                 } else if (mode == 1) {
                     grad[id] = part[m][q][e] + g;
                 } else {
@@ -862,12 +867,105 @@ __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const f
         }
 }
 
-template <bool VEC, bool SMALL = false, bool PRE = false>
+// The next window's draw from the θ a 128-tile epilogue just wrote (mode 2;
+// lds_theta_grad_sgd_draw at 128-tile shapes, config 5): the sampler's Philox
+// words per (row quad, column) — each lane's 16 outputs of a 32 × 32
+// accumulator are 4 row quads of one column, the sampler tile kernel's counter
+// shape — the same integer compare, bit rows by ballot (32-column segments,
+// four per 128-column row, joined in LDS), column words from each lane's own
+// bits, then one 16-byte store per (graph, row) of the tile's two words and one
+// degree atomic: the bits and degrees of lds_sample_graphs_multi on the
+// updated θ.  `lds` is the dead staging buffer (>= 32 KB).
+constexpr int kT128Grp = 8;  // graphs per draw group (4 KB of LDS each)
+
+__device__ __forceinline__ void t128_draw(const uint32_t (&thr)[2][2][16], uint32_t* lds, const DrawArgs& dr, int n,
+                                          int i0, int j0, int wr, int wc, int lane, int t) {
+    uint32_t* const rwb = lds;                                                 // [grp][128 rows][4 segs]
+    uint64_t* const cwb = reinterpret_cast<uint64_t*>(lds + kT128Grp * 512);  // [grp][2 halves][128 cols]
+    const bool diag = i0 == j0;
+    const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
+#pragma unroll 1
+    for (int base = 0; base < dr.graphs; base += kT128Grp) {
+        const int gn = min(kT128Grp, dr.graphs - base);
+        __syncthreads();  // the stage buffer (first group) / the previous group's words are consumed
+#pragma unroll 1
+        for (int q = 0; q < gn; ++q) {
+            const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const uint32_t j = (uint32_t)(j0 + wc * 64 + qq * 32 + (lane & 31));
+                uint64_t colw = 0;  // rows wr·64 … + 63 of column j
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
+                    uint32_t x[16];
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const U32x4 o = philox4x32_10(U32x4{j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr}, dr.k0, dr.k1);
+                        x[4 * qd] = o.x;
+                        x[4 * qd + 1] = o.y;
+                        x[4 * qd + 2] = o.z;
+                        x[4 * qd + 3] = o.w;
+                    }
+                    uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const bool bit = (x[e] >> 8) < thr[m][qq][e];
+                        const uint64_t w = __ballot(bit);
+                        mylo = lane == e ? (uint32_t)w : mylo;
+                        myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                        colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                    }
+                    if (lane < 16) {  // element e = lane: rows rr and rr + 4, column segment wc·2 + qq
+                        const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
+                        rwb[(q * 128 + rr) * 4 + wc * 2 + qq] = mylo;
+                        rwb[(q * 128 + rr + 4) * 4 + wc * 2 + qq] = myhi;
+                    }
+                }
+                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+                if (lane < 32) cwb[(q * 2 + wr) * 128 + wc * 64 + qq * 32 + lane] = colw;
+            }
+        }
+        __syncthreads();
+        // one (row, two words) pair per work item: rows of I (part 0), rows of J (part 1)
+        for (int it = t; it < gn * 256; it += 256) {
+            const int q = it >> 8, part1 = (it >> 7) & 1, x = it & 127;
+            if (diag && part1) continue;
+            const int row = (part1 ? j0 : i0) + x;
+            if (row >= n) continue;
+            uint64_t* __restrict__ gb = dr.bits + (int64_t)(base + q) * n * dr.words;
+            int* __restrict__ da = dr.dacc + (int64_t)(base + q) * dr.wsi;
+            const uint32_t* rws = rwb + (q * 128 + x) * 4;
+            uint64_t w0, w1;
+            int wbase;
+            if (part1) {  // column x of J: its rows of I (the mirrored entries)
+                w0 = cwb[(q * 2 + 0) * 128 + x];
+                w1 = cwb[(q * 2 + 1) * 128 + x];
+                wbase = i0 >> 6;
+            } else {
+                w0 = (uint64_t)rws[0] | ((uint64_t)rws[1] << 32);
+                w1 = (uint64_t)rws[2] | ((uint64_t)rws[3] << 32);
+                wbase = j0 >> 6;
+                if (diag) {  // strict upper (row words) | strict lower (column words) | self-loop
+                    w0 |= cwb[(q * 2 + 0) * 128 + x];
+                    w1 |= cwb[(q * 2 + 1) * 128 + x];
+                    if (x < 64) w0 |= 1ull << x;
+                    else w1 |= 1ull << (x - 64);
+                }
+            }
+            *reinterpret_cast<ulonglong2*>(gb + (int64_t)row * dr.words + wbase) = ulonglong2{w0, w1};
+            const int pc = __popcll(w0) + __popcll(w1);
+            if (pc != 0) atomicAdd(&da[row], pc);
+        }
+    }
+}
+
+template <bool VEC, bool SMALL = false, bool PRE = false, bool DRAW = false>
 __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
-    float gscale, int group, int per_xcd, Planes pl) {
+    float gscale, int group, int per_xcd, Planes pl, DrawArgs dr = DrawArgs{}) {
     constexpr int kPL = kPL2 + (PRE ? 4 : 0);
     __shared__ __attribute__((aligned(16))) uint32_t lds[12 * kPL];
     __shared__ float Ri[kT2], Rj[kT2];
@@ -1014,7 +1112,13 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
         }
         compute();
     }
-    t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
+    if constexpr (DRAW) {
+        uint32_t thr[2][2][16];
+        t128_epilogue<SMALL, true>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane, thr);
+        t128_draw(thr, lds, dr, n, i0, j0, wr, wc, lane, t);
+    } else {
+        t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1787,7 +1891,8 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
                                        int* deg_ws, int form, void* stream) {
     LDS_CHECK_ARG(form >= 0 && form <= 9);
     LDS_CHECK_ARG(u && v && theta && scalars && bits && deg_ws && n > 0 && k >= 0 && ld >= k);
-    LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64 && nr >= 0);
+    // the 128-tile draws store two words per (graph, row): whole 128-column word pairs
+    LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && (words & 1) == 0 && words >= 2 * ((n + 127) / 128) && nr >= 0);
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
     LDS_CHECK_ARG((ld & 3) == 0 && (k & 7) == 0 && ((uintptr_t)u & 15) == 0 && ((uintptr_t)v & 15) == 0);
     const int nb = (n + kTile - 1) / kTile;
@@ -1796,11 +1901,26 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
     const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
     DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                 counter_offset, counter_base, graphs};
-    // the 64-tile form (form 6) unless the eight-wave 128-tile form (9) is
-    // asked for; both give identical θ, bits and degrees.  MI355X (tools/
-    // microbench/tg_draw_ab.py): 61.8 vs 63.6 µs at Cora, 86 vs 114 at
-    // Citeseer, 2.61 vs 2.91 ms at n = 20 000 (six graphs, k = 264).
-    if (form == 9) {
+    // by shape (form 1): the 64-tile form (6) while the 128-tile grid cannot
+    // fill the chip (as launch_theta_grad's rule), else the 128-tile form in
+    // XCD-grouped order (5); 9 the eight-wave 128-tile form; every form gives
+    // identical θ, bits and degrees.  MI355X (tools/microbench/tg_draw_ab.py,
+    // six graphs, k = 264): 64-tile 61.8 vs eight-wave 63.6 µs at Cora, 86 vs
+    // 114 at Citeseer, 2.61 vs 2.91 ms at n = 20 000.
+    const int nb2 = (n + kT2 - 1) / kT2;
+    const int nt2 = nb2 * (nb2 + 1) / 2;
+    if (form == 1) form = (nt2 >= 1024 || k >= 1024) ? 5 : 6;
+    if (form == 4 || form == 5 || form == 7 || form == 8) {
+        const int per2 = (nt2 + 7) / 8;
+        if (n <= 46340 && form != 7)
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true, false, true>), dim3(8 * per2), dim3(256), 0,
+                               (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup,
+                               per2, Planes{nullptr, nullptr}, dr);
+        else
+            hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, false, false, true>), dim3(8 * per2), dim3(256), 0,
+                               (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup,
+                               per2, Planes{nullptr, nullptr}, dr);
+    } else if (form == 9) {
         launch_w8((hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1.0f, &dr);
     } else {
         hipLaunchKernelGGL((theta_grad_bf3_kernel<16, true, false, true, true>), dim3(8 * per), dim3(256), 0,

@@ -790,7 +790,7 @@ class LdsEngine:
         gb = self.gbatch
         if self._prefetched:  # bits + degrees drawn by the last hyper step (lds_theta_grad_sgd_draw)
             nat.call("lds_sample_fill_csr", nat.ptr(gb.bits), self.n, self.words, nat.ptr(gb.deg), count * self.S,
-                     nat.ptr(gb.row_ptr), nat.ptr(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell),
+                     nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell),
                      nat.ptr(self.nflag), self._stream())
             self._prefetched = False
         else:
@@ -816,24 +816,18 @@ class LdsEngine:
 
     def _prefetch_ok(self, T: int, k0: int, exchange: bool = False, check_flag: bool = True) -> bool:
         """The next window's draw can ride in this hyper step: plain LDS θ, a
-        full window, CSR graphs; with an exchange (dθ all-reduced before the
-        SGD step) in the SGD + clamp pass (lds_sgd_sample_graphs, any S),
-        else in the θ-grad kernel: single sample, the 64-tile split-bf16 form
-        with aligned operands (lds_theta_grad_sgd_draw)."""
+        full window; with an exchange (dθ all-reduced before the SGD step) in
+        the SGD + clamp pass (lds_sgd_sample_graphs, any S, CSR graphs), else
+        in the θ-grad kernel: single sample, a split-bf16 form with aligned
+        operands (lds_theta_grad_sgd_draw: the 64-tile form at Cora-sized
+        shapes, the 128-tile form at large n, where the bitmask-aggregated
+        window then needs only s from the drawn degrees)."""
         if not ((self.prefetch_draw or not check_flag) and self.theta_fn is None and self.outer_update is None
-                and not self.bitmask_agg and T == self.tau and self.gbatch.count == self.tau + 1):
+                and T == self.tau and self.gbatch.count == self.tau + 1):
             return False
         if exchange:
-            return True
-        if self.S != 1:
-            return False
-        form = self._form_name()
-        nb2 = (self.n + 127) // 128
-        # the by-shape rule of csrc/thetagrad.hip launch_theta_grad (form 1 -> 6
-        # unless 128-tiles: nt128 >= 1024, or k >= 1024), so the fused kernel
-        # replaces exactly the launch the plain hyper step would make
-        by_shape_64 = form == "bf16x3" and nb2 * (nb2 + 1) // 2 < 1024 and k0 < 1024
-        if not (by_shape_64 or form == "bf16x3-t64k16-grouped"):
+            return not self.bitmask_agg
+        if self.S != 1 or self._form_name() == "fp32":
             return False
         return self.ldk % 4 == 0 and k0 % 8 == 0 and nat.ptr(self.U) % 16 == 0 and nat.ptr(self.V) % 16 == 0
 

@@ -573,3 +573,51 @@ def test_prefetched_draw_with_exchange_equals_eager(samples):
         for k, v in a.get_params(s).items():
             assert torch.equal(v, b.get_params(s)[k]), (s, k)
     assert a.scalars_host() == b.scalars_host()
+
+
+@pytest.mark.parametrize("form", ["bf16x3", "bf16x3-t128-grouped"])
+def test_bitmask_engine_prefetched_draw_equals_eager(form):
+    """Long-row (bitmask-aggregation) engine, the config-5 path, at a small n:
+    with capture_window(prefetch=True) the hyper step's θ-grad kernel (the
+    64-tile or the 128-tile form) draws the next window's graphs, the window
+    computes only s from the drawn degrees (lds_sample_fill_csr, col = NULL)
+    and aggregates from the bits.  Bitwise equal to eager windows that draw
+    their own graphs (tile sampler + popcount degrees)."""
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.rng import Generator as Gen
+    from oracle import lds_oracle as O
+    n, f_in, c = 700, 24, 5
+    g = torch.Generator().manual_seed(17)
+    x = torch.rand(n, f_in, generator=g)
+    x = (x / x.sum(1, keepdim=True)).to("cuda")
+    y = torch.randint(0, c, (n,), generator=g).to("cuda")
+    perm = torch.randperm(n, generator=g)
+    masks = []
+    for idx in (perm[:100], perm[100:250]):
+        m = torch.zeros(n, dtype=torch.bool)
+        m[idx] = True
+        masks.append(m.to("cuda"))
+    theta0 = torch.rand(n * (n + 1) // 2, generator=g).to("cuda")
+    engines = []
+    for _ in range(2):
+        torch.manual_seed(4)
+        params = {k: v.to("cuda") for k, v in O.init_params(f_in, 16, c).items()}
+        e = LdsEngine(x, y, masks[0], masks[1], theta0.clone(), c, dropout=0.5, outer_lr=0.1, lr_decay=0.99,
+                      tau=3, generator=Gen(11, 0), params=params, long_rows=True)
+        assert e.bitmask_agg
+        e.theta_form = form
+        e.inner_step()
+        e.hyper_step()
+        engines.append(e)
+    a, b = engines
+    a.capture_window(3, prefetch=True)
+    assert a.prefetch_draw and a._prefetched
+    a.replay(3)
+    for _ in range(3):
+        b.run_window(3)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+    assert a.scalars_host() == b.scalars_host()
+    assert a.sampled_nnz() == b.sampled_nnz() > 0

@@ -585,7 +585,7 @@ def test_theta_grad_pipe_bit_exact(device, n, k, mode):
         assert torch.equal(outs[0][1], o[1])
 
 
-@pytest.mark.parametrize("draw_form", ["bf16x3", "bf16x3-t64k16-grouped"])
+@pytest.mark.parametrize("draw_form", ["bf16x3", "bf16x3-t64k16-grouped", "bf16x3-t128-grouped", "bf16x3-t128-w8"])
 @pytest.mark.parametrize("n,k,graphs", [(2708, 264, 6), (300, 40, 3), (130, 8, 1), (700, 24, 2), (1000, 16, 21),
                                         (64, 8, 2), (129, 24, 9)])
 def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs, draw_form):

@@ -19,6 +19,8 @@ from ldsgnn import ops  # noqa: E402
 from ldsgnn.rng import TAG_GRAPH, tag_for  # noqa: E402
 
 BF16_PEAK_TF = 2500.0
+# draw forms compared (the first is the reference for the bit-identity check)
+DRAW_FORMS = tuple(os.environ.get("DRAW_FORMS", "bf16x3-t64k16-grouped,bf16x3-t128-w8").split(","))
 
 
 def chain_us(fn, dev, copies=20, reps=10):
@@ -60,7 +62,6 @@ def run(name, n, k, graphs, plain_forms):
     bits = torch.zeros((graphs, n, words), dtype=torch.int64, device=dev)
     deg = torch.zeros((graphs, wsi), dtype=torch.int32, device=dev)
     seed, tag = 99, tag_for(TAG_GRAPH, 0)
-    st = nat.stream_of(dev)
     flop = 24.0 * k * n * (n + 1) / 2  # bf16 MFMA flop (six products per fp32 product)
     out = {"workload": name, "n": n, "k": k, "graphs": graphs}
 
@@ -70,7 +71,7 @@ def run(name, n, k, graphs, plain_forms):
                  nat.ptr(deg), ops.form_code(), nat.stream_of(dev))
 
     results = {}
-    for form in ("bf16x3-t64k16-grouped", "bf16x3"):
+    for form in DRAW_FORMS:
         prev = ops.theta_grad_form(form)
         try:
             theta.copy_(theta0)
@@ -88,15 +89,14 @@ def run(name, n, k, graphs, plain_forms):
             out["draw_" + form] = {"chain_us": t - zt, "bf16_frac": flop / (t - zt) / 1e6 / BF16_PEAK_TF}
         finally:
             ops.theta_grad_form(prev)
-    a, b = results["bf16x3-t64k16-grouped"], results["bf16x3"]
-    out["draw_identical"] = {"theta": bool(torch.equal(a[0], b[0])), "grad": bool(torch.equal(a[1], b[1])),
-                             "bits": bool(torch.equal(a[2], b[2])), "deg": bool(torch.equal(a[3], b[3]))}
+    a = results[DRAW_FORMS[0]]
+    out["draw_identical"] = {f: all(bool(torch.equal(x, y)) for x, y in zip(a, results[f])) for f in DRAW_FORMS[1:]}
     for form in plain_forms:
         prev = ops.theta_grad_form(form)
         try:
             def fn():
                 nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, 1, nat.ptr(theta), n,
-                         nat.ptr(grad), 2, nat.ptr(scal), 1.0, ops.form_code(), st)
+                         nat.ptr(grad), 2, nat.ptr(scal), 1.0, ops.form_code(), nat.stream_of(dev))
             theta.copy_(theta0)
             fn()
             torch.cuda.synchronize()
