@@ -1329,7 +1329,9 @@ class LdsEngine:
 
     def sampled_nnz(self) -> int:
         """Stored entries (self-loops included) of the last window's outer
-        graph, sample 0 (host sync)."""
+        graph, sample 0 (host sync).  Bitmask mode after a prefetching hyper
+        step: the bits already hold the next window's graphs, so this counts
+        the next window's outer graph."""
         if self.bitmask_agg:  # no CSR: count the set bits (end_window clears the degrees)
             return int(_popcount(self.gbatch.bits[self.tau, 0]))
         return int(self.gbatch.row_ptr[self.tau, 0, self.n].item())
