@@ -531,8 +531,6 @@ struct DrawArgs {
     int graphs;
 };
 
-constexpr int kPreDraw = 2;  // graphs of a fused draw whose Philox words the 64-tile k-loop computes
-
 template <int KC, bool VEC, bool PRE = false, bool PART = true, bool DRAW = false>
 __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
@@ -642,31 +640,6 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
             }
         }
     };
-    // DRAW: the Philox words of the first kPreDraw graphs do not depend on θ,
-    // so they are computed inside the k-loop (one call per chunk, beside the
-    // staging and MFMAs, where the waves otherwise wait on LDS and barriers)
-    // and kept as their top 16 bits; the epilogue compares those against the
-    // top 16 bits of each threshold and recomputes a quad only on a tie
-    // (probability 2^-16 per draw).  Same draws, same bits.
-    uint32_t pre[kPreDraw][8];
-    const int rq0d = (i0 + wr * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0 (draw)
-    const uint32_t cbd = (DRAW && dr.counter_base != nullptr) ? *dr.counter_base : 0u;
-    auto pre_call = [&](int c) {  // call c: graph c >> 2, row quads m = c & 3 (c wave-uniform)
-        if constexpr (DRAW) {
-            if (c >= 4 * kPreDraw || (c >> 2) >= dr.graphs) return;
-            const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0d + 2 * (c & 3)), dr.tag,
-                                                dr.counter + cbd + (uint32_t)(c >> 2)},
-                                          dr.k0, dr.k1);
-            const uint32_t a = (o.y & 0xffff0000u) | (o.x >> 16), b = (o.w & 0xffff0000u) | (o.z >> 16);
-#pragma unroll
-            for (int cc = 0; cc < 4 * kPreDraw; ++cc) {
-                if (cc == c) {
-                    pre[cc >> 2][2 * (cc & 3)] = a;
-                    pre[cc >> 2][2 * (cc & 3) + 1] = b;
-                }
-            }
-        }
-    };
     if constexpr (PRE) {
         static_assert(!PRE || KC == 16, "pre-split staging: 16-wide k chunks");
         for (int c = 0; c < nch; ++c) {
@@ -683,11 +656,7 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
             __syncthreads();
             if (k0 + KC < k) bf3_load<KC, VEC>(u, v, ld, k, n, gi, gj, k0 + KC, st);
             compute(k0);
-            if constexpr (DRAW) pre_call(k0 / KC);
         }
-    }
-    if constexpr (DRAW) {  // short k: the calls the loop did not reach
-        for (int c = (k + KC - 1) / KC; c < 4 * kPreDraw; ++c) pre_call(c);
     }
     __syncthreads();
 
@@ -731,70 +700,39 @@ __global__ __launch_bounds__(256) void theta_grad_bf3_kernel(
         const bool diag = i0 == j0;
         const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
         const int rq0 = (i0 + wr * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
-        // graph q of a group: its 16 bits of this lane -> row words (ballots) and column words in LDS
-        auto emit = [&](int q, uint32_t bm) {  // bit e of bm: element e's draw
-            uint64_t colw = 0;
-            uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const bool bit = (bm >> e) & 1u;
-                const uint64_t w = __ballot(bit);
-                mylo = lane == e ? (uint32_t)w : mylo;
-                myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
-                colw |= (uint64_t)bit << ((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5) + wr * 32);
-            }
-            colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
-            if (lane < 16) {  // element e = lane: rows r (h = 0) and r + 4 (h = 1), columns wc·32 …
-                const int r = wr * 32 + (lane & 3) + 8 * (lane >> 2);
-                rw[q][r][wc] = mylo;
-                rw[q][r + 4][wc] = myhi;
-            }
-            if (lane < 32) cwp[q][wr][wc * 32 + lane] = colw;
-        };
 #pragma unroll 1
         for (int base = 0; base < dr.graphs; base += kGrp) {
             const int gn = min(kGrp, dr.graphs - base);
 #pragma unroll 1
             for (int q = 0; q < gn; ++q) {
                 const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
-                // the graphs drawn in the k-loop: their Philox words' top 16 bits decide
-                // unless they equal the threshold's (then the low 8 bits do: recompute)
-                const bool early = base + q < kPreDraw;
-                uint32_t bm = 0;
-                bool tie = false;
-                if (early) {
-                    uint32_t pq[8];
+                uint32_t x[16];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        uint32_t v = pre[0][i];
-#pragma unroll
-                        for (int g = 1; g < kPreDraw; ++g) v = (base + q == g) ? pre[g][i] : v;
-                        pq[i] = v;
-                    }
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const uint32_t h = (pq[e >> 1] >> (16 * (e & 1))) & 0xffffu;
-                        const uint32_t th = thr[e] >> 8;
-                        bm |= (uint32_t)(h < th) << e;
-                        tie |= h == th && (thr[e] & 255u) != 0u;
-                    }
+                for (int m = 0; m < 4; ++m) {
+                    const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * m), dr.tag, ctr}, dr.k0,
+                                                  dr.k1);
+                    x[4 * m] = o.x;
+                    x[4 * m + 1] = o.y;
+                    x[4 * m + 2] = o.z;
+                    x[4 * m + 3] = o.w;
                 }
-                if (!early || __ballot(tie) != 0) {  // wave-uniform: the full words
-                    uint32_t x[16];
+                uint64_t colw = 0;
+                uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * m), dr.tag, ctr},
-                                                      dr.k0, dr.k1);
-                        x[4 * m] = o.x;
-                        x[4 * m + 1] = o.y;
-                        x[4 * m + 2] = o.z;
-                        x[4 * m + 3] = o.w;
-                    }
-                    bm = 0;
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) bm |= (uint32_t)((x[e] >> 8) < thr[e]) << e;
+                for (int e = 0; e < 16; ++e) {
+                    const bool bit = (x[e] >> 8) < thr[e];
+                    const uint64_t w = __ballot(bit);
+                    mylo = lane == e ? (uint32_t)w : mylo;
+                    myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                    colw |= (uint64_t)bit << ((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5) + wr * 32);
                 }
-                emit(q, bm);
+                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+                if (lane < 16) {  // element e = lane: rows r (h = 0) and r + 4 (h = 1), columns wc·32 …
+                    const int r = wr * 32 + (lane & 3) + 8 * (lane >> 2);
+                    rw[q][r][wc] = mylo;
+                    rw[q][r + 4][wc] = myhi;
+                }
+                if (lane < 32) cwp[q][wr][wc * 32 + lane] = colw;
             }
             __syncthreads();
             const int q = t >> 6, tt = t & 63;
