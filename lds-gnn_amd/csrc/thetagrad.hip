@@ -1299,7 +1299,7 @@ constexpr int kW8Lds = 2 * 12 * kPL2 * 4;  // bytes of the two stage buffers (96
 constexpr int kW8Grp = 8;                  // graphs per draw group (4 KB of LDS each)
 
 template <bool SMALL, bool PART, bool DRAW>
-__global__ __launch_bounds__(512, 2) void theta_grad_w8_kernel(
+__global__ __launch_bounds__(512, 1) void theta_grad_w8_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
@@ -1483,23 +1483,28 @@ __global__ __launch_bounds__(512, 2) void theta_grad_w8_kernel(
             for (int q = 0; q < gn; ++q) {
                 const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
                 uint64_t colw = 0;
+                // both accumulators' eight Philox calls issued together: at two
+                // waves per SIMD the rounds' multiply latency needs the ILP
+                uint32_t x[2][16];
 #pragma unroll
                 for (int m = 0; m < 2; ++m) {
                     const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
-                    uint32_t x[16];
 #pragma unroll
                     for (int qd = 0; qd < 4; ++qd) {
                         const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr},
                                                       dr.k0, dr.k1);
-                        x[4 * qd] = o.x;
-                        x[4 * qd + 1] = o.y;
-                        x[4 * qd + 2] = o.z;
-                        x[4 * qd + 3] = o.w;
+                        x[m][4 * qd] = o.x;
+                        x[m][4 * qd + 1] = o.y;
+                        x[m][4 * qd + 2] = o.z;
+                        x[m][4 * qd + 3] = o.w;
                     }
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
                     uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
 #pragma unroll
                     for (int e = 0; e < 16; ++e) {
-                        const bool bit = (x[e] >> 8) < thr[m][e];
+                        const bool bit = (x[m][e] >> 8) < thr[m][e];
                         const uint64_t w = __ballot(bit);
                         mylo = lane == e ? (uint32_t)w : mylo;
                         myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
