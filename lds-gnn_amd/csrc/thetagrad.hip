@@ -1618,7 +1618,13 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
     // and the pipelined 128-tile (form 8) where its one block per CU still runs
     // every tile in one round and k is long (Cora S = 16: 494 vs 546 µs; at
     // Citeseer S = 16, 351 tiles, 847 vs 674; at n = 20 000, 2.29 vs 1.93 ms)
-    if (form == 1) form = (nt2 <= 256 && k >= 1024) ? 8 : (nt2 >= 1024 || k >= 1024) ? 5 : 6;
+    // round 3 (tools/microbench/tg_draw_ab.py, profiles/r03_theta_forms.jsonl):
+    // the eight-wave 128-tile (form 9) wherever its one block per CU runs every
+    // tile in one round (Cora S = 1: 41.8 µs against 47.4 pipelined, 49.0
+    // 64-tile; S = 16: 399 against 422), else the 128-tile form in XCD-grouped
+    // order (Citeseer S = 1: 59.9 against 63.6; S = 16: 577 against 728;
+    // n = 20 000: 1.77 against 1.93 ms)
+    if (form == 1) form = nt2 <= 256 ? 9 : 5;
     // the branch-free staging needs whole 8-wide k groups in 16-byte aligned rows
     const bool fast = vec4 && (k & 7) == 0;
     if (form == 9 && !pre && fast) {
@@ -1914,7 +1920,11 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
     // 114 at Citeseer, 2.61 vs 2.91 ms at n = 20 000.
     const int nb2 = (n + kT2 - 1) / kT2;
     const int nt2 = nb2 * (nb2 + 1) / 2;
-    if (form == 1) form = (nt2 >= 1024 || k >= 1024) ? 5 : 6;
+    // by shape, with the draw (same tool): the eight-wave form at Cora-sized
+    // grids (62.2 µs against 63.2 for the 64-tile), the 64-tile form in between
+    // (Citeseer: 82.8 against 97.4 for the 128-tile, 112 eight-wave), the
+    // 128-tile form at large n (2.49 against 2.63 ms at n = 20 000)
+    if (form == 1) form = nt2 <= 256 ? 9 : nt2 >= 1024 ? 5 : 6;
     if (form == 4 || form == 5 || form == 7 || form == 8) {
         const int per2 = (nt2 + 7) / 8;
         if (n <= 46340 && form != 7)

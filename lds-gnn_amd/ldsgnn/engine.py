@@ -313,6 +313,11 @@ class LdsEngine:
         # MI355X the replayed graph did not overlap the branches and the
         # chunks' read-modify-write of dθ cost 2.3x the single launch (r01).
         self.split_theta_grad = False
+        # window draw split (replica samples): graph 0 on the main stream, the
+        # window's other graphs on the side stream beside inner step 0 (a
+        # captured graph keeps the fork / join as edges)
+        self.async_draw = False
+        self._draw_pending = False
         # θ-grad assembly form of this engine's launches (ldsgnn.ops.THETA_GRAD_FORMS
         # name; None: the module default ops.theta_grad_form() at launch time)
         self.theta_form = None
@@ -793,13 +798,37 @@ class LdsEngine:
                      nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell),
                      nat.ptr(self.nflag), self._stream())
             self._prefetched = False
+        elif self.async_draw and count > 1 and not self.long_rows:
+            # graph 0 on the main stream; graphs 1 .. count-1 on the side stream,
+            # beside inner step 0 (joined before step 1: _join_draw)
+            self._draw_range(0, 1, self._stream())
+            side = self.side
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            self._draw_range(1, count - 1, side.cuda_stream)
+            self._draw_pending = True
         else:
-            nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), self.n, self.seed, self.tag_graph, 1,
-                     nat.ptr(self.scalars), self.pending_graph, count, self.S, nat.ptr(gb.bits), self.words,
-                     nat.ptr(gb.deg), nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s),
-                     nat.ptr(gb.ell), nat.ptr(self.nflag), 1 if self._ws_clean else 0, self._stream())
+            self._draw_range(0, count, self._stream())
         self._ws_clean = False
         self._block_ptrs(gb.graphs[:count])
+
+    def _draw_range(self, g0: int, count: int, stream: int):
+        """Graphs g0 .. g0 + count - 1 of the window (all samples), counters
+        pending + g0 + g, into the batch's graph slots g0 + g."""
+        gb, S, P = self.gbatch, self.S, nat.ptr
+
+        def at(t: torch.Tensor) -> int:  # graph g0 of a [count][S][...] batch array
+            return P(t) + g0 * t[0].numel() * t.element_size()
+        nat.call("lds_sample_graphs_multi", P(self.theta), self.n, self.seed, self.tag_graph, 1, P(self.scalars),
+                 self.pending_graph + g0, count, S, at(gb.bits), self.words, at(gb.deg), at(gb.row_ptr),
+                 at(gb.col) if not self.bitmask_agg else 0, max(self.cap, 1), at(gb.s), at(gb.ell),
+                 P(self.nflag), 1 if self._ws_clean else 0, stream)
+
+    def _join_draw(self):
+        """The window's later graphs (drawn on the side stream) are complete
+        before their first use."""
+        if self._draw_pending:
+            torch.cuda.current_stream(self.dev).wait_stream(self.side)
+            self._draw_pending = False
 
     def discard_prefetched_draws(self):
         """Forget graphs a hyper step drew for the next window (θ about to be
@@ -843,6 +872,8 @@ class LdsEngine:
             self.metrics = torch.zeros((self.tau + 1, self.S, 2), dtype=torch.float32, device=self.dev)
             self._refresh_adam_table()  # entries for the new step offsets
         sl = self.slots[t]
+        if t > 0:
+            self._join_draw()
         if self.theta_fn is not None:
             assert not presampled
             self._sample_per_draw(sl.g, t)
@@ -879,6 +910,7 @@ class LdsEngine:
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
         out = self.outer
+        self._join_draw()
         if self.theta_fn is not None:
             assert not presampled
             self._sample_per_draw(out.g, T)
@@ -1288,6 +1320,7 @@ class LdsEngine:
                 if self._deg_next is None:
                     self._deg_next = torch.zeros_like(self.gbatch.deg)
                 self._sample_batch(tau + 1)  # bits + degrees of this window's graphs
+                self._join_draw()
                 self._prefetched = True
         else:
             if self._prefetched or not self._ws_clean:
@@ -1297,6 +1330,7 @@ class LdsEngine:
 
     def replay(self, windows: int = 1):
         graphs, tau, reducer, prefetched = self._graph_capture
+        self._join_draw()  # an eager split draw still running on the side stream
         self._enter_window_state(prefetched, tau)
         if reducer is None:
             (_, one), (group, multi) = graphs[0], graphs[-1]

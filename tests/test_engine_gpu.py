@@ -626,3 +626,36 @@ def test_bitmask_engine_prefetched_draw_equals_eager(form):
     a.replay(1)
     torch.cuda.synchronize()
     assert torch.equal(a.theta, b.theta)
+
+
+@pytest.mark.parametrize("samples", [1, 3])
+def test_async_window_draw_equals_eager(samples):
+    """The split window draw (graph 0 on the main stream, graphs 1..τ on the
+    side stream beside inner step 0, joined before step 1): eager windows and
+    a captured, replayed window give bit-identical θ, weights and scalars to
+    the one-launch draw."""
+    from tests.parity_harness import run_engine_samples_and_oracle
+
+    def mk():
+        if samples == 1:
+            return run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+        return run_engine_samples_and_oracle(samples=samples, n=150, f_in=26, classes=5, steps=1, tau=5,
+                                             dropout=0.5, seed=7, replica0=2)["engine"]
+    a, b, c = mk(), mk(), mk()
+    a.async_draw = b.async_draw = True
+    for _ in range(2):
+        a.run_window(5)
+        c.run_window(5)
+    b.capture_window(5, windows=2)
+    b.replay(2)
+    for _ in range(2):
+        a.run_window(5)
+        c.run_window(5)
+    b.replay(2)  # capture runs nothing: b replays 4 windows in all, as a and c run
+    torch.cuda.synchronize()
+    for e in (a, b):
+        assert torch.equal(e.theta, c.theta)
+        for s_ in range(samples):
+            for k, v in e.get_params(s_).items():
+                assert torch.equal(v, c.get_params(s_)[k]), (s_, k)
+        assert e.scalars_host() == c.scalars_host()
