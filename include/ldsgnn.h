@@ -205,6 +205,15 @@ int lds_spmm_norm_blocked(const int* bptr, const int* col, const float* s, int n
  * lds_spmm_norm (src/models/layers.py:44, src/utils/graph.py:136-153).
  * ws: lds_bitmask_agg_ws_bytes(n) bytes of device memory. */
 int64_t lds_bitmask_agg_ws_bytes(int n);
+/* lds_aggregate_bitmask without its final pass: the lds_bitmask_agg_splits(n)
+ * partial sums Σ_{j in split p} Ã_ij s_j z_j (n × 16 each) are left at byte
+ * offset lds_bitmask_agg_part_offset(n) of ws, for a consumer that forms
+ * y_i = s_i · Σ_p part_p[i] in split order (LdsBatch.agg_splits): the same
+ * bits as lds_aggregate_bitmask's y with beta = 0. */
+int lds_bitmask_agg_splits(int n);
+int64_t lds_bitmask_agg_part_offset(int n);
+int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, const float* s, int n, const float* z,
+                                   int ldz, void* ws, void* stream);
 int lds_aggregate_bitmask(const uint64_t* bits, int words, const float* s, int n,
                           const float* z, int ldz, float* y, int ldy, int beta,
                           void* ws, void* stream);
@@ -404,7 +413,11 @@ typedef struct LdsBatch {
     const int32_t* heavy_rows;
     const uint8_t* heavy_flag;
     int32_t n_heavy;
-    int32_t reserved;
+    /* > 0: the precomputed aggregation `agg` an entry point is given holds
+     * agg_splits partial arrays (n × 16 each, consecutive): the kernel takes
+     * Â·Z[i] = s_i · Σ_p agg_p[i] (p in order) — lds_aggregate_bitmask_partials
+     * output, its final pass folded into the consumer.  0: agg is Â·Z. */
+    int32_t agg_splits;
 } LdsBatch;
 
 /* lds_sample_bitmask with the draw counter read from device memory:

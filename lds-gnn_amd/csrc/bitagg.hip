@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kThreads) void bitagg_main_kernel(const uint64_t* _
                                                           const int8_t* __restrict__ zq, int chunks, int splits,
                                                           float* __restrict__ part, const uint32_t* __restrict__ colmax,
                                                           const float* __restrict__ s, float* __restrict__ y, int ldy,
-                                                          int beta) {
+                                                          int beta, int partials_only) {
     __shared__ __attribute__((aligned(16))) int8_t bsh[2 * kChunkBytes];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kThreads) void bitagg_main_kernel(const uint64_t* _
                 const int64_t v = (int64_t)acc[t][0][i] + ((int64_t)acc[t][1][i] << 8) +
                                   ((int64_t)acc[t][2][i] << 16) + ((int64_t)acc[t][3][i] << 24);
                 const float pv = (float)ldexp((double)v, -e);
-                if (splits == 1) {  // one split: y = s_i · part here (bitagg_final_kernel's arithmetic)
+                if (splits == 1 && !partials_only) {  // one split: y = s_i · part here (bitagg_final_kernel's arithmetic)
                     float* o = y + (int64_t)row * ldy + f;
                     const float r = s[row] * pv;
                     *o = beta ? *o + r : r;
@@ -340,7 +340,7 @@ extern "C" int lds_aggregate_bitmask(const uint64_t* bits, int words, const floa
     hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st,
                        s, n, z, ldz, (const uint32_t*)w.colmax, w.zq, nc);
     hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(kThreads), 0, st, bits, words, n,
-                       (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax, s, y, ldy, beta);
+                       (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax, s, y, ldy, beta, 0);
     // several splits: their partials are summed by a separate launch.  A
     // last-block-per-row-group reduction in the main kernel (ticket counter,
     // device-scope fences around it) was measured at 151 vs 28.5 µs per call
@@ -349,5 +349,29 @@ extern "C" int lds_aggregate_bitmask(const uint64_t* bits, int words, const floa
     if (ks > 1)
         hipLaunchKernelGGL(bitagg_final_kernel, dim3((unsigned)(((int64_t)n * 4 + 255) / 256)), dim3(256), 0, st,
                        (const float*)w.part, ks, n, s, y, ldy, beta);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_bitmask_agg_splits(int n) { return n > 0 ? splits_of(n) : 0; }
+
+extern "C" int64_t lds_bitmask_agg_part_offset(int n) {
+    if (n <= 0) return 0;
+    return (int64_t)kMaxBlocks * kF * 4 + (int64_t)chunks_of(n) * kChunkBytes;
+}
+
+extern "C" int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, const float* s, int n, const float* z,
+                                              int ldz, void* ws, void* stream) {
+    LDS_CHECK_ARG(bits && s && z && ws && n > 0 && n <= (1 << 20));
+    LDS_CHECK_ARG(words >= (n + 63) / 64 && (words & 1) == 0 && ldz >= kF);
+    LDS_CHECK_ARG(((uintptr_t)ws & 15) == 0);
+    hipStream_t st = (hipStream_t)stream;
+    const Ws w = carve(ws, n);
+    const int nc = chunks_of(n), ks = splits_of(n);
+    hipLaunchKernelGGL(bitagg_colmax_kernel, dim3(kMaxBlocks), dim3(256), 0, st, s, n, z, ldz, w.colmax);
+    hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st,
+                       s, n, z, ldz, (const uint32_t*)w.colmax, w.zq, nc);
+    hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(kThreads), 0, st, bits, words, n,
+                       (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax, s, (float*)nullptr, 0, 0,
+                       1);
     LDS_RETURN_LAST_ERROR();
 }

@@ -58,6 +58,10 @@ __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1
         c = U32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
+        // the round keys advance in place: without this the compiler hoists
+        // all twenty into SGPRs, which the θ-grad draw epilogues then spill
+        // (84 → 66 spills in the eight-wave form, 19 → 2 in the 64-tile one)
+        asm volatile("" : "+s"(k0), "+s"(k1));
     }
     return c;
 }

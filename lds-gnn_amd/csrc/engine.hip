@@ -104,6 +104,7 @@ struct Batch {
     const int* heavy;       // row plan (include/ldsgnn.h LdsBatch)
     const uint8_t* hflag;
     int nh;
+    int asplit;             // > 0: `agg` holds asplit partial n × 16 arrays (LdsBatch.agg_splits)
 };
 
 // kB = false (single-sample launch): no offset code at all.
@@ -229,11 +230,25 @@ __device__ __forceinline__ RowSel select_row(int n, const int* __restrict__ rp, 
 template <int W, bool kAgg>
 __device__ __forceinline__ float agg_value(const RowSel& r, const int* __restrict__ col,
                                            const float* __restrict__ s, const int2* __restrict__ ell,
-                                           const float* __restrict__ z, const float* __restrict__ agg) {
+                                           const float* __restrict__ z, const float* __restrict__ agg,
+                                           const Batch& bt, int n) {
     const int t = threadIdx.x & 63;
     const int h = t & (HID - 1);
     if constexpr (kAgg) {
-        return r.row >= 0 ? agg[r.row * HID + h] : 0.f;
+        if (r.row < 0) return 0.f;
+        if (bt.asplit > 0) {  // the bitmask aggregation's split partials: s_i · Σ_p part_p (p in order)
+            float v[8];
+            const int m = min(bt.asplit, 8);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) v[p] = p < m ? agg[(int64_t)p * n * HID + r.row * HID + h] : 0.f;
+            float a = 0.f;
+#pragma unroll
+            for (int p = 0; p < 8; ++p)
+                if (p < m) a += v[p];
+            for (int p = 8; p < bt.asplit; ++p) a += agg[(int64_t)p * n * HID + r.row * HID + h];
+            return s[r.row] * a;
+        }
+        return agg[r.row * HID + h];
     } else {
         __shared__ float part[W][HID];
         float acc = 0.f;
@@ -554,7 +569,7 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
 #pragma unroll
         for (int k = 0; k < HID; ++k) w1v[k] = k < c ? w.w1[k * HID + lane] : 0.f;
     }
-    const float y = agg_value<4, kAgg>(rsel, col, s, ell, h0, agg);
+    const float y = agg_value<4, kAgg>(rsel, col, s, ell, h0, agg, bt, n);
     if (!rsel.lead) return;
     const int row = rsel.row;
     float hd = fmaxf(y, 0.f);
@@ -596,7 +611,7 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     lossrow = boff<kB>(lossrow, bt.row);
     corrrow = boff<kB>(corrrow, bt.row);
     const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
-    const float o = agg_value<4, kAgg>(rsel, col, s, ell, h2, agg);
+    const float o = agg_value<4, kAgg>(rsel, col, s, ell, h2, agg, bt, n);
     if (!rsel.lead) return;
     const int row = rsel.row;
     const bool act = lane < c;
@@ -654,7 +669,7 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     w.w1 = boff<kB>(w.w1, bt.par);
     bkeys<kB>(keys, bt);
     const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
-    const float g2 = agg_value<4, kAgg>(rsel, col, s, ell, d_o, agg);  // zero past c (dO is)
+    const float g2 = agg_value<4, kAgg>(rsel, col, s, ell, d_o, agg, bt, n);  // zero past c (dO is)
     if (!rsel.lead) return;
     const int row = rsel.row;
     if (g0) dh2[row * HID + lane] = g2;
@@ -931,7 +946,7 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
             gwv[k] = k < c ? gw1bar[k * HID + lane] : 0.f;
         }
     }
-    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh0bar, agg);  // dY0bar
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh0bar, agg, bt, n);  // dY0bar
     if (!rsel.lead) return;
     if (g0) emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_dh0bar, o_dy0, o_dh0, ag);
     const float a = ag * mask;  // dH1dbar
@@ -974,7 +989,7 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     V = boff<kB>(V, bt.uv);
     R = boff<kB>(R, bt.row);
     const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
-    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh2bar, agg);  // dObar
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh2bar, agg, bt, n);  // dObar
     if (!rsel.lead) return;
     const int row = rsel.row;
     const int ix = row * HID + lane;
@@ -1018,7 +1033,7 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     R = boff<kB>(R, bt.row);
     bkeys<kB>(keys, bt);
     const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
-    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, obar, agg);  // H2bar (zero past c)
+    const float ag = agg_value<4, kAgg>(rsel, col, s, ell, obar, agg, bt, n);  // H2bar (zero past c)
     if (!rsel.lead) return;
     const int row = rsel.row;
     const int ix = row * HID + lane;
@@ -1661,7 +1676,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
             o_y0 = y0[ix];
         }
     }
-    float g = agg_value<16, kAgg>(rsel, col, s, ell, dy0, agg);
+    float g = agg_value<16, kAgg>(rsel, col, s, ell, dy0, agg, bt, n);
     if (valid && g0) dh0[ix] = g;
     if (U != nullptr && valid && g0)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
         emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_dy0, o_h0, o_y0, g);
@@ -1715,7 +1730,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
         o_h0 = h0[ix];
         o_y0 = y0[ix];
     }
-    const float ag = agg_value<16, kAgg>(rsel, col, s, ell, y0bar, agg);
+    const float ag = agg_value<16, kAgg>(rsel, col, s, ell, y0bar, agg, bt, n);
     if (valid && g0) {
         emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_y0bar, o_h0, o_y0, ag);
         h0bar[ix] = ag;
@@ -2091,8 +2106,9 @@ static inline int wave_blocks(int n) { return (n + 3) / 4; }
 
 // Kernel-side strides of a host LdsBatch (NULL: one sample); returns grid.y.
 static inline int mk_batch(const LdsBatch* b, Batch& bt) {
-    bt = Batch{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0u, nullptr, nullptr, 0};
+    bt = Batch{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0u, nullptr, nullptr, 0, 0};
     if (b == nullptr) return 1;
+    bt.asplit = b->agg_splits > 0 ? b->agg_splits : 0;
     bt.heavy = b->heavy_rows;  // the row plan applies to single-sample launches too
     bt.hflag = b->heavy_flag;
     bt.nh = b->n_heavy > 0 && b->heavy_rows && b->heavy_flag ? b->n_heavy : 0;

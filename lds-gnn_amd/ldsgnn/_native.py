@@ -21,7 +21,7 @@ c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
 P = c_void_p  # device pointers travel as integers
 
 # name -> argtypes (restype is always int = hipError_t, except where noted)
-_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes"}  # byte counts
+_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset"}  # byte counts
 SIGNATURES = {
     "lds_abi_version": [],
     "lds_graph_node_census": [P, P, c_int],
@@ -53,6 +53,9 @@ SIGNATURES = {
     "lds_spmm_norm_blocked": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P],
     "lds_bitmask_agg_ws_bytes": [c_int],
     "lds_aggregate_bitmask": [P, c_int, P, c_int, P, c_int, P, c_int, c_int, P, P],
+    "lds_bitmask_agg_splits": [c_int],
+    "lds_bitmask_agg_part_offset": [c_int],
+    "lds_aggregate_bitmask_partials": [P, c_int, P, c_int, P, c_int, P, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_int, P],
@@ -231,7 +234,7 @@ class LdsBatch(ctypes.Structure):
     _fields_ = [("samples", ctypes.c_int32), ("tag_step", ctypes.c_uint32)] + [
         (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")] + [
         ("heavy_rows", ctypes.c_void_p), ("heavy_flag", ctypes.c_void_p), ("n_heavy", ctypes.c_int32),
-        ("reserved", ctypes.c_int32)]
+        ("agg_splits", ctypes.c_int32)]
 
 
 def batch_ptr(b) -> int:

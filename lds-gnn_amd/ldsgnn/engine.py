@@ -237,6 +237,7 @@ class LdsEngine:
         if long_rows_kernel not in ("bitmask", "blocked"):
             raise ValueError("long_rows_kernel: 'bitmask' or 'blocked'")
         self.bitmask_agg = self.long_rows and long_rows_kernel == "bitmask"
+        self.agg_splits = 0  # bitmask aggregation: its partial arrays, summed by the consumers
         # graph buffers: CSR column capacity n² per graph (int32 positions);
         # none when the bitmask aggregation reads the sampled bits directly
         if not self.bitmask_agg and n * n >= (1 << 31):
@@ -269,6 +270,8 @@ class LdsEngine:
             self.agg = torch.zeros((S, n, HID), dtype=torch.float32, device=dev)
             if self.bitmask_agg:
                 self.agg_ws = torch.empty(int(nat.lib.lds_bitmask_agg_ws_bytes(n)), dtype=torch.uint8, device=dev)
+                self.agg_part_off = int(nat.lib.lds_bitmask_agg_part_offset(n))
+                self.agg_splits = int(nat.lib.lds_bitmask_agg_splits(n))
             else:
                 nb = nat.lib.lds_spmm_block_count(n)
                 self.spmm_part = torch.zeros((nb, n, HID), dtype=torch.float32, device=dev)
@@ -410,7 +413,8 @@ class LdsEngine:
             return nat.LdsBatch(samples=S, tag_step=1, act=n * HID, row=n, rp=n + 1, col=self.cap,
                                 ell=n * 2 * ELL, par=self.np, xval=xval_stride, xd=self.x_nnz, uv=self.ldk,
                                 part=self.nred * _RED_LEN, met=2, heavy_rows=nat.ptr(self.heavy_rows),
-                                heavy_flag=nat.ptr(self.heavy_flag), n_heavy=self.n_heavy)
+                                heavy_flag=nat.ptr(self.heavy_flag), n_heavy=self.n_heavy,
+                                agg_splits=self.agg_splits)
         self._bt = mk(0)  # X values argument = the shared X
         self._btx = mk(self.x_nnz if self.train_flag else 0)  # X values argument = the slot's stored Xd
         self._bt2 = mk(0)  # the two-hop kernels: their own row plan
@@ -632,10 +636,10 @@ class LdsEngine:
         (aggregate in-kernel)."""
         if not self.long_rows:
             return 0
-        if self.bitmask_agg:
-            nat.call("lds_aggregate_bitmask", nat.ptr(g.bits), self.words, nat.ptr(g.s), self.n, nat.ptr(z), HID,
-                     nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), self._stream())
-            return nat.ptr(self.agg)
+        if self.bitmask_agg:  # the split partials; the consuming kernel sums them (LdsBatch.agg_splits)
+            nat.call("lds_aggregate_bitmask_partials", nat.ptr(g.bits), self.words, nat.ptr(g.s), self.n,
+                     nat.ptr(z), HID, nat.ptr(self.agg_ws), self._stream())
+            return nat.ptr(self.agg_ws) + self.agg_part_off
         nat.call("lds_spmm_norm_blocked", nat.ptr(g.bptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z), HID,
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
         return nat.ptr(self.agg)

@@ -293,6 +293,34 @@ def test_bitmask_agg_repeatable_on_dirty_workspace(device, n):
     assert float((outs[0].double() - ref).abs().max() / ref.abs().max()) < RTOL
 
 
+@pytest.mark.parametrize("n", [65, 1500, 3000])
+def test_bitmask_agg_partials_fold_bit_exact(device, n):
+    """lds_aggregate_bitmask_partials leaves the split partial sums; a consumer
+    forming s_i · Σ_p part_p[i] in split order (what the engine kernels do with
+    LdsBatch.agg_splits) reproduces lds_aggregate_bitmask's y bit for bit."""
+    g = torch.Generator().manual_seed(n + 7)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n), track_grad=False)
+    z = torch.randn(n, 16, generator=g).to(device)
+    st = nat.stream_of(z.device)
+    ws = torch.empty(int(nat.lib.lds_bitmask_agg_ws_bytes(n)), dtype=torch.uint8, device=device)
+    y = torch.empty(n, 16, device=device)
+    nat.call("lds_aggregate_bitmask", nat.ptr(graph.bits), graph.bits.size(1), nat.ptr(graph.s), n, nat.ptr(z), 16,
+             nat.ptr(y), 16, 0, nat.ptr(ws), st)
+    ws2 = torch.full_like(ws, 0x55)
+    nat.call("lds_aggregate_bitmask_partials", nat.ptr(graph.bits), graph.bits.size(1), nat.ptr(graph.s), n,
+             nat.ptr(z), 16, nat.ptr(ws2), st)
+    ks = int(nat.lib.lds_bitmask_agg_splits(n))
+    off = int(nat.lib.lds_bitmask_agg_part_offset(n))
+    part = ws2[off:off + ks * n * 16 * 4].view(torch.float32).view(ks, n, 16)
+    acc = torch.zeros(n, 16, device=device)
+    for p in range(ks):  # in split order, as the consumers add them
+        acc = acc + part[p]
+    got = graph.s.view(n, 1) * acc
+    torch.cuda.synchronize()
+    assert torch.equal(got, y)
+
+
 def test_pretrain_step_vs_oracle(device):
     """Fused pre-training epoch (weighted BCE + clamp/symmetrisation backward +
     Adam on packed θ, one launch) against the reference's dense restatement
