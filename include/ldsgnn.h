@@ -442,6 +442,19 @@ int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int 
                         float keep, float scale, float* xd_csr, float* xd_csc,
                         const int* csr2csc, const int* xhead, const int* xinfo, int head_vals,
                         const LdsBatch* batch, void* stream);
+/* lds_sample_fill_csr (CSR, s, ELL head of `graphs` drawn graphs) and
+ * lds_engine_x_linear (one replica sample) in ONE launch: the first inner
+ * step's X product does not read the window's graphs, so a window that starts
+ * from prefetched draws runs both halves side by side (blocks split by role)
+ * with one dependent boundary instead of two.  Arguments as the two calls. */
+int lds_engine_fill_x_linear(const uint64_t* bits, int words, const int* deg_ws, int graphs,
+                             int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
+                             const uint8_t* node_flags, const int* xrp, const int* xcol,
+                             const float* xval, int n, const float* wt, const float* bias, float* out,
+                             uint64_t seed, uint32_t tag_x, const void* scalars, int fwd_off, int train,
+                             float keep, float scale, float* xd_csr, float* xd_csc, const int* csr2csc,
+                             const int* xhead, const int* xinfo, int head_vals, const LdsBatch* batch,
+                             void* stream);
 /* out[f][:] (+)= Σ_i dropout(X)[i][f] · d[i][:]  (+ wd · w)   (X in CSC). */
 int lds_engine_xt_linear(const int* xcp, const int* xrow, const float* xval, int fin,
                          const float* d, float* out, const float* w, float wd,

@@ -16,6 +16,7 @@
 // memory (EngineScalars) so a whole τ-window is capturable as one HIP graph and
 // replays advance them.
 #include "common.hpp"
+#include "fill.hpp"
 #include "../../include/ldsgnn.h"
 
 namespace lds {
@@ -459,13 +460,13 @@ __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const i
 // out[i][h] = bias[h] + Σ_f Xd[i][f] · Wt[f][h]      (H0 = Xd W0ᵀ + b0)
 // Xd = dropout(X) with key (tag_x, fwd counter) when `train`, else X.
 template <bool kB>
-__global__ __launch_bounds__(256) void x_linear_kernel(
+__device__ __forceinline__ void x_linear_rows(int bx,
     const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc,
     const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
-    const int row = blockIdx.x * 4 + wave_id();
+    const int row = bx * 4 + wave_id();
     if (row >= n) return;
     xval = boff<kB>(xval, bt.xval);
     wt = boff<kB>(wt, bt.par);
@@ -490,6 +491,40 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
         acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
     }
     if (lane < HID) out[row * HID + lane] = bl + acc;
+}
+
+template <bool kB>
+__global__ __launch_bounds__(256) void x_linear_kernel(
+    const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
+    const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
+    const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
+    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc,
+    const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
+    x_linear_rows<kB>(blockIdx.x, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep, scale, xd_csr,
+                      xd_csc, csr2csc, xhead, xinfo, head_vals, bt);
+}
+
+// A window's first launch with prefetched draws: the CSR / s / ELL fill of its
+// graphs (fill.hpp; blocks [0, fill_blocks)) and the first inner step's
+// dropout(X)·W0ᵀ (the rest), which does not read the graphs — one launch and
+// one dependent boundary instead of two.
+__global__ __launch_bounds__(256) void fill_x_linear_kernel(
+    const uint64_t* __restrict__ bits, int words, const int* __restrict__ dacc, int wsi, int graphs,
+    int* __restrict__ row_ptr, int* __restrict__ gcol, int64_t capacity, float* __restrict__ gs,
+    int2* __restrict__ ell, const uint8_t* __restrict__ flags,
+    const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
+    const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
+    const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
+    float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc,
+    const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
+    const int fb = (n + 15) / 16;
+    const int b = blockIdx.x;
+    if (b < fb * graphs) {
+        fill_csr_block(b % fb, b / fb, bits, n, words, dacc, wsi, row_ptr, gcol, capacity, gs, ell, flags);
+        return;
+    }
+    x_linear_rows<false>(b - fb * graphs, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep, scale,
+                         xd_csr, xd_csc, csr2csc, xhead, xinfo, head_vals, bt);
 }
 
 // out[f][h] (= or +=) Σ_i Xd[i][f] · D[i][h]  (+ wd · w[f][h])   via CSC of X.
@@ -2161,6 +2196,32 @@ extern "C" int lds_engine_x_linear(const int* xrp, const int* xcol, const float*
                        xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, xhead,
                        (const int2*)xinfo, head_vals, bt);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_engine_fill_x_linear(const uint64_t* bits, int words, const int* deg_ws, int graphs,
+                                        int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
+                                        const uint8_t* node_flags, const int* xrp, const int* xcol,
+                                        const float* xval, int n, const float* wt, const float* bias, float* out,
+                                        uint64_t seed, uint32_t tag_x, const void* scalars, int fwd_off, int train,
+                                        float keep, float scale, float* xd_csr, float* xd_csc, const int* csr2csc,
+                                        const int* xhead, const int* xinfo, int head_vals, const LdsBatch* batch,
+                                        void* stream) {
+    LDS_CHECK_ARG(bits && deg_ws && row_ptr && col && s && n > 0 && n <= kEllIndex + 1 && col_stride > 0);
+    LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64);
+    LDS_CHECK_ARG(xrp && xcol && xval && wt && out && scalars && batch_ok(batch));
+    LDS_CHECK_ARG(xd_csc == nullptr || (xd_csr && csr2csc));
+    LDS_CHECK_ARG(xhead == nullptr || xinfo != nullptr);
+    Batch bt;
+    const int ns = mk_batch(batch, bt);
+    LDS_CHECK_ARG(ns == 1);  // one replica sample (the prefetched-draw path)
+    const int64_t blocks = (int64_t)((n + 15) / 16) * graphs + (n + 3) / 4;
+    LDS_CHECK_ARG(blocks < (1ll << 31));
+    hipLaunchKernelGGL(fill_x_linear_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, bits, words,
+                       deg_ws, lds_sample_ws_ints(n), graphs, row_ptr, col, col_stride, s, (int2*)ell, node_flags,
+                       xrp, xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars,
+                       fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, xhead, (const int2*)xinfo, head_vals,
+                       bt);
     LDS_RETURN_LAST_ERROR();
 }
 

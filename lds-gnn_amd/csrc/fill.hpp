@@ -1,0 +1,177 @@
+// The CSR / s / ELL fill of drawn graphs (one 256-thread block per 16 rows of
+// one graph), shared by the sampler's fill launch (sampler.hip) and the
+// engine's window-start launch that runs the fill beside the first X product
+// (engine.hip, lds_engine_fill_x_linear).
+#pragma once
+
+#include "common.hpp"
+
+namespace lds {
+
+// ELL j field: index | node flags (common.hpp kEllIndex); no flags: the index.
+__device__ __forceinline__ int ell_index(int j, const uint8_t* __restrict__ flags) {
+    return flags != nullptr ? (j | ((int)flags[j] << kEllFlagShift)) : j;
+}
+
+// Rows with at least this many entries use the word-at-a-time compaction.
+constexpr int kDenseRowFill = 1024;
+
+// One row of the fused fill with a whole wave (rows of kDenseRowFill or more
+// entries, or a wave that holds one): ascending columns into col from
+// position pre, the first 64 into head.
+__device__ __forceinline__ void fill_row_wave(const uint64_t* __restrict__ rb_bits, int nbw, int64_t pre, int deg,
+                                              int* __restrict__ col, int64_t capacity, int* __restrict__ head) {
+    const int lane = wave_lane();
+    int64_t base = pre;
+    if (deg < kDenseRowFill) {  // each lane pops its own word's bits
+        for (int w0 = 0; w0 < nbw; w0 += 64) {
+            const int w = w0 + lane;
+            uint64_t word = w < nbw ? rb_bits[w] : 0ull;
+            const int cnt = __popcll(word);
+            const int incl = wave_incl_scan_int(cnt);
+            int64_t pos = base + (incl - cnt);
+            while (word) {
+                const int bit = __ffsll((unsigned long long)word) - 1;
+                const int j = w * 64 + bit;
+                if (pos < capacity) col[pos] = j;
+                if (pos - pre < kEllWidth) head[pos - pre] = j;
+                ++pos;
+                word &= word - 1;
+            }
+            base += __builtin_amdgcn_readlane(incl, 63);
+        }
+        return;
+    }
+    // dense rows: for every non-zero word (uniform loop over a ballot) lane l
+    // tests bit l; the word's entries go out as one contiguous store
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int w0 = 0; w0 < nbw; w0 += 64) {
+        const int w = w0 + lane;
+        const uint64_t word = w < nbw ? rb_bits[w] : 0ull;
+        uint64_t nz = __ballot(word != 0ull);
+        while (nz) {
+            const int src = __ffsll((unsigned long long)nz) - 1;
+            nz &= nz - 1;
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)word, src);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(word >> 32), src);
+            const uint64_t wd = ((uint64_t)hi << 32) | lo;
+            const bool set = (wd >> lane) & 1ull;
+            const int64_t pos = base + __popcll(wd & below);
+            if (set) {
+                const int j = (w0 + src) * 64 + lane;
+                if (pos < capacity) col[pos] = j;
+                if (pos - pre < kEllWidth) head[pos - pre] = j;
+            }
+            base += __popcll(wd);
+        }
+    }
+}
+
+// The CSR fill of the fused sampler: the tile kernel's degree counts give
+// each row its CSR offset directly — the block's 256 threads sum the degrees
+// of all rows before its first row (one coalesced pass, a block reduction),
+// the block's own 16 degrees are scanned in one 16-lane row — so no scan
+// launch runs between the draw and the fill.  A 16-lane group per row: lane
+// h pops the bits of words h, h+16, ... (positions from a 16-lane scan of
+// their counts), keeping the first 64 columns in LDS; the ELL head is
+// written last, four entries per lane, whose s_j = deg_j^-1/2
+// (inv_sqrt_degree) and flag byte are parallel loads.  A wave holding a row
+// of kDenseRowFill or more entries fills its four rows one at a time with the
+// whole wave instead.  (One wave per row: 11.2 µs per Cora window of 6
+// graphs; four rows per wave: see DESIGN.)
+__device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* __restrict__ bits, int n, int words,
+                                               const int* __restrict__ dacc, int wsi, int* __restrict__ row_ptr,
+                                               int* __restrict__ col, int64_t capacity, float* __restrict__ s,
+                                               int2* __restrict__ ell, const uint8_t* __restrict__ flags) {
+    __shared__ int red[4];
+    __shared__ int dblk[16];  // exclusive scan of the block's 16 row degrees
+    __shared__ int head[16][kEllWidth];
+    const int wave = wave_id();
+    const int lane = wave_lane();
+    const int h = lane & 15, k = wave * 4 + (lane >> 4);  // row k of the block (this lane's group)
+    const int row0 = bx * 16;
+    const int row = row0 + k;
+    const int g = by;
+    bits += (int64_t)g * n * words;
+    dacc += (int64_t)g * wsi;
+    row_ptr += (int64_t)g * (n + 1);
+    col += (int64_t)g * capacity;
+    s += (int64_t)g * n;
+    const int nbw = (n + 63) / 64;
+    const bool live = row < n;
+    const uint64_t* rb_bits = bits + (int64_t)row * words;
+    // the row's own operands first (independent of the block prefix)
+    const int deg = live ? dacc[row] : 0;
+    const uint64_t word0 = (live && h < nbw) ? rb_bits[h] : 0ull;
+    if (wave == 0 && lane < 16) {
+        const int d = row0 + lane < n ? dacc[row0 + lane] : 0;
+        dblk[lane] = row16_incl_scan_int(d) - d;
+    }
+    // degrees of the rows before the block: 8 independent loads per thread per round
+    int acc = 0;
+    for (int r0b = 0; r0b < row0; r0b += 8 * 256) {
+        int v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int r = r0b + q * 256 + (int)threadIdx.x;
+            v[q] = r < row0 ? dacc[r] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q];
+    }
+    acc = wave_sum_int(acc);
+    if (lane == 0) red[wave] = acc;
+    __syncthreads();
+    const int bpre = red[0] + red[1] + red[2] + red[3];
+    const int pre = bpre + dblk[k];
+    if (live && h == 0) {  // (clamped: a workspace that was not zero on entry cannot send readers past col)
+        row_ptr[row] = (int)min((int64_t)pre, capacity);
+        if (row == n - 1) row_ptr[n] = (int)min((int64_t)pre + deg, capacity);
+        s[row] = inv_sqrt_degree(deg);
+    }
+    if (__ballot(live && deg >= kDenseRowFill) == 0) {
+        int64_t base = pre;
+        for (int w0 = 0; w0 < nbw; w0 += 16) {  // uniform: every group walks the same word count
+            const int w = w0 + h;
+            uint64_t word = w0 == 0 ? word0 : ((live && w < nbw) ? rb_bits[w] : 0ull);
+            const int cnt = __popcll(word);
+            const int incl = row16_incl_scan_int(cnt);
+            int64_t pos = base + (incl - cnt);
+            while (word) {
+                const int bit = __ffsll((unsigned long long)word) - 1;
+                const int j = w * 64 + bit;
+                if (pos < capacity) col[pos] = j;
+                if (pos - pre < kEllWidth) head[k][pos - pre] = j;
+                ++pos;
+                word &= word - 1;
+            }
+            base += row16_last_int(incl);
+        }
+    } else {
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {  // the wave's four rows, one at a time
+            const int kq = wave * 4 + q, rq = row0 + kq;
+            if (rq >= n) break;
+            fill_row_wave(bits + (int64_t)rq * words, nbw, (int64_t)bpre + dblk[kq], dacc[rq], col, capacity,
+                          head[kq]);
+        }
+    }
+    if (ell == nullptr || !live) return;
+    // the head columns of this wave's rows are in LDS (written by this wave only)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int2* __restrict__ er = ell + ((int64_t)g * n + row) * kEllWidth;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int e = h + 16 * m;
+        int2 v = make_int2(row, 0);  // padding: a valid index with weight 0
+        if (e < deg) {
+            const int j = head[k][e];
+            v = make_int2(ell_index(j, flags), __float_as_int(inv_sqrt_degree(dacc[j])));
+        }
+        er[e] = v;
+    }
+}
+
+}  // namespace lds

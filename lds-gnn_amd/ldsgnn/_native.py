@@ -74,6 +74,9 @@ SIGNATURES = {
     "lds_sample_bitmask_dev": [P, c_int, c_uint64, c_uint32, P, c_uint32, P, c_int, P],
     "lds_engine_x_linear": [P, P, P, c_int, P, P, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
                             P, P, P, P, P, c_int, P, P],
+    "lds_engine_fill_x_linear": [P, c_int, P, c_int, P, P, c_int64, P, P, P,
+                                 P, P, P, c_int, P, P, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
+                                 P, P, P, P, P, c_int, P, P],
     "lds_engine_xt_linear": [P, P, P, c_int, P, P, P, c_float, c_int, c_uint64, c_uint32, P, c_int, c_int,
                              c_float, c_float, P],
     "lds_engine_fwd_layer1": [P, P, P, P, c_int, P, P, P, P, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int,

@@ -321,6 +321,10 @@ class LdsEngine:
         # captured graph keeps the fork / join as edges)
         self.async_draw = False
         self._draw_pending = False
+        # prefetched window fill launched together with the first X product
+        # (lds_engine_fill_x_linear); the fill is deferred until that launch
+        self.fuse_fill = True
+        self._pending_fill = None
         # θ-grad assembly form of this engine's launches (ldsgnn.ops.THETA_GRAD_FORMS
         # name; None: the module default ops.theta_grad_form() at launch time)
         self.theta_form = None
@@ -485,6 +489,7 @@ class LdsEngine:
         the reference's samples take RNG draws), eval-mode forward with the
         flat parameters, NLL / accuracy on the validation and test masks,
         averaged over samples; one host sync.  Single-sample engines."""
+        self._flush_fill()
         self._drop_prefetch()
         if self.S != 1:
             raise NotImplementedError("empirical_mean runs on single-sample engines")
@@ -656,9 +661,15 @@ class LdsEngine:
         # on the tape: the step's later products read them instead of redrawing
         keep_xd = train and sl.xd_csr is not None
         xd = (nat.ptr(sl.xd_csr), nat.ptr(sl.xd_csc), nat.ptr(self.csr2csc)) if keep_xd else (0, 0, 0)
-        nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n,
-                 nat.ptr(w0t), nat.ptr(b0), nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars),
-                 fwd_off, train, self.keep, self.scale, *xd, nat.ptr(self.xhead), nat.ptr(self.xinfo), 1, bt, st)
+        xargs = (nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(self.xval), n, nat.ptr(w0t), nat.ptr(b0),
+                 nat.ptr(sl.h0), self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off, train, self.keep,
+                 self.scale, *xd, nat.ptr(self.xhead), nat.ptr(self.xinfo), 1, bt, st)
+        if self._pending_fill is not None and bt == self.bt:  # the window's fill rides in this launch
+            nat.call("lds_engine_fill_x_linear", *self._pending_fill, *xargs)
+            self._pending_fill = None
+        else:
+            self._flush_fill()
+            nat.call("lds_engine_x_linear", *xargs)
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
                  self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask),
@@ -796,11 +807,16 @@ class LdsEngine:
         """Draw the window's `count` graphs in one batched launch set; graph g
         takes draw counter (pending + g), exactly the counter the step-by-step
         path would give it."""
+        self._flush_fill()
         gb = self.gbatch
         if self._prefetched:  # bits + degrees drawn by the last hyper step (lds_theta_grad_sgd_draw)
-            nat.call("lds_sample_fill_csr", nat.ptr(gb.bits), self.n, self.words, nat.ptr(gb.deg), count * self.S,
-                     nat.ptr(gb.row_ptr), self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell),
-                     nat.ptr(self.nflag), self._stream())
+            fill = (nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), count * self.S, nat.ptr(gb.row_ptr),
+                    self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell), nat.ptr(self.nflag))
+            if self.fuse_fill and self.S == 1 and not self.long_rows:
+                # deferred: the first inner step's X product launches it (lds_engine_fill_x_linear)
+                self._pending_fill = fill
+            else:
+                nat.call("lds_sample_fill_csr", fill[0], self.n, *fill[1:], self._stream())
             self._prefetched = False
         elif self.async_draw and count > 1 and not self.long_rows:
             # graph 0 on the main stream; graphs 1 .. count-1 on the side stream,
@@ -814,6 +830,13 @@ class LdsEngine:
             self._draw_range(0, count, self._stream())
         self._ws_clean = False
         self._block_ptrs(gb.graphs[:count])
+
+    def _flush_fill(self):
+        """A deferred window fill runs now (something else needs the graphs
+        before the first X product)."""
+        if self._pending_fill is not None:
+            f, self._pending_fill = self._pending_fill, None
+            nat.call("lds_sample_fill_csr", f[0], self.n, *f[1:], self._stream())
 
     def _draw_range(self, g0: int, count: int, stream: int):
         """Graphs g0 .. g0 + count - 1 of the window (all samples), counters
@@ -877,6 +900,7 @@ class LdsEngine:
             self._refresh_adam_table()  # entries for the new step offsets
         sl = self.slots[t]
         if t > 0:
+            self._flush_fill()
             self._join_draw()
         if self.theta_fn is not None:
             assert not presampled
@@ -914,6 +938,7 @@ class LdsEngine:
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
         out = self.outer
+        self._flush_fill()
         self._join_draw()
         if self.theta_fn is not None:
             assert not presampled
@@ -1334,6 +1359,7 @@ class LdsEngine:
 
     def replay(self, windows: int = 1):
         graphs, tau, reducer, prefetched = self._graph_capture
+        self._flush_fill()
         self._join_draw()  # an eager split draw still running on the side stream
         self._enter_window_state(prefetched, tau)
         if reducer is None:
