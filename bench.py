@@ -163,6 +163,14 @@ def algo_cost(name, eng, n_calls_per_window):
         return "hbm", g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)
     if name == "lds_engine_x_linear":
         return "hbm", S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act
+    if name == "lds_engine_fill_x_linear":  # the window fill and the first X product in one launch
+        g = eng.tau + 1
+        words = nat.lib.lds_bitmask_words(n)
+        return "hbm", (g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)
+                       + S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act)
+    if name == "lds_aggregate_bitmask_partials":
+        chunks = (n + 511) // 512
+        return "mfma_i8", 2.0 * n * chunks * 512 * 16 * 4
     if name == "lds_engine_xt_adam":
         return "hbm", S * (4 * (eng.fin + 1) + 8 * xnnz) + act + S * 28 * P + 4 * eng.nred * 304 * S
     if name in ("lds_engine_fwd_layer1", "lds_engine_rev_a", "lds_engine_rev_c"):

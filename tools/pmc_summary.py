@@ -27,9 +27,14 @@ ENTRY_KERNELS = {
     "lds_sample_fill_csr": ["lds::fill_csr_fused_kernel"],
     # θ-grad + SGD; with the next window's draw fused in: the DRAW = true instance
     "lds_theta_grad_sgd": ["theta_grad_bf3_kernel<16, true, false, true, false>", "theta_grad_bf3_t128",
-                           "theta_grad_bf3_pipe", "theta_grad_mfma"],
-    "lds_theta_grad_sgd_draw": ["theta_grad_bf3_kernel<16, true, false, true, true>"],
-    "lds_engine_x_linear": ["x_linear_kernel"],
+                           "theta_grad_bf3_pipe", "theta_grad_mfma", "theta_grad_w8_kernel<true, false, false>",
+                           "theta_grad_w8_kernel<false, false, false>"],
+    "lds_theta_grad_sgd_draw": ["theta_grad_bf3_kernel<16, true, false, true, true>",
+                                "theta_grad_w8_kernel<true, false, true>", "theta_grad_w8_kernel<false, false, true>",
+                                "theta_grad_bf3_t128_kernel<true, true, false, true>",
+                                "theta_grad_bf3_t128_kernel<true, false, false, true>"],
+    "lds_engine_x_linear": ["lds::x_linear_kernel"],
+    "lds_engine_fill_x_linear": ["fill_x_linear_kernel"],
     "lds_engine_fwd_layer1": ["fwd_layer1_kernel"],
     "lds_engine_fwd_layer2": ["fwd_layer2_kernel"],
     "lds_engine_bwd_layer2": ["bwd_layer2_kernel"],
