@@ -15,6 +15,7 @@
 #   c5cpu      the config-5 line with its CPU baseline       c5_cpu_TAG.json
 #   samples    Cora S = 8 / 16, Citeseer S = 16 lines        s_<ds>_<S>_TAG.json
 #   scpu       the Citeseer S = 16 line with its CPU baseline s_cpu_TAG.json
+#   accuracy   LDS τ = 5 fused engine, 10 seeds, Cora + Citeseer acc_<ds>_tau5_TAG.jsonl
 #   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
 set -o pipefail
 tag=${1:?usage: tools/gpu.sh TAG STEP...}
@@ -65,6 +66,11 @@ for step in "$@"; do
     scpu)
         run 400 python bench.py --dataset citeseer --samples 16 --steps 100 --warmup 10 \
             > $O/s_cpu_$tag.json 2> $O/s_cpu_$tag.err || exit $? ;;
+    accuracy)
+        for ds in cora citeseer; do
+            run 600 python -u tools/accuracy_run.py --dataset $ds --seeds 10 --tau 5 --fused \
+                > $O/acc_${ds}_tau5_$tag.jsonl 2> $O/acc_${ds}_tau5_$tag.err || exit $?
+        done ;;
     multirank)
         run 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29517 bench.py --gpus 2 --backend gloo --steps 50 --warmup 10 --no-cpu-baseline \
