@@ -299,6 +299,28 @@ int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k,
 /* The chunk-major split words of the first k columns of x (rows × ld fp32)
  * into planes (ceil(k/16) chunks of rows × 48 uint16). */
 int lds_split_planes(const float* x, int rows, int ld, int k, uint16_t* planes, void* stream);
+/* Form 10 of the assembly (round 3): the eight-wave 128 × 128 tile staged by
+ * direct global -> LDS loads of pre-split operands, three stage buffers in
+ * flight.  up / vp: the split words of U and V in the 128-row-tile layout of
+ * lds_split_planes_t128 (made for these n rows and k columns).  Modes and
+ * arguments as lds_theta_grad_ex; graphs > 0 (mode 2 only) also draws the
+ * next window's graphs from the θ it writes, as lds_theta_grad_sgd_draw
+ * (words even, >= 2·ceil(n/128)).  Same result bits as every split-bf16 form.
+ * Replaces, fused: src/trainers/outer.py:77-81 and src/models/sampling.py:68. */
+int lds_theta_grad_direct(const uint16_t* up, const uint16_t* vp, int k, const float* r, int ldr_row,
+                          int ldr_col, int nr, float* theta, int n, float* grad, int mode,
+                          const void* scalars, float gscale, uint64_t seed, uint32_t tag,
+                          const uint32_t* counter_base, uint32_t counter_offset, int graphs,
+                          uint64_t* bits, int words, int* deg_ws, void* stream);
+/* uint16 count of the form-10 planes of `rows` rows × k columns:
+ * ceil(k/16) · ceil(rows/128) · 6144.  Host-only. */
+int64_t lds_planes_t128_elems(int rows, int k);
+/* x (rows × ld fp32, first k columns) -> its form-10 planes: value x(i, kk),
+ * word s (0 hi, 1 mid, 2 lo) at uint16 offset
+ *   (((c·nt + T)·3 + s)·128 + r)·16 + 8·(h ^ ((r >> 3) & 1)) + (kk & 7),
+ * c = kk >> 4, T = i >> 7, r = i & 127, h = (kk >> 3) & 1, nt = ceil(rows/128);
+ * rows and columns past the ends are written as zeros.  planes 16-byte aligned. */
+int lds_split_planes_t128(const float* x, int rows, int ld, int k, uint16_t* planes, void* stream);
 /* `form`: the arithmetic form of every θ-gradient assembly above, chosen per
  * call (no process-wide state; a captured HIP graph holds the form it was
  * captured with in its launch):

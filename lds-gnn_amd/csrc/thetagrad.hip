@@ -1270,6 +1270,143 @@ __global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
     t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
 }
 
+constexpr int kW8Lds = 2 * 12 * kPL2 * 4;  // bytes of the two stage buffers (96 KB)
+constexpr int kW8Grp = 8;                  // graphs per draw group (4 KB of LDS each)
+
+// Epilogue of the eight-wave 128-tile kernels (forms 9 and 10; wave (wr, wc)
+// owns outputs wr·64 … + 63 × wc·32 … + 31 of the tile, lane column j): dθ =
+// gscale·(acc + R_i + R_j) on the strict upper triangle, clamp-backward mask,
+// the mode's stores and, with DRAW (mode 2), the next window's draw from the
+// θ just written, its words joined in the dead stage buffers (`lds_dyn`).
+template <bool SMALL, bool DRAW>
+__device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float (&th)[2][16],
+                                            const float (&part)[2][16], const float* Ri, const float* Rj,
+                                            float* __restrict__ theta, float* __restrict__ grad, int n, int mode,
+                                            const double* __restrict__ lr_dev, float gscale, int i0, int j0, int wr,
+                                            int wc, int lane, int t, uint32_t* lds_dyn, const DrawArgs& dr) {
+    const int64_t nn = n;
+    const int jl = wc * 32 + (lane & 31);
+    const int j = j0 + jl;
+    auto row_of = [&](int m, int e) { return wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); };
+    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+    uint32_t thr[2][16];  // DRAW: the next draw's integer thresholds (sampler.hip)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int li = row_of(m, e);
+            const int i = i0 + li;
+            thr[m][e] = 0u;
+            if (i >= n || j >= n || j < i) continue;
+            const int64_t id = tri_at_t<SMALL>(i, j, nn);
+            const float t0 = th[m][e];
+            float g = 0.f;
+            if (j > i) {
+                const float gs = gscale * (acc[m][e] + Ri[li] + Rj[jl]);
+                g = mode == 3 ? part[m][e] + gs : gs;
+                if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+            }
+            if (mode == 3) {
+                grad[id] = g;
+                theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+            } else if (mode == 2) {
+                if (grad != nullptr) grad[id] = g;
+                const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                theta[id] = tn;
+                if (DRAW && j > i) thr[m][e] = (uint32_t)ceilf(tn * 16777216.0f);
+            } else if (mode == 1) {
+                grad[id] = part[m][e] + g;
+            } else {
+                grad[id] = g;
+            }
+        }
+    if constexpr (DRAW) {
+        // LDS (the dead stage buffers): per graph of a group, row segments
+        // rw[row][wc] (uint32: 32 columns) and column words cw[h][col] (uint64:
+        // 64 rows of half h)
+        uint32_t* const rwb = lds_dyn;                                              // kW8Grp × 128 × 4
+        uint64_t* const cwb = reinterpret_cast<uint64_t*>(lds_dyn + kW8Grp * 512);  // kW8Grp × 2 × 128
+        const bool diag = i0 == j0;
+        const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
+#pragma unroll 1
+        for (int base = 0; base < dr.graphs; base += kW8Grp) {
+            const int gn = min(kW8Grp, dr.graphs - base);
+            __syncthreads();  // the stage buffers (first group) / the previous group's words are consumed
+#pragma unroll 1
+            for (int q = 0; q < gn; ++q) {
+                const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
+                uint64_t colw = 0;
+                // both accumulators' eight Philox calls issued together: at two
+                // waves per SIMD the rounds' multiply latency needs the ILP
+                uint32_t x[2][16];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr},
+                                                      dr.k0, dr.k1);
+                        x[m][4 * qd] = o.x;
+                        x[m][4 * qd + 1] = o.y;
+                        x[m][4 * qd + 2] = o.z;
+                        x[m][4 * qd + 3] = o.w;
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const bool bit = (x[m][e] >> 8) < thr[m][e];
+                        const uint64_t w = __ballot(bit);
+                        mylo = lane == e ? (uint32_t)w : mylo;
+                        myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                        colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                    }
+                    if (lane < 16) {  // element e = lane: rows rr and rr + 4 of columns wc·32 …
+                        const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
+                        rwb[(q * 128 + rr) * 4 + wc] = mylo;
+                        rwb[(q * 128 + rr + 4) * 4 + wc] = myhi;
+                    }
+                }
+                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+                if (lane < 32) cwb[(q * 2 + wr) * 128 + wc * 32 + lane] = colw;
+            }
+            __syncthreads();
+            // one (row, two words) pair per work item: rows of I (part 0), rows of J (part 1)
+            for (int it = t; it < gn * 256; it += 512) {
+                const int q = it >> 8, part1 = (it >> 7) & 1, x = it & 127;
+                if (diag && part1) continue;
+                const int row = (part1 ? j0 : i0) + x;
+                if (row >= n) continue;
+                uint64_t* __restrict__ gb = dr.bits + (int64_t)(base + q) * n * dr.words;
+                int* __restrict__ da = dr.dacc + (int64_t)(base + q) * dr.wsi;
+                const uint32_t* rws = rwb + (q * 128 + x) * 4;
+                uint64_t w0, w1;
+                int wbase;
+                if (part1) {  // column x of J: its rows of I (the mirrored entries)
+                    w0 = cwb[(q * 2 + 0) * 128 + x];
+                    w1 = cwb[(q * 2 + 1) * 128 + x];
+                    wbase = i0 >> 6;
+                } else {
+                    w0 = (uint64_t)rws[0] | ((uint64_t)rws[1] << 32);
+                    w1 = (uint64_t)rws[2] | ((uint64_t)rws[3] << 32);
+                    wbase = j0 >> 6;
+                    if (diag) {  // strict upper (row words) | strict lower (column words) | self-loop
+                        w0 |= cwb[(q * 2 + 0) * 128 + x];
+                        w1 |= cwb[(q * 2 + 1) * 128 + x];
+                        if (x < 64) w0 |= 1ull << x;
+                        else w1 |= 1ull << (x - 64);
+                    }
+                }
+                *reinterpret_cast<ulonglong2*>(gb + (int64_t)row * dr.words + wbase) = ulonglong2{w0, w1};
+                const int pc = __popcll(w0) + __popcll(w1);
+                if (pc != 0) atomicAdd(&da[row], pc);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Eight-wave pipelined 128 × 128 form (form 9).  Form 8 runs one wave per
 // SIMD: its 176 split VALU, 12 ds_write and 24 ds_read_b128 per chunk issue
@@ -1295,8 +1432,6 @@ __global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
 // atomic per row and graph (half the 64-tile form's atomics).  All eight waves
 // run the Philox work, two per SIMD: the VALU issues at its full rate.
 // ---------------------------------------------------------------------------
-constexpr int kW8Lds = 2 * 12 * kPL2 * 4;  // bytes of the two stage buffers (96 KB)
-constexpr int kW8Grp = 8;                  // graphs per draw group (4 KB of LDS each)
 
 template <bool SMALL, bool PART, bool DRAW>
 __global__ __launch_bounds__(512, 1) void theta_grad_w8_kernel(
@@ -1435,123 +1570,259 @@ __global__ __launch_bounds__(512, 1) void theta_grad_w8_kernel(
         __syncthreads();
     }
 
-    const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
-    uint32_t thr[2][16];  // DRAW: the next draw's integer thresholds (sampler.hip)
+    w8_epilogue<SMALL, DRAW>(acc, th, part, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane, t,
+                             lds_dyn, dr);
+}
+
+// ---------------------------------------------------------------------------
+// Direct-staged eight-wave 128 × 128 form (form 10, round 3).  Form 9's chunk
+// is bound by its staging phase, not by its 24 MFMAs per wave: every thread
+// splits its quarter rows (≈60 VALU per wave and chunk) and writes them with
+// 12 ds_write_b64, and the barrier that publishes them drains every load in
+// flight (__syncthreads() waits vmcnt(0)), so the next chunk's loads are
+// exposed once per chunk.  Here the operands arrive pre-split (U and V as
+// three bf16 planes in the tile layout below, written by
+// lds_split_planes_t128 or by whoever produces the factors) and the stage is
+// a verbatim copy: each (16-wide chunk, 128-row tile) block of an operand is
+// 12 KB, laid out exactly as form 9's LDS planes (rows of 8 dwords, halves
+// swapped by row bit 3), so every wave moves 6 of the chunk's 48 KB with
+// direct global -> LDS loads (global_load_lds_dwordx4: no VGPR round trip, no
+// ds_write, no split).  The stage is a ring of three buffers (144 KB):
+// chunk c + 2 streams in while chunk c is multiplied, and a chunk's barrier
+// waits only for the loads of chunk c itself (counted vmcnt, raw s_barrier;
+// the loads are issued from inline asm, which keeps the compiler from
+// draining them before every LDS read).  Same chunks, same LDS planes, same
+// MFMA sequence per accumulator as forms 2-9: identical bits.
+//
+// Plane layout (uint16 offsets; nt = ceil(rows / 128) row tiles, rows and
+// k zero-padded to whole tiles / 16-wide chunks): value x(i, kk), split word
+// s (0 = high, 1 = middle, 2 = low) at
+//   (((c·nt + T)·3 + s)·128 + r)·16 + 8·(h ^ ((r >> 3) & 1)) + (kk & 7),
+//   c = kk >> 4, T = i >> 7, r = i & 127, h = (kk >> 3) & 1.
+// ---------------------------------------------------------------------------
+constexpr int kDmaStages = 3;
+constexpr int kDmaStageBytes = 12 * kPL2 * 4;                 // 48 KB: U_I, V_I, U_J, V_J × 3 planes
+constexpr int kDmaLds = kDmaStages * kDmaStageBytes;           // 144 KB
+constexpr int kTileBlk = 3 * kT2 * 16;                         // uint16 per (chunk, row tile) block of one operand
+
+__host__ __device__ __forceinline__ int64_t t128_plane_at(int64_t i, int kk, int s, int nt) {
+    const int r = (int)(i & (kT2 - 1));
+    const int h = ((kk >> 3) & 1) ^ ((r >> 3) & 1);
+    return ((((int64_t)(kk >> 4) * nt + (i >> 7)) * 3 + s) * kT2 + r) * 16 + 8 * h + (kk & 7);
+}
+
+// 16 bytes per lane from global address p to LDS byte address m0 + 16·lane
+// (m0 wave-uniform).  Issued from asm: the compiler does not see an LDS DMA
+// in flight, so it inserts no vmcnt(0) before the k-loop's LDS reads; the
+// kernel counts the loads itself (s_waitcnt vmcnt before each barrier).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; the asm sets it before its one use
+__device__ __forceinline__ void lds_dma16(const void* p, uint32_t m0) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <bool SMALL, bool PART, bool DRAW>
+__global__ __launch_bounds__(512, 1) void theta_grad_dma_kernel(
+    const uint16_t* __restrict__ up, const uint16_t* __restrict__ vp, int nt, int k,
+    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
+    float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
+    float gscale, int group, int per_xcd, DrawArgs dr) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
+    __shared__ float Ri[kT2], Rj[kT2];
+
+    const int nb = (n + kT2 - 1) / kT2;
+    const int ntiles = nb * (nb + 1) / 2;
+    int bi, bj;
+    {
+        const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+        if (L >= ntiles) return;  // whole block: no barrier reached
+        grouped_tile(L, nb, group, bi, bj);
+    }
+    const int i0 = bi * kT2, j0 = bj * kT2;
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    const int64_t nn = n;
+    const int nch = (k + 15) / 16;
+
+    // stage fill: wave w copies the 1-KB blocks w, w + 8, …, w + 40 of a chunk
+    // (block b: operand b / 12 = U_I, V_I, U_J, V_J, its bytes 1024·(b % 12) …)
+    const uint32_t lds_base =
+        (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)lds_dyn);
+    const int64_t cstride = (int64_t)nt * kTileBlk;  // uint16 per chunk of one operand
+    const uint16_t* const opb[4] = {up + (int64_t)bi * kTileBlk, vp + (int64_t)bi * kTileBlk,
+                                    up + (int64_t)bj * kTileBlk, vp + (int64_t)bj * kTileBlk};
+    auto fill = [&](int c, int buf) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const int b = wave + 8 * q;
+            const int a = b / 12, p = b - 12 * a;
+            const uint16_t* src = (a == 0 ? opb[0] : a == 1 ? opb[1] : a == 2 ? opb[2] : opb[3]) + c * cstride +
+                                  512 * p + 8 * lane;
+            lds_dma16(src, lds_base + (uint32_t)(buf * kDmaStageBytes + 1024 * b));
+        }
+    };
+    if (nch > 0) fill(0, 0);
+    if (nch > 1) fill(1, 1);
+    if (nch > 2) fill(2, 2);
+
+    // the epilogue's θ (and partial-grad) operands, issued before the k loop
+    const int jl = wc * 32 + (lane & 31);
+    const int j = j0 + jl;
+    auto row_of = [&](int m, int e) { return wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); };
+    float th[2][16], part[2][16];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const int li = row_of(m, e);
-            const int i = i0 + li;
-            thr[m][e] = 0u;
-            if (i >= n || j >= n || j < i) continue;
-            const int64_t id = tri_at_t<SMALL>(i, j, nn);
-            const float t0 = th[m][e];
-            float g = 0.f;
-            if (j > i) {
-                const float gs = gscale * (acc[m][e] + Ri[li] + Rj[jl]);
-                g = mode == 3 ? part[m][e] + gs : gs;
-                if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
-            }
-            if (mode == 3) {
-                grad[id] = g;
-                theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-            } else if (mode == 2) {
-                if (grad != nullptr) grad[id] = g;
-                const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                theta[id] = tn;
-                if (DRAW && j > i) thr[m][e] = (uint32_t)ceilf(tn * 16777216.0f);
-            } else if (mode == 1) {
-                grad[id] = part[m][e] + g;
-            } else {
-                grad[id] = g;
-            }
+            const int i = i0 + row_of(m, e);
+            const bool in = i < n && j < n && j >= i;
+            const int64_t id = in ? tri_at_t<SMALL>(i, j, nn) : 0;
+            th[m][e] = (in && theta != nullptr) ? theta[id] : 0.f;
+            part[m][e] = (PART && in) ? grad[id] : 0.f;
         }
-    if constexpr (DRAW) {
-        // LDS (the dead stage buffers): per graph of a group, row segments
-        // rw[row][wc] (uint32: 32 columns) and column words cw[h][col] (uint64:
-        // 64 rows of half h)
-        uint32_t* const rwb = lds_dyn;                                              // kW8Grp × 128 × 4
-        uint64_t* const cwb = reinterpret_cast<uint64_t*>(lds_dyn + kW8Grp * 512);  // kW8Grp × 2 × 128
-        const bool diag = i0 == j0;
-        const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
-#pragma unroll 1
-        for (int base = 0; base < dr.graphs; base += kW8Grp) {
-            const int gn = min(kW8Grp, dr.graphs - base);
-            __syncthreads();  // the stage buffers (first group) / the previous group's words are consumed
-#pragma unroll 1
-            for (int q = 0; q < gn; ++q) {
-                const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
-                uint64_t colw = 0;
-                // both accumulators' eight Philox calls issued together: at two
-                // waves per SIMD the rounds' multiply latency needs the ILP
-                uint32_t x[2][16];
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
-#pragma unroll
-                    for (int qd = 0; qd < 4; ++qd) {
-                        const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr},
-                                                      dr.k0, dr.k1);
-                        x[m][4 * qd] = o.x;
-                        x[m][4 * qd + 1] = o.y;
-                        x[m][4 * qd + 2] = o.z;
-                        x[m][4 * qd + 3] = o.w;
-                    }
-                }
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const bool bit = (x[m][e] >> 8) < thr[m][e];
-                        const uint64_t w = __ballot(bit);
-                        mylo = lane == e ? (uint32_t)w : mylo;
-                        myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
-                        colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
-                    }
-                    if (lane < 16) {  // element e = lane: rows rr and rr + 4 of columns wc·32 …
-                        const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
-                        rwb[(q * 128 + rr) * 4 + wc] = mylo;
-                        rwb[(q * 128 + rr + 4) * 4 + wc] = myhi;
-                    }
-                }
-                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
-                if (lane < 32) cwb[(q * 2 + wr) * 128 + wc * 32 + lane] = colw;
-            }
-            __syncthreads();
-            // one (row, two words) pair per work item: rows of I (part 0), rows of J (part 1)
-            for (int it = t; it < gn * 256; it += 512) {
-                const int q = it >> 8, part1 = (it >> 7) & 1, x = it & 127;
-                if (diag && part1) continue;
-                const int row = (part1 ? j0 : i0) + x;
-                if (row >= n) continue;
-                uint64_t* __restrict__ gb = dr.bits + (int64_t)(base + q) * n * dr.words;
-                int* __restrict__ da = dr.dacc + (int64_t)(base + q) * dr.wsi;
-                const uint32_t* rws = rwb + (q * 128 + x) * 4;
-                uint64_t w0, w1;
-                int wbase;
-                if (part1) {  // column x of J: its rows of I (the mirrored entries)
-                    w0 = cwb[(q * 2 + 0) * 128 + x];
-                    w1 = cwb[(q * 2 + 1) * 128 + x];
-                    wbase = i0 >> 6;
-                } else {
-                    w0 = (uint64_t)rws[0] | ((uint64_t)rws[1] << 32);
-                    w1 = (uint64_t)rws[2] | ((uint64_t)rws[3] << 32);
-                    wbase = j0 >> 6;
-                    if (diag) {  // strict upper (row words) | strict lower (column words) | self-loop
-                        w0 |= cwb[(q * 2 + 0) * 128 + x];
-                        w1 |= cwb[(q * 2 + 1) * 128 + x];
-                        if (x < 64) w0 |= 1ull << x;
-                        else w1 |= 1ull << (x - 64);
-                    }
-                }
-                *reinterpret_cast<ulonglong2*>(gb + (int64_t)row * dr.words + wbase) = ulonglong2{w0, w1};
-                const int pc = __popcll(w0) + __popcll(w1);
-                if (pc != 0) atomicAdd(&da[row], pc);
-            }
-        }
+
+    if (t < 2 * kT2) {
+        const int rr = t & (kT2 - 1);
+        const int row = (t < kT2 ? i0 : j0) + rr;
+        float racc = 0.f;
+        if (row < n) racc = row_r_sum(r, (int64_t)row * ldr, ldrc, nr);
+        (t < kT2 ? Ri : Rj)[rr] = racc;
     }
+    // the first three chunks staged: the compiler does not count the asm loads, so
+    // its barrier would not wait for them (nor for the θ loads, issued after)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();                     // R sums and the stage visible to every wave
+
+    const int fo = 4 * ((lane >> 5) ^ ((lane >> 3) & 1));  // fragment rows: bit 3 = lane bit 3
+    const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
+    const int rb = (wc * 32 + (lane & 31)) * kS2 + fo;
+    f32x16 acc[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+
+    // Half-chunk software pipeline: the fragments of one product pair (pr 0:
+    // U_I × V_J, planes 0-2 and 9-11; pr 1: V_I × U_J, planes 3-5 and 6-8) are
+    // read while the other pair's MFMAs run — pr 1 of chunk c during pr 0 of
+    // c, pr 0 of chunk c + 1 (after the chunk barrier) during pr 1 of c — so
+    // the LDS read latency and the barrier hide behind MFMAs in flight.  The
+    // ring holds chunk c + 1 (read next), c + 2 (in flight) and c + 3 (filled
+    // into chunk c's buffer once every wave has read it).
+    typedef bf16x8 Half[2][3 + 3];  // [m][s] A fragments of rows m·32 …, [0][3 + s] the B fragments
+    auto read_half = [&](int c, int pr, Half& f) {
+        const uint32_t* cur = lds_dyn + (c % kDmaStages) * (kDmaStageBytes / 4);
+        const int pa = pr == 0 ? 0 : 3, pb = pr == 0 ? 9 : 6;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            f[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra0));
+            f[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra1));
+            f[0][3 + s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pb + s) * kPL2 + rb));
+        }
+    };
+    auto mfmas = [&](const Half& f) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const bf16x8* a = f[m];
+            const bf16x8* b = f[0] + 3;
+            f32x16 cc = acc[m];
+            cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], cc, 0, 0, 0);
+            acc[m] = cc;
+        }
+    };
+    Half h0, h1;
+    if (nch > 0) read_half(0, 0, h0);
+    for (int c = 0; c < nch; ++c) {
+        read_half(c, 1, h1);
+        mfmas(h0);
+        if (c + 1 < nch) {
+            // this wave's loads of chunk c + 1 done (those of c + 2 may be in
+            // flight) and its reads of chunk c returned; the barrier makes both
+            // hold for every wave
+            if (c + 2 < nch) __builtin_amdgcn_s_waitcnt(0x0076);  // vmcnt(6) expcnt(7) lgkmcnt(0)
+            else __builtin_amdgcn_s_waitcnt(0x0070);              // vmcnt(0) lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");  // no LDS access of the next chunk above the barrier
+            if (c + 3 < nch) fill(c + 3, c % kDmaStages);
+            read_half(c + 1, 0, h0);
+        }
+        mfmas(h1);
+    }
+    __syncthreads();  // every wave done with the stage (the draw reuses it)
+
+    w8_epilogue<SMALL, DRAW>(acc, th, part, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane, t,
+                             lds_dyn, dr);
+}
+
+// x (rows × ld fp32, its first k columns) -> the split3 planes of form 10
+// (t128_plane_at; rows padded to whole 128-row tiles and k to whole 16-wide
+// chunks with zeros).  One thread per (row, 8-wide half chunk): 32 bytes read,
+// three 16-byte stores, consecutive threads on consecutive rows' halves.
+__global__ __launch_bounds__(256) void split_planes_t128_kernel(const float* __restrict__ x, int rows, int ld, int k,
+                                                                int nt, int nch, uint16_t* __restrict__ planes) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // ((c·nt + T)·128 + r)·2 + h
+    if (e >= (int64_t)nch * nt * kT2 * 2) return;
+    const int h = (int)(e & 1);
+    const int64_t ct = e >> 1;  // (c·nt + T)·128 + r
+    const int r = (int)(ct & (kT2 - 1));
+    const int64_t cT = ct >> 7;
+    const int c = (int)(cT / nt);
+    const int64_t i = (cT - (int64_t)c * nt) * kT2 + r;
+    const int kk0 = 16 * c + 8 * h;
+    float xv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xv[q] = (i < rows && kk0 + q < k) ? x[i * ld + kk0 + q] : 0.f;
+    uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split3_pair(xv[2 * q], xv[2 * q + 1], hw[q], mw[q], lw[q]);
+    *reinterpret_cast<u32x4*>(planes + t128_plane_at(i, kk0, 0, nt)) = u32x4{hw[0], hw[1], hw[2], hw[3]};
+    *reinterpret_cast<u32x4*>(planes + t128_plane_at(i, kk0, 1, nt)) = u32x4{mw[0], mw[1], mw[2], mw[3]};
+    *reinterpret_cast<u32x4*>(planes + t128_plane_at(i, kk0, 2, nt)) = u32x4{lw[0], lw[1], lw[2], lw[3]};
+}
+
+template <bool SMALL, bool PART, bool DRAW>
+static void launch_dma_inst(int grid, hipStream_t st, const uint16_t* up, const uint16_t* vp, int nt, int k,
+                            const float* r, int ldr, int nr, float* theta, int n, float* grad, int mode,
+                            const double* lr, int ldrc, float gscale, int per, const DrawArgs& dr) {
+    static bool attr_set = false;  // > 64 KB of dynamic LDS must be enabled per kernel
+    if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_dma_kernel<SMALL, PART, DRAW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDmaLds);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((theta_grad_dma_kernel<SMALL, PART, DRAW>), dim3(grid), dim3(512), kDmaLds, st, up, vp, nt, k,
+                       r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, 8, per, dr);
+}
+
+static void launch_dma(hipStream_t st, const uint16_t* up, const uint16_t* vp, int nt, int k, const float* r, int ldr,
+                       int nr, float* theta, int n, float* grad, int mode, const double* lr, int ldrc, float gscale,
+                       const DrawArgs* dr) {
+    const int nb2 = (n + kT2 - 1) / kT2;
+    const int nt2 = nb2 * (nb2 + 1) / 2;
+    const int per = (nt2 + 7) / 8;
+    const int grid = 8 * per;
+    const bool small = n <= 46340;
+    const bool part = mode == 1 || mode == 3;
+#define LDS_DMA_ARGS grid, st, up, vp, nt, k, r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, per
+    if (dr != nullptr) {  // mode 2 only (checked by the caller)
+        if (small) launch_dma_inst<true, false, true>(LDS_DMA_ARGS, *dr);
+        else launch_dma_inst<false, false, true>(LDS_DMA_ARGS, *dr);
+        return;
+    }
+    const DrawArgs none{};
+    if (small && part) launch_dma_inst<true, true, false>(LDS_DMA_ARGS, none);
+    else if (small) launch_dma_inst<true, false, false>(LDS_DMA_ARGS, none);
+    else if (part) launch_dma_inst<false, true, false>(LDS_DMA_ARGS, none);
+    else launch_dma_inst<false, false, false>(LDS_DMA_ARGS, none);
+#undef LDS_DMA_ARGS
 }
 
 // Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
@@ -1942,6 +2213,42 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
                            (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup,
                            per, Planes{nullptr, nullptr}, dr);
     }
+    LDS_RETURN_LAST_ERROR();
+}
+
+// Form 10's operands: the split3 planes of U / V in the 128-row-tile layout
+// (t128_plane_at), uint16 count for `rows` rows and k columns.
+extern "C" int64_t lds_planes_t128_elems(int rows, int k) {
+    if (rows <= 0 || k <= 0) return 0;
+    return (int64_t)((k + 15) / 16) * ((rows + kT2 - 1) / kT2) * kTileBlk;
+}
+
+extern "C" int lds_split_planes_t128(const float* x, int rows, int ld, int k, uint16_t* planes, void* stream) {
+    LDS_CHECK_ARG(x && planes && rows > 0 && k > 0 && ld >= k && ((uintptr_t)planes & 15) == 0);
+    const int nt = (rows + kT2 - 1) / kT2, nch = (k + 15) / 16;
+    const int64_t tot = (int64_t)nch * nt * kT2 * 2;
+    hipLaunchKernelGGL(split_planes_t128_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, rows, ld, k, nt, nch, planes);
+    LDS_RETURN_LAST_ERROR();
+}
+
+extern "C" int lds_theta_grad_direct(const uint16_t* up, const uint16_t* vp, int k, const float* r, int ldr_row,
+                                     int ldr_col, int nr, float* theta, int n, float* grad, int mode,
+                                     const void* scalars, float gscale, uint64_t seed, uint32_t tag,
+                                     const uint32_t* counter_base, uint32_t counter_offset, int graphs, uint64_t* bits,
+                                     int words, int* deg_ws, void* stream) {
+    LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3 && graphs >= 0 && graphs <= 65535);
+    LDS_CHECK_ARG(k == 0 || (up != nullptr && vp != nullptr && ((((uintptr_t)up) | ((uintptr_t)vp)) & 15) == 0));
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
+    LDS_CHECK_ARG(mode < 2 ? grad != nullptr : (theta != nullptr && scalars != nullptr));
+    LDS_CHECK_ARG(mode != 3 || grad != nullptr);
+    LDS_CHECK_ARG(graphs == 0 || (mode == 2 && bits && deg_ws && (words & 1) == 0 && words >= 2 * ((n + 127) / 128)));
+    const double* lr = mode >= 2 ? reinterpret_cast<const double*>((const char*)scalars + 16) : nullptr;
+    const int nt = (n + kT2 - 1) / kT2;
+    const DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                      counter_offset, counter_base, graphs};
+    launch_dma((hipStream_t)stream, up, vp, nt, k, r, ldr_row, nr, theta, n, grad, mode, lr, ldr_col, gscale,
+               graphs > 0 ? &dr : nullptr);
     LDS_RETURN_LAST_ERROR();
 }
 

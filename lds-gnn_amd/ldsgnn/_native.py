@@ -21,7 +21,7 @@ c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
 P = c_void_p  # device pointers travel as integers
 
 # name -> argtypes (restype is always int = hipError_t, except where noted)
-_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset"}  # byte counts
+_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset", "lds_planes_t128_elems"}  # byte counts
 SIGNATURES = {
     "lds_abi_version": [],
     "lds_graph_node_census": [P, P, c_int],
@@ -44,6 +44,10 @@ SIGNATURES = {
     "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int,
                               P],
     "lds_split_planes": [P, c_int, c_int, c_int, P, P],
+    "lds_planes_t128_elems": [c_int, c_int],
+    "lds_split_planes_t128": [P, c_int, c_int, c_int, P, P],
+    "lds_theta_grad_direct": [P, P, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_uint64, c_uint32,
+                              P, c_uint32, c_int, P, c_int, P, P],
     "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],

@@ -666,3 +666,90 @@ def test_theta_grad_sgd_draw_equals_sgd_then_draw(device, n, k, graphs, draw_for
             for b in range(64):
                 pc += (x >> b) & 1
         assert torch.equal(deg[gi, :n].long(), pc), gi
+
+
+@pytest.mark.parametrize("n,k", [(2708, 264), (300, 40), (130, 8), (129, 21), (64, 16), (1, 8), (700, 0)])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_theta_grad_direct_bit_exact(device, n, k, mode):
+    """Form 10 (lds_theta_grad_direct: pre-split planes of
+    lds_split_planes_t128 staged by direct global -> LDS loads, three stage
+    buffers) against the 128-tile form on the fp32 operands: identical θ and
+    dθ bits in every mode, ragged k and n (zero-padded tiles and chunks), k = 0
+    and n = 1."""
+    g = torch.Generator().manual_seed(7 * n + k + mode)
+    ld = k + 4
+    u = torch.randn(n, ld, generator=g).to(device)
+    v = (torch.randn(n, ld, generator=g) * 0.3).to(device)
+    r = torch.randn(2, n, generator=g).to(device)
+    theta = (torch.rand(n * (n + 1) // 2, generator=g) * 1.2 - 0.1).to(device)
+    base = torch.randn(n * (n + 1) // 2, generator=g).to(device)
+    scal = torch.zeros(64, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(0.05)
+    st = nat.stream_of(torch.device(device))
+    kk = max(k, 1)
+    ne = nat.lib.lds_planes_t128_elems(n, kk)
+    up = torch.full((ne,), -1, dtype=torch.int16, device=device)  # garbage: every word must be written
+    vp = torch.full((ne,), -1, dtype=torch.int16, device=device)
+    if k > 0:
+        nat.call("lds_split_planes_t128", nat.ptr(u), n, ld, k, nat.ptr(up), st)
+        nat.call("lds_split_planes_t128", nat.ptr(v), n, ld, k, nat.ptr(vp), st)
+    outs = []
+    th = theta.clone()
+    grad = base.clone()
+    prev = ops.theta_grad_form("bf16x3-t128-grouped")
+    try:
+        nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
+                 nat.ptr(grad), mode, nat.ptr(scal), 0.5, ops.form_code(), st)
+    finally:
+        ops.theta_grad_form(prev)
+    outs.append((th, grad))
+    th = theta.clone()
+    grad = base.clone()
+    nat.call("lds_theta_grad_direct", nat.ptr(up), nat.ptr(vp), k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
+             nat.ptr(grad), mode, nat.ptr(scal), 0.5, 0, 0, 0, 0, 0, 0, 0, 0, st)
+    torch.cuda.synchronize()
+    outs.append((th, grad))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,k,graphs", [(2708, 264, 6), (300, 40, 3), (130, 8, 1), (1000, 16, 21), (129, 24, 9)])
+def test_theta_grad_direct_draw_equals_sgd_draw(device, n, k, graphs):
+    """Form 10 with the next window's draw in its epilogue against
+    lds_theta_grad_sgd_draw (form 9): identical θ, bit rows and degree
+    accumulators."""
+    g = torch.Generator().manual_seed(n + 3 * k + graphs)
+    ld = k + 8
+    u = torch.randn(n, ld, generator=g).to(device)
+    v = (torch.randn(n, ld, generator=g) * 0.3).to(device)
+    r = torch.randn(n, generator=g).to(device)
+    theta = (torch.rand(n * (n + 1) // 2, generator=g) * 0.4).to(device)
+    scal = torch.zeros(64, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(0.05)
+    st = nat.stream_of(torch.device(device))
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    base = torch.tensor([11, 0, 0, 0], dtype=torch.int32, device=device)
+    seed, tag, off = 4321, tag_for(TAG_GRAPH, 3), 6
+    res = []
+    for direct in (False, True):
+        th = theta.clone()
+        bits = torch.zeros((graphs, n, words), dtype=torch.int64, device=device)
+        deg = torch.zeros((graphs, wsi), dtype=torch.int32, device=device)
+        if direct:
+            ne = nat.lib.lds_planes_t128_elems(n, k)
+            up = torch.empty(ne, dtype=torch.int16, device=device)
+            vp = torch.empty(ne, dtype=torch.int16, device=device)
+            nat.call("lds_split_planes_t128", nat.ptr(u), n, ld, k, nat.ptr(up), st)
+            nat.call("lds_split_planes_t128", nat.ptr(v), n, ld, k, nat.ptr(vp), st)
+            nat.call("lds_theta_grad_direct", nat.ptr(up), nat.ptr(vp), k, nat.ptr(r), 1, 1, 1, nat.ptr(th), n, 0,
+                     2, nat.ptr(scal), 1.0, seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words,
+                     nat.ptr(deg), st)
+        else:
+            nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), ld, k, nat.ptr(r), 1, 1, nat.ptr(th), n, 0,
+                     nat.ptr(scal), seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg), 9, st)
+        torch.cuda.synchronize()
+        res.append((th, bits, deg))
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert torch.equal(a, b)
