@@ -210,6 +210,24 @@ int64_t lds_bitmask_agg_ws_bytes(int n);
  * offset lds_bitmask_agg_part_offset(n) of ws, for a consumer that forms
  * y_i = s_i · Σ_p part_p[i] in split order (LdsBatch.agg_splits): the same
  * bits as lds_aggregate_bitmask's y with beta = 0. */
+/* CSR-SpMM for dense sampled graphs (long rows, e.g. BASELINE config 5):
+ * y (= or +=) diag(s)·A·diag(s)·z for the 0/1 matrix A given as CSR
+ * (row_ptr, col: distinct columns per row, any order), F = 16 features — the
+ * operator of lds_spmm_norm.  The column-index stream is read once; each
+ * 16-row tile's entries become a bit tile in LDS that the int8 matrix cores
+ * multiply with the fixed-point digits of s⊙z (lds_aggregate_bitmask's
+ * quantisation: exact integer sums, one rounding per digit at 2^-31 of the
+ * column maximum).  n <= lds_spmm_dense_max_n(); col 16-byte aligned; ws:
+ * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned; grid 0 = one persistent
+ * workgroup per CU.  Three launches (column maxima, digits, the product);
+ * quantize = 0 skips the first two (ws holds the digits of this s, z from an
+ * earlier call).
+ * Replaces torch.mm(normalize_adjacency_matrix(A), Z) (src/models/layers.py:44,
+ * src/utils/graph.py:136-153). */
+int64_t lds_spmm_dense_ws_bytes(int n);
+int lds_spmm_dense_max_n(void);
+int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
+                        float* y, int ldy, int beta, void* ws, int grid, int quantize, void* stream);
 int lds_bitmask_agg_splits(int n);
 int64_t lds_bitmask_agg_part_offset(int n);
 int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, const float* s, int n, const float* z,

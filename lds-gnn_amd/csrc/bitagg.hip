@@ -319,6 +319,253 @@ __global__ __launch_bounds__(256) void bitagg_final_kernel(const float* __restri
     for (int j = 0; j < 4; ++j) o[j] = beta ? o[j] + r[j] : r[j];
 }
 
+// ---------------------------------------------------------------------------
+// CSR-SpMM for dense sampled graphs (BASELINE config 5: N = 20 000, ~N/2
+// entries per row; lds_spmm_norm_dense).  The operator of lds_spmm_norm —
+// torch.mm(normalize_adjacency_matrix(A), Z) (src/models/layers.py:44,
+// src/utils/graph.py:136-153) on the sampled graph's CSR — with the column
+// index stream (4 bytes per entry, 0.8 GB per call at config 5) read once
+// from HBM and nothing else of size nnz touched:
+//  - per 16-row tile, 8 streaming waves read the tile's CSR rows (each lane
+//    16 consecutive entries per step, four 16-byte loads, two steps in
+//    flight) and set the entries' bits in a 16-row bit tile in LDS (OR in
+//    registers, then one or two LDS ORs per lane and step);
+//  - 4 MFMA waves multiply the previous tile's bits with the fixed-point
+//    digits of s⊙Z on the int8 matrix cores, exactly as lds_aggregate_bitmask
+//    does from the sampler's bitmask (same digits and k order, exact int32
+//    sums), while the streaming waves fill the next tile: two bit-tile
+//    buffers, one barrier per tile.  MFMA wave m owns k-steps 2m, 2m + 1 of
+//    every 512-column chunk, i.e. dwords ≡ m (mod 4) of each bit row, and
+//    clears exactly those after its last read, so no other wave waits on it.
+//  - Why not gathers: one 64-byte row of s⊙Z per entry is 12.8 GB of LDS
+//    reads per call at this density, more than the LDS delivers in the time
+//    the index stream takes; here each tile reads s⊙Z as 1.3 MB of digits
+//    from L2.
+// Workgroups are persistent (one per CU; tiles b, b + grid, …).  Columns
+// must be distinct within a row (a CSR of a 0/1 matrix); their order is free.
+// ---------------------------------------------------------------------------
+constexpr int kDnStream = 8;                       // streaming waves (rows 2w, 2w + 1 of each tile)
+constexpr int kDnMma = 8;                          // MFMA waves (k-steps 2·(m >> 1), + 1 of the chunks of parity m & 1)
+constexpr int kDnThreads = 64 * (kDnStream + kDnMma);
+constexpr int kDnMaxChunks = 47;                   // n <= 24 064: two bit tiles + rings <= 160 KB
+constexpr int kDnUnits = 8;                        // 1-KB ring units per streaming wave (a step takes two)
+constexpr int kDnStep = 512;                       // entries per step (lane l: entries p + 8l … + 7)
+
+constexpr int kDnMaxGrid = 512;                    // workgroups (partials scratch in ws)
+constexpr int kDnPartBytes = 2 * kDnMma * 256 * 8;  // per workgroup: a tile's int64 partials, double-buffered
+
+int dense_lds_bytes(int chunks) { return 2 * 16 * 16 * chunks * 4 + kDnStream * kDnUnits * 1024; }
+
+__device__ __forceinline__ void dn_or(uint32_t* p, uint32_t m) {
+    if (m != 0u) atomicOr(p, m);
+}
+
+// A streaming wave's position (wave-uniform): tile `it` of this workgroup,
+// row slot rr (row 2·wave + rr of the tile), the entries [p, p + 512) of that
+// row's [beg, end), p ≡ 0 mod 4.
+struct Step {
+    int it, rr, beg, end, p;
+};
+// The next step: the row's next 512 entries, else the next non-empty row
+// slot, else the next tile (it == my_tiles: past the last).
+__device__ __forceinline__ void dn_advance(Step& s, const int* __restrict__ rp, int n, int my_tiles, int wave) {
+    if (s.rr >= 0) {
+        s.p += kDnStep;
+        if (s.p < s.end) return;
+    }
+    while (true) {
+        if (++s.rr == 2) {
+            s.rr = 0;
+            ++s.it;
+        }
+        if (s.it >= my_tiles) return;
+        const int row = ((int)blockIdx.x + s.it * (int)gridDim.x) * 16 + 2 * wave + s.rr;
+        if (row >= n) continue;
+        s.beg = __builtin_amdgcn_readfirstlane(rp[row]);
+        s.end = __builtin_amdgcn_readfirstlane(rp[row + 1]);
+        s.p = s.beg & ~3;
+        if (s.beg < s.end) return;
+    }
+}
+
+// DBG (ablations for timing only, wrong results): 1 no MFMA waves, 2 no bit
+// setting either (the index stream alone), 3 no streaming, 4 MFMA waves on
+// constant digits (no digit loads).  The product path is DBG = 0.
+template <int DBG>
+__global__ __launch_bounds__(kDnThreads, 1) void csr_dense_agg_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, int n, const int8_t* __restrict__ zq, int chunks,
+    const uint32_t* __restrict__ colmax, const float* __restrict__ s, float* __restrict__ y, int ldy, int beta,
+    int64_t* __restrict__ parts) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dn_lds[];
+    __shared__ int e_sh[kF];
+    const int rs = 16 * chunks;                          // dwords per bit-tile row
+    uint32_t* const tiles = dn_lds;                      // [2][16][rs]
+    uint32_t* const ring = dn_lds + 2 * 16 * rs;         // [kDnStream][kDnUnits][256]
+    // [2][kDnMma][16 rows][16 f] int64 partials of this workgroup (global scratch, L2)
+    int64_t* const red = parts + (size_t)blockIdx.x * (kDnPartBytes / 8);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int ntile = (n + 15) / 16;
+    const int my_tiles = ntile > (int)blockIdx.x ? (ntile - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int nnz = rp[n];
+
+    for (int d = 4 * t; d < 2 * 16 * rs; d += 4 * kDnThreads)
+        *reinterpret_cast<uint4*>(tiles + d) = make_uint4(0u, 0u, 0u, 0u);
+    if (t < 64) {  // per-feature exponents (lds_aggregate_bitmask's quantisation)
+        const uint32_t m = colmax_of(colmax, t);
+        if (t < kF) e_sh[t] = col_exponent(m);
+    }
+
+    // Streaming waves: their index stream through a ring of 1-KB LDS units
+    // filled by direct loads three steps ahead, across rows and tiles (the next
+    // tile's entries land before the tile barrier; their bits are set after it).
+    Step is{0, -1, 0, 0, 0}, ps{0, -1, 0, 0, 0};
+    int kis = 0, kps = 0;  // steps issued / processed
+    const uint32_t ring_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)ring) +
+                              (uint32_t)(wave * kDnUnits * 1024);
+    const uint32_t* myring = ring + wave * kDnUnits * 256;
+    auto issue = [&]() {
+        const uint32_t unit = (uint32_t)((2 * kis) % kDnUnits);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int a = is.p + 256 * h + 4 * lane;
+            const int* src = a + 4 <= nnz ? col + a : col;  // past the array: a dummy block (reloaded below)
+            lds_dma16(src, ring_lds + (unit + h) * 1024u);
+        }
+        ++kis;
+        dn_advance(is, rp, n, my_tiles, wave);
+    };
+    if (wave < kDnStream) {
+        dn_advance(is, rp, n, my_tiles, wave);
+        ps = is;
+        for (int d = 0; d < 3 && is.it < my_tiles; ++d) issue();
+    }
+    __syncthreads();
+
+    const int mw = wave - kDnStream;  // MFMA wave index
+    const int r16 = lane & 15, g = lane >> 4;
+    for (int it = 0; it <= my_tiles; ++it) {
+        const int buf = it & 1;
+        if (wave < kDnStream) {
+            while (DBG != 3 && ps.it == it && it < my_tiles) {
+                if (is.it < my_tiles) issue();
+                // step kps landed: at most the three younger steps (two loads each) in flight
+                if (kis - kps == 4) __builtin_amdgcn_s_waitcnt(0x0F76);  // vmcnt(6)
+                else __builtin_amdgcn_s_waitcnt(0x0F70);                 // vmcnt(0)
+                asm volatile("" ::: "memory");
+                const uint32_t* sl = myring + ((2 * kps) % kDnUnits) * 256 + 8 * lane;
+                const int4 c0 = *reinterpret_cast<const int4*>(sl);
+                const int4 c1 = *reinterpret_cast<const int4*>(sl + 4);
+                int c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                uint32_t* rb = tiles + buf * 16 * rs + (2 * wave + ps.rr) * rs;
+                const int p = ps.p + 8 * lane;
+                // interior step (every entry of it is the row's, none from a dummy block): the fast path
+                const bool interior = ps.p >= ps.beg && ps.p + kDnStep <= ps.end && ps.p + kDnStep + 4 <= nnz;
+                bool done = false;
+                if (DBG < 2 && interior) {
+                    const uint32_t wf = (uint32_t)c[0] >> 5, wl = (uint32_t)c[7] >> 5;  // columns ascending
+                    if (wl - wf <= 1u) {
+                        const int base = (int)(wf << 5);
+                        uint64_t m = 0;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) m |= 1ull << (c[e] - base);
+                        dn_or(rb + wf, (uint32_t)m);
+                        dn_or(rb + wf + 1, (uint32_t)(m >> 32));
+                        done = true;
+                    }
+                }
+                if (DBG < 2 && !done) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int idx = p + e;
+                        if (idx >= ps.beg && idx < ps.end) {
+                            const int v = (idx & ~3) + 4 > nnz ? col[idx] : c[e];
+                            atomicOr(rb + (v >> 5), 1u << (v & 31));
+                        }
+                    }
+                }
+                ++kps;
+                dn_advance(ps, rp, n, my_tiles, wave);
+            }
+        } else if ((DBG == 0 || DBG >= 3) && it >= 1) {
+            // multiply tile it - 1 (its bits in buffer buf ^ 1): k-steps 2·pm, 2·pm + 1
+            // of the chunks of parity cp, the digits from L2 through a ring of
+            // register sets three k-steps ahead; then clear the dwords of the buffer
+            // this wave read (dword pm of every group of its chunks: no other wave
+            // reads them)
+            const int pm = mw >> 1, cp = mw & 1;
+            uint32_t* tb = tiles + (buf ^ 1) * 16 * rs;
+            const uint32_t* ta = tb + r16 * rs + 4 * g + pm;  // + 16·c
+            v4i acc[kLimbs];
+#pragma unroll
+            for (int L = 0; L < kLimbs; ++L) acc[L] = v4i{0, 0, 0, 0};
+            const v4i* zv = reinterpret_cast<const v4i*>(zq) + (2 * pm * kLimbs) * 64 + lane;
+            constexpr int kRing = 4;
+            const int ncp = (chunks - cp + 1) / 2;  // this wave's chunks cp, cp + 2, …
+            const int nj = 2 * ncp;                 // j = 2i + h: chunk cp + 2i, k-step 2·pm + h
+            v4i bq[kRing][kLimbs];
+            auto bload = [&](int j, v4i (&b)[kLimbs]) {
+                const int c = cp + 2 * (j >> 1), h = j & 1;
+#pragma unroll
+                for (int L = 0; L < kLimbs; ++L)
+                    b[L] = DBG == 4 ? v4i{j, h, L, 1} : j < nj ? zv[(int64_t)c * (kChunkBytes / 16) + (h * kLimbs + L) * 64] : v4i{0, 0, 0, 0};
+            };
+#pragma unroll
+            for (int d = 0; d < kRing - 1; ++d) bload(d, bq[d]);
+            uint32_t w = 0u;
+#pragma unroll 1
+            for (int j0 = 0; j0 < nj; j0 += kRing) {
+#pragma unroll
+                for (int d = 0; d < kRing; ++d) {
+                    const int j = j0 + d;
+                    if (j < nj) {
+                        bload(j + kRing - 1, bq[(d + kRing - 1) % kRing]);
+                        const int h = d & 1;  // kRing even: j & 1 == d & 1
+                        if (h == 0) w = ta[16 * (cp + 2 * (j >> 1))];
+                        const int sh = 4 * h;  // k-step 2·pm + h: dword pm, shift 4·(q & 1)
+                        v4i a;
+                        a.x = (int)((w >> sh) & 0x01010101u);
+                        a.y = (int)((w >> (sh + 1)) & 0x01010101u);
+                        a.z = (int)((w >> (sh + 2)) & 0x01010101u);
+                        a.w = (int)((w >> (sh + 3)) & 0x01010101u);
+#pragma unroll
+                        for (int L = 0; L < kLimbs; ++L)
+                            acc[L] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[d][L], acc[L], 0, 0, 0);
+                    }
+                }
+            }
+            int64_t* rd = red + ((it - 1) & 1) * (kDnMma * 256) + mw * 256;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                rd[(4 * g + i) * 16 + r16] = (int64_t)acc[0][i] + ((int64_t)acc[1][i] << 8) +
+                                             ((int64_t)acc[2][i] << 16) + ((int64_t)acc[3][i] << 24);
+            // dwords 16c + 4g' + pm of every row, c ≡ cp (mod 2): lane = (row, g')
+            for (int e = lane; e < 16 * 4 * ncp; e += 64) {
+                const int row = e & 15, gg = (e >> 4) & 3, c = cp + 2 * (e >> 6);
+                tb[row * rs + 16 * c + 4 * gg + pm] = 0u;
+            }
+        }
+        __syncthreads();
+        if (it >= 1 && wave >= kDnStream && t < 64 * kDnStream + 256) {  // tile it - 1: partials summed, scaled, stored
+            const int tile = (int)blockIdx.x + (it - 1) * (int)gridDim.x;
+            const int64_t* rdb = red + ((it - 1) & 1) * (kDnMma * 256);
+            {
+                const int o = t - 64 * kDnStream;  // output lr·16 + f
+                const int lr = o >> 4, f = o & 15;
+                const int row = tile * 16 + lr;
+                if (row < n) {
+                    int64_t v = 0;
+#pragma unroll
+                    for (int m = 0; m < kDnMma; ++m) v += rdb[m * 256 + o];
+                    const float r = s[row] * (float)ldexp((double)v, -e_sh[f]);
+                    float* out = y + (int64_t)row * ldy + f;
+                    *out = beta ? *out + r : r;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace lds
 
 using namespace lds;
@@ -373,5 +620,54 @@ extern "C" int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, c
     hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(kThreads), 0, st, bits, words, n,
                        (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax, s, (float*)nullptr, 0, 0,
                        1);
+    LDS_RETURN_LAST_ERROR();
+}
+
+// Workspace of lds_spmm_norm_dense: lds_aggregate_bitmask's column maxima and
+// digit chunks.
+extern "C" int64_t lds_spmm_dense_ws_bytes(int n) {
+    if (n <= 0) return 0;
+    return (int64_t)kMaxBlocks * kF * 4 + (int64_t)chunks_of(n) * kChunkBytes + (int64_t)kDnMaxGrid * kDnPartBytes;
+}
+
+extern "C" int lds_spmm_dense_max_n(void) { return kDnMaxChunks * kChunk; }
+
+extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z,
+                                   int ldz, float* y, int ldy, int beta, void* ws, int grid, int quantize,
+                                   void* stream) {
+    LDS_CHECK_ARG(row_ptr && col && s && z && y && ws && n > 0 && n <= kDnMaxChunks * kChunk);
+    LDS_CHECK_ARG(ldz >= kF && ldy >= kF && grid >= 0);
+    LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
+    hipStream_t st = (hipStream_t)stream;
+    const Ws w = carve(ws, n);
+    const int nc = chunks_of(n);
+    if (quantize) {
+        hipLaunchKernelGGL(bitagg_colmax_kernel, dim3(kMaxBlocks), dim3(256), 0, st, s, n, z, ldz, w.colmax);
+        hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st, s, n, z,
+                           ldz, (const uint32_t*)w.colmax, w.zq, nc);
+    }
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    const int ntile = (n + 15) / 16;
+    int g = grid > 0 ? grid : cus;
+    if (g > kDnMaxGrid) g = kDnMaxGrid;
+    if (g > ntile) g = ntile;
+    int64_t* parts = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(ws) + (int64_t)kMaxBlocks * kF * 4 +
+                                                (int64_t)nc * kChunkBytes);
+    const int lds = dense_lds_bytes(nc);
+    static int attr_bytes = 0;  // > 64 KB of dynamic LDS must be enabled per kernel
+    if (attr_bytes < lds) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_dense_agg_kernel<0>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return (int)e;
+        attr_bytes = lds;
+    }
+    hipLaunchKernelGGL(csr_dense_agg_kernel<0>, dim3(g), dim3(kDnThreads), lds, st, row_ptr, col, n,
+                       (const int8_t*)w.zq, nc, (const uint32_t*)w.colmax, s, y, ldy, beta, parts);
     LDS_RETURN_LAST_ERROR();
 }

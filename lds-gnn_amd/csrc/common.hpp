@@ -157,4 +157,17 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// 16 bytes per lane from global address p to LDS byte address m0 + 16·lane
+// (m0 wave-uniform).  Issued from asm: the compiler does not see an LDS DMA
+// in flight, so it inserts no vmcnt(0) before the kernel's LDS reads; the
+// kernel counts these loads itself (s_waitcnt vmcnt).  Vector-memory
+// operations count in issue order, so loads the compiler adds only make such
+// a count stricter.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; the asm sets it before its one use
+__device__ __forceinline__ void lds_dma16(const void* p, uint32_t m0) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 }  // namespace lds

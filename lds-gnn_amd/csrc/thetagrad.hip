@@ -1611,16 +1611,6 @@ __host__ __device__ __forceinline__ int64_t t128_plane_at(int64_t i, int kk, int
     return ((((int64_t)(kk >> 4) * nt + (i >> 7)) * 3 + s) * kT2 + r) * 16 + 8 * h + (kk & 7);
 }
 
-// 16 bytes per lane from global address p to LDS byte address m0 + 16·lane
-// (m0 wave-uniform).  Issued from asm: the compiler does not see an LDS DMA
-// in flight, so it inserts no vmcnt(0) before the k-loop's LDS reads; the
-// kernel counts the loads itself (s_waitcnt vmcnt before each barrier).
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; the asm sets it before its one use
-__device__ __forceinline__ void lds_dma16(const void* p, uint32_t m0) {
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0) : "memory", "m0");
-}
-#pragma clang diagnostic pop
 
 template <bool SMALL, bool PART, bool DRAW>
 __global__ __launch_bounds__(512, 1) void theta_grad_dma_kernel(

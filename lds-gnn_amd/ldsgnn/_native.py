@@ -21,7 +21,7 @@ c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
 P = c_void_p  # device pointers travel as integers
 
 # name -> argtypes (restype is always int = hipError_t, except where noted)
-_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset", "lds_planes_t128_elems"}  # byte counts
+_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset", "lds_planes_t128_elems", "lds_spmm_dense_ws_bytes"}  # byte counts
 SIGNATURES = {
     "lds_abi_version": [],
     "lds_graph_node_census": [P, P, c_int],
@@ -60,6 +60,9 @@ SIGNATURES = {
     "lds_bitmask_agg_splits": [c_int],
     "lds_bitmask_agg_part_offset": [c_int],
     "lds_aggregate_bitmask_partials": [P, c_int, P, c_int, P, c_int, P, P],
+    "lds_spmm_dense_ws_bytes": [c_int],
+    "lds_spmm_dense_max_n": [],
+    "lds_spmm_norm_dense": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, c_int, c_int, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_int, P],

@@ -165,3 +165,35 @@ def test_long_row_window_n20000_matches_in_kernel_aggregation(device):
     gs = float(b["grad"].abs().max())
     assert float((a["grad"] - b["grad"]).abs().max()) < 1e-4 * gs
     assert torch.allclose(a["theta"], b["theta"], rtol=TOL, atol=1e-6)
+
+
+def test_spmm_dense_n20000_vs_bitmask_csr_and_fp64_rows(device, dense_graph):
+    """The config-5 CSR-SpMM (lds_spmm_norm_dense: the CSR index stream into
+    LDS bit tiles, int8 matrix-core product) on the full-size sampled graph:
+    against fp64 rows, the bitmask aggregation and the column-blocked CSR
+    kernel, and repeatable bit for bit."""
+    graph = dense_graph
+    z = torch.randn(N, 16, generator=torch.Generator().manual_seed(3)).to(device)
+    ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(N)), dtype=torch.uint8, device=device)
+    outs = []
+    for _ in range(2):
+        y = torch.empty(N, 16, device=device)
+        nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), N, nat.ptr(z),
+                 16, nat.ptr(y), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    y = outs[0]
+    y_bit = graph.spmm_bitmask(z)
+    y_csr = graph.spmm(z)
+    rp = graph.row_ptr.cpu()
+    zd = z.double().cpu()
+    s = graph.s.double().cpu()
+    for i in _rows(N, 6, 11):
+        cols = graph.col[int(rp[i]):int(rp[i + 1])].long().cpu()
+        ref = s[i] * (s[cols, None] * zd[cols]).sum(0)
+        scale = (s[i] * (s[cols, None] * zd[cols]).abs().sum(0)).clamp(min=1e-30)
+        assert float(((y[i].double().cpu() - ref).abs() / scale).max()) < TOL, i
+    colscale = (y_csr.abs().max(0).values.double() + 1e-30)
+    assert float(((y.double() - y_csr.double()).abs().max(0).values / colscale).max()) < TOL
+    assert float(((y.double() - y_bit.double()).abs().max(0).values / colscale).max()) < TOL

@@ -753,3 +753,76 @@ def test_theta_grad_direct_draw_equals_sgd_draw(device, n, k, graphs):
     for other in res[1:]:
         for a, b in zip(res[0], other):
             assert torch.equal(a, b)
+
+
+def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, grid=0):
+    dev = z.device
+    ws = torch.full((int(nat.lib.lds_spmm_dense_ws_bytes(n)),), 0x5A, dtype=torch.uint8, device=dev)
+    y = out if out is not None else torch.empty(n, ldy, device=dev)
+    nat.call("lds_spmm_norm_dense", nat.ptr(graph_rp), nat.ptr(graph_col), nat.ptr(s), n, nat.ptr(z), ldz,
+             nat.ptr(y), ldy, beta, nat.ptr(ws), grid, 1, nat.stream_of(dev))
+    torch.cuda.synchronize()
+    return y
+
+
+@pytest.mark.parametrize("n,high,grid", [(1, 1.0, 0), (17, 1.0, 0), (700, 1.0, 0), (1500, 1.0, 3), (2600, 0.5, 0),
+                                         (3000, 0.02, 0), (3001, 1.0, 7)])
+def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
+    """lds_spmm_norm_dense (CSR streamed into LDS bit tiles, int8 matrix-core
+    product) vs the dense fp64 product, the bitmask aggregation (same digits:
+    identical bits where that takes one split) and the CSR row kernel: ragged
+    n, dense and sparse rows (the sparse fallback of the bit setting), a
+    persistent grid smaller than the tile count, columns of extreme scale.
+    Per-column tolerance 1e-5 of max_i Σ_k |Â_ik z_kf|."""
+    g = torch.Generator().manual_seed(n + 29)
+    theta = torch.rand(n * (n + 1) // 2, generator=g) * high
+    graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n + 1), track_grad=False)
+    z = torch.randn(n, 16, generator=g)
+    z[:, 3] *= 1e-30
+    z[:, 7] *= 1e30
+    z[:, 11] = 0.0
+    z[: n // 2, 13] *= 1e6
+    zd = z.to(device)
+    y = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=grid).cpu().double()
+    a = graph.normalized_dense().cpu().double()
+    ref = a @ z.double()
+    scale = (a.abs() @ z.double().abs()).max(0).values.clamp(min=1e-300)
+    assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL
+    assert torch.all(y[:, 11] == 0)
+    y_bit = graph.spmm_bitmask(zd).cpu().double()
+    if nat.lib.lds_bitmask_agg_splits(n) == 1:
+        assert torch.equal(y, y_bit)
+    assert float(((y - y_bit).abs().max(0).values / scale).max()) < RTOL
+    # beta = 1 into a strided Y from a strided Z
+    zs = torch.zeros(n, 24, device=device)
+    zs[:, :16] = zd
+    out = torch.ones(n, 20, device=device)
+    _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zs, ldz=24, out=out, ldy=20, beta=1, grid=grid)
+    o = out.cpu().double()
+    assert float(((o[:, :16] - ref - 1.0).abs().max(0).values / scale.clamp(min=1.0)).max()) < RTOL
+    assert torch.all(o[:, 16:] == 1.0)
+
+
+def test_spmm_dense_empty_rows_and_unsorted_columns(device):
+    """A general 0/1 CSR: empty rows give 0, a row's columns in any order (the
+    bits are set by OR), long rows straddling the 1024-entry steps."""
+    n = 1300
+    g = torch.Generator().manual_seed(5)
+    a = (torch.rand(n, n, generator=g) < 0.45)
+    a[7] = False
+    a[500:520] = False
+    a[n - 1] = False
+    rows, cols = a.nonzero(as_tuple=True)
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(a.sum(1), 0)
+    col = cols.clone().int()
+    for i in (3, 900):  # reverse two rows' column order
+        b, e = int(rp[i]), int(rp[i + 1])
+        col[b:e] = col[b:e].flip(0)
+    s = torch.rand(n, generator=g) + 0.5
+    z = torch.randn(n, 16, generator=g)
+    y = _spmm_dense(rp.int().to(device), col.to(device), s.to(device), n, z.to(device)).cpu().double()
+    ref = s.double()[:, None] * (a.double() @ (s.double()[:, None] * z.double()))
+    scale = (a.double() @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
+    assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL
+    assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0)

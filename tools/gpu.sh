@@ -17,6 +17,7 @@
 #   scpu       the Citeseer S = 16 line with its CPU baseline s_cpu_TAG.json
 #   accuracy   LDS τ = 5 fused engine, 10 seeds, Cora + Citeseer acc_<ds>_tau5_TAG.jsonl
 #   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
+#   spmm5      config-5 CSR-SpMM kernels + kernel trace + PMC spmm5_TAG.json, spmm5_prof_TAG/, spmm5_pmc_TAG_*/
 set -o pipefail
 tag=${1:?usage: tools/gpu.sh TAG STEP...}
 shift
@@ -78,6 +79,15 @@ for step in "$@"; do
         run 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29518 bench.py --gpus 2 --backend gloo --samples 8 --steps 50 --warmup 10 \
             --no-cpu-baseline > $O/bench_2rank_gloo_s8_$tag.log 2>&1 || exit $? ;;
+    spmm5)
+        run 200 python tools/spmm_config5.py > $O/spmm5_$tag.json 2> $O/spmm5_$tag.err || exit $?
+        run 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/spmm5_prof_$tag -o run -- \
+            python3 tools/spmm_config5.py > $O/spmm5_prof_$tag.log 2>&1 || exit $?
+        for c in FETCH_SIZE WRITE_SIZE; do
+            lc=$(echo $c | cut -d_ -f1 | tr 'A-Z' 'a-z')
+            run 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/spmm5_pmc_${tag}_$lc -o run -- \
+                python3 tools/spmm_config5.py > $O/spmm5_pmc_${tag}_$lc.log 2>&1 || exit $?
+        done ;;
     *)
         echo "unknown step $step" >&2
         exit 2 ;;
