@@ -53,7 +53,7 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
 METRIC = "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X"
-PMC_RECORD = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_RECORD = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
 
 
 def world_info():
@@ -148,7 +148,8 @@ def algo_cost(name, eng, n_calls_per_window):
     graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)  # row_ptr, col, s, ELL head
     tri = n * (n + 1) // 2
     P = eng.np
-    if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex", "lds_theta_grad_sgd_draw"):
+    if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex", "lds_theta_grad_sgd_draw",
+                "lds_theta_grad_direct"):
         # (_draw: the next window's graph draw rides in the epilogue; priced on the θ-grad's flops)
         k = eng.S * eng.ldk if eng.S > 1 else eng.window_columns(eng.tau, eng.c)
         return "mfma", 6.0 * 4.0 * k * tri   # split bf16: six bf16 MFMA products per fp32 product
@@ -318,8 +319,10 @@ def roofline_of(row, args):
                 "frac": achieved / HBM_PEAK_GBS}
     roof.update(kernel=row["entry"], avg_us=row["avg_us"], launches_per_window=row["launches_per_window"],
                 share_of_window=None)
-    if row["entry"] == "lds_theta_grad_sgd_draw":  # priced on the assembly's flops alone
+    if row["entry"] in ("lds_theta_grad_sgd_draw", "lds_theta_grad_direct"):  # priced on the assembly's flops alone
         roof["includes"] = "the next window's graph draw (tau+1 graphs, Philox VALU) in the epilogue"
+    if row["entry"] == "lds_theta_grad_direct":
+        roof["form"] = "bf16x3-direct (form 10: pre-split planes staged by direct global->LDS loads)"
     roof["traffic"], roof["traffic_source"] = pmc_traffic(row["entry"], args)
     return roof
 

@@ -212,7 +212,8 @@ int64_t lds_bitmask_agg_ws_bytes(int n);
  * bits as lds_aggregate_bitmask's y with beta = 0. */
 /* CSR-SpMM for dense sampled graphs (long rows, e.g. BASELINE config 5):
  * y (= or +=) diag(s)·A·diag(s)·z for the 0/1 matrix A given as CSR
- * (row_ptr, col: distinct columns per row, any order), F = 16 features — the
+ * (row_ptr, col: distinct columns per row, any order; ascending is the fast
+ * path), F = 16 features — the
  * operator of lds_spmm_norm.  The column-index stream is read once; each
  * 16-row tile's entries become a bit tile in LDS that the int8 matrix cores
  * multiply with the fixed-point digits of s⊙z (lds_aggregate_bitmask's

@@ -463,12 +463,19 @@ __global__ __launch_bounds__(kDnThreads, 1) void csr_dense_agg_kernel(
                 const bool interior = ps.p >= ps.beg && ps.p + kDnStep <= ps.end && ps.p + kDnStep + 4 <= nnz;
                 bool done = false;
                 if (DBG < 2 && interior) {
-                    const uint32_t wf = (uint32_t)c[0] >> 5, wl = (uint32_t)c[7] >> 5;  // columns ascending
-                    if (wl - wf <= 1u) {
-                        const int base = (int)(wf << 5);
-                        uint64_t m = 0;
+                    // the eight columns within the 64 from the first one's word (the
+                    // dense, ascending case): one 64-bit mask, two LDS ORs
+                    const uint32_t wf = (uint32_t)c[0] >> 5;
+                    const int base = (int)(wf << 5);
+                    uint32_t out = 0u;
+                    uint64_t m = 0;
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) m |= 1ull << (c[e] - base);
+                    for (int e = 0; e < 8; ++e) {
+                        const uint32_t r = (uint32_t)(c[e] - base);
+                        out |= r >> 6;  // nonzero: outside [base, base + 64)
+                        m |= 1ull << (r & 63);
+                    }
+                    if (out == 0u) {
                         dn_or(rb + wf, (uint32_t)m);
                         dn_or(rb + wf + 1, (uint32_t)(m >> 32));
                         done = true;

@@ -170,4 +170,38 @@ __device__ __forceinline__ void lds_dma16(const void* p, uint32_t m0) {
 }
 #pragma clang diagnostic pop
 
+// The split-bf16 planes of a factor matrix in the 128-row-tile layout of the
+// direct-staged θ-grad form (thetagrad.hip form 10, include/ldsgnn.h
+// lds_split_planes_t128): value x(i, kk), word s (0 hi, 1 mid, 2 lo) at this
+// uint16 offset (nt = row tiles).
+__host__ __device__ __forceinline__ int64_t t128_plane_at(int64_t i, int kk, int s, int nt) {
+    const int r = (int)(i & 127);
+    const int h = ((kk >> 3) & 1) ^ ((r >> 3) & 1);
+    return ((((int64_t)(kk >> 4) * nt + (i >> 7)) * 3 + s) * 128 + r) * 16 + 8 * h + (kk & 7);
+}
+
+// One (U, V) factor entry: fp32 at row·ld + col (ld > 0), or, with ld = -nt,
+// U / V as the split planes above (uint16) — what the factor producers write
+// when the window's θ-grad runs the direct-staged form.
+__device__ __forceinline__ void put_uv(float* __restrict__ U, float* __restrict__ V, int ld, int row, int col,
+                                       float u, float v) {
+    if (ld > 0) {
+        U[(int64_t)row * ld + col] = u;
+        V[(int64_t)row * ld + col] = v;
+        return;
+    }
+    const int64_t o = t128_plane_at(row, col, 0, -ld);
+    uint16_t* up = reinterpret_cast<uint16_t*>(U);
+    uint16_t* vp = reinterpret_cast<uint16_t*>(V);
+    uint16_t h, m, l;
+    split3_one(u, h, m, l);
+    up[o] = h;
+    up[o + 2048] = m;
+    up[o + 4096] = l;
+    split3_one(v, h, m, l);
+    vp[o] = h;
+    vp[o + 2048] = m;
+    vp[o + 4096] = l;
+}
+
 }  // namespace lds

@@ -300,8 +300,7 @@ __device__ __forceinline__ void emit_factor(float* __restrict__ U, float* __rest
                                             bool assign = false) {
     const float d = gsum16(g * y + z * ag);
     if (lane < width) {
-        U[(int64_t)row * ldk + off + lane] = si * g;
-        V[(int64_t)row * ldk + off + lane] = si * z;
+        put_uv(U, V, ldk, row, off + lane, si * g, si * z);
     }
     if (lane == 0) {
         const float r = -0.5f * si * si * d;
@@ -315,8 +314,7 @@ __device__ __forceinline__ void emit_factor_pre(float* __restrict__ U, float* __
                                                 int lane, float si, float g, float z, float y, float ag) {
     const float d = gsum16(g * y + z * ag);
     if (lane < width) {
-        U[(int64_t)row * ldk + off + lane] = si * g;
-        V[(int64_t)row * ldk + off + lane] = si * z;
+        put_uv(U, V, ldk, row, off + lane, si * g, si * z);
     }
     if (lane == 0) R[row] = rprev + (-0.5f * si * si * d);
 }
@@ -1276,8 +1274,7 @@ __device__ __forceinline__ float emit_uv(float* __restrict__ U, float* __restric
                                          int row, int lane, float si, float g, float z, float y, float ag) {
     const float d = gsum16(g * y + z * ag);
     if (lane < width) {
-        U[(int64_t)row * ldk + off + lane] = si * g;
-        V[(int64_t)row * ldk + off + lane] = si * z;
+        put_uv(U, V, ldk, row, off + lane, si * g, si * z);
     }
     return -0.5f * si * si * d;
 }

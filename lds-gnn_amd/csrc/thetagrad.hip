@@ -1605,11 +1605,6 @@ constexpr int kDmaStageBytes = 12 * kPL2 * 4;                 // 48 KB: U_I, V_I
 constexpr int kDmaLds = kDmaStages * kDmaStageBytes;           // 144 KB
 constexpr int kTileBlk = 3 * kT2 * 16;                         // uint16 per (chunk, row tile) block of one operand
 
-__host__ __device__ __forceinline__ int64_t t128_plane_at(int64_t i, int kk, int s, int nt) {
-    const int r = (int)(i & (kT2 - 1));
-    const int h = ((kk >> 3) & 1) ^ ((r >> 3) & 1);
-    return ((((int64_t)(kk >> 4) * nt + (i >> 7)) * 3 + s) * kT2 + r) * 16 + 8 * h + (kk & 7);
-}
 
 
 template <bool SMALL, bool PART, bool DRAW>
@@ -2036,7 +2031,8 @@ using namespace lds;
 extern "C" int lds_theta_grad(const float* u, const float* v, int ld, int k, const float* r,
                               int ldr, int nr, const float* theta, int n, float* grad,
                               int accumulate, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 9);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
+    if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(grad != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
@@ -2064,7 +2060,8 @@ extern "C" int lds_theta_grad_valu(const float* u, const float* v, int ld, int k
 extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k, const float* r,
                                   int ldr, int nr, float* theta, int n, float* grad,
                                   const void* scalars, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 9);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
+    if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(theta != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
@@ -2080,7 +2077,8 @@ extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
 extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k, const float* r,
                                         int ldr, int nr, float* theta, int n, float* grad,
                                         const void* scalars, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 9);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
+    if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(theta != nullptr && grad != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr >= nr));
@@ -2095,7 +2093,8 @@ extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, 
 extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                                  int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
                                  int mode, const void* scalars, float gscale, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 9);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
+    if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
     LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
@@ -2117,7 +2116,8 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
 extern "C" int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k, const float* r,
                                      int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad, int mode,
                                      const void* scalars, float gscale, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 9);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
+    if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
     LDS_CHECK_ARG(k == 0 || (up != nullptr && vp != nullptr && ld >= k));
     LDS_CHECK_ARG((k & 7) == 0);
@@ -2161,7 +2161,8 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
                                        uint64_t seed, uint32_t tag, const uint32_t* counter_base,
                                        uint32_t counter_offset, int graphs, uint64_t* bits, int words,
                                        int* deg_ws, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 9);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
+    if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(u && v && theta && scalars && bits && deg_ws && n > 0 && k >= 0 && ld >= k);
     // the 128-tile draws store two words per (graph, row): whole 128-column word pairs
     LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && (words & 1) == 0 && words >= 2 * ((n + 127) / 128) && nr >= 0);

@@ -325,6 +325,10 @@ class LdsEngine:
         # (lds_engine_fill_x_linear); the fill is deferred until that launch
         self.fuse_fill = True
         self._pending_fill = None
+        # factor planes for the direct-staged θ-grad (form "bf16x3-direct", and
+        # the by-shape default on Cora-sized grids): see _planes_window
+        self.uv_planes = True
+        self._planes_now = False
         # θ-grad assembly form of this engine's launches (ldsgnn.ops.THETA_GRAD_FORMS
         # name; None: the module default ops.theta_grad_form() at launch time)
         self.theta_form = None
@@ -354,6 +358,11 @@ class LdsEngine:
         self.U = torch.zeros((self.n, self.ldu), dtype=torch.float32, device=self.dev)
         self.V = torch.zeros_like(self.U)
         self.R = torch.zeros((self.S, self.n), dtype=torch.float32, device=self.dev)
+        # the same factors as split-bf16 planes in the direct-staged θ-grad's
+        # 128-row-tile layout (include/ldsgnn.h lds_split_planes_t128), written
+        # by the factor producers instead of U / V in windows that assemble dθ
+        # with lds_theta_grad_direct (_planes_window); allocated on first use
+        self.Up = self.Vp = None
         self._make_batches()
 
     # rows expected to have more than this many entries get a block of their own
@@ -773,24 +782,24 @@ class LdsEngine:
         g = sl.g
         if outer_factors:
             base = self.t * self.kg
-            U, V, R = nat.ptr(self.U), nat.ptr(self.V), self._r_of(self.t)
+            (U, V, ldu), R = self._uv(), self._r_of(self.t)
         else:
-            base, U, V, R = 0, 0, 0, 0
+            base, U, V, R, ldu = 0, 0, 0, 0, self.ldu
         rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
         if self.two_hop and (mask_bit == 1 or self.two_hop_outer):
             nat.call("lds_engine_fwd2_bwd2", rp, cl, s, el, n, nat.ptr(self.nflag), mask_bit, nat.ptr(sl.h2),
                      nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), inv_count,
                      nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, nat.ptr(sl.y0), nat.ptr(sl.dh2), nat.ptr(sl.dy0),
                      nat.ptr(w1), self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep,
-                     self.scale, U, V, self.ldu, R, base + HID, self.cw, 1, nat.ptr(sl.dmask), self.bt2, st)
+                     self.scale, U, V, ldu, R, base + HID, self.cw, 1, nat.ptr(sl.dmask), self.bt2, st)
         else:
             nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
                      nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
-                     self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, self.ldu, R, base + HID, self.cw,
+                     self.keep, self.scale, nat.ptr(sl.o), nat.ptr(sl.h2), U, V, ldu, R, base + HID, self.cw,
                      1, nat.ptr(sl.dmask), self._agg(g, sl.d_o), self.bt, st)
         # dH0 + first stage of gW1 = dH2ᵀ H1d, gb0 = Σ dH0, gb1 = Σ dH2, loss / correct
         nat.call("lds_engine_bwd1_reduce", rp, cl, s, el, n, nat.ptr(sl.dy0), nat.ptr(sl.dh0), nat.ptr(sl.y0),
-                 nat.ptr(sl.h0), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
+                 nat.ptr(sl.h0), U, V, ldu, R, base, nat.ptr(sl.dh2), nat.ptr(sl.h1d), nat.ptr(sl.lossrow),
                  nat.ptr(sl.corrrow), c, nat.ptr(self.partials), self._agg(g, sl.dy0), self.bt, st)
         first = 1 if adam_mode == 2 else 0
         adam = self._adam_args(adam_mode, adam_t, first)
@@ -870,6 +879,36 @@ class LdsEngine:
             self._prefetched = False
             self._ws_clean = False
 
+    def _planes_window(self, T: int, grad_reducer) -> bool:
+        """This hyper step assembles dθ with the direct-staged form
+        (lds_theta_grad_direct: the factor producers write split-bf16 planes,
+        the θ-grad kernel stages them by direct global -> LDS loads): one
+        sample, a full window (its columns are the same every window, so no
+        stale plane columns), dθ fused with SGD (no exchange, no model outer
+        step, no per-draw θ), and the form "bf16x3-direct" or the by-shape
+        default where the 128-tile grid is at most one tile per CU (Cora-sized
+        graphs; MI355X: 55.0 vs 62.4 µs with the next window's draw,
+        profiles/r03_theta_direct_forms.jsonl).  Same result bits as the
+        fp32-operand forms."""
+        form = self._form_name()
+        if not self.uv_planes or self.S != 1 or T != self.tau or grad_reducer is not None:
+            return False
+        if self.outer_update is not None or self.theta_fn is not None or self.split_theta_grad:
+            return False
+        nb = (self.n + 127) // 128
+        return form == "bf16x3-direct" or (form == "bf16x3" and nb * (nb + 1) // 2 <= 256)
+
+    def _uv(self):
+        """(U, V, ld) of the factor producers' launches: fp32 rows (ld > 0) or,
+        in a planes window, the split planes (ld = -row tiles)."""
+        if self._planes_now:
+            if self.Up is None:
+                ne = int(nat.lib.lds_planes_t128_elems(self.n, self.ktot))
+                self.Up = torch.zeros(ne, dtype=torch.int16, device=self.dev)
+                self.Vp = torch.zeros(ne, dtype=torch.int16, device=self.dev)
+            return nat.ptr(self.Up), nat.ptr(self.Vp), -((self.n + 127) // 128)
+        return nat.ptr(self.U), nat.ptr(self.V), self.ldu
+
     def _prefetch_ok(self, T: int, k0: int, exchange: bool = False, check_flag: bool = True) -> bool:
         """The next window's draw can ride in this hyper step: plain LDS θ, a
         full window; with an exchange (dθ all-reduced before the SGD step) in
@@ -885,6 +924,8 @@ class LdsEngine:
             return not self.bitmask_agg
         if self.S != 1 or self._form_name() == "fp32":
             return False
+        if self._planes_now:
+            return True
         return self.ldk % 4 == 0 and k0 % 8 == 0 and nat.ptr(self.U) % 16 == 0 and nat.ptr(self.V) % 16 == 0
 
     def inner_step(self, presampled: bool = False):
@@ -937,6 +978,7 @@ class LdsEngine:
         T = self.t
         if T * self.kg + HID + self.cw > self.ldk:
             self._alloc_factors()
+        self._planes_now = self._planes_window(T, grad_reducer)
         out = self.outer
         self._flush_fill()
         self._join_draw()
@@ -978,6 +1020,17 @@ class LdsEngine:
             if split:
                 nat.call("lds_theta_grad_sgd_accum", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0,
                          nat.ptr(self.R), 1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad), nat.ptr(self.scalars), self._form(), st)
+            elif self._planes_now:  # direct-staged form on the planes; + the next window's draw when prefetching
+                graphs, bits, deg = 0, 0, 0
+                if presampled and self._prefetch_ok(T, k0):
+                    if self._deg_next is None:
+                        self._deg_next = torch.zeros_like(self.gbatch.deg)
+                    graphs, bits, deg = self.gbatch.count, nat.ptr(self.gbatch.bits), nat.ptr(self._deg_next)
+                    drew = True
+                nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1, 1,
+                         nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0, 2,
+                         nat.ptr(self.scalars), 1.0, self.seed, self.tag_graph, nat.ptr(self.scalars),
+                         self.pending_graph, graphs, bits, self.words, deg, st)
             elif presampled and self._prefetch_ok(T, k0):  # + the next window's draw, from the θ written here
                 if self._deg_next is None:
                     self._deg_next = torch.zeros_like(self.gbatch.deg)
@@ -1007,6 +1060,7 @@ class LdsEngine:
                  self.bt, st)
         self._prefetched = drew
         self._ws_clean = not drew
+        self._planes_now = False
         self.pending_graph = 0
         self.pending_fwd = 0
         self.t = 0
@@ -1161,7 +1215,7 @@ class LdsEngine:
         _, _, w1, _ = self._views(self.w[t])
         base = t * self.kg
         rp, cl, s, el = nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell)
-        U, V, R = nat.ptr(self.U), nat.ptr(self.V), self._r_of(t)
+        (U, V, ldu), R = self._uv(), self._r_of(t)
         tr = self.train_flag
         xcsr, xcsc = self._xvals(sl)  # Xd of step t (no redraw: train = 0 below)
         nat.call("lds_engine_x_linear", nat.ptr(self.xrp), nat.ptr(self.xcol), nat.ptr(xcsr), n,
@@ -1171,25 +1225,25 @@ class LdsEngine:
         nat.call("lds_engine_rev_a", rp, cl, s, el, n, nat.ptr(self.dh0bar), nat.ptr(sl.dy0), nat.ptr(sl.dh0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.dh2), nat.ptr(w1), nat.ptr(gw1), nat.ptr(gb1), c,
                  nat.ptr(self.dh1dbar), nat.ptr(self.dh2bar), nat.ptr(self.h1dbar), self.seed, self.tag_h,
-                 nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, self.ldu, R,
+                 nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V, ldu, R,
                  base + HID + 2 * self.cw, nat.ptr(sl.dmask), self._agg(g, self.dh0bar), self.bt, st)
         if self.two_hop:  # dŌ, Ōbar on the train rows only, H2bar from them: one launch
             nat.call("lds_engine_rev_bc", rp, cl, s, el, n, nat.ptr(self.nflag), 1, nat.ptr(self.dh2bar),
                      nat.ptr(sl.d_o), nat.ptr(sl.dh2), nat.ptr(sl.p), nat.ptr(sl.h2), nat.ptr(sl.o), self.inv_train, c,
                      nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), nat.ptr(self.h2bar), nat.ptr(self.y0bar),
                      self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
-                     self.ldu, R, base + HID + self.cw, base + HID, self.cw, nat.ptr(sl.dmask), self.bt2, st)
+                     ldu, R, base + HID + self.cw, base + HID, self.cw, nat.ptr(sl.dmask), self.bt2, st)
         else:
             nat.call("lds_engine_rev_b", rp, cl, s, el, n, nat.ptr(self.dh2bar), nat.ptr(sl.d_o), nat.ptr(sl.dh2),
-                     nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, self.ldu,
+                     nat.ptr(sl.p), nat.ptr(self.train_mask), self.inv_train, c, nat.ptr(self.obar), U, V, ldu,
                      R, base + HID + self.cw, self.cw, self._agg(g, self.dh2bar), self.bt, st)
             nat.call("lds_engine_rev_c", rp, cl, s, el, n, nat.ptr(self.obar), nat.ptr(sl.h2), nat.ptr(sl.o),
                      nat.ptr(self.h1dbar), nat.ptr(sl.y0), nat.ptr(w1), c, nat.ptr(self.h2bar), nat.ptr(self.y0bar),
                      self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, tr, self.keep, self.scale, U, V,
-                     self.ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self._agg(g, self.obar), self.bt, st)
+                     ldu, R, base + HID, self.cw, nat.ptr(sl.dmask), self._agg(g, self.obar), self.bt, st)
         # H0bar + first stage of W̄1 += dH2ᵀ dH1dbar + H2barᵀ H1d;  b̄0 += Σ H0bar;  b̄1 += Σ H2bar
         nat.call("lds_engine_rev_d_reduce", rp, cl, s, el, n, nat.ptr(self.y0bar), nat.ptr(sl.h0), nat.ptr(sl.y0),
-                 nat.ptr(self.h0bar), U, V, self.ldu, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
+                 nat.ptr(self.h0bar), U, V, ldu, R, base, nat.ptr(sl.dh2), nat.ptr(self.dh1dbar),
                  nat.ptr(self.h2bar), nat.ptr(sl.h1d), c, nat.ptr(self.partials), self._agg(g, self.y0bar), self.bt,
                  st)
         if t == 0:  # W̄ of the window's first weights feeds nothing (only θ is trained): no W0 products
@@ -1215,7 +1269,7 @@ class LdsEngine:
         # offsets, Adam-table length, the θ-grad form, whether dθ is written,
         # and the buffer layout (last)
         key = (kind, self.t, self.pending_graph, self.pending_fwd, self.train_flag, self._tab_count(),
-               self._form_name(), self.keep_grad, self._layout_version)
+               self._form_name(), self.keep_grad, self.uv_planes, self._layout_version)
         cache = self._step_graphs
         stale = [k for k in cache if k[-1] != self._layout_version]
         for k in stale:  # captures over re-laid buffers never replay again: free their pools

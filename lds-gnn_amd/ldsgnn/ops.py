@@ -426,7 +426,7 @@ def theta_grad(u: torch.Tensor, v: torch.Tensor, r: torch.Tensor, n: int,
 
 THETA_GRAD_FORMS = {"fp32": 0, "bf16x3": 1, "bf16x3-t64k16": 2, "bf16x3-t64k32": 3, "bf16x3-t128": 4,
                     "bf16x3-t128-grouped": 5, "bf16x3-t64k16-grouped": 6, "bf16x3-t128-grouped-i64": 7,
-                    "bf16x3-t128-pipe": 8, "bf16x3-t128-w8": 9}
+                    "bf16x3-t128-pipe": 8, "bf16x3-t128-w8": 9, "bf16x3-direct": 10}
 
 
 _theta_form = "bf16x3"
@@ -439,7 +439,10 @@ def theta_grad_form(form: Optional[str] = None) -> str:
     fp32 operands split into three bf16 words, six bf16 MFMAs per product,
     fp32 accuracy; tile shape chosen by problem size), one pinned split-bf16
     variant (64-tiles with 16- or 32-wide k chunks, 128-tiles in plain or
-    XCD-grouped order, the pipelined 128-tiles), or "fp32" (fp32-in MFMA).
+    XCD-grouped order, the pipelined 128-tiles), "bf16x3-direct" (the
+    direct-staged eight-wave 128-tile on pre-split planes: an LdsEngine then
+    has its factor producers write the planes; entry points on fp32 operands
+    run the by-shape form), or "fp32" (fp32-in MFMA).
     Returns the previous default.  An LdsEngine with its own `theta_form`
     ignores this default; HIP graphs keep the form they were captured with."""
     global _theta_form

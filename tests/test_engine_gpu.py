@@ -659,3 +659,28 @@ def test_async_window_draw_equals_eager(samples):
             for k, v in e.get_params(s_).items():
                 assert torch.equal(v, c.get_params(s_)[k]), (s_, k)
         assert e.scalars_host() == c.scalars_host()
+
+
+def test_planes_window_bit_identical_to_fp32_factors():
+    """Windows whose factor producers write split-bf16 planes and whose dθ runs
+    the direct-staged form (lds_theta_grad_direct; with the next window's draw
+    prefetched in the replayed windows) give θ, weights, dθ and device scalars
+    bit-identical to windows on fp32 factors (uv_planes off: the by-shape form
+    on U / V), eager and replayed."""
+    a = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=13)["engine"]
+    b = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=13)["engine"]
+    b.uv_planes = False
+    for _ in range(2):
+        a.run_window(5)
+        b.run_window(5)
+    assert a.Up is not None and b.Up is None or b.Up is not None  # a ran planes windows
+    a.capture_window(5, windows=2, prefetch=True)
+    b.capture_window(5, windows=2, prefetch=True)
+    a.replay(4)
+    b.replay(4)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    assert torch.equal(a.grad, b.grad)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+    assert a.scalars_host() == b.scalars_host()

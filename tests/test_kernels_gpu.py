@@ -574,7 +574,7 @@ def test_theta_grad_form_default_and_errors(device):
     u = torch.zeros((16, 8), device=device)
     g = torch.zeros(16 * 17 // 2, device=device)
     with pytest.raises(nat.NativeError):
-        nat.call("lds_theta_grad", nat.ptr(u), nat.ptr(u), 8, 8, 0, 0, 0, 0, 16, nat.ptr(g), 0, 10,
+        nat.call("lds_theta_grad", nat.ptr(u), nat.ptr(u), 8, 8, 0, 0, 0, 0, 16, nat.ptr(g), 0, 11,
                  nat.stream_of(torch.device(device)))
 
 
@@ -819,6 +819,14 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     for i in (3, 900):  # reverse two rows' column order
         b, e = int(rp[i]), int(rp[i + 1])
         col[b:e] = col[b:e].flip(0)
+    for i in (11, 1200):  # shuffle two rows (groups of eight whose ends lie close but whose middles do not)
+        b, e = int(rp[i]), int(rp[i + 1])
+        col[b:e] = col[b:e][torch.randperm(e - b, generator=g)]
+    b = int(rp[40])  # one group: ends ascending and one word apart, a middle entry far away
+    seg = col[b:b + 8].clone()
+    far = int(col[int(rp[41]) - 1])
+    col[b + 3] = far
+    col[int(rp[41]) - 1] = seg[3]
     s = torch.rand(n, generator=g) + 0.5
     z = torch.randn(n, 16, generator=g)
     y = _spmm_dense(rp.int().to(device), col.to(device), s.to(device), n, z.to(device)).cpu().double()

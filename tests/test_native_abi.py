@@ -78,7 +78,7 @@ def test_theta_grad_form_is_a_per_call_argument():
         ops.theta_grad_form("bf16x4")
     # a valid call shape with form 10: hipErrorInvalidValue from the form check
     fake = 1 << 20  # never dereferenced: the argument checks run first
-    assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, 10, None) == 1
+    assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, 11, None) == 1
     assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, -1, None) == 1
 
 

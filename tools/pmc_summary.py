@@ -29,6 +29,7 @@ ENTRY_KERNELS = {
     "lds_theta_grad_sgd": ["theta_grad_bf3_kernel<16, true, false, true, false>", "theta_grad_bf3_t128",
                            "theta_grad_bf3_pipe", "theta_grad_mfma", "theta_grad_w8_kernel<true, false, false>",
                            "theta_grad_w8_kernel<false, false, false>"],
+    "lds_theta_grad_direct": ["theta_grad_dma_kernel"],
     "lds_theta_grad_sgd_draw": ["theta_grad_bf3_kernel<16, true, false, true, true>",
                                 "theta_grad_w8_kernel<true, false, true>", "theta_grad_w8_kernel<false, false, true>",
                                 "theta_grad_bf3_t128_kernel<true, true, false, true>",
