@@ -262,7 +262,11 @@ def window_breakdown(eng, reducer, args, device, k=20):
     real = nat.call
 
     def rec(name, *a):
-        calls.append((name, a))
+        # with the window's degree counts as this call found them: chains of a
+        # drawing launch (the θ-grad epilogue, spread draws appended to
+        # lds_engine_fwd_layer1) accumulate into them, and a later chain must
+        # not fill from inflated counts
+        calls.append((name, a, eng.gbatch.deg.clone()))
         real(name, *a)
 
     nat.call = rec
@@ -272,9 +276,10 @@ def window_breakdown(eng, reducer, args, device, k=20):
         nat.call = real
     torch.cuda.synchronize()
     per = {}
-    for name, a in calls:
+    for name, a, deg in calls:
         if name == "lds_sample_graphs_multi":  # repeated draws clear their own workspace (ws_zeroed = 0)
             a = a[:-2] + (0,) + a[-1:]
+        eng.gbatch.deg.copy_(deg)
         us = chain_us(lambda st, name=name, a=a: real(name, *(a[:-1] + (st,))), device, k)
         per.setdefault(name, []).append(us)
     rows = []

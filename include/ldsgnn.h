@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 10
+#define LDS_ABI_VERSION 11
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -440,6 +440,35 @@ int lds_engine_scalars_size(void);
  *   uv  : factor COLUMN offset per sample (U, V are n × (samples·ldk); the
  *         ldk argument is then the row stride samples·ldk)
  *   part: reduction partials   met: metrics rows (2 floats) */
+/* Side work of an engine launch (ABI 11): blocks appended to the grid of
+ * lds_engine_fwd_layer1 / lds_engine_fwd2_bwd2 (single-sample launches) that
+ *   - draw one graph (theta != NULL): bits and degree counts exactly as one
+ *     graph of lds_sample_graphs_multi (counter *counter_base + counter_offset,
+ *     `deg` zero on entry, lds_sample_ws_ints(n) ints), and / or
+ *   - fill one drawn graph (fill_bits != NULL): CSR, s and the ELL head from
+ *     its bits and degree counts, as lds_sample_fill_csr for one graph.
+ * The engine draws graph t + 1 of a window beside inner step t's first
+ * aggregation and fills it beside the second (the replaced reference calls:
+ * the per-step sample(), src/trainers/bilevel.py:105, src/models/sampling.py:68). */
+typedef struct LdsSideWork {
+    const float* theta;
+    uint64_t seed;
+    uint32_t tag;
+    uint32_t counter_offset;
+    const uint32_t* counter_base;
+    uint64_t* bits;
+    int32_t words;
+    int32_t* deg;
+    const uint64_t* fill_bits;
+    const int32_t* fill_deg;
+    int32_t* row_ptr;
+    int32_t* col;
+    int64_t col_capacity;
+    float* s;
+    int32_t* ell;
+    const uint8_t* node_flags;
+} LdsSideWork;
+
 typedef struct LdsBatch {
     int32_t samples;
     uint32_t tag_step;
@@ -459,6 +488,9 @@ typedef struct LdsBatch {
      * Â·Z[i] = s_i · Σ_p agg_p[i] (p in order) — lds_aggregate_bitmask_partials
      * output, its final pass folded into the consumer.  0: agg is Â·Z. */
     int32_t agg_splits;
+    /* ABI 11: side work appended to this launch's grid (NULL: none);
+     * lds_engine_fwd_layer1 and lds_engine_fwd2_bwd2 with samples == 1. */
+    const LdsSideWork* side;
 } LdsBatch;
 
 /* lds_sample_bitmask with the draw counter read from device memory:

@@ -17,6 +17,7 @@
 // replays advance them.
 #include "common.hpp"
 #include "fill.hpp"
+#include "side.hpp"
 #include "../../include/ldsgnn.h"
 
 namespace lds {
@@ -106,6 +107,7 @@ struct Batch {
     const uint8_t* hflag;
     int nh;
     int asplit;             // > 0: `agg` holds asplit partial n × 16 arrays (LdsBatch.agg_splits)
+    SideWork side;          // blocks appended to the grid (LdsBatch.side, side.hpp)
 };
 
 // kB = false (single-sample launch): no offset code at all.
@@ -578,6 +580,8 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
+    if constexpr (!kB && !kAgg)
+        if (side_block(bt.side, n)) return;  // a draw tile of the window's next graph (side.hpp)
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
@@ -1314,6 +1318,8 @@ __global__ __launch_bounds__(256) void fwd2_bwd2_kernel(
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth, int r_assign,
     const float* __restrict__ dmask, Batch bt) {
+    if constexpr (!kB)
+        if (side_block(bt.side, n)) return;  // a fill block of the window's next graph (side.hpp)
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;
     rp = boff<kB>(rp, bt.rp);
@@ -2149,6 +2155,20 @@ static inline int mk_batch(const LdsBatch* b, Batch& bt) {
     bt.xval = b->xval; bt.xd = b->xd; bt.uv = b->uv; bt.part = b->part; bt.met = b->met; bt.tag = b->tag_step;
     return b->samples;
 }
+// Side work of a launch (LdsBatch.side, side.hpp) into bt.side; returns the
+// blocks to append to grid.x, or -1 if the launch cannot carry it (batched
+// samples, the precomputed-aggregation variant, incomplete pointers).
+static inline int side_blocks(const LdsBatch* b, int n, int ns, bool plain, Batch& bt) {
+    if (b == nullptr || b->side == nullptr) return 0;
+    const LdsSideWork* h = b->side;
+    if (ns != 1 || !plain || h->words < (n + 63) / 64 || n > kEllIndex + 1) return -1;
+    if (h->theta != nullptr && (h->bits == nullptr || h->deg == nullptr)) return -1;
+    if (h->fill_bits != nullptr &&
+        (h->fill_deg == nullptr || h->row_ptr == nullptr || h->col == nullptr || h->s == nullptr || h->col_capacity <= 0))
+        return -1;
+    bt.side = side_of(h, n);
+    return bt.side.draw_blocks + bt.side.fill_blocks;
+}
 static inline int plan_heavy(const LdsBatch* b) {
     return b != nullptr && b->n_heavy > 0 && b->heavy_rows && b->heavy_flag ? b->n_heavy : 0;
 }
@@ -2244,7 +2264,9 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, b1};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp,
+    const int extra = side_blocks(batch, n, ns, agg == nullptr, bt);
+    LDS_CHECK_ARG(extra >= 0);
+    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch) + extra, ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -2416,7 +2438,9 @@ extern "C" int lds_engine_fwd2_bwd2(const int* rp, const int* col, const float* 
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_LAUNCH_B(fwd2_bwd2_kernel, ns, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0,
+    const int extra = side_blocks(batch, n, ns, true, bt);
+    LDS_CHECK_ARG(extra >= 0);
+    LDS_LAUNCH_B(fwd2_bwd2_kernel, ns, dim3(wave_blocks(n) + plan_heavy(batch) + extra, ns), dim3(256), 0,
                  (hipStream_t)stream, rp, col, s, (const int2*)ell, n, node_flags, mask_bit, h2, o, p, d_o, label,
                  inv_count, lossrow, corrrow, c, y0, dh2, dy0, w, mk_keys(seed, 0, tag_h),
                  (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff, fwidth, r_assign,

@@ -103,6 +103,11 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
     // the row's own operands first (independent of the block prefix)
     const int deg = live ? dacc[row] : 0;
     const uint64_t word0 = (live && h < nbw) ? rb_bits[h] : 0ull;
+    // head entries past the row's drawn count read as the row itself: a degree
+    // workspace that was not zero on entry (deg above the bits' count) then
+    // yields wrong weights, never an index outside the graph
+#pragma unroll
+    for (int m = 0; m < 4; ++m) head[k][h + 16 * m] = live ? row : 0;
     if (wave == 0 && lane < 16) {
         const int d = row0 + lane < n ? dacc[row0 + lane] : 0;
         dblk[lane] = row16_incl_scan_int(d) - d;

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -244,7 +244,18 @@ class LdsBatch(ctypes.Structure):
     _fields_ = [("samples", ctypes.c_int32), ("tag_step", ctypes.c_uint32)] + [
         (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")] + [
         ("heavy_rows", ctypes.c_void_p), ("heavy_flag", ctypes.c_void_p), ("n_heavy", ctypes.c_int32),
-        ("agg_splits", ctypes.c_int32)]
+        ("agg_splits", ctypes.c_int32), ("side", ctypes.c_void_p)]
+
+
+class LdsSideWork(ctypes.Structure):
+    """include/ldsgnn.h LdsSideWork: a graph draw and / or fill carried by
+    extra blocks of a single-sample fwd_layer1 / fwd2_bwd2 launch."""
+    _fields_ = [("theta", ctypes.c_void_p), ("seed", ctypes.c_uint64), ("tag", ctypes.c_uint32),
+                ("counter_offset", ctypes.c_uint32), ("counter_base", ctypes.c_void_p), ("bits", ctypes.c_void_p),
+                ("words", ctypes.c_int32), ("deg", ctypes.c_void_p), ("fill_bits", ctypes.c_void_p),
+                ("fill_deg", ctypes.c_void_p), ("row_ptr", ctypes.c_void_p), ("col", ctypes.c_void_p),
+                ("col_capacity", ctypes.c_int64), ("s", ctypes.c_void_p), ("ell", ctypes.c_void_p),
+                ("node_flags", ctypes.c_void_p)]
 
 
 def batch_ptr(b) -> int:

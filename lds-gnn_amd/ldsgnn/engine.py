@@ -35,10 +35,12 @@ S = 1 is the reference's single chain.
 """
 from __future__ import annotations
 
+import ctypes
 from collections import OrderedDict
 from typing import List, Optional
 
 import numpy as np
+
 import torch
 
 from . import _native as nat
@@ -255,6 +257,16 @@ class LdsEngine:
         self.prefetch_draw = False
         self._prefetched = False
         self._deg_next = None
+        # spread draws (with prefetch): the hyper step draws only graph 0 of
+        # the next window; inner step t draws graph t + 1 in blocks appended
+        # to its first aggregation and fills it beside its second
+        # (LdsSideWork, include/ldsgnn.h).  Off by default: on MI355X (Cora,
+        # τ = 5) the θ-grad entry drops 57.7 -> 42.3 µs but each appended
+        # draw re-reads θ and lengthens fwd_layer1 by 5.3 µs (4.2 -> 9.4),
+        # 13.48k vs 14.10k steps/s (profiles/r03_spread_draw.json)
+        self.spread_draw = False
+        self._prefetched_spread = False  # the prefetched state holds graph 0 only
+        self._spread_window = False  # this window's graphs 1..τ come from side work
 
         # tape
         self.tau = max(1, int(tau))
@@ -436,6 +448,38 @@ class LdsEngine:
         self.bt = nat.batch_ptr(self._bt)
         self.btx = nat.batch_ptr(self._btx)
         self.bt2 = nat.batch_ptr(self._bt2)
+        self._side_bt = {}  # inner step -> (fwd_layer1 batch, fwd2_bwd2 batch) with side work
+
+    def _side_batches(self, t: int):
+        """LdsBatch copies for inner step t of a spread window: the first
+        aggregation draws graph t + 1 (counter pending + t + 1, the counter
+        the window's batched draw gives it), the second fills its CSR / s /
+        ELL head.  Kept alive on self (the launches read them on the host)."""
+        hit = self._side_bt.get(t)
+        if hit is not None:
+            return hit
+        gb, P, g = self.gbatch, nat.ptr, t + 1
+
+        def at(x: torch.Tensor) -> int:
+            return P(x) + g * x[0].numel() * x.element_size()
+        draw = nat.LdsSideWork(theta=P(self.theta), seed=self.seed, tag=self.tag_graph, counter_offset=g,
+                               counter_base=P(self.scalars), bits=at(gb.bits), words=self.words, deg=at(gb.deg))
+        fill = nat.LdsSideWork(words=self.words, fill_bits=at(gb.bits), fill_deg=at(gb.deg), row_ptr=at(gb.row_ptr),
+                               col=at(gb.col), col_capacity=max(self.cap, 1), s=at(gb.s), ell=at(gb.ell),
+                               node_flags=P(self.nflag))
+        b1 = nat.LdsBatch.from_buffer_copy(self._bt)
+        b2 = nat.LdsBatch.from_buffer_copy(self._bt2)
+        b1.side, b2.side = ctypes.addressof(draw), ctypes.addressof(fill)
+        hit = self._side_bt[t] = (b1, b2, draw, fill, nat.batch_ptr(b1), nat.batch_ptr(b2))
+        return hit
+
+    def _spread_ok(self, T: int, grad_reducer=None) -> bool:
+        """Spread draws apply: one sample, the two-hop kernels (inner steps
+        end in lds_engine_fwd2_bwd2), short rows (the plain aggregation
+        launches carry the side blocks), one θ, a full window, no exchange."""
+        return (self.spread_draw and self.S == 1 and self.two_hop and not self.long_rows and self.theta_fn is None
+                and self.outer_update is None and grad_reducer is None and T == self.tau
+                and self.gbatch.count == self.tau + 1)
 
     def _grow(self, slots: int):
         self._layout_version += 1
@@ -659,7 +703,7 @@ class LdsEngine:
         return nat.ptr(self.agg)
 
     def _forward(self, sl: _Slot, w: torch.Tensor, mask, inv_count, train: int, fwd_off: int, bt=None,
-                 loss_in_backward: bool = False):
+                 loss_in_backward: bool = False, bt_l1=None):
         """X-linear, layer 1 and (unless loss_in_backward: the two-hop
         backward computes it) the loss layer."""
         st, n, c = self._stream(), self.n, self.c
@@ -682,7 +726,7 @@ class LdsEngine:
         nat.call("lds_engine_fwd_layer1", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h0),
                  nat.ptr(sl.y0), nat.ptr(sl.h1d), nat.ptr(sl.h2), nat.ptr(w1), nat.ptr(b1), c, self.seed,
                  self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep, self.scale, nat.ptr(sl.dmask),
-                 self._agg(g, sl.h0), bt, st)
+                 self._agg(g, sl.h0), bt if bt_l1 is None else bt_l1, st)
         if loss_in_backward and self.two_hop:
             return
         nat.call("lds_engine_fwd_layer2", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), nat.ptr(g.ell), n, nat.ptr(sl.h2),
@@ -771,7 +815,7 @@ class LdsEngine:
 
     def _backward(self, sl: _Slot, w: torch.Tensor, gout: torch.Tensor, train: int, fwd_off: int,
                   metrics_row: torch.Tensor, outer_factors: bool, adam_mode: int, adam_t: int,
-                  mask_bit: int = 0, inv_count: float = 0.0):
+                  mask_bit: int = 0, inv_count: float = 0.0, bt2=None):
         """First-order backward into `gout` (data gradient, no weight decay),
         fused with the Adam forward of inner step adam_t (adam_mode 1) or the
         Adam reverse of inner step adam_t (adam_mode 2, hyper step).  With the
@@ -791,7 +835,8 @@ class LdsEngine:
                      nat.ptr(sl.o), nat.ptr(sl.p), nat.ptr(sl.d_o), nat.ptr(self.label), inv_count,
                      nat.ptr(sl.lossrow), nat.ptr(sl.corrrow), c, nat.ptr(sl.y0), nat.ptr(sl.dh2), nat.ptr(sl.dy0),
                      nat.ptr(w1), self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train, self.keep,
-                     self.scale, U, V, ldu, R, base + HID, self.cw, 1, nat.ptr(sl.dmask), self.bt2, st)
+                     self.scale, U, V, ldu, R, base + HID, self.cw, 1, nat.ptr(sl.dmask),
+                     self.bt2 if bt2 is None else bt2, st)
         else:
             nat.call("lds_engine_bwd_layer2", rp, cl, s, el, n, nat.ptr(sl.d_o), nat.ptr(sl.y0), nat.ptr(sl.dh2),
                      nat.ptr(sl.dy0), nat.ptr(w1), c, self.seed, self.tag_h, nat.ptr(self.scalars), fwd_off, train,
@@ -818,8 +863,12 @@ class LdsEngine:
         path would give it."""
         self._flush_fill()
         gb = self.gbatch
+        self._spread_window = False
         if self._prefetched:  # bits + degrees drawn by the last hyper step (lds_theta_grad_sgd_draw)
-            fill = (nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), count * self.S, nat.ptr(gb.row_ptr),
+            # spread: graph 0 only; the inner steps draw and fill the rest
+            self._spread_window = self._prefetched_spread
+            nfill = 1 if self._prefetched_spread else count * self.S
+            fill = (nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), nfill, nat.ptr(gb.row_ptr),
                     self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell), nat.ptr(self.nflag))
             if self.fuse_fill and self.S == 1 and not self.long_rows:
                 # deferred: the first inner step's X product launches it (lds_engine_fill_x_linear)
@@ -877,6 +926,7 @@ class LdsEngine:
         it then finds); gbatch.deg holds their degrees, so it is cleared first."""
         if self._prefetched:
             self._prefetched = False
+            self._prefetched_spread = False
             self._ws_clean = False
 
     def _planes_window(self, T: int, grad_reducer) -> bool:
@@ -952,10 +1002,11 @@ class LdsEngine:
             self._sample(sl.g)
         fwd_off = self.pending_fwd
         self._fwd_of[t] = fwd_off
+        side = self._side_batches(t) if presampled and self._spread_window else (None,) * 6
         self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off,
-                      loss_in_backward=True)
+                      loss_in_backward=True, bt_l1=side[4])
         self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False, 1, t,
-                       mask_bit=1, inv_count=self.inv_train)
+                       mask_bit=1, inv_count=self.inv_train, bt2=side[5])
         if self.train_flag:
             self.pending_fwd += 1
         self.t = t + 1
@@ -1014,6 +1065,7 @@ class LdsEngine:
             k0 = self.kg  # the last chunk (graph 0) + R on the main stream
         else:
             k0 = T * self.kg + HID + self.cw
+        spread = self._spread_ok(T, grad_reducer)  # the next window draws graphs 1..τ itself
         if self.S > 1:
             drew = self._assemble_samples(k0, grad_reducer, presampled)
         elif grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
@@ -1025,7 +1077,8 @@ class LdsEngine:
                 if presampled and self._prefetch_ok(T, k0):
                     if self._deg_next is None:
                         self._deg_next = torch.zeros_like(self.gbatch.deg)
-                    graphs, bits, deg = self.gbatch.count, nat.ptr(self.gbatch.bits), nat.ptr(self._deg_next)
+                    graphs = 1 if spread else self.gbatch.count
+                    bits, deg = nat.ptr(self.gbatch.bits), nat.ptr(self._deg_next)
                     drew = True
                 nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1, 1,
                          nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0, 2,
@@ -1038,7 +1091,8 @@ class LdsEngine:
                 nat.call("lds_theta_grad_sgd_draw", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R),
                          1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
                          nat.ptr(self.scalars), self.seed, self.tag_graph, nat.ptr(self.scalars), self.pending_graph,
-                         gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next), self._form(), st)
+                         1 if spread else gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next),
+                         self._form(), st)
                 drew = True
             else:
                 nat.call("lds_theta_grad_sgd", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1,
@@ -1059,6 +1113,8 @@ class LdsEngine:
                  self._tab_count(), P(self.gbatch.deg), P(self._deg_next) if drew else 0, self.gbatch.deg.numel(),
                  self.bt, st)
         self._prefetched = drew
+        self._prefetched_spread = drew and spread and self.S == 1 and grad_reducer is None
+        self._spread_window = False
         self._ws_clean = not drew
         self._planes_now = False
         self.pending_graph = 0
@@ -1358,7 +1414,8 @@ class LdsEngine:
         # assume: prefetched draws present, or none and a clean degree buffer
         self.prefetch_draw = bool(prefetch) and \
             self._prefetch_ok(tau, tau * self.kg + HID + self.cw, exchange=grad_reducer is not None, check_flag=False)
-        self._enter_window_state(self.prefetch_draw, tau)
+        spread = self.prefetch_draw and self._spread_ok(tau, grad_reducer)
+        self._enter_window_state(self.prefetch_draw, tau, spread)
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
@@ -1371,7 +1428,7 @@ class LdsEngine:
                             self.run_window(tau)
                 graphs.append((w, nat.seal_graph(graph, f"{w}-window group")))
             torch.cuda.current_stream(self.dev).wait_stream(s)
-            self._graph_capture = (tuple(graphs), tau, None, self.prefetch_draw)
+            self._graph_capture = (tuple(graphs), tau, None, self.prefetch_draw, spread)
             return graphs[0][1]
         head, tail = nat.new_graph(), nat.new_graph()
         pool = torch.cuda.graph_pool_handle()
@@ -1389,33 +1446,46 @@ class LdsEngine:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         nat.seal_graph(head, "window (to the exchange)")
         nat.seal_graph(tail, "window (after the exchange)")
-        self._graph_capture = ((head, tail), tau, grad_reducer, self.prefetch_draw)
+        self._graph_capture = ((head, tail), tau, grad_reducer, self.prefetch_draw, spread)
         return head, tail
 
-    def _enter_window_state(self, prefetched: bool, tau: int) -> None:
+    def _enter_window_state(self, prefetched: bool, tau: int, spread: bool = False) -> None:
         """Bring the device to the window-start state a captured window
         assumes: with prefetch, the window's τ+1 graphs already drawn (bits +
         degrees; drawn here, eagerly, if a discard, an out-of-window draw or a
-        non-prefetching step dropped them); without, no prefetched graphs and
-        a zeroed degree workspace (the captured draw accumulates into it)."""
+        non-prefetching step dropped them) — with spread draws graph 0 only
+        and zero degrees for graphs 1..τ (their side draws accumulate into
+        them); without, no prefetched graphs and a zeroed degree workspace
+        (the captured draw accumulates into it)."""
         if prefetched:
-            if not self._prefetched:
-                if self._deg_next is None:
-                    self._deg_next = torch.zeros_like(self.gbatch.deg)
-                self._sample_batch(tau + 1)  # bits + degrees of this window's graphs
+            if self._deg_next is None:
+                self._deg_next = torch.zeros_like(self.gbatch.deg)
+            if not self._prefetched or self._prefetched_spread != spread:
+                self._flush_fill()
                 self._join_draw()
+                self.gbatch.deg.zero_()
+                self._prefetched = False
+                self._ws_clean = True
+                if spread:
+                    self._draw_range(0, 1, self._stream())  # bits + degrees (+ CSR) of graph 0
+                else:
+                    self._sample_batch(tau + 1)  # bits + degrees of this window's graphs
+                    self._join_draw()
                 self._prefetched = True
+                self._prefetched_spread = spread
+                self._ws_clean = False
         else:
             if self._prefetched or not self._ws_clean:
                 self.gbatch.deg.zero_()
             self._prefetched = False
+            self._prefetched_spread = False
             self._ws_clean = True
 
     def replay(self, windows: int = 1):
-        graphs, tau, reducer, prefetched = self._graph_capture
+        graphs, tau, reducer, prefetched, spread = self._graph_capture
         self._flush_fill()
         self._join_draw()  # an eager split draw still running on the side stream
-        self._enter_window_state(prefetched, tau)
+        self._enter_window_state(prefetched, tau, spread)
         if reducer is None:
             (_, one), (group, multi) = graphs[0], graphs[-1]
             for _ in range(windows // group):
