@@ -79,24 +79,53 @@ Ws carve(void* ws, int n) {
 }  // namespace
 
 // Per-block column maxima of |s_k z_kf| (non-negative floats compare as
-// their bit patterns).  grid = kMaxBlocks, 256 threads = 16 rows × 16 features.
-__global__ __launch_bounds__(256) void bitagg_colmax_kernel(const float* __restrict__ s, int n,
-                                                            const float* __restrict__ z, int ldz,
-                                                            uint32_t* __restrict__ colmax) {
-    const int f = threadIdx.x & 15;
-    uint32_t m = 0;
-#pragma unroll 4
-    for (int k = blockIdx.x * 16 + (threadIdx.x >> 4); k < n; k += kMaxBlocks * 16)
-        m = max(m, __float_as_uint(fabsf(s[k] * z[(int64_t)k * ldz + f])));
-    // 4 rows per wave share a feature: lanes f, f+16, f+32, f+48
-    m = max(m, (uint32_t)__shfl_xor((int)m, 16));
-    m = max(m, (uint32_t)__shfl_xor((int)m, 32));
-    __shared__ uint32_t red[4][16];
-    if ((threadIdx.x & 63) < 16) red[threadIdx.x >> 6][f] = m;
+// their bit patterns), kColBlocks partials.  1024 threads = 256 rows × four
+// feature quads per pass (one float4 of Z per thread when Z is 16-byte
+// aligned), so at N = 20 000 every thread has its loads in flight at once:
+// one round trip, where 256 blocks of 16 rows × 16 features took five.  The
+// launch itself did not get faster (4.93 vs 4.95 µs at N = 20 000: the floor
+// of a dependent launch there), but a quarter of the partials makes the
+// readers' reductions (colmax_of) one round of loads.  The maximum is
+// order-independent: the same values as any other partition.
+constexpr int kColBlocks = 64;    // column-max partials written (of the kMaxBlocks slots)
+template <bool kVec>
+__global__ __launch_bounds__(1024) void bitagg_colmax_kernel(const float* __restrict__ s, int n,
+                                                             const float* __restrict__ z, int ldz,
+                                                             uint32_t* __restrict__ colmax) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int fq = t & 3;  // features 4fq .. 4fq + 3
+    uint32_t m[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 2
+    for (int k = blockIdx.x * 256 + (t >> 2); k < n; k += kColBlocks * 256) {
+        const float sk = s[k];
+        const float* zr = z + (int64_t)k * ldz + 4 * fq;
+        float v[4];
+        if constexpr (kVec) {
+            const float4 w = *reinterpret_cast<const float4*>(zr);
+            v[0] = w.x, v[1] = w.y, v[2] = w.z, v[3] = w.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = zr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] = max(m[i], __float_as_uint(fabsf(sk * v[i])));
+    }
+    // the 16 lanes of a wave holding quad fq: xor over lane bits 2..5
+#pragma unroll
+    for (int sh = 4; sh < 64; sh <<= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] = max(m[i], (uint32_t)__shfl_xor((int)m[i], sh));
+    __shared__ uint32_t red[16][kF];
+    if (lane < 4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wave][4 * lane + i] = m[i];
     __syncthreads();
-    if (threadIdx.x < 16)
-        colmax[blockIdx.x * kF + threadIdx.x] =
-            max(max(red[0][threadIdx.x], red[1][threadIdx.x]), max(red[2][threadIdx.x], red[3][threadIdx.x]));
+    if (t < kF) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) r = max(r, red[w][t]);
+        colmax[blockIdx.x * kF + t] = r;
+    }
 }
 
 __device__ __forceinline__ int col_exponent(uint32_t maxbits) {
@@ -107,57 +136,67 @@ __device__ __forceinline__ int col_exponent(uint32_t maxbits) {
     return 30 - E;
 }
 
-// max over the kMaxBlocks partials of feature lane & 15 (lanes f, f+16,
+// max over the kColBlocks partials of feature lane & 15 (lanes f, f+16,
 // f+32, f+48 all end with feature f's value)
 __device__ __forceinline__ uint32_t colmax_of(const uint32_t* __restrict__ colmax, int lane) {
     const int f = lane & 15;
     uint32_t m = 0;
-    for (int b = lane >> 4; b < kMaxBlocks; b += 4) m = max(m, colmax[b * kF + f]);
+#pragma unroll
+    for (int b = lane >> 4; b < kColBlocks; b += 4) m = max(m, colmax[b * kF + f]);
     m = max(m, (uint32_t)__shfl_xor((int)m, 16));
     m = max(m, (uint32_t)__shfl_xor((int)m, 32));
     return m;
 }
 
 // Fixed-point digits of s⊙Z in the chunk layout [chunk][q][limb][g][f][16 B]:
-// one thread per lane fragment (chunk c, k-step q, lane group g, feature f)
-// = 16 columns, written as one 16-byte store per limb.  Columns past n are 0.
+// one thread per dword of a lane fragment (chunk c, k-step q, lane group g,
+// feature f, dword dd) = 4 columns, one 4-byte store per limb (a wave's 64
+// threads: one 256-byte run per limb).  The thread's s·z products are loaded
+// before the column maxima are reduced (every thread of the block reads a
+// quarter of the partials), so the block pays one round trip, not three.
+// Columns past n are 0.
 __global__ __launch_bounds__(256) void bitagg_quant_kernel(const float* __restrict__ s, int n,
                                                            const float* __restrict__ z, int ldz,
                                                            const uint32_t* __restrict__ colmax,
                                                            int8_t* __restrict__ zq, int chunks) {
+    __shared__ uint32_t red[4][kF];
     __shared__ int e_sh[kF];
-    if (threadIdx.x < 64) {
-        const uint32_t m = colmax_of(colmax, threadIdx.x);
-        if (threadIdx.x < kF) e_sh[threadIdx.x] = col_exponent(m);
+    const int t = threadIdx.x, lane = t & 63;
+    const int idx = blockIdx.x * 256 + t;   // (((c·8 + q)·4 + g)·16 + f)·4 + dd
+    const bool live = idx < chunks * kSteps * 4 * kF * 4;
+    const int dd = idx & 3, f = (idx >> 2) & 15, g = (idx >> 6) & 3, q = (idx >> 8) & 7, c = idx >> 11;
+    const int kb = c * kChunk + 128 * g + 32 * (q >> 1) + 4 * (q & 1) + dd;
+    float tv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int k = kb + 8 * b;
+        tv[b] = (live && k < n) ? s[k] * z[(int64_t)k * ldz + f] : 0.f;
     }
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = t >> 4; b < kColBlocks; b += 16) m = max(m, colmax[b * kF + (t & 15)]);
+    m = max(m, (uint32_t)__shfl_xor((int)m, 16));
+    m = max(m, (uint32_t)__shfl_xor((int)m, 32));
+    if (lane < kF) red[t >> 6][lane] = m;
     __syncthreads();
-    const int idx = blockIdx.x * 256 + threadIdx.x;   // ((c·8 + q)·4 + g)·16 + f
-    if (idx >= chunks * kSteps * 4 * kF) return;
-    const int f = idx & 15, g = (idx >> 4) & 3, q = (idx >> 6) & 7, c = idx >> 9;
+    if (t < kF) e_sh[t] = col_exponent(max(max(red[0][t], red[1][t]), max(red[2][t], red[3][t])));
+    __syncthreads();
+    if (!live) return;
     const int e = e_sh[f];
-    const int kb = c * kChunk + 128 * g + 32 * (q >> 1) + 4 * (q & 1);
-    uint32_t out[kLimbs][4];
+    uint32_t out[kLimbs] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int dd = 0; dd < 4; ++dd) {
+    for (int b = 0; b < 4; ++b) {
+        int v = kb + 8 * b < n ? (int)rintf(ldexpf(tv[b], e)) : 0;
 #pragma unroll
-        for (int L = 0; L < kLimbs; ++L) out[L][dd] = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int k = kb + dd + 8 * b;
-            int v = 0;
-            if (k < n) v = (int)rintf(ldexpf(s[k] * z[(int64_t)k * ldz + f], e));
-#pragma unroll
-            for (int L = 0; L < kLimbs; ++L) {
-                const int d = ((v + 128) & 255) - 128;   // balanced digit in [-128, 127]
-                out[L][dd] |= (uint32_t)(d & 255) << (8 * b);
-                v = (v - d) >> 8;
-            }
+        for (int L = 0; L < kLimbs; ++L) {
+            const int d = ((v + 128) & 255) - 128;   // balanced digit in [-128, 127]
+            out[L] |= (uint32_t)(d & 255) << (8 * b);
+            v = (v - d) >> 8;
         }
     }
 #pragma unroll
     for (int L = 0; L < kLimbs; ++L)
-        *(uint4*)(zq + (int64_t)c * kChunkBytes + (q * kLimbs + L) * 1024 + g * 256 + f * 16) =
-            uint4{out[L][0], out[L][1], out[L][2], out[L][3]};
+        *(uint32_t*)(zq + (int64_t)c * kChunkBytes + (q * kLimbs + L) * 1024 + g * 256 + f * 16 + dd * 4) = out[L];
 }
 
 // This lane's mask bits for chunk c: row r of each tile, words 8c + 2g, +1.
@@ -577,6 +616,13 @@ __global__ __launch_bounds__(kDnThreads, 1) void csr_dense_agg_kernel(
 
 using namespace lds;
 
+static void launch_colmax(const float* s, int n, const float* z, int ldz, uint32_t* colmax, hipStream_t st) {
+    if ((ldz & 3) == 0 && ((uintptr_t)z & 15) == 0)
+        hipLaunchKernelGGL(bitagg_colmax_kernel<true>, dim3(kColBlocks), dim3(1024), 0, st, s, n, z, ldz, colmax);
+    else
+        hipLaunchKernelGGL(bitagg_colmax_kernel<false>, dim3(kColBlocks), dim3(1024), 0, st, s, n, z, ldz, colmax);
+}
+
 extern "C" int64_t lds_bitmask_agg_ws_bytes(int n) {
     if (n <= 0) return 0;
     return (int64_t)kMaxBlocks * kF * 4 + (int64_t)chunks_of(n) * kChunkBytes + (int64_t)splits_of(n) * n * kF * 4;
@@ -590,8 +636,8 @@ extern "C" int lds_aggregate_bitmask(const uint64_t* bits, int words, const floa
     hipStream_t st = (hipStream_t)stream;
     const Ws w = carve(ws, n);
     const int nc = chunks_of(n), ks = splits_of(n);
-    hipLaunchKernelGGL(bitagg_colmax_kernel, dim3(kMaxBlocks), dim3(256), 0, st, s, n, z, ldz, w.colmax);
-    hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st,
+    launch_colmax(s, n, z, ldz, w.colmax, st);
+    hipLaunchKernelGGL(bitagg_quant_kernel, dim3(nc * kSteps * 4 * kF * 4 / 256), dim3(256), 0, st,
                        s, n, z, ldz, (const uint32_t*)w.colmax, w.zq, nc);
     hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(kThreads), 0, st, bits, words, n,
                        (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax, s, y, ldy, beta, 0);
@@ -621,8 +667,8 @@ extern "C" int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, c
     hipStream_t st = (hipStream_t)stream;
     const Ws w = carve(ws, n);
     const int nc = chunks_of(n), ks = splits_of(n);
-    hipLaunchKernelGGL(bitagg_colmax_kernel, dim3(kMaxBlocks), dim3(256), 0, st, s, n, z, ldz, w.colmax);
-    hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st,
+    launch_colmax(s, n, z, ldz, w.colmax, st);
+    hipLaunchKernelGGL(bitagg_quant_kernel, dim3(nc * kSteps * 4 * kF * 4 / 256), dim3(256), 0, st,
                        s, n, z, ldz, (const uint32_t*)w.colmax, w.zq, nc);
     hipLaunchKernelGGL(bitagg_main_kernel, dim3(row_groups_of(n), ks), dim3(kThreads), 0, st, bits, words, n,
                        (const int8_t*)w.zq, nc, ks, w.part, (const uint32_t*)w.colmax, s, (float*)nullptr, 0, 0,
@@ -649,8 +695,8 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
     const Ws w = carve(ws, n);
     const int nc = chunks_of(n);
     if (quantize) {
-        hipLaunchKernelGGL(bitagg_colmax_kernel, dim3(kMaxBlocks), dim3(256), 0, st, s, n, z, ldz, w.colmax);
-        hipLaunchKernelGGL(bitagg_quant_kernel, dim3((nc * kSteps * 4 * kF + 255) / 256), dim3(256), 0, st, s, n, z,
+        launch_colmax(s, n, z, ldz, w.colmax, st);
+        hipLaunchKernelGGL(bitagg_quant_kernel, dim3(nc * kSteps * 4 * kF * 4 / 256), dim3(256), 0, st, s, n, z,
                            ldz, (const uint32_t*)w.colmax, w.zq, nc);
     }
     static int cus = 0;
