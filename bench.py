@@ -549,6 +549,8 @@ def main():
                     "default: bf16x3, the split-bf16 MFMA form picked by shape)")
     ap.add_argument("--async-draw", action="store_true", help="engine: draw a window's graphs 1..τ on a side "
                     "stream beside inner step 0 (graph 0 on the main stream; without prefetched draws)")
+    ap.add_argument("--xt-pair", type=int, default=0, choices=[0, 1, 2], help="engine: W0 products over pairs of "
+                    "replica samples (0 by shape, 1 off, 2 on; LdsEngine.set_xt_pair)")
     ap.add_argument("--samples", type=int, default=1, help="Monte-Carlo replica samples per GPU, batched in "
                     "every launch (BASELINE configs 3/4); value is then sample-steps/s")
     ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
@@ -608,6 +610,8 @@ def main():
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
         eng, reducer = make_engine(runner, args.tau, world, args.samples)
         eng.async_draw = bool(args.async_draw)
+        if args.xt_pair:
+            eng.set_xt_pair(args.xt_pair)
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
@@ -712,7 +716,8 @@ def main():
                        "replicas_in_sync": in_sync, "graph_model": args.graph_model,
                        "windows_per_graph": (args.graph_windows if reducer is None else 1)
                        if use_engine and use_graph else None,
-                       "prefetched_draw": prefetched, "async_draw": bool(args.async_draw)},
+                       "prefetched_draw": prefetched, "async_draw": bool(args.async_draw),
+                       "xt_pair": args.xt_pair},
             "steady_state": steady,
             "strong_scaling": strong,
             "window": window,

@@ -491,6 +491,11 @@ typedef struct LdsBatch {
     /* ABI 11: side work appended to this launch's grid (NULL: none);
      * lds_engine_fwd_layer1 and lds_engine_fwd2_bwd2 with samples == 1. */
     const LdsSideWork* side;
+    /* ABI 11: lds_engine_xt_adam over pairs of samples (two per wave sharing
+     * one walk of X's column indices; same sums): 0 by shape, 1 off, 2 on
+     * (needs an even sample count, no heavy columns, column heads, no
+     * xt_part, train == 0). */
+    int32_t xt_pair;
 } LdsBatch;
 
 /* lds_sample_bitmask with the draw counter read from device memory:

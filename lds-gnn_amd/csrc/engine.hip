@@ -445,6 +445,66 @@ __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const i
     return groups_sum(acc);
 }
 
+// x_wave_dot_head<true, 2> (train = 0) for TWO samples that share the
+// column's indices: lanes 0-31 sample a, 32-63 sample b.  Group h (0 / 1) of
+// a sample runs the chunk streams h and h + 2 of the one-sample walk, each in
+// an accumulator of its own in the same entry order, and the streams are
+// combined as groups_sum combines the four groups: (s0 + s1) + (s2 + s3) —
+// the same bits as two one-sample walks.  The index loads of a and b are the
+// same addresses in one instruction (one access), the value and row loads
+// are the samples' own.
+__device__ __forceinline__ float x_wave_dot_head_pair(int p0, int nnz, const int* __restrict__ head,
+                                                      const int* __restrict__ idx, const float* __restrict__ val_a,
+                                                      const float* __restrict__ val_b, const float* __restrict__ src_a,
+                                                      const float* __restrict__ src_b) {
+    const int lane = threadIdx.x & (HID - 1);
+    const int grp = (threadIdx.x >> 4) & 3;
+    const int h = grp & 1;
+    const float* __restrict__ val = grp >= 2 ? val_b : val_a;
+    const float* __restrict__ src = grp >= 2 ? src_b : src_a;
+    float acc[2] = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int q = h + 2 * u;
+        const int e = 16 * q + lane;
+        const int j = head[e];
+        const float x = e < nnz ? val[p0 + e] : 0.f;
+        if (16 * q < nnz) {  // group-uniform, as in the one-sample walk
+            float sk[HID];
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+            LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc[u] = fmaf(rbc_f<K>(x), sk[K], acc[u]);
+            LDS_R16(LDS_F)
+#undef LDS_F
+        }
+    }
+    const int end = p0 + nnz;
+    for (int pb = p0 + 64 + h * HID; pb < end; pb += 4 * HID) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int pu = pb + 2 * HID * u;  // stream h + 2u: its chunk of this round
+            if (pu < end) {
+                const int p = pu + lane;
+                int j = 0;
+                float x = 0.f;
+                if (p < end) {
+                    j = idx[p];
+                    x = val[p];
+                }
+                float sk[HID];
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+                LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc[u] = fmaf(rbc_f<K>(x), sk[K], acc[u]);
+                LDS_R16(LDS_F)
+#undef LDS_F
+            }
+        }
+    }
+    return xor16_add(acc[0]) + xor16_add(acc[1]);
+}
+
 template <bool kCsc>
 __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const int* __restrict__ idx,
                                             const float* __restrict__ val, int r,
@@ -2053,6 +2113,72 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     }
 }
 
+// Per-sample views of a batched launch's arrays (sample smp; the one-sample
+// kernels take it from blockIdx.y through boff).
+template <typename T>
+__device__ __forceinline__ T* soff(T* p, int64_t stride, int smp) {
+    return p == nullptr ? p : p + (int64_t)smp * stride;
+}
+__device__ __forceinline__ void sample_views(FinalArgs& f, AdamArgs& a, const Batch& bt, int smp) {
+    f.partials = soff(f.partials, bt.part, smp);
+    f.dst = soff(f.dst, bt.par, smp);
+    f.metrics = soff(f.metrics, bt.met, smp);
+    a.w0 = soff(a.w0, bt.par, smp);
+    a.m0 = soff(a.m0, bt.par, smp);
+    a.v0 = soff(a.v0, bt.par, smp);
+    a.w1 = soff(a.w1, bt.par, smp);
+    a.m1 = soff(a.m1, bt.par, smp);
+    a.v1 = soff(a.v1, bt.par, smp);
+    a.gp = soff(a.gp, bt.par, smp);
+    a.wbar = soff(a.wbar, bt.par, smp);
+    a.mbar = soff(a.mbar, bt.par, smp);
+    a.vbar = soff(a.vbar, bt.par, smp);
+    a.gbar = soff(a.gbar, bt.par, smp);
+}
+
+// xt_adam_kernel<true> over pairs of samples (LdsBatch.xt_pair): grid.y =
+// samples / 2, a wave takes one column for samples 2y and 2y + 1
+// (x_wave_dot_head_pair: one index walk, the same sums), lanes 0-15 and 32-47
+// complete the two W0 entries' Adam; the last two blocks run the samples'
+// final reductions.  Light columns only (no heavy-column plan), column heads,
+// no split partials, train = 0 (the stored Xd).
+__global__ __launch_bounds__(1024) void xt_adam_pair_kernel(
+    const int* __restrict__ xrow, const float* __restrict__ xval, int fin, const float* __restrict__ d,
+    const EngineScalars* __restrict__ sc, FinalArgs fin_args, AdamArgs adam, const int4* __restrict__ xtinfo,
+    const int* __restrict__ xthead, Batch bt) {
+    const int s0 = 2 * (int)blockIdx.y;
+    if (fin_args.partials != nullptr && (int)blockIdx.x >= (int)gridDim.x - 2) {
+        sample_views(fin_args, adam, bt, s0 + (int)blockIdx.x - ((int)gridDim.x - 2));
+        final_block_1024<16>(fin_args, adam, sc);
+        return;
+    }
+    const int wave = wave_id();
+    const int lane = threadIdx.x & 63;
+    const int slot = (int)blockIdx.x * 16 + wave;
+    if (slot >= fin) return;  // light blocks never reach a barrier
+    sample_views(fin_args, adam, bt, s0 + (lane >> 5));
+    const int4 inf = xtinfo[slot];
+    const int f = inf.x;
+    const int idx = f * HID + (lane & (HID - 1));
+    const bool owner = (lane & 31) < HID;
+    AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
+    float prev = 0.f;
+    if (owner) {
+        o = adam_load(adam, idx);
+        if (fin_args.accumulate) prev = fin_args.dst[idx];
+    }
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
+    const float acc = x_wave_dot_head_pair(inf.y, inf.z, xthead + (int64_t)slot * 64, xrow,
+                                           soff(xval, bt.xval, s0), soff(xval, bt.xval, s0 + 1),
+                                           soff(d, bt.act, s0), soff(d, bt.act, s0 + 1));
+    if (owner) {
+        const float val = fin_args.accumulate ? prev + acc : acc;
+        fin_args.dst[idx] = val;
+        adam_apply(adam, idx, val, o, step_size, c2);
+    }
+}
+
 // End of a window: slot T -> slot 0 for w, m, v, and advance the scalars.
 __global__ __launch_bounds__(256) void end_window_kernel(int np, const float* __restrict__ wT,
                                                          const float* __restrict__ mT,
@@ -2169,6 +2295,11 @@ static inline int side_blocks(const LdsBatch* b, int n, int ns, bool plain, Batc
     bt.side = side_of(h, n);
     return bt.side.draw_blocks + bt.side.fill_blocks;
 }
+// lds_engine_xt_adam pairs samples per wave by shape from this many samples
+// on (MI355X, profiles/r03_xt_pair_ab.jsonl: Citeseer S = 16 56.6 -> 41.6 µs
+// per call, Cora S = 16 30.9 -> 28.8; at Cora S = 8 the doubled walk per wave
+// costs more than the shared index loads save, 15.7 -> 19.2)
+constexpr int kXtPairMinSamples = 16;
 static inline int plan_heavy(const LdsBatch* b) {
     return b != nullptr && b->n_heavy > 0 && b->heavy_rows && b->heavy_flag ? b->n_heavy : 0;
 }
@@ -2581,9 +2712,22 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
     AdamArgs a = mk_adam_args(adam_mode, first, w0, m0, v0, w1, m1, v1, gp, wbar, mbar, vbar, gbar, hyper,
                               adam_tab, n_wd, step_off);
     FinalArgs f{partials, nblocks, c, off_b0, off_w1, off_b1, accumulate, out, metrics};
-    const int blocks = n_heavy + (fin - n_heavy + 15) / 16 + (partials != nullptr ? 1 : 0);
     Batch bt;
     const int ns = mk_batch(batch, bt);
+    // pairs of samples per wave (LdsBatch.xt_pair): by shape from
+    // kXtPairMinSamples samples on
+    const int mode = batch != nullptr ? batch->xt_pair : 1;
+    LDS_CHECK_ARG(mode >= 0 && mode <= 2);
+    const bool can_pair = ns >= 2 && ns % 2 == 0 && n_heavy == 0 && xt_part == nullptr && xthead != nullptr &&
+                          train == 0;
+    LDS_CHECK_ARG(mode != 2 || can_pair);
+    if (can_pair && (mode == 2 || (mode == 0 && ns >= kXtPairMinSamples))) {
+        const int pblocks = (fin + 15) / 16 + (partials != nullptr ? 2 : 0);
+        hipLaunchKernelGGL(xt_adam_pair_kernel, dim3(pblocks, ns / 2), dim3(1024), 0, (hipStream_t)stream, xrow,
+                           xval, fin, d, (const EngineScalars*)scalars, f, a, (const int4*)xtinfo, xthead, bt);
+        LDS_RETURN_LAST_ERROR();
+    }
+    const int blocks = n_heavy + (fin - n_heavy + 15) / 16 + (partials != nullptr ? 1 : 0);
     LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(1024), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
                        a, xt_part, xt_splits, order, n_heavy, (const int4*)xtinfo, xthead, bt);

@@ -244,7 +244,7 @@ class LdsBatch(ctypes.Structure):
     _fields_ = [("samples", ctypes.c_int32), ("tag_step", ctypes.c_uint32)] + [
         (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")] + [
         ("heavy_rows", ctypes.c_void_p), ("heavy_flag", ctypes.c_void_p), ("n_heavy", ctypes.c_int32),
-        ("agg_splits", ctypes.c_int32), ("side", ctypes.c_void_p)]
+        ("agg_splits", ctypes.c_int32), ("side", ctypes.c_void_p), ("xt_pair", ctypes.c_int32)]
 
 
 class LdsSideWork(ctypes.Structure):

@@ -743,6 +743,21 @@ class LdsEngine:
         self._xt_plan()
         self._layout_version = getattr(self, "_layout_version", 0) + 1  # captured step graphs are stale
 
+    def set_xt_pair(self, mode: int):
+        """W0 products (lds_engine_xt_adam) over pairs of replica samples, two
+        per wave sharing one walk of X's column indices (same sums): 0 by
+        shape (the library's rule), 1 off, 2 on (an even sample count; the
+        column plan then has no heavy columns).  Call between windows, before
+        capture_window."""
+        if mode not in (0, 1, 2):
+            raise ValueError("xt_pair: 0 (by shape), 1 (off) or 2 (on)")
+        if mode == 2 and self.S % 2:
+            raise ValueError("xt_pair = 2 needs an even number of samples")
+        self.xt_pair = mode
+        self._btx.xt_pair = mode
+        self._xt_plan()
+        self._layout_version += 1  # captured step graphs are stale
+
     def _xt_plan(self):
         """lds_engine_xt_adam's column plan (X is fixed): the columns with more
         than 128 entries first (a 1024-thread block each), then the rest (one
@@ -753,7 +768,9 @@ class LdsEngine:
         # blocks); from 16 on every column stays one wave, where the
         # 1024-thread heavy blocks only fragment the CU (Cora S = 16 31.0 vs
         # 30.9; Citeseer S = 16 73.4 vs 59.6 µs)
-        heavy = (lens > 128) if self.xt_splits <= 1 and self.S <= 8 else torch.zeros_like(lens, dtype=torch.bool)
+        # (and none when the W0 products pair samples per wave: set_xt_pair(2))
+        heavy = (lens > 128) if self.xt_splits <= 1 and self.S <= 8 and getattr(self, "xt_pair", 0) != 2 \
+            else torch.zeros_like(lens, dtype=torch.bool)
         idx = torch.arange(self.fin, device=self.dev)
         self.xt_order = torch.cat([idx[heavy], idx[~heavy]]).to(torch.int32).contiguous()
         self.xt_heavy = int(heavy.sum())

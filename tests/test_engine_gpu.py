@@ -742,3 +742,35 @@ def test_spread_draws_equal_window_draws():
         c.run_window(5)
     torch.cuda.synchronize()
     same(a, c)
+
+
+def test_xt_adam_sample_pairs_bit_identical():
+    """lds_engine_xt_adam with two replica samples per wave (one walk of X's
+    column indices for both, LdsBatch.xt_pair = 2) gives bitwise the same W0
+    products, Adam states, θ and scalars as one sample per wave (xt_pair = 1),
+    eager and replayed; odd sample counts refuse the forced mode."""
+    from tests.parity_harness import run_engine_samples_and_oracle
+
+    def mk():
+        return run_engine_samples_and_oracle(samples=4, n=150, f_in=26, classes=5, steps=1, tau=5, dropout=0.5,
+                                             seed=7, replica0=2)["engine"]
+    a, b = mk(), mk()
+    a.set_xt_pair(2)
+    b.set_xt_pair(1)
+    for _ in range(2):
+        a.run_window(5)
+        b.run_window(5)
+    a.capture_window(5, windows=2)
+    b.capture_window(5, windows=2)
+    a.replay(2)
+    b.replay(2)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    for s_ in range(4):
+        for k, v in a.get_params(s_).items():
+            assert torch.equal(v, b.get_params(s_)[k]), (s_, k)
+    assert a.scalars_host() == b.scalars_host()
+    c = run_engine_samples_and_oracle(samples=3, n=150, f_in=26, classes=5, steps=1, tau=5, dropout=0.5,
+                                      seed=7, replica0=2)["engine"]
+    with pytest.raises(ValueError):
+        c.set_xt_pair(2)
