@@ -55,7 +55,14 @@ __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1
         (void)cc1;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        c = U32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        // hi ^ c ^ k as one v_bitop3_b32 (XOR3 truth table 0x96, the round key
+        // as its SGPR operand; gfx950 has no v_xor3_b32 and the compiler emits
+        // two v_xor_b32): 626 -> 758 G Philox calls/s on MI355X, same words
+        // (tools/microbench/philox_rate.hip)
+        uint32_t x0, x2;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(x0) : "v"(hi1), "v"(c.y), "s"(k0));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(x2) : "v"(hi0), "v"(c.w), "s"(k1));
+        c = U32x4{x0, lo1, x2, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
         // the round keys advance in place: without this the compiler hoists
