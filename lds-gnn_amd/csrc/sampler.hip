@@ -107,14 +107,20 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     for (int r = 0; r < 16; ++r)
         thr[r] = th[r] >= 0.0f ? (uint32_t)ceilf(fminf(th[r], 1.0f) * 16777216.0f) : 0u;
     // kLoop: items (graph blockIdx.y + g, sample z), g < graphs, g-major, over
-    // this one θ tile load (graph blockIdx.y + g draws counter + g)
+    // this one θ tile load (graph blockIdx.y + g draws counter + g); with
+    // grid.z > 1 the samples are split into grid.z consecutive ranges, one per
+    // block (more waves per SIMD to hide the Philox chains and the stores; the
+    // tile's θ is then loaded once per range — the same draws either way)
+    const int zper = kLoop ? (samples + (int)gridDim.z - 1) / (int)gridDim.z : 1;
+    const int zs = kLoop ? (int)blockIdx.z * zper : 0;
+    const int zc = kLoop ? max(0, min(samples, zs + zper) - zs) : 1;
     const int z0 = kLoop ? 0 : (int)blockIdx.z;
-    const int z1 = kLoop ? samples * graphs : z0 + 1;
+    const int z1 = kLoop ? zc * graphs : z0 + 1;
     const bool rvalid = lane < 16 && r0 + lane < n;  // lane r stores row r0 + r's word
     // item -> (graph index, sample, counter, tag, its bits / degree slices)
     auto item = [&](int it, int& gidx, int& z) {
-        const int gl = kLoop ? it / samples : 0;
-        z = kLoop ? it - gl * samples : it;
+        const int gl = kLoop ? it / zc : 0;
+        z = kLoop ? zs + (it - gl * zc) : it;
         gidx = (int)blockIdx.y + gl;
         return gl;
     };
@@ -529,6 +535,13 @@ extern "C" int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const
     LDS_RETURN_LAST_ERROR();
 }
 
+// the batched draw's target block count (16 waves per SIMD-slot's worth on
+// 256 CUs at 4 waves per block).  MI355X, window draw per call (sample
+// splits): Cora S = 16 358 µs unsplit, 317 at 2048 blocks, 310 at 4096, 314
+// at 8192; Citeseer S = 16 475 / 429 / 423 / 415; Cora S = 8 189 / 177 /
+// 175 / 180 (profiles/r03_draw_split.jsonl)
+constexpr int kDrawBlocks = 4096;
+
 extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                                        uint32_t tag_step, const uint32_t* counter_base,
                                        uint32_t counter_offset, int count, int samples, uint64_t* bits,
@@ -562,14 +575,17 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
     // replica samples and the window's graphs loop inside the block over one
     // θ tile load (θ read once per window)
     const int loop_graphs = count;
+    // replica samples split over grid.z so the launch has >= kDrawBlocks blocks
+    // (one sample range per block; same draws)
+    const int zsplit = std::max(1, std::min(samples, (kDrawBlocks + ntiles - 1) / ntiles));
     if (samples > 1 || (loop_graphs > 1 && count > 1)) {
         if (fused)
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true>), dim3(ntiles, count / loop_graphs, 1),
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true>), dim3(ntiles, count / loop_graphs, zsplit),
                                dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
                                counter_base, (const float*)nullptr, bits, words, ntiles, tag_step, samples, loop_graphs,
                                dacc, wsi);
         else
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, false>), dim3(ntiles, count / loop_graphs, 1),
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, false>), dim3(ntiles, count / loop_graphs, zsplit),
                                dim3(256), 0, st, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
                                counter_base, (const float*)nullptr, bits, words, ntiles, tag_step, samples, loop_graphs,
                                dacc, wsi);
