@@ -1332,45 +1332,56 @@ __device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float 
         for (int base = 0; base < dr.graphs; base += kW8Grp) {
             const int gn = min(kW8Grp, dr.graphs - base);
             __syncthreads();  // the stage buffers (first group) / the previous group's words are consumed
+            // two graphs per pass: both accumulators' eight Philox calls of
+            // each graph (sixteen chains per lane) issued together — at two
+            // waves per SIMD the rounds' multiply latency needs the ILP
 #pragma unroll 1
-            for (int q = 0; q < gn; ++q) {
-                const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q);
-                uint64_t colw = 0;
-                // both accumulators' eight Philox calls issued together: at two
-                // waves per SIMD the rounds' multiply latency needs the ILP
-                uint32_t x[2][16];
+            for (int q = 0; q < gn; q += 2) {
+                const int gq = min(2, gn - q);  // wave-uniform
+                uint32_t x[2][2][16];
 #pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
+                for (int gg = 0; gg < 2; ++gg) {
+                    if (gg >= gq) break;
+                    const uint32_t ctr = dr.counter + cb + (uint32_t)(base + q + gg);
 #pragma unroll
-                    for (int qd = 0; qd < 4; ++qd) {
-                        const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr},
-                                                      dr.k0, dr.k1);
-                        x[m][4 * qd] = o.x;
-                        x[m][4 * qd + 1] = o.y;
-                        x[m][4 * qd + 2] = o.z;
-                        x[m][4 * qd + 3] = o.w;
+                    for (int m = 0; m < 2; ++m) {
+                        const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;  // row quad of e = 0
+#pragma unroll
+                        for (int qd = 0; qd < 4; ++qd) {
+                            const U32x4 o = philox4x32_10(
+                                U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr}, dr.k0, dr.k1);
+                            x[gg][m][4 * qd] = o.x;
+                            x[gg][m][4 * qd + 1] = o.y;
+                            x[gg][m][4 * qd + 2] = o.z;
+                            x[gg][m][4 * qd + 3] = o.w;
+                        }
                     }
                 }
 #pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+                for (int gg = 0; gg < 2; ++gg) {
+                    if (gg >= gq) break;
+                    const int qg = q + gg;
+                    uint64_t colw = 0;
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const bool bit = (x[m][e] >> 8) < thr[m][e];
-                        const uint64_t w = __ballot(bit);
-                        mylo = lane == e ? (uint32_t)w : mylo;
-                        myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
-                        colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                    for (int m = 0; m < 2; ++m) {
+                        uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) {
+                            const bool bit = (x[gg][m][e] >> 8) < thr[m][e];
+                            const uint64_t w = __ballot(bit);
+                            mylo = lane == e ? (uint32_t)w : mylo;
+                            myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
+                            colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                        }
+                        if (lane < 16) {  // element e = lane: rows rr and rr + 4 of columns wc·32 …
+                            const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
+                            rwb[(qg * 128 + rr) * 4 + wc] = mylo;
+                            rwb[(qg * 128 + rr + 4) * 4 + wc] = myhi;
+                        }
                     }
-                    if (lane < 16) {  // element e = lane: rows rr and rr + 4 of columns wc·32 …
-                        const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
-                        rwb[(q * 128 + rr) * 4 + wc] = mylo;
-                        rwb[(q * 128 + rr + 4) * 4 + wc] = myhi;
-                    }
+                    colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
+                    if (lane < 32) cwb[(qg * 2 + wr) * 128 + wc * 32 + lane] = colw;
                 }
-                colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
-                if (lane < 32) cwb[(q * 2 + wr) * 128 + wc * 32 + lane] = colw;
             }
             __syncthreads();
             // one (row, two words) pair per work item: rows of I (part 0), rows of J (part 1)
