@@ -18,6 +18,7 @@
 #   accuracy   LDS τ = 5 fused engine, 10 seeds, Cora + Citeseer acc_<ds>_tau5_TAG.jsonl
 #   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
 #   spmm5      config-5 CSR-SpMM kernels + kernel trace + PMC spmm5_TAG.json, spmm5_prof_TAG/, spmm5_pmc_TAG_*/
+#   xtpair     W0 products one vs two samples per wave (Citeseer S = 16, Cora S = 16 / 8) xp_<ds>_<S>_<mode>_TAG.json
 set -o pipefail
 tag=${1:?usage: tools/gpu.sh TAG STEP...}
 shift
@@ -58,6 +59,12 @@ for step in "$@"; do
     c5cpu)
         run 900 python -u bench.py --dataset synthetic20k --steps 10 --warmup 5 --cpu-steps 1 \
             > $O/c5_cpu_$tag.json 2> $O/c5_cpu_$tag.err || exit $? ;;
+    xtpair)
+        for spec in "citeseer 16 1" "citeseer 16 2" "cora 16 1" "cora 16 2" "cora 8 1" "cora 8 2"; do
+            set -- $spec
+            run 300 python bench.py --dataset $1 --samples $2 --xt-pair $3 --steps 100 --warmup 10 --no-cpu-baseline \
+                > $O/xp_${1}_$2_$3_$tag.json 2> $O/xp_${1}_$2_$3_$tag.err || exit $?
+        done ;;
     samples)
         for spec in "cora 8" "cora 16" "citeseer 16"; do
             set -- $spec
