@@ -744,6 +744,10 @@ int lds_engine_adam_table(const void* scalars, const double* betas_dev, float* a
  * anything but kernel and empty nodes.
  * ------------------------------------------------------------------------- */
 int lds_graph_node_census(void* graph, int* counts, int ncounts);
+/* Upload an instantiated graph's executable (hipGraphUpload) on `stream`, so
+ * its first replay does not pay the one-time upload: the engine uploads every
+ * sealed capture before the first replay.  Host only. */
+int lds_graph_upload(void* graph_exec, void* stream);
 
 #ifdef __cplusplus
 }

@@ -32,3 +32,8 @@ extern "C" int lds_graph_node_census(void* graph, int* counts, int ncounts) {
     }
     return 0;
 }
+
+extern "C" int lds_graph_upload(void* graph_exec, void* stream) {
+    LDS_CHECK_ARG(graph_exec != nullptr);
+    return (int)hipGraphUpload(reinterpret_cast<hipGraphExec_t>(graph_exec), (hipStream_t)stream);
+}

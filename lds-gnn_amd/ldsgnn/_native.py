@@ -25,6 +25,7 @@ _RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset", "lds_
 SIGNATURES = {
     "lds_abi_version": [],
     "lds_graph_node_census": [P, P, c_int],
+    "lds_graph_upload": [P, P],
     "lds_bitmask_words": [c_int],
     "lds_philox_uniform": [c_uint64, c_uint32, c_uint32, c_int, c_int, P, P],
     "lds_sample_bitmask": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P],
@@ -223,6 +224,11 @@ def new_graph() -> "torch.cuda.CUDAGraph":
     return torch.cuda.CUDAGraph(keep_graph=True)
 
 
+# seal_graph uploads every instantiated capture (hipGraphUpload) before its
+# first replay
+UPLOAD_GRAPHS = True
+
+
 def seal_graph(graph: "torch.cuda.CUDAGraph", what: str) -> "torch.cuda.CUDAGraph":
     """Refuse a captured graph that holds anything but kernel (and empty)
     nodes, then instantiate it.  A memset node in a replayed step graph
@@ -235,6 +241,8 @@ def seal_graph(graph: "torch.cuda.CUDAGraph", what: str) -> "torch.cuda.CUDAGrap
     if bad:
         raise RuntimeError(f"captured {what} holds non-kernel graph nodes {bad}: refusing to replay it")
     graph.instantiate()
+    if UPLOAD_GRAPHS:  # the executable uploaded now, not on its first replay
+        call("lds_graph_upload", graph.raw_cuda_graph_exec(), stream_of(torch.cuda.current_device()))
     return graph
 
 
