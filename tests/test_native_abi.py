@@ -85,3 +85,31 @@ def test_theta_grad_form_is_a_per_call_argument():
 def test_graph_census_argument_errors_need_no_gpu():
     import ldsgnn._native as nat
     assert nat.lib.lds_graph_node_census(None, None, 0) == 1
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors of LdsBatch and LdsSideWork (ldsgnn._native) have
+    the sizes and field offsets the C compiler gives include/ldsgnn.h."""
+    import shutil
+    import subprocess
+    import ldsgnn._native as nat
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        import pytest
+        pytest.skip("no C compiler")
+    lines = []
+    for st in (nat.LdsBatch, nat.LdsSideWork):
+        lines.append(f'printf("{st.__name__} size %zu\\n", sizeof({st.__name__}));')
+        for f, _ in st._fields_:
+            lines.append(f'printf("{st.__name__} {f} %zu\\n", offsetof({st.__name__}, {f}));')
+    src = tmp_path / "layout.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"ldsgnn.h\"\nint main(void){\n" +
+                   "\n".join(lines) + "\nreturn 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(line.split()[:2]): int(line.split()[2]) for line in out if line}
+    for st in (nat.LdsBatch, nat.LdsSideWork):
+        assert got[(st.__name__, "size")] == ctypes.sizeof(st), st.__name__
+        for f, _ in st._fields_:
+            assert got[(st.__name__, f)] == getattr(st, f).offset, (st.__name__, f)
