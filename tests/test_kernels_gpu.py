@@ -834,3 +834,42 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     scale = (a.double() @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
     assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL
     assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0)
+
+
+@pytest.mark.parametrize("samples,count,n", [(5, 3, 700), (16, 2, 257)])
+def test_batched_draw_sample_ranges_equal_single_draws(device, samples, count, n):
+    """The window draw with replica samples split over grid.z (sample ranges
+    per block; at these sizes every sample gets its own block range) against
+    one single draw per (graph, sample) with that sample's tag: identical
+    bits, and degree counts equal to the rows' popcounts (the fused CSR path
+    the engine uses)."""
+    g = torch.Generator(device=device).manual_seed(n + samples)
+    theta = torch.rand(n * (n + 1) // 2, generator=g, device=device)
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    st = nat.stream_of(device)
+    base = torch.tensor([5, 0, 0, 0], dtype=torch.int32, device=device)
+    G = count * samples
+    bits = torch.empty((count, samples, n, words), dtype=torch.int64, device=device)
+    deg = torch.empty((count, samples, wsi), dtype=torch.int32, device=device)
+    row_ptr = torch.empty((G, n + 1), dtype=torch.int32, device=device)
+    col = torch.empty((G, n * n), dtype=torch.int32, device=device)
+    s = torch.empty((G, n), dtype=torch.float32, device=device)
+    ell = torch.empty((G, n * 2 * 64), dtype=torch.int32, device=device)
+    seed, tag, off = 77, tag_for(TAG_GRAPH, 0), 2
+    nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), off, count, samples,
+             nat.ptr(bits), words, nat.ptr(deg), nat.ptr(row_ptr), nat.ptr(col), n * n, nat.ptr(s), nat.ptr(ell),
+             0, 0, st)
+    one = torch.empty((n, words), dtype=torch.int64, device=device)
+    nb = (n + 63) // 64
+    for gi in range(count):
+        for z in range(samples):
+            nat.call("lds_sample_bitmask", nat.ptr(theta), n, seed, tag + z, 5 + off + gi, 0, nat.ptr(one), words,
+                     st)
+            assert torch.equal(bits[gi, z, :, :nb], one[:, :nb]), (gi, z)
+            pc = torch.zeros(n, dtype=torch.int64, device=device)
+            for w in range(nb):  # popcount per row, word by word
+                x = one[:, w]
+                for b in range(64):
+                    pc += (x >> b) & 1
+            assert torch.equal(deg[gi, z, :n].long(), pc), (gi, z)
