@@ -262,10 +262,10 @@ def window_breakdown(eng, reducer, args, device, k=20):
     real = nat.call
 
     def rec(name, *a):
-        # with the window's degree counts as this call found them: chains of a
-        # drawing launch (the θ-grad epilogue, spread draws appended to
-        # lds_engine_fwd_layer1) accumulate into them, and a later chain must
-        # not fill from inflated counts
+        # with the window's degree counts as this call found them: a chain of
+        # a drawing launch (the θ-grad epilogue) accumulates into them 20 times
+        # over, and a later chain must not fill from those inflated counts
+        # (round 3's bench_sp1 fault)
         calls.append((name, a, eng.gbatch.deg.clone()))
         real(name, *a)
 
@@ -278,7 +278,7 @@ def window_breakdown(eng, reducer, args, device, k=20):
     per = {}
     for name, a, deg in calls:
         if name == "lds_sample_graphs_multi":  # repeated draws clear their own workspace (ws_zeroed = 0)
-            a = a[:-2] + (0,) + a[-1:]
+            a = a[:-3] + (0,) + a[-2:]
         eng.gbatch.deg.copy_(deg)
         us = chain_us(lambda st, name=name, a=a: real(name, *(a[:-1] + (st,))), device, k)
         per.setdefault(name, []).append(us)

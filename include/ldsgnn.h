@@ -34,13 +34,26 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 11
+#define LDS_ABI_VERSION 12
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
 
 /* Text for a return code (hipGetErrorString). Never NULL. */
 const char* lds_error_string(int err);
+
+/* Device error word (ABI 12).  Kernels that meet an input they cannot use
+ * faithfully set bits in a caller-provided uint32 (the `err` arguments; the
+ * engine's is EngineScalars.error) instead of reading through it, and the
+ * host raises when it reads a non-zero word:
+ *   LDS_DEVERR_FILL_DEGREE — a CSR fill (lds_sample_fill_csr,
+ *     lds_sample_graphs_multi, lds_engine_fill_x_linear) found a row whose
+ *     drawn bits hold a different number of entries than its degree count in
+ *     deg_ws (a workspace that was not zero on entry, or counts of another
+ *     draw).  row_ptr follows the counts, so the row's slots past its drawn
+ *     entries are written with the row's own index (valid, never outside the
+ *     graph) instead of being left as whatever col held. */
+#define LDS_DEVERR_FILL_DEGREE 1u
 
 /* Number of uint64 words per bitmask row for n nodes (ceil(n/64) rounded up
  * to an even count so every row starts 16-byte aligned). Host-only. */
@@ -127,7 +140,7 @@ int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, 
  * and ell may be NULL). */
 int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_ws, int graphs,
                         int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
-                        const uint8_t* node_flags, void* stream);
+                        const uint8_t* node_flags, uint32_t* err, void* stream);
 
 /* lds_sample_graphs for `samples` replicas at once: graph (g, b), g < count,
  * b < samples, is draw counter *counter_base + counter_offset + g with tag
@@ -143,13 +156,15 @@ int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_w
  * need not be zero; row_ptr and ell may then be NULL.  node_flags (n bytes,
  * may be NULL): each ELL entry's j field carries the neighbour's flag byte in
  * bits 24-31 (index = j & 0xFFFFFF; the engine's bit 0 = train mask, bit 1 =
- * opt mask, read by the two-hop kernels). */
+ * opt mask, read by the two-hop kernels).  err (may be NULL): device error
+ * word, LDS_DEVERR_FILL_DEGREE when a row's degree count (ws_zeroed = 1 with a
+ * workspace that was not zero) does not match its drawn bits. */
 int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                             uint32_t tag_step, const uint32_t* counter_base,
                             uint32_t counter_offset, int count, int samples, uint64_t* bits,
                             int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
                             float* s, int* ell, const uint8_t* node_flags, int ws_zeroed,
-                            void* stream);
+                            uint32_t* err, void* stream);
 /* Batched form for a window of graphs drawn from the same θ: graph g
  * (0 <= g < count) uses draw counter *counter_base + counter_offset + g and
  * writes bits + g·n·words, deg_ws + g·lds_sample_ws_ints(n),
@@ -410,7 +425,8 @@ int lds_pretrain_step(float* theta, int n, const uint64_t* train_bits, int words
  * Per-node arrays are n × 16 fp32 (hidden width 16; c <= 16 classes padded to
  * 16 columns).  `scalars` points to the engine's device-resident
  * EngineScalars {u32 graph_ctr, u32 fwd_ctr, i32 adam_step, i32 hyper_steps,
- * f64 outer_lr, f64 lr_decay} (lds_engine_scalars_size() bytes); kernels read
+ * f64 outer_lr, f64 lr_decay, u32 error, u32 pad} (lds_engine_scalars_size()
+ * bytes; `error` is the engine's device error word, LDS_DEVERR_*); kernels read
  * the RNG counters / Adam step / lr from it so one captured HIP graph of a
  * whole τ-window replays with advancing state.  `fwd_off`, `step_off` are
  * offsets added to those counters.  Factor outputs (U, V, R) feed
@@ -440,35 +456,6 @@ int lds_engine_scalars_size(void);
  *   uv  : factor COLUMN offset per sample (U, V are n × (samples·ldk); the
  *         ldk argument is then the row stride samples·ldk)
  *   part: reduction partials   met: metrics rows (2 floats) */
-/* Side work of an engine launch (ABI 11): blocks appended to the grid of
- * lds_engine_fwd_layer1 / lds_engine_fwd2_bwd2 (single-sample launches) that
- *   - draw one graph (theta != NULL): bits and degree counts exactly as one
- *     graph of lds_sample_graphs_multi (counter *counter_base + counter_offset,
- *     `deg` zero on entry, lds_sample_ws_ints(n) ints), and / or
- *   - fill one drawn graph (fill_bits != NULL): CSR, s and the ELL head from
- *     its bits and degree counts, as lds_sample_fill_csr for one graph.
- * The engine draws graph t + 1 of a window beside inner step t's first
- * aggregation and fills it beside the second (the replaced reference calls:
- * the per-step sample(), src/trainers/bilevel.py:105, src/models/sampling.py:68). */
-typedef struct LdsSideWork {
-    const float* theta;
-    uint64_t seed;
-    uint32_t tag;
-    uint32_t counter_offset;
-    const uint32_t* counter_base;
-    uint64_t* bits;
-    int32_t words;
-    int32_t* deg;
-    const uint64_t* fill_bits;
-    const int32_t* fill_deg;
-    int32_t* row_ptr;
-    int32_t* col;
-    int64_t col_capacity;
-    float* s;
-    int32_t* ell;
-    const uint8_t* node_flags;
-} LdsSideWork;
-
 typedef struct LdsBatch {
     int32_t samples;
     uint32_t tag_step;
@@ -488,9 +475,6 @@ typedef struct LdsBatch {
      * Â·Z[i] = s_i · Σ_p agg_p[i] (p in order) — lds_aggregate_bitmask_partials
      * output, its final pass folded into the consumer.  0: agg is Â·Z. */
     int32_t agg_splits;
-    /* ABI 11: side work appended to this launch's grid (NULL: none);
-     * lds_engine_fwd_layer1 and lds_engine_fwd2_bwd2 with samples == 1. */
-    const LdsSideWork* side;
     /* ABI 11: lds_engine_xt_adam over pairs of samples (two per wave sharing
      * one walk of X's column indices; same sums): 0 by shape, 1 off, 2 on
      * (needs an even sample count, no heavy columns, column heads, no
@@ -524,7 +508,8 @@ int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int 
  * lds_engine_x_linear (one replica sample) in ONE launch: the first inner
  * step's X product does not read the window's graphs, so a window that starts
  * from prefetched draws runs both halves side by side (blocks split by role)
- * with one dependent boundary instead of two.  Arguments as the two calls. */
+ * with one dependent boundary instead of two.  Arguments as the two calls;
+ * the fill reports into the scalars' error word. */
 int lds_engine_fill_x_linear(const uint64_t* bits, int words, const int* deg_ws, int graphs,
                              int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
                              const uint8_t* node_flags, const int* xrp, const int* xcol,

@@ -612,6 +612,261 @@ __global__ __launch_bounds__(kDnThreads, 1) void csr_dense_agg_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// CSR-SpMM for dense sampled graphs, row-block form (round 4; the product
+// path of lds_spmm_norm_dense).  csr_dense_agg_kernel above multiplies each
+// 16-row bit tile as soon as it is streamed, so every tile reads all of s⊙Z's
+// digits (1.3 MB at N = 20 000) from L2: 1.6 GB per call, twice the index
+// stream, on the same CUs — and the two streams serialise (its ablations:
+// 140 µs streaming alone, 71 µs MFMA alone, 230 µs together).  Here each
+// workgroup owns ONE contiguous block of rows (R = ceil(n / grid), at most
+// kRbMaxTiles·16) and runs two phases:
+//  A. all 16 waves stream the block's CSR rows (wave w: local rows w, w + 16,
+//     …) through per-wave rings of 1-KB LDS-DMA units (512-entry steps, two
+//     in flight behind the one being read, across rows), set each entry's bit
+//     in a per-wave LDS row buffer (one 64-bit mask and two LDS ORs per lane
+//     for 8 entries within 64 columns, a per-entry path otherwise) and, at the
+//     row's end, write the bit row to a workgroup-private scratch slab
+//     (global, L2-resident: R rows × n bits) and clear the buffer;
+//  B. the block's rows multiply s⊙Z's digits once: per 512-column chunk the
+//     digits (32 KB) and the block's bit rows of the chunk (64 B per row) are
+//     staged in LDS by direct global -> LDS loads, three chunks in flight;
+//     wave w runs limb w & 3, k-steps 2(w >> 2), +1 of the chunk for every
+//     row tile (lds_aggregate_bitmask's digits, k order and exact int32
+//     sums); the 16 waves' sums meet in LDS as int64 adds (exact, order-free),
+//     then y = s_i · 2^-e_f · Σ.
+// Per CU the digits are read once per call (1.3 MB from L2), not once per
+// 16-row tile.  Columns must be distinct within a row; order is free.
+// ---------------------------------------------------------------------------
+constexpr int kRbWaves = 16;
+constexpr int kRbThreads = 64 * kRbWaves;
+constexpr int kRbUnits = 6;                  // 1-KB ring units per wave: three 512-entry steps
+constexpr int kRbRing = kRbUnits / 2;        // steps in a wave's ring
+constexpr int kRbMaxTiles = 6;               // 16-row tiles per workgroup (R <= 96)
+constexpr int kRbStages = 3;                 // phase-B chunk stages in flight
+constexpr int kRbMaxGrid = 512;
+
+// Scratch rows of the bit slabs for any grid <= kRbMaxGrid: G·T·16 <= n + 17·G.
+int64_t rb_scratch_rows(int n) { return (int64_t)n + 17 * kRbMaxGrid; }
+__host__ __device__ constexpr int rb_stage_bytes(int tiles) { return kChunkBytes + tiles * 1024; }
+int rb_lds_bytes(int chunks, int tiles) {
+    const int a = kRbWaves * kRbUnits * 1024 + kRbWaves * 64 * chunks;      // rings + row buffers
+    const int b = kRbStages * rb_stage_bytes(tiles) + tiles * 16 * kF * 8;  // stages + int64 sums
+    return a > b ? a : b;
+}
+
+// A wave's position in its CSR stream (wave-uniform): its k-th row (local row
+// wave + 16k of the block), entries [p, p + 512) of [beg, end), p ≡ 0 mod 4;
+// k == kend: past the last.
+struct RbStep {
+    int k, beg, end, p;
+};
+__device__ __forceinline__ void rb_advance(RbStep& s, const int* __restrict__ rp, int r0, int nrows, int kend,
+                                           int wave) {
+    if (s.k >= 0) {
+        s.p += kDnStep;
+        if (s.p < s.end) return;
+    }
+    while (true) {
+        if (++s.k >= kend) {
+            s.k = kend;
+            return;
+        }
+        const int row = r0 + wave + 16 * s.k;
+        s.beg = __builtin_amdgcn_readfirstlane(rp[row]);
+        s.end = __builtin_amdgcn_readfirstlane(rp[row + 1]);
+        s.p = s.beg & ~3;
+        if (s.beg < s.end) return;
+    }
+}
+
+template <int kTiles>
+__global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
+    int chunks, const uint32_t* __restrict__ colmax, const float* __restrict__ s, float* __restrict__ y, int ldy,
+    int beta, uint32_t* __restrict__ slab_all) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rb_lds[];
+    __shared__ int e_sh[kF];
+    const int rs = 16 * chunks;  // dwords per bit row
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int r0 = (int)blockIdx.x * rows_per_wg;
+    const int nrows = min(rows_per_wg, n - r0);
+    if (nrows <= 0) return;  // (uniform: the whole workgroup)
+    const int nnz = rp[n];
+    const int tiles = (rows_per_wg + 15) / 16;  // (the last block may use fewer)
+    uint32_t* const slab = slab_all + (int64_t)blockIdx.x * (tiles * 16) * rs;  // this block's bit rows
+    if (t < 64) {  // per-feature exponents (lds_aggregate_bitmask's quantisation)
+        const uint32_t m = colmax_of(colmax, t);
+        if (t < kF) e_sh[t] = col_exponent(m);
+    }
+
+    // ---- phase A: stream the block's rows into bit rows --------------------
+    uint32_t* const rowbuf = rb_lds + kRbWaves * kRbUnits * 256 + wave * rs;
+    for (int d = 4 * lane; d < rs; d += 256) *reinterpret_cast<uint4*>(rowbuf + d) = make_uint4(0u, 0u, 0u, 0u);
+    const int kend = nrows > wave ? (nrows - 1 - wave) / 16 + 1 : 0;  // this wave's rows
+    const uint32_t ring_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)rb_lds) +
+                              (uint32_t)(wave * kRbUnits * 1024);
+    const uint32_t* myring = rb_lds + wave * kRbUnits * 256;
+    RbStep is{-1, 0, 0, 0}, ps{-1, 0, 0, 0};
+    int kis = 0, kps = 0, cur = 0;  // steps issued / processed; next row to write out
+    // write the wave's bit rows cur .. k - 1 to the slab (the buffer holds row
+    // cur's bits; the rows after it are empty) and clear the buffer
+    auto flush_to = [&](int k) {
+        for (; cur < k; ++cur) {
+            uint32_t* dst = slab + (int64_t)(wave + 16 * cur) * rs;
+            for (int d = 4 * lane; d < rs; d += 256) {
+                uint4* b = reinterpret_cast<uint4*>(rowbuf + d);
+                *reinterpret_cast<uint4*>(dst + d) = *b;
+                *b = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+    };
+    auto issue = [&]() {
+        const uint32_t unit = (uint32_t)(2 * (kis % kRbRing));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int a = is.p + 256 * h + 4 * lane;
+            const int* src = a + 4 <= nnz ? col + a : col;  // past the array: a dummy block (reloaded below)
+            lds_dma16(src, ring_lds + (unit + h) * 1024u);
+        }
+        ++kis;
+        rb_advance(is, rp, r0, nrows, kend, wave);
+    };
+    rb_advance(is, rp, r0, nrows, kend, wave);
+    ps = is;
+    for (int d = 0; d < kRbRing - 1 && is.k < kend; ++d) issue();
+    while (ps.k < kend) {
+        if (is.k < kend) issue();
+        // step kps landed: at most the younger steps (two loads each) in flight
+        const int ahead = kis - kps;
+        if (ahead >= 3) __builtin_amdgcn_s_waitcnt(0x0F74);       // vmcnt(4)
+        else if (ahead == 2) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0)
+        asm volatile("" ::: "memory");
+        if (ps.k != cur) flush_to(ps.k);
+        const uint32_t* sl = myring + (2 * (kps % kRbRing)) * 256 + 8 * lane;
+        const int4 c0 = *reinterpret_cast<const int4*>(sl);
+        const int4 c1 = *reinterpret_cast<const int4*>(sl + 4);
+        const int c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const int p = ps.p + 8 * lane;
+        const bool interior = ps.p >= ps.beg && ps.p + kDnStep <= ps.end && ps.p + kDnStep + 4 <= nnz;
+        bool done = false;
+        if (interior) {
+            // the eight columns within the 64 from the first one's word (the
+            // dense, ascending case): one 64-bit mask, two LDS ORs
+            const uint32_t wf = (uint32_t)c[0] >> 5;
+            const int base = (int)(wf << 5);
+            uint32_t out = 0u;
+            uint64_t m = 0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const uint32_t r = (uint32_t)(c[e] - base);
+                out |= r >> 6;  // nonzero: outside [base, base + 64)
+                m |= 1ull << (r & 63);
+            }
+            if (out == 0u) {
+                dn_or(rowbuf + wf, (uint32_t)m);
+                dn_or(rowbuf + wf + 1, (uint32_t)(m >> 32));
+                done = true;
+            }
+        }
+        if (!done) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int idx = p + e;
+                if (idx >= ps.beg && idx < ps.end) {
+                    const int v = (idx & ~3) + 4 > nnz ? col[idx] : c[e];
+                    atomicOr(rowbuf + (v >> 5), 1u << (v & 31));
+                }
+            }
+        }
+        ++kps;
+        rb_advance(ps, rp, r0, nrows, kend, wave);
+    }
+    flush_to(kend);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slab rows are written before any wave stages them
+    __syncthreads();
+
+    // ---- phase B: the block's bit rows × the digits, chunk by chunk --------
+    int8_t* const stage0 = reinterpret_cast<int8_t*>(rb_lds);
+    const int sbytes = rb_stage_bytes(kTiles);
+    unsigned long long* const sums =
+        reinterpret_cast<unsigned long long*>(stage0 + kRbStages * sbytes);  // [kTiles·16][16] int64
+    for (int i = t; i < kTiles * 16 * kF; i += kRbThreads) sums[i] = 0ull;
+    const uint32_t stage_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)rb_lds);
+    // chunk c's stage: 32 digit blocks of 1 KB, then `tiles` blocks of the bit
+    // rows' 64-byte chunk segments (lane l: row 16T + (l >> 2), 16 bytes l & 3)
+    const int nblk = 32 + tiles;
+    auto stage = [&](int c, int buf) {
+        for (int i = wave; i < nblk; i += kRbWaves) {
+            const uint32_t dst = stage_lds + (uint32_t)(buf * sbytes + i * 1024);
+            if (i < 32) {
+                lds_dma16(zq + (int64_t)c * kChunkBytes + i * 1024 + lane * 16, dst);
+            } else {
+                const int T = i - 32;
+                lds_dma16(slab + (int64_t)(16 * T + (lane >> 2)) * rs + 16 * c + 4 * (lane & 3), dst);
+            }
+        }
+    };
+    const int mine = (nblk - 1 - wave) / kRbWaves + 1;  // stage loads this wave issues per chunk (>= 2)
+    const int L = wave & 3, pm = wave >> 2;              // limb; k-steps 2pm, 2pm + 1 (dword pm of each group)
+    const int r16 = lane & 15, g = lane >> 4;
+    v4i acc[kTiles];
+#pragma unroll
+    for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+    for (int c = 0; c < kRbStages - 1 && c < chunks; ++c) stage(c, c);
+    for (int c = 0; c < chunks; ++c) {
+        // chunk c landed (the younger chunk's loads may stay in flight), and every
+        // wave is past chunk c - 1 (whose buffer the next stage call refills)
+        if (c + 1 < chunks) {
+            if (mine >= 3) __builtin_amdgcn_s_waitcnt(0x0F73);  // vmcnt(3)
+            else __builtin_amdgcn_s_waitcnt(0x0F72);            // vmcnt(2)
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        __syncthreads();
+        if (c + kRbStages - 1 < chunks) stage(c + kRbStages - 1, (c + kRbStages - 1) % kRbStages);
+        const int8_t* sb = stage0 + (c % kRbStages) * sbytes;
+        const v4i* bs = reinterpret_cast<const v4i*>(sb);
+        const v4i b0 = bs[((2 * pm) * kLimbs + L) * 64 + lane];
+        const v4i b1 = bs[((2 * pm + 1) * kLimbs + L) * 64 + lane];
+        const uint32_t* tb = reinterpret_cast<const uint32_t*>(sb + kChunkBytes);
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T) {
+            if (T < tiles) {
+                const uint32_t w = tb[T * 256 + r16 * 16 + 4 * g + pm];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int sh = 4 * h;
+                    v4i a;
+                    a.x = (int)((w >> sh) & 0x01010101u);
+                    a.y = (int)((w >> (sh + 1)) & 0x01010101u);
+                    a.z = (int)((w >> (sh + 2)) & 0x01010101u);
+                    a.w = (int)((w >> (sh + 3)) & 0x01010101u);
+                    acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, h ? b1 : b0, acc[T], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // C/D: col = lane & 15 (feature), row = 4(lane >> 4) + i; limb L weighs 2^(8L)
+#pragma unroll
+    for (int T = 0; T < kTiles; ++T)
+        if (T < tiles)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                atomicAdd(sums + (T * 16 + 4 * g + i) * kF + r16,
+                          (unsigned long long)((int64_t)acc[T][i] * ((int64_t)1 << (8 * L))));
+    __syncthreads();
+    for (int o = t; o < nrows * kF; o += kRbThreads) {
+        const int lr = o >> 4, f = o & 15;
+        const int row = r0 + lr;
+        const float r = s[row] * (float)ldexp((double)(int64_t)sums[o], -e_sh[f]);
+        float* out = y + (int64_t)row * ldy + f;
+        *out = beta ? *out + r : r;
+    }
+}
+
 }  // namespace lds
 
 using namespace lds;
@@ -677,19 +932,40 @@ extern "C" int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, c
 }
 
 // Workspace of lds_spmm_norm_dense: lds_aggregate_bitmask's column maxima and
-// digit chunks.
+// digit chunks, then the row-block kernel's bit slabs (or the tile kernel's
+// partials, the larger of the two).
+static int64_t dense_scratch_off(int n) { return (int64_t)kMaxBlocks * kF * 4 + (int64_t)chunks_of(n) * kChunkBytes; }
 extern "C" int64_t lds_spmm_dense_ws_bytes(int n) {
     if (n <= 0) return 0;
-    return (int64_t)kMaxBlocks * kF * 4 + (int64_t)chunks_of(n) * kChunkBytes + (int64_t)kDnMaxGrid * kDnPartBytes;
+    const int64_t slabs = rb_scratch_rows(n) * 64 * chunks_of(n);
+    const int64_t parts = (int64_t)kDnMaxGrid * kDnPartBytes;
+    return dense_scratch_off(n) + (slabs > parts ? slabs : parts);
 }
 
 extern "C" int lds_spmm_dense_max_n(void) { return kDnMaxChunks * kChunk; }
 
+static int device_cus() {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus > 0 ? cus : 256;
+}
+
+// > 64 KB of dynamic LDS must be enabled per kernel (and device): set on
+// every launch, it is a cheap host call.
+template <typename K>
+static hipError_t allow_lds(K kernel, int bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               bytes);
+}
+
+// grid: > 0 workgroups of the row-block kernel (0: one per CU); < 0: the
+// round-3 tile kernel (csr_dense_agg_kernel) on -grid workgroups (A/B timing).
 extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                    int ldz, float* y, int ldy, int beta, void* ws, int grid, int quantize,
                                    void* stream) {
     LDS_CHECK_ARG(row_ptr && col && s && z && y && ws && n > 0 && n <= kDnMaxChunks * kChunk);
-    LDS_CHECK_ARG(ldz >= kF && ldy >= kF && grid >= 0);
+    LDS_CHECK_ARG(ldz >= kF && ldy >= kF);
     LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
     hipStream_t st = (hipStream_t)stream;
     const Ws w = carve(ws, n);
@@ -699,28 +975,42 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
         hipLaunchKernelGGL(bitagg_quant_kernel, dim3(nc * kSteps * 4 * kF * 4 / 256), dim3(256), 0, st, s, n, z,
                            ldz, (const uint32_t*)w.colmax, w.zq, nc);
     }
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
-    const int ntile = (n + 15) / 16;
-    int g = grid > 0 ? grid : cus;
-    if (g > kDnMaxGrid) g = kDnMaxGrid;
-    if (g > ntile) g = ntile;
-    int64_t* parts = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(ws) + (int64_t)kMaxBlocks * kF * 4 +
-                                                (int64_t)nc * kChunkBytes);
-    const int lds = dense_lds_bytes(nc);
-    static int attr_bytes = 0;  // > 64 KB of dynamic LDS must be enabled per kernel
-    if (attr_bytes < lds) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_dense_agg_kernel<0>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    char* scratch = reinterpret_cast<char*>(ws) + dense_scratch_off(n);
+    const int cus = device_cus();
+    if (grid < 0) {  // the tile kernel
+        const int ntile = (n + 15) / 16;
+        int g = -grid;
+        if (g > kDnMaxGrid) g = kDnMaxGrid;
+        if (g > ntile) g = ntile;
+        const int lds = dense_lds_bytes(nc);
+        const hipError_t e = allow_lds(&csr_dense_agg_kernel<0>, lds);
         if (e != hipSuccess) return (int)e;
-        attr_bytes = lds;
+        hipLaunchKernelGGL(csr_dense_agg_kernel<0>, dim3(g), dim3(kDnThreads), lds, st, row_ptr, col, n,
+                           (const int8_t*)w.zq, nc, (const uint32_t*)w.colmax, s, y, ldy, beta,
+                           reinterpret_cast<int64_t*>(scratch));
+        LDS_RETURN_LAST_ERROR();
     }
-    hipLaunchKernelGGL(csr_dense_agg_kernel<0>, dim3(g), dim3(kDnThreads), lds, st, row_ptr, col, n,
-                       (const int8_t*)w.zq, nc, (const uint32_t*)w.colmax, s, y, ldy, beta, parts);
+    int g = grid > 0 ? grid : cus;
+    const int gmin = (n + 16 * kRbMaxTiles - 1) / (16 * kRbMaxTiles);  // at most kRbMaxTiles tiles per block
+    if (g < gmin) g = gmin;
+    if (g > kRbMaxGrid) g = kRbMaxGrid;
+    const int R = (n + g - 1) / g;
+    LDS_CHECK_ARG(R <= 16 * kRbMaxTiles);
+    g = (n + R - 1) / R;  // every block has rows
+    const int tiles = (R + 15) / 16;
+    LDS_CHECK_ARG((int64_t)g * tiles * 16 <= rb_scratch_rows(n));
+    uint32_t* slabs = reinterpret_cast<uint32_t*>(scratch);
+#define LDS_RB_LAUNCH(TT)                                                                                        \
+    do {                                                                                                         \
+        const int lds = rb_lds_bytes(nc, TT);                                                                    \
+        const hipError_t e = allow_lds(&csr_rowblock_agg_kernel<TT>, lds);                                       \
+        if (e != hipSuccess) return (int)e;                                                                      \
+        hipLaunchKernelGGL(csr_rowblock_agg_kernel<TT>, dim3(g), dim3(kRbThreads), lds, st, row_ptr, col, n, R, \
+                           (const int8_t*)w.zq, nc, (const uint32_t*)w.colmax, s, y, ldy, beta, slabs);         \
+    } while (0)
+    if (tiles <= 2) LDS_RB_LAUNCH(2);
+    else if (tiles <= 4) LDS_RB_LAUNCH(4);
+    else LDS_RB_LAUNCH(6);
+#undef LDS_RB_LAUNCH
     LDS_RETURN_LAST_ERROR();
 }

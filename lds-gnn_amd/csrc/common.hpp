@@ -19,6 +19,8 @@ constexpr int kEllWidth = 64;  // neighbours per row in a graph's ELL head ({j, 
 // byte (e.g. train / opt mask bits, include/ldsgnn.h) above them.
 constexpr int kEllIndex = 0x00FFFFFF;
 constexpr int kEllFlagShift = 24;
+// Device error word bits (include/ldsgnn.h LDS_DEVERR_*).
+constexpr uint32_t kDevErrFillDegree = 1u;
 
 // Packed upper-triangle index of (i, j), i <= j, of an n×n matrix in
 // torch.triu_indices(n, n) row-major order (src/utils/graph.py:41-45).

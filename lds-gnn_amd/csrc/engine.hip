@@ -17,7 +17,6 @@
 // replays advance them.
 #include "common.hpp"
 #include "fill.hpp"
-#include "side.hpp"
 #include "../../include/ldsgnn.h"
 
 namespace lds {
@@ -91,6 +90,8 @@ struct EngineScalars {
     int32_t hyper_steps;  // hyper steps taken so far
     double outer_lr;      // current SGD lr on θ (StepLR applied after each hyper step)
     double lr_decay;      // StepLR gamma (1.0 = none)
+    uint32_t error;       // device error word (include/ldsgnn.h LDS_DEVERR_*): set by kernels, read by the host
+    uint32_t pad;
 };
 
 struct Keys {
@@ -107,7 +108,6 @@ struct Batch {
     const uint8_t* hflag;
     int nh;
     int asplit;             // > 0: `agg` holds asplit partial n × 16 arrays (LdsBatch.agg_splits)
-    SideWork side;          // blocks appended to the grid (LdsBatch.side, side.hpp)
 };
 
 // kB = false (single-sample launch): no offset code at all.
@@ -576,11 +576,12 @@ __global__ __launch_bounds__(256) void fill_x_linear_kernel(
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc,
-    const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
+    const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt,
+    uint32_t* __restrict__ err) {
     const int fb = (n + 15) / 16;
     const int b = blockIdx.x;
     if (b < fb * graphs) {
-        fill_csr_block(b % fb, b / fb, bits, n, words, dacc, wsi, row_ptr, gcol, capacity, gs, ell, flags);
+        fill_csr_block(b % fb, b / fb, bits, n, words, dacc, wsi, row_ptr, gcol, capacity, gs, ell, flags, err);
         return;
     }
     x_linear_rows<false>(b - fb * graphs, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep, scale,
@@ -640,8 +641,6 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
-    if constexpr (!kB && !kAgg)
-        if (side_block(bt.side, n)) return;  // a draw tile of the window's next graph (side.hpp)
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
     if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
@@ -1378,8 +1377,6 @@ __global__ __launch_bounds__(256) void fwd2_bwd2_kernel(
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth, int r_assign,
     const float* __restrict__ dmask, Batch bt) {
-    if constexpr (!kB)
-        if (side_block(bt.side, n)) return;  // a fill block of the window's next graph (side.hpp)
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;
     rp = boff<kB>(rp, bt.rp);
@@ -2281,20 +2278,6 @@ static inline int mk_batch(const LdsBatch* b, Batch& bt) {
     bt.xval = b->xval; bt.xd = b->xd; bt.uv = b->uv; bt.part = b->part; bt.met = b->met; bt.tag = b->tag_step;
     return b->samples;
 }
-// Side work of a launch (LdsBatch.side, side.hpp) into bt.side; returns the
-// blocks to append to grid.x, or -1 if the launch cannot carry it (batched
-// samples, the precomputed-aggregation variant, incomplete pointers).
-static inline int side_blocks(const LdsBatch* b, int n, int ns, bool plain, Batch& bt) {
-    if (b == nullptr || b->side == nullptr) return 0;
-    const LdsSideWork* h = b->side;
-    if (ns != 1 || !plain || h->words < (n + 63) / 64 || n > kEllIndex + 1) return -1;
-    if (h->theta != nullptr && (h->bits == nullptr || h->deg == nullptr)) return -1;
-    if (h->fill_bits != nullptr &&
-        (h->fill_deg == nullptr || h->row_ptr == nullptr || h->col == nullptr || h->s == nullptr || h->col_capacity <= 0))
-        return -1;
-    bt.side = side_of(h, n);
-    return bt.side.draw_blocks + bt.side.fill_blocks;
-}
 // lds_engine_xt_adam pairs samples per wave by shape from this many samples
 // on (MI355X, profiles/r03_xt_pair_ab.jsonl: Citeseer S = 16 56.6 -> 41.6 µs
 // per call, Cora S = 16 30.9 -> 28.8; at Cora S = 8 the doubled walk per wave
@@ -2324,6 +2307,11 @@ static inline int plan_heavy(const LdsBatch* b) {
 
 static inline bool batch_ok(const LdsBatch* b) {
     return b == nullptr || (b->samples >= 1 && b->samples <= 65535 && (b->ell & 1) == 0);
+}
+// The error word of an engine's scalars (fill kernels report into it).
+static inline uint32_t* engine_error_word(const void* scalars) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(const_cast<void*>(scalars)) +
+                                       offsetof(EngineScalars, error));
 }
 static inline Keys mk_keys(uint64_t seed, uint32_t tag_x, uint32_t tag_h) {
     return Keys{(uint32_t)seed, (uint32_t)(seed >> 32), tag_x, tag_h};
@@ -2369,7 +2357,7 @@ extern "C" int lds_engine_fill_x_linear(const uint64_t* bits, int words, const i
                        deg_ws, lds_sample_ws_ints(n), graphs, row_ptr, col, col_stride, s, (int2*)ell, node_flags,
                        xrp, xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars,
                        fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, xhead, (const int2*)xinfo, head_vals,
-                       bt);
+                       bt, engine_error_word(scalars));
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -2395,9 +2383,7 @@ extern "C" int lds_engine_fwd_layer1(const int* rp, const int* col, const float*
     GcnW w{nullptr, nullptr, w1, b1};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    const int extra = side_blocks(batch, n, ns, agg == nullptr, bt);
-    LDS_CHECK_ARG(extra >= 0);
-    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch) + extra, ns), dim3(256), 0, (hipStream_t)stream, rp,
+    LDS_LAUNCH_BA(fwd_layer1_kernel, ns, agg, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0, (hipStream_t)stream, rp,
                        col, s, (const int2*)ell, n, h0, y0, h1d, h2, w, c, mk_keys(seed, 0, tag_h),
                        (const EngineScalars*)scalars, fwd_off, train, keep, scale, dmask, agg, bt);
     LDS_RETURN_LAST_ERROR();
@@ -2569,9 +2555,7 @@ extern "C" int lds_engine_fwd2_bwd2(const int* rp, const int* col, const float* 
     GcnW w{nullptr, nullptr, w1, nullptr};
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    const int extra = side_blocks(batch, n, ns, true, bt);
-    LDS_CHECK_ARG(extra >= 0);
-    LDS_LAUNCH_B(fwd2_bwd2_kernel, ns, dim3(wave_blocks(n) + plan_heavy(batch) + extra, ns), dim3(256), 0,
+    LDS_LAUNCH_B(fwd2_bwd2_kernel, ns, dim3(wave_blocks(n) + plan_heavy(batch), ns), dim3(256), 0,
                  (hipStream_t)stream, rp, col, s, (const int2*)ell, n, node_flags, mask_bit, h2, o, p, d_o, label,
                  inv_count, lossrow, corrrow, c, y0, dh2, dy0, w, mk_keys(seed, 0, tag_h),
                  (const EngineScalars*)scalars, fwd_off, train, keep, scale, U, V, ldk, R, foff, fwidth, r_assign,

@@ -19,8 +19,9 @@ constexpr int kDenseRowFill = 1024;
 // One row of the fused fill with a whole wave (rows of kDenseRowFill or more
 // entries, or a wave that holds one): ascending columns into col from
 // position pre, the first 64 into head.
-__device__ __forceinline__ void fill_row_wave(const uint64_t* __restrict__ rb_bits, int nbw, int64_t pre, int deg,
-                                              int* __restrict__ col, int64_t capacity, int* __restrict__ head) {
+// Returns the entries the row's bits hold (written from pre on, up to capacity).
+__device__ __forceinline__ int64_t fill_row_wave(const uint64_t* __restrict__ rb_bits, int nbw, int64_t pre, int deg,
+                                                 int* __restrict__ col, int64_t capacity, int* __restrict__ head) {
     const int lane = wave_lane();
     int64_t base = pre;
     if (deg < kDenseRowFill) {  // each lane pops its own word's bits
@@ -40,7 +41,7 @@ __device__ __forceinline__ void fill_row_wave(const uint64_t* __restrict__ rb_bi
             }
             base += __builtin_amdgcn_readlane(incl, 63);
         }
-        return;
+        return base - pre;
     }
     // dense rows: for every non-zero word (uniform loop over a ballot) lane l
     // tests bit l; the word's entries go out as one contiguous store
@@ -65,6 +66,24 @@ __device__ __forceinline__ void fill_row_wave(const uint64_t* __restrict__ rb_bi
             base += __popcll(wd);
         }
     }
+    return base - pre;
+}
+
+// A row whose bits hold `got` entries where its degree count says `deg`
+// (a degree workspace that was not zero on entry, or counts from another
+// draw): row_ptr came from the counts, so slots [pre + got, pre + deg) would
+// keep whatever col held before — stale or never-written indices that the
+// aggregations gather through.  They are written with the row itself (a
+// valid index: wrong weights, never an address outside the graph) and the
+// device error word gets kDevErrFillDegree, which the host reads and raises
+// (include/ldsgnn.h "Device error word").  got > deg (counts short of the
+// bits) spills into the next row's slots, still with valid indices; flagged
+// the same way.  lane / lanes: this row's threads (16 or 64).
+__device__ __forceinline__ void fill_degree_guard(int64_t pre, int64_t got, int deg, int row, int* __restrict__ col,
+                                                  int64_t capacity, int lane, int lanes, uint32_t* __restrict__ err) {
+    if (got == (int64_t)deg) return;
+    for (int64_t q = pre + got + lane; q < pre + deg && q < capacity; q += lanes) col[q] = row;
+    if (lane == 0 && err != nullptr) atomicOr(err, kDevErrFillDegree);
 }
 
 // The CSR fill of the fused sampler: the tile kernel's degree counts give
@@ -82,7 +101,8 @@ __device__ __forceinline__ void fill_row_wave(const uint64_t* __restrict__ rb_bi
 __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* __restrict__ bits, int n, int words,
                                                const int* __restrict__ dacc, int wsi, int* __restrict__ row_ptr,
                                                int* __restrict__ col, int64_t capacity, float* __restrict__ s,
-                                               int2* __restrict__ ell, const uint8_t* __restrict__ flags) {
+                                               int2* __restrict__ ell, const uint8_t* __restrict__ flags,
+                                               uint32_t* __restrict__ err) {
     __shared__ int red[4];
     __shared__ int dblk[16];  // exclusive scan of the block's 16 row degrees
     __shared__ int head[16][kEllWidth];
@@ -152,13 +172,16 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
             }
             base += row16_last_int(incl);
         }
+        if (live) fill_degree_guard(pre, base - pre, deg, row, col, capacity, h, 16, err);
     } else {
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {  // the wave's four rows, one at a time
             const int kq = wave * 4 + q, rq = row0 + kq;
             if (rq >= n) break;
-            fill_row_wave(bits + (int64_t)rq * words, nbw, (int64_t)bpre + dblk[kq], dacc[rq], col, capacity,
-                          head[kq]);
+            const int64_t pq = (int64_t)bpre + dblk[kq];
+            const int dq = dacc[rq];
+            const int64_t got = fill_row_wave(bits + (int64_t)rq * words, nbw, pq, dq, col, capacity, head[kq]);
+            fill_degree_guard(pq, got, dq, rq, col, capacity, lane, 64, err);
         }
     }
     if (ell == nullptr || !live) return;

@@ -345,8 +345,9 @@ __global__ __launch_bounds__(256) void fill_csr_fused_kernel(const uint64_t* __r
                                                               int* __restrict__ row_ptr, int* __restrict__ col,
                                                               int64_t capacity, float* __restrict__ s,
                                                               int2* __restrict__ ell,
-                                                              const uint8_t* __restrict__ flags) {
-    fill_csr_block(blockIdx.x, blockIdx.y, bits, n, words, dacc, wsi, row_ptr, col, capacity, s, ell, flags);
+                                                              const uint8_t* __restrict__ flags,
+                                                              uint32_t* __restrict__ err) {
+    fill_csr_block(blockIdx.x, blockIdx.y, bits, n, words, dacc, wsi, row_ptr, col, capacity, s, ell, flags, err);
 }
 
 __global__ void csr_degree_scale_kernel(const int* __restrict__ row_ptr, int n,
@@ -479,12 +480,6 @@ __global__ void __launch_bounds__(256) zero_ints_kernel(int* __restrict__ p, int
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) p[i] = 0;
 }
 
-// 1 (default): the window's graphs loop inside the tile block over one θ
-// load; 0: one block per (tile, graph) unless θ is past the MALL.  Measured at
-// Cora (6 graphs per window): 31.0 µs / 21.9 MB fetched per launch looping
-// against 30.8 µs / 113.9 MB, bench 12.64k vs 12.60k steps/s.  Returns the
-// previous setting.
-
 // The outer SGD step + clamp (lds_engine_sgd_clamp) and the NEXT window's
 // draw of `count` graphs × `samples` replicas from the θ it writes, in one
 // pass over the triangle: graph g, sample b takes counter counter_offset + g
@@ -521,7 +516,7 @@ __global__ __launch_bounds__(256) void degree_scale_kernel(const int* __restrict
 // s only (row_ptr, ell unused, may be NULL).
 extern "C" int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const int* deg_ws, int graphs,
                                    int* row_ptr, int* col, int64_t col_stride, float* s, int* ell,
-                                   const uint8_t* node_flags, void* stream) {
+                                   const uint8_t* node_flags, uint32_t* err, void* stream) {
     LDS_CHECK_ARG(bits && deg_ws && s && n > 0 && n <= kEllIndex + 1);
     LDS_CHECK_ARG(col == nullptr || (row_ptr != nullptr && col_stride > 0));
     LDS_CHECK_ARG(graphs > 0 && graphs <= 65535 && words >= (n + 63) / 64);
@@ -531,7 +526,8 @@ extern "C" int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const
         LDS_RETURN_LAST_ERROR();
     }
     hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 15) / 16, graphs), dim3(256), 0, (hipStream_t)stream, bits,
-                       n, words, deg_ws, lds_sample_ws_ints(n), row_ptr, col, col_stride, s, (int2*)ell, node_flags);
+                       n, words, deg_ws, lds_sample_ws_ints(n), row_ptr, col, col_stride, s, (int2*)ell, node_flags,
+                       err);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -547,7 +543,7 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
                                        uint32_t counter_offset, int count, int samples, uint64_t* bits,
                                        int words, int* deg_ws, int* row_ptr, int* col, int64_t col_stride,
                                        float* s, int* ell, const uint8_t* node_flags, int ws_zeroed,
-                                       void* stream) {
+                                       uint32_t* err, void* stream) {
     // col == NULL: bitmask, degrees and s only (the bitmask aggregation of
     // dense graphs reads no CSR); row_ptr / ell are then not written.
     // deg_ws: lds_sample_ws_ints(n) ints per graph (degrees first); with CSR
@@ -605,7 +601,7 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
         LDS_RETURN_LAST_ERROR();
     }
     hipLaunchKernelGGL(fill_csr_fused_kernel, dim3((n + 15) / 16, graphs), dim3(256), 0, st, bits, n, words,
-                       (const int*)deg_ws, wsi, row_ptr, col, col_stride, s, (int2*)ell, node_flags);
+                       (const int*)deg_ws, wsi, row_ptr, col, col_stride, s, (int2*)ell, node_flags, err);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -614,7 +610,7 @@ extern "C" int lds_sample_graphs(const float* theta, int n, uint64_t seed, uint3
                                  uint64_t* bits, int words, int* deg_ws, int* row_ptr, int* col,
                                  int64_t col_stride, float* s, int* ell, void* stream) {
     return lds_sample_graphs_multi(theta, n, seed, tag, 0u, counter_base, counter_offset, count, 1, bits,
-                                   words, deg_ws, row_ptr, col, col_stride, s, ell, nullptr, 0, stream);
+                                   words, deg_ws, row_ptr, col, col_stride, s, ell, nullptr, 0, nullptr, stream);
 }
 
 extern "C" int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32_t tag,

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -36,9 +36,9 @@ SIGNATURES = {
     "lds_sample_graphs": [P, c_int, c_uint64, c_uint32, P, c_uint32, c_int, P, c_int, P, P, P, c_int64, P, P,
                           P],
     "lds_sample_graphs_multi": [P, c_int, c_uint64, c_uint32, c_uint32, P, c_uint32, c_int, c_int, P, c_int, P,
-                                P, P, c_int64, P, P, P, c_int, P],
+                                P, P, c_int64, P, P, P, c_int, P, P],
     "lds_sample_ws_ints": [c_int],
-    "lds_sample_fill_csr": [P, c_int, c_int, P, c_int, P, P, c_int64, P, P, P, P],
+    "lds_sample_fill_csr": [P, c_int, c_int, P, c_int, P, P, c_int64, P, P, P, P, P],
     "lds_sgd_sample_graphs": [P, P, P, c_int, c_uint64, c_uint32, c_uint32, c_uint32, c_int, c_int, P, c_int, P,
                               P],
     "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int, P],
@@ -129,6 +129,25 @@ SIGNATURES = {
 
 class NativeError(RuntimeError):
     """A hot-path entry point returned a HIP error."""
+
+
+class DeviceError(RuntimeError):
+    """A kernel reported an input it could not use faithfully through a
+    device error word (include/ldsgnn.h "Device error word")."""
+
+
+DEVERR_FILL_DEGREE = 1  # LDS_DEVERR_FILL_DEGREE
+
+_DEVERR_TEXT = {DEVERR_FILL_DEGREE: "a CSR fill found a row whose degree count differs from its drawn bits "
+                                    "(degree workspace not zero on entry, or counts of another draw); its "
+                                    "slots past the drawn entries hold the row's own index"}
+
+
+def raise_device_error(word: int, what: str) -> None:
+    """Raise DeviceError for a non-zero device error word."""
+    if word:
+        msgs = [t for b, t in _DEVERR_TEXT.items() if word & b] or [f"unknown bits {word:#x}"]
+        raise DeviceError(f"{what}: device error word {word:#x}: " + "; ".join(msgs))
 
 
 def _load() -> ctypes.CDLL:
@@ -252,18 +271,7 @@ class LdsBatch(ctypes.Structure):
     _fields_ = [("samples", ctypes.c_int32), ("tag_step", ctypes.c_uint32)] + [
         (f, ctypes.c_int64) for f in ("act", "row", "rp", "col", "ell", "par", "xval", "xd", "uv", "part", "met")] + [
         ("heavy_rows", ctypes.c_void_p), ("heavy_flag", ctypes.c_void_p), ("n_heavy", ctypes.c_int32),
-        ("agg_splits", ctypes.c_int32), ("side", ctypes.c_void_p), ("xt_pair", ctypes.c_int32)]
-
-
-class LdsSideWork(ctypes.Structure):
-    """include/ldsgnn.h LdsSideWork: a graph draw and / or fill carried by
-    extra blocks of a single-sample fwd_layer1 / fwd2_bwd2 launch."""
-    _fields_ = [("theta", ctypes.c_void_p), ("seed", ctypes.c_uint64), ("tag", ctypes.c_uint32),
-                ("counter_offset", ctypes.c_uint32), ("counter_base", ctypes.c_void_p), ("bits", ctypes.c_void_p),
-                ("words", ctypes.c_int32), ("deg", ctypes.c_void_p), ("fill_bits", ctypes.c_void_p),
-                ("fill_deg", ctypes.c_void_p), ("row_ptr", ctypes.c_void_p), ("col", ctypes.c_void_p),
-                ("col_capacity", ctypes.c_int64), ("s", ctypes.c_void_p), ("ell", ctypes.c_void_p),
-                ("node_flags", ctypes.c_void_p)]
+        ("agg_splits", ctypes.c_int32), ("xt_pair", ctypes.c_int32)]
 
 
 def batch_ptr(b) -> int:

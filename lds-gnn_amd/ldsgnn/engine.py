@@ -208,11 +208,13 @@ class LdsEngine:
         self.off_b1 = self.off_w1 + c * HID
         self.n_wd = self.off_w1  # group 0 = layer_in (weight + bias)
 
-        # device scalars {u32 graph_ctr, u32 fwd_ctr, i32 adam_step, i32 hyper, f64 lr, f64 decay}
-        assert nat.lib.lds_engine_scalars_size() == 32
-        self.scalars = torch.zeros(32, dtype=torch.uint8, device=dev)
+        # device scalars {u32 graph_ctr, u32 fwd_ctr, i32 adam_step, i32 hyper, f64 lr, f64 decay,
+        # u32 error, u32 pad}: `error` is the device error word the window fills report into
+        assert nat.lib.lds_engine_scalars_size() == 40
+        self.scalars = torch.zeros(40, dtype=torch.uint8, device=dev)
         self._i32 = self.scalars[:16].view(torch.int32)
-        self._f64 = self.scalars[16:].view(torch.float64)
+        self._f64 = self.scalars[16:32].view(torch.float64)
+        self._err = self.scalars[32:36].view(torch.int32)
         self._i32.copy_(torch.tensor([self.gen.graph_counter, self.gen.forward_counter, 0, 0], dtype=torch.int32))
         self._f64.copy_(torch.tensor([outer_lr, 1.0 if lr_decay is None else lr_decay], dtype=torch.float64))
 
@@ -257,16 +259,6 @@ class LdsEngine:
         self.prefetch_draw = False
         self._prefetched = False
         self._deg_next = None
-        # spread draws (with prefetch): the hyper step draws only graph 0 of
-        # the next window; inner step t draws graph t + 1 in blocks appended
-        # to its first aggregation and fills it beside its second
-        # (LdsSideWork, include/ldsgnn.h).  Off by default: on MI355X (Cora,
-        # τ = 5) the θ-grad entry drops 57.7 -> 42.3 µs but each appended
-        # draw re-reads θ and lengthens fwd_layer1 by 5.3 µs (4.2 -> 9.4),
-        # 13.48k vs 14.10k steps/s (profiles/r03_spread_draw.json)
-        self.spread_draw = False
-        self._prefetched_spread = False  # the prefetched state holds graph 0 only
-        self._spread_window = False  # this window's graphs 1..τ come from side work
 
         # tape
         self.tau = max(1, int(tau))
@@ -448,38 +440,6 @@ class LdsEngine:
         self.bt = nat.batch_ptr(self._bt)
         self.btx = nat.batch_ptr(self._btx)
         self.bt2 = nat.batch_ptr(self._bt2)
-        self._side_bt = {}  # inner step -> (fwd_layer1 batch, fwd2_bwd2 batch) with side work
-
-    def _side_batches(self, t: int):
-        """LdsBatch copies for inner step t of a spread window: the first
-        aggregation draws graph t + 1 (counter pending + t + 1, the counter
-        the window's batched draw gives it), the second fills its CSR / s /
-        ELL head.  Kept alive on self (the launches read them on the host)."""
-        hit = self._side_bt.get(t)
-        if hit is not None:
-            return hit
-        gb, P, g = self.gbatch, nat.ptr, t + 1
-
-        def at(x: torch.Tensor) -> int:
-            return P(x) + g * x[0].numel() * x.element_size()
-        draw = nat.LdsSideWork(theta=P(self.theta), seed=self.seed, tag=self.tag_graph, counter_offset=g,
-                               counter_base=P(self.scalars), bits=at(gb.bits), words=self.words, deg=at(gb.deg))
-        fill = nat.LdsSideWork(words=self.words, fill_bits=at(gb.bits), fill_deg=at(gb.deg), row_ptr=at(gb.row_ptr),
-                               col=at(gb.col), col_capacity=max(self.cap, 1), s=at(gb.s), ell=at(gb.ell),
-                               node_flags=P(self.nflag))
-        b1 = nat.LdsBatch.from_buffer_copy(self._bt)
-        b2 = nat.LdsBatch.from_buffer_copy(self._bt2)
-        b1.side, b2.side = ctypes.addressof(draw), ctypes.addressof(fill)
-        hit = self._side_bt[t] = (b1, b2, draw, fill, nat.batch_ptr(b1), nat.batch_ptr(b2))
-        return hit
-
-    def _spread_ok(self, T: int, grad_reducer=None) -> bool:
-        """Spread draws apply: one sample, the two-hop kernels (inner steps
-        end in lds_engine_fwd2_bwd2), short rows (the plain aggregation
-        launches carry the side blocks), one θ, a full window, no exchange."""
-        return (self.spread_draw and self.S == 1 and self.two_hop and not self.long_rows and self.theta_fn is None
-                and self.outer_update is None and grad_reducer is None and T == self.tau
-                and self.gbatch.count == self.tau + 1)
 
     def _grow(self, slots: int):
         self._layout_version += 1
@@ -575,6 +535,7 @@ class LdsEngine:
             sums.append(torch.stack([sl.lossrow[0].sum(), sl.corrrow[0].sum(), self._eval_rows[0].sum(),
                                      self._eval_rows[1].sum()]))
         host = torch.stack(sums).double().cpu().numpy()
+        self.check_device_error()
         return (float(np.mean(host[:, 0] * inv_v)), float(np.mean(host[:, 1] * inv_v)),
                 float(np.mean(host[:, 2] * inv_t)), float(np.mean(host[:, 3] * inv_t)))
 
@@ -605,7 +566,7 @@ class LdsEngine:
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta), n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, E, 1, nat.ptr(g.bits), self.words,
                  nat.ptr(self._evb_deg), nat.ptr(g.row_ptr), nat.ptr(g.col), self.cap, nat.ptr(g.s),
-                 nat.ptr(g.ell), nat.ptr(self.nflag), 0, st)
+                 nat.ptr(g.ell), nat.ptr(self.nflag), 0, self._err_ptr(), st)
         self.pending_graph += E
         self._forward(sl, self._evb_w, vm, inv_v, 0, 0, bt=bt)  # val rows -> sl.lossrow / corrrow [E, n]
         rl, rc = self._evb_rows[0], self._evb_rows[1]
@@ -613,6 +574,7 @@ class LdsEngine:
                  nat.ptr(sl.h2), 0, 0, 0, nat.ptr(self.label), nat.ptr(tm), inv_t, nat.ptr(rl), nat.ptr(rc), c, 0,
                  bt, st)
         host = torch.stack([sl.lossrow.sum(1), sl.corrrow.sum(1), rl.sum(1), rc.sum(1)], 1).double().cpu().numpy()
+        self.check_device_error()
         return (float(np.mean(host[:, 0] * inv_v)), float(np.mean(host[:, 1] * inv_v)),
                 float(np.mean(host[:, 2] * inv_t)), float(np.mean(host[:, 3] * inv_t)))
 
@@ -675,7 +637,7 @@ class LdsEngine:
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta if theta is None else theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(g.bits), self.words,
                  nat.ptr(self.deg), nat.ptr(g.row_ptr), self._col_arg(g.col), self.cap, nat.ptr(g.s),
-                 nat.ptr(g.ell), nat.ptr(self.nflag), 0, self._stream())
+                 nat.ptr(g.ell), nat.ptr(self.nflag), 0, self._err_ptr(), self._stream())
         self._block_ptrs([g])
         self.pending_graph += 1
 
@@ -880,18 +842,14 @@ class LdsEngine:
         path would give it."""
         self._flush_fill()
         gb = self.gbatch
-        self._spread_window = False
         if self._prefetched:  # bits + degrees drawn by the last hyper step (lds_theta_grad_sgd_draw)
-            # spread: graph 0 only; the inner steps draw and fill the rest
-            self._spread_window = self._prefetched_spread
-            nfill = 1 if self._prefetched_spread else count * self.S
-            fill = (nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), nfill, nat.ptr(gb.row_ptr),
+            fill = (nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), count * self.S, nat.ptr(gb.row_ptr),
                     self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell), nat.ptr(self.nflag))
             if self.fuse_fill and self.S == 1 and not self.long_rows:
                 # deferred: the first inner step's X product launches it (lds_engine_fill_x_linear)
                 self._pending_fill = fill
             else:
-                nat.call("lds_sample_fill_csr", fill[0], self.n, *fill[1:], self._stream())
+                nat.call("lds_sample_fill_csr", fill[0], self.n, *fill[1:], self._err_ptr(), self._stream())
             self._prefetched = False
         elif self.async_draw and count > 1 and not self.long_rows:
             # graph 0 on the main stream; graphs 1 .. count-1 on the side stream,
@@ -911,7 +869,7 @@ class LdsEngine:
         before the first X product)."""
         if self._pending_fill is not None:
             f, self._pending_fill = self._pending_fill, None
-            nat.call("lds_sample_fill_csr", f[0], self.n, *f[1:], self._stream())
+            nat.call("lds_sample_fill_csr", f[0], self.n, *f[1:], self._err_ptr(), self._stream())
 
     def _draw_range(self, g0: int, count: int, stream: int):
         """Graphs g0 .. g0 + count - 1 of the window (all samples), counters
@@ -923,7 +881,7 @@ class LdsEngine:
         nat.call("lds_sample_graphs_multi", P(self.theta), self.n, self.seed, self.tag_graph, 1, P(self.scalars),
                  self.pending_graph + g0, count, S, at(gb.bits), self.words, at(gb.deg), at(gb.row_ptr),
                  at(gb.col) if not self.bitmask_agg else 0, max(self.cap, 1), at(gb.s), at(gb.ell),
-                 P(self.nflag), 1 if self._ws_clean else 0, stream)
+                 P(self.nflag), 1 if self._ws_clean else 0, self._err_ptr(), stream)
 
     def _join_draw(self):
         """The window's later graphs (drawn on the side stream) are complete
@@ -943,7 +901,6 @@ class LdsEngine:
         it then finds); gbatch.deg holds their degrees, so it is cleared first."""
         if self._prefetched:
             self._prefetched = False
-            self._prefetched_spread = False
             self._ws_clean = False
 
     def _planes_window(self, T: int, grad_reducer) -> bool:
@@ -1019,11 +976,10 @@ class LdsEngine:
             self._sample(sl.g)
         fwd_off = self.pending_fwd
         self._fwd_of[t] = fwd_off
-        side = self._side_batches(t) if presampled and self._spread_window else (None,) * 6
         self._forward(sl, self.w[t], self.train_mask, self.inv_train, self.train_flag, fwd_off,
-                      loss_in_backward=True, bt_l1=side[4])
+                      loss_in_backward=True)
         self._backward(sl, self.w[t], self.g, self.train_flag, fwd_off, self.metrics[t], False, 1, t,
-                       mask_bit=1, inv_count=self.inv_train, bt2=side[5])
+                       mask_bit=1, inv_count=self.inv_train)
         if self.train_flag:
             self.pending_fwd += 1
         self.t = t + 1
@@ -1082,7 +1038,6 @@ class LdsEngine:
             k0 = self.kg  # the last chunk (graph 0) + R on the main stream
         else:
             k0 = T * self.kg + HID + self.cw
-        spread = self._spread_ok(T, grad_reducer)  # the next window draws graphs 1..τ itself
         if self.S > 1:
             drew = self._assemble_samples(k0, grad_reducer, presampled)
         elif grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
@@ -1094,7 +1049,7 @@ class LdsEngine:
                 if presampled and self._prefetch_ok(T, k0):
                     if self._deg_next is None:
                         self._deg_next = torch.zeros_like(self.gbatch.deg)
-                    graphs = 1 if spread else self.gbatch.count
+                    graphs = self.gbatch.count
                     bits, deg = nat.ptr(self.gbatch.bits), nat.ptr(self._deg_next)
                     drew = True
                 nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1, 1,
@@ -1108,7 +1063,7 @@ class LdsEngine:
                 nat.call("lds_theta_grad_sgd_draw", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R),
                          1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
                          nat.ptr(self.scalars), self.seed, self.tag_graph, nat.ptr(self.scalars), self.pending_graph,
-                         1 if spread else gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next),
+                         gb.count, nat.ptr(gb.bits), self.words, nat.ptr(self._deg_next),
                          self._form(), st)
                 drew = True
             else:
@@ -1130,8 +1085,6 @@ class LdsEngine:
                  self._tab_count(), P(self.gbatch.deg), P(self._deg_next) if drew else 0, self.gbatch.deg.numel(),
                  self.bt, st)
         self._prefetched = drew
-        self._prefetched_spread = drew and spread and self.S == 1 and grad_reducer is None
-        self._spread_window = False
         self._ws_clean = not drew
         self._planes_now = False
         self.pending_graph = 0
@@ -1431,8 +1384,7 @@ class LdsEngine:
         # assume: prefetched draws present, or none and a clean degree buffer
         self.prefetch_draw = bool(prefetch) and \
             self._prefetch_ok(tau, tau * self.kg + HID + self.cw, exchange=grad_reducer is not None, check_flag=False)
-        spread = self.prefetch_draw and self._spread_ok(tau, grad_reducer)
-        self._enter_window_state(self.prefetch_draw, tau, spread)
+        self._enter_window_state(self.prefetch_draw, tau)
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         if grad_reducer is None:
@@ -1445,7 +1397,7 @@ class LdsEngine:
                             self.run_window(tau)
                 graphs.append((w, nat.seal_graph(graph, f"{w}-window group")))
             torch.cuda.current_stream(self.dev).wait_stream(s)
-            self._graph_capture = (tuple(graphs), tau, None, self.prefetch_draw, spread)
+            self._graph_capture = (tuple(graphs), tau, None, self.prefetch_draw)
             return graphs[0][1]
         head, tail = nat.new_graph(), nat.new_graph()
         pool = torch.cuda.graph_pool_handle()
@@ -1463,46 +1415,39 @@ class LdsEngine:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         nat.seal_graph(head, "window (to the exchange)")
         nat.seal_graph(tail, "window (after the exchange)")
-        self._graph_capture = ((head, tail), tau, grad_reducer, self.prefetch_draw, spread)
+        self._graph_capture = ((head, tail), tau, grad_reducer, self.prefetch_draw)
         return head, tail
 
-    def _enter_window_state(self, prefetched: bool, tau: int, spread: bool = False) -> None:
+    def _enter_window_state(self, prefetched: bool, tau: int) -> None:
         """Bring the device to the window-start state a captured window
         assumes: with prefetch, the window's τ+1 graphs already drawn (bits +
         degrees; drawn here, eagerly, if a discard, an out-of-window draw or a
-        non-prefetching step dropped them) — with spread draws graph 0 only
-        and zero degrees for graphs 1..τ (their side draws accumulate into
-        them); without, no prefetched graphs and a zeroed degree workspace
-        (the captured draw accumulates into it)."""
+        non-prefetching step dropped them); without, no prefetched graphs and
+        a zeroed degree workspace (the captured draw accumulates into it)."""
         if prefetched:
             if self._deg_next is None:
                 self._deg_next = torch.zeros_like(self.gbatch.deg)
-            if not self._prefetched or self._prefetched_spread != spread:
+            if not self._prefetched:
                 self._flush_fill()
                 self._join_draw()
                 self.gbatch.deg.zero_()
                 self._prefetched = False
                 self._ws_clean = True
-                if spread:
-                    self._draw_range(0, 1, self._stream())  # bits + degrees (+ CSR) of graph 0
-                else:
-                    self._sample_batch(tau + 1)  # bits + degrees of this window's graphs
-                    self._join_draw()
+                self._sample_batch(tau + 1)  # bits + degrees of this window's graphs
+                self._join_draw()
                 self._prefetched = True
-                self._prefetched_spread = spread
                 self._ws_clean = False
         else:
             if self._prefetched or not self._ws_clean:
                 self.gbatch.deg.zero_()
             self._prefetched = False
-            self._prefetched_spread = False
             self._ws_clean = True
 
     def replay(self, windows: int = 1):
-        graphs, tau, reducer, prefetched, spread = self._graph_capture
+        graphs, tau, reducer, prefetched = self._graph_capture
         self._flush_fill()
         self._join_draw()  # an eager split draw still running on the side stream
-        self._enter_window_state(prefetched, tau, spread)
+        self._enter_window_state(prefetched, tau)
         if reducer is None:
             (_, one), (group, multi) = graphs[0], graphs[-1]
             for _ in range(windows // group):
@@ -1517,17 +1462,35 @@ class LdsEngine:
             tail.replay()
 
     # ------------------------------------------------------------ metrics
+    def _err_ptr(self) -> int:
+        """Address of the device error word (EngineScalars.error) the graph
+        fills report into (include/ldsgnn.h LDS_DEVERR_*)."""
+        return nat.ptr(self.scalars) + 32
+
+    def check_device_error(self) -> None:
+        """Raise nat.DeviceError if a kernel set the device error word since
+        the last check (host sync); the word is cleared first, so the engine
+        can be reset and reused.  Every host read of results (metrics,
+        scalars, empirical_mean) checks it."""
+        word = int(self._err.item())
+        if word:
+            self._err.zero_()
+            nat.raise_device_error(word & 0xFFFFFFFF, "LdsEngine")
+
     def inner_metrics(self, t: int):
         """(loss, acc) of inner step t of the last window, averaged over the
         replica samples (host sync)."""
+        self.check_device_error()
         row = self.metrics[t].double().mean(0).cpu()
         return float(row[0]) * self.inv_train, float(row[1]) * self.inv_train
 
     def outer_metrics(self):
+        self.check_device_error()
         row = self.metrics[self.tau].double().mean(0).cpu()
         return float(row[0]) * self.inv_opt, float(row[1]) * self.inv_opt
 
     def scalars_host(self):
+        self.check_device_error()
         i = self._i32.cpu().tolist()
         f = self._f64.cpu().tolist()
         return dict(graph_ctr=i[0], fwd_ctr=i[1], adam_step=i[2], hyper_steps=i[3], outer_lr=f[0], lr_decay=f[1])

@@ -118,7 +118,7 @@ def test_batched_sampler_n20000_equals_single_draws(device):
     s = torch.empty((count, 1, n), dtype=torch.float32, device=device)
     seed, tag = 99, tag_for(TAG_GRAPH, 0)
     nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 1, count, 1,
-             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, 0, 0, st)
+             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, 0, 0, 0, st)
     one = torch.empty((n, words), dtype=torch.int64, device=device)
     nb = (n + 63) // 64
     for gi in range(count):
@@ -169,9 +169,9 @@ def test_long_row_window_n20000_matches_in_kernel_aggregation(device):
 
 def test_spmm_dense_n20000_vs_bitmask_csr_and_fp64_rows(device, dense_graph):
     """The config-5 CSR-SpMM (lds_spmm_norm_dense: the CSR index stream into
-    LDS bit tiles, int8 matrix-core product) on the full-size sampled graph:
+    bit rows, int8 matrix-core product) on the full-size sampled graph:
     against fp64 rows, the bitmask aggregation and the column-blocked CSR
-    kernel, and repeatable bit for bit."""
+    kernel, repeatable bit for bit and equal to the round-3 tile kernel."""
     graph = dense_graph
     z = torch.randn(N, 16, generator=torch.Generator().manual_seed(3)).to(device)
     ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(N)), dtype=torch.uint8, device=device)
@@ -181,8 +181,12 @@ def test_spmm_dense_n20000_vs_bitmask_csr_and_fp64_rows(device, dense_graph):
         nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), N, nat.ptr(z),
                  16, nat.ptr(y), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
         outs.append(y)
+    y_tile = torch.empty(N, 16, device=device)  # the round-3 tile kernel (grid < 0): the same exact sums
+    nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), N, nat.ptr(z),
+             16, nat.ptr(y_tile), 16, 0, nat.ptr(ws), -256, 1, nat.stream_of(device))
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], y_tile)
     y = outs[0]
     y_bit = graph.spmm_bitmask(z)
     y_csr = graph.spmm(z)

@@ -686,62 +686,50 @@ def test_planes_window_bit_identical_to_fp32_factors():
     assert a.scalars_host() == b.scalars_host()
 
 
-def test_spread_draws_equal_window_draws():
-    """Spread draws (LdsEngine.spread_draw, with prefetch on single-sample
-    two-hop engines): the hyper step draws only graph 0 of the next window, inner step
-    t draws graph t + 1 in blocks appended to lds_engine_fwd_layer1 and fills
-    it in blocks appended to lds_engine_fwd2_bwd2 (LdsSideWork).  Against
-    prefetching windows that draw all τ + 1 graphs in the hyper step and
-    against eager windows: bitwise-identical θ, weights, scalars, graph bits
-    and CSR / s / ELL of the side-filled graphs; switching spread off between
-    captures redraws the window-start state."""
-    mk = lambda: run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5,  # noqa: E731
-                                       seed=9)["engine"]
-    a, b, c = mk(), mk(), mk()
-    a.spread_draw, b.spread_draw = True, False
-    a.capture_window(5, windows=2, prefetch=True)
-    b.capture_window(5, windows=2, prefetch=True)
-    assert a._graph_capture[-1] and not b._graph_capture[-1]
-    a.replay(3)
-    b.replay(3)
-    for _ in range(3):
-        c.run_window(5)
+def test_fill_degree_mismatch_raises_device_error():
+    """The round-3 bench_sp1 fault: a window whose degree
+    counts exceed its drawn bits (a drawing launch chained over the same
+    workspace) had its CSR / ELL slots past the drawn entries left as
+    whatever col held, and the aggregations gathered through them.  The fill
+    now writes those slots with the row's own index and sets the engine's
+    device error word (EngineScalars.error); the next host read raises
+    ldsgnn._native.DeviceError.  Here: inflated counts for graph 2 of a
+    captured prefetching window, col filled with an out-of-range index first
+    (never-written memory) — the replay completes, every CSR position the row
+    pointers cover holds a valid index, the padded slots hold their row, the
+    metrics read raises once and the next clean window reads normally."""
+    from ldsgnn import _native as nat
+    eng = run_engine_and_oracle(n=260, f_in=30, classes=5, steps=1, tau=5, dropout=0.5, seed=9)["engine"]
+    eng.capture_window(5, prefetch=True)
+    eng.replay(1)
+    eng.outer_metrics()  # clean windows: no error
+    n = eng.n
+    gb = eng.gbatch
+    bump = torch.zeros_like(gb.deg[2, 0])
+    bump[:40] = 3
+    bump[100:105] = 70  # past the 64-entry ELL head
+    true_deg = gb.deg[2, 0].clone()
+    gb.deg[2, 0] += bump
+    gb.col.fill_(0x7FFFFFFF)
+    eng.replay(1)
     torch.cuda.synchronize()
-
-    def same(x, y):
-        assert torch.equal(x.theta, y.theta)
-        for k, v in x.get_params().items():
-            assert torch.equal(v, y.get_params()[k]), k
-        assert x.scalars_host() == y.scalars_host()
-    same(a, c)
-    same(b, c)
-    ga, gb = a.gbatch, b.gbatch
-    assert torch.equal(ga.bits[0], gb.bits[0])  # the next window's graph 0, prefetched by both
-    for t in range(1, 6):  # the last window's graphs 1..τ: side-filled (a) vs window-start fill (b)
-        ra, rb = ga.graphs[t], gb.graphs[t]
-        assert torch.equal(ra.row_ptr, rb.row_ptr), t
-        nnz = int(ra.row_ptr.view(-1)[-1])
-        assert torch.equal(ra.col.view(-1)[:nnz], rb.col.view(-1)[:nnz]), t
-        assert torch.equal(ra.s, rb.s), t
-        assert torch.equal(ra.ell, rb.ell), t
-    # spread off for a's next capture: the window-start state is redrawn in full
-    a.spread_draw = False
-    a.capture_window(5, prefetch=True)
-    assert not a._graph_capture[-1]
-    a.replay(2)
-    for _ in range(2):
-        c.run_window(5)
-    # ... and back on, after eager steps dropped the prefetch
-    a.spread_draw = True
-    for e in (a, c):
-        e.inner_step()
-        e.hyper_step()
-    a.capture_window(5, prefetch=True)
-    a.replay(2)
-    for _ in range(2):
-        c.run_window(5)
-    torch.cuda.synchronize()
-    same(a, c)
+    with pytest.raises(nat.DeviceError):
+        eng.outer_metrics()
+    g = gb.graphs[2]
+    rp = g.row_ptr[0].long().cpu()
+    col = g.col[0].cpu()
+    nnz = int(rp[n])
+    assert nnz == int((true_deg + bump).sum())
+    assert int(col[:nnz].min()) >= 0 and int(col[:nnz].max()) < n
+    td = true_deg.long().cpu()
+    for r in (0, 39, 100, 104):
+        pad = col[int(rp[r]) + int(td[r]):int(rp[r + 1])]
+        assert pad.numel() == int(bump[r]) and bool((pad == r).all()), r
+    ell = g.ell[0].view(n, 64, 2).cpu()
+    assert int((ell[:, :, 0] & 0xFFFFFF).max()) < n
+    eng.outer_metrics()  # the word was cleared by the raise; nothing new
+    eng.replay(1)
+    eng.outer_metrics()  # a window from consistent counts: no error
 
 
 def test_xt_adam_sample_pairs_bit_identical():

@@ -406,7 +406,7 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
     s = torch.empty((count, samples, n), dtype=torch.float32, device=device)
     seed, tag = 1234, tag_for(TAG_GRAPH, 5)
     nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 2, count, samples,
-             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, 0, 0, st)
+             nat.ptr(bits), words, nat.ptr(deg), 0, 0, 0, nat.ptr(s), 0, 0, 0, 0, st)
     one = torch.empty((n, words), dtype=torch.int64, device=device)
     nb = (n + 63) // 64
     for gi in range(count):
@@ -419,6 +419,49 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
                 for k in range(64):
                     pc += (x >> k) & 1
             assert torch.equal(deg[gi, b, :n].long(), pc), (gi, b)
+
+def test_fill_guard_pads_inflated_degrees(device):
+    """lds_sample_graphs_multi promised a zero degree workspace (ws_zeroed =
+    1) that is not: every row's count exceeds its drawn bits.  The fill
+    writes the drawn columns, pads each row's remaining slots with the row
+    index (col was garbage before), leaves no CSR position outside [0, n) and
+    sets LDS_DEVERR_FILL_DEGREE in the error word; a consistent call leaves
+    the word alone.  Both fill forms: 16-lane rows and whole-wave dense rows."""
+    for n, dense in ((300, 0.3), (1500, 0.9)):
+        g = torch.Generator().manual_seed(n)
+        theta = (torch.rand(n * (n + 1) // 2, generator=g) * dense).to(device)
+        words = nat.lib.lds_bitmask_words(n)
+        wsi = nat.lib.lds_sample_ws_ints(n)
+        st = nat.stream_of(theta.device)
+        base = torch.zeros(4, dtype=torch.int32, device=device)
+        bits = torch.empty((n, words), dtype=torch.int64, device=device)
+        rp = torch.empty(n + 1, dtype=torch.int32, device=device)
+        s = torch.empty(n, dtype=torch.float32, device=device)
+        ell = torch.empty(n * 128, dtype=torch.int32, device=device)
+        err = torch.zeros(1, dtype=torch.int32, device=device)
+        cap = n * n
+        outs = []
+        for extra in (0, 5):
+            ws = torch.full((wsi,), extra, dtype=torch.int32, device=device)
+            col = torch.full((cap,), 0x7FFFFFFF, dtype=torch.int32, device=device)
+            nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, 11, tag_for(TAG_GRAPH, 0), 1, nat.ptr(base), 0,
+                     1, 1, nat.ptr(bits), words, nat.ptr(ws), nat.ptr(rp), nat.ptr(col), cap, nat.ptr(s),
+                     nat.ptr(ell), 0, 1, nat.ptr(err), st)
+            torch.cuda.synchronize()
+            assert int(err.item()) == (1 if extra else 0), (n, extra)
+            err.zero_()
+            outs.append((rp.clone().long().cpu(), col.cpu(), ws[:n].long().cpu()))
+        (rp0, col0, d0), (rp1, col1, d1) = outs
+        assert torch.equal(d1, d0 + 5)
+        nnz = int(rp1[n])
+        assert nnz == int(d0.sum()) + 5 * n
+        assert int(col1[:nnz].min()) >= 0 and int(col1[:nnz].max()) < n
+        for r in range(0, n, max(1, n // 37)):
+            got = col1[int(rp1[r]):int(rp1[r + 1])]
+            k = int(d0[r])
+            assert torch.equal(got[:k], col0[int(rp0[r]):int(rp0[r + 1])]), r
+            assert bool((got[k:] == r).all()), r
+
 
 
 @pytest.mark.parametrize("n,count,samples,dense", [(300, 3, 2, 0.3), (1000, 2, 1, 0.05), (2100, 2, 1, 0.9)])
@@ -447,7 +490,7 @@ def test_fused_sampler_csr_equals_staged_path(device, n, count, samples, dense):
         s = torch.empty((G, n), dtype=torch.float32, device=device)
         ell = torch.empty((G, n * 128), dtype=torch.int32, device=device)
         nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 1, count, samples,
-                 nat.ptr(bits), words, nat.ptr(ws), nat.ptr(rp), nat.ptr(col), cap, nat.ptr(s), nat.ptr(ell), 0, zeroed, st)
+                 nat.ptr(bits), words, nat.ptr(ws), nat.ptr(rp), nat.ptr(col), cap, nat.ptr(s), nat.ptr(ell), 0, zeroed, 0, st)
         outs.append((rp.clone(), col.clone(), s.clone(), ell.clone(), ws[:, :n].clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
@@ -765,15 +808,19 @@ def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, 
     return y
 
 
-@pytest.mark.parametrize("n,high,grid", [(1, 1.0, 0), (17, 1.0, 0), (700, 1.0, 0), (1500, 1.0, 3), (2600, 0.5, 0),
-                                         (3000, 0.02, 0), (3001, 1.0, 7)])
+@pytest.mark.parametrize("n,high,grid", [(1, 1.0, 0), (17, 1.0, 0), (700, 1.0, 0), (1500, 1.0, 3), (1500, 1.0, -3),
+                                         (2600, 0.5, 0), (3000, 0.02, 0), (3001, 1.0, 7), (3001, 1.0, -7),
+                                         (3001, 1.0, 40)])
 def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
-    """lds_spmm_norm_dense (CSR streamed into LDS bit tiles, int8 matrix-core
+    """lds_spmm_norm_dense (CSR streamed into LDS bit rows, int8 matrix-core
     product) vs the dense fp64 product, the bitmask aggregation (same digits:
     identical bits where that takes one split) and the CSR row kernel: ragged
-    n, dense and sparse rows (the sparse fallback of the bit setting), a
-    persistent grid smaller than the tile count, columns of extreme scale.
-    Per-column tolerance 1e-5 of max_i Σ_k |Â_ik z_kf|."""
+    n, dense and sparse rows (the sparse fallback of the bit setting), grids
+    that force the most rows per block (the row-block kernel, grid > 0) or a
+    persistent grid smaller than the tile count (the tile kernel, grid < 0),
+    columns of extreme scale.  The row-block and tile kernels give the same
+    bits (exact integer sums, same final arithmetic).  Per-column tolerance
+    1e-5 of max_i Σ_k |Â_ik z_kf|."""
     g = torch.Generator().manual_seed(n + 29)
     theta = torch.rand(n * (n + 1) // 2, generator=g) * high
     graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n + 1), track_grad=False)
@@ -784,6 +831,8 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     z[: n // 2, 13] *= 1e6
     zd = z.to(device)
     y = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=grid).cpu().double()
+    y_other = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=0 if grid < 0 else -256).cpu().double()
+    assert torch.equal(y, y_other)
     a = graph.normalized_dense().cpu().double()
     ref = a @ z.double()
     scale = (a.abs() @ z.double().abs()).max(0).values.clamp(min=1e-300)
@@ -829,11 +878,12 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     col[int(rp[41]) - 1] = seg[3]
     s = torch.rand(n, generator=g) + 0.5
     z = torch.randn(n, 16, generator=g)
-    y = _spmm_dense(rp.int().to(device), col.to(device), s.to(device), n, z.to(device)).cpu().double()
     ref = s.double()[:, None] * (a.double() @ (s.double()[:, None] * z.double()))
     scale = (a.double() @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
-    assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL
-    assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0)
+    for grid in (0, 13, -256):  # row-block kernel (one block per CU; 13 blocks of 100 rows), tile kernel
+        y = _spmm_dense(rp.int().to(device), col.to(device), s.to(device), n, z.to(device), grid=grid).cpu().double()
+        assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL, grid
+        assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0), grid
 
 
 @pytest.mark.parametrize("samples,count,n", [(5, 3, 700), (16, 2, 257)])
@@ -859,7 +909,7 @@ def test_batched_draw_sample_ranges_equal_single_draws(device, samples, count, n
     seed, tag, off = 77, tag_for(TAG_GRAPH, 0), 2
     nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), off, count, samples,
              nat.ptr(bits), words, nat.ptr(deg), nat.ptr(row_ptr), nat.ptr(col), n * n, nat.ptr(s), nat.ptr(ell),
-             0, 0, st)
+             0, 0, 0, st)
     one = torch.empty((n, words), dtype=torch.int64, device=device)
     nb = (n + 63) // 64
     for gi in range(count):

@@ -88,7 +88,7 @@ def test_graph_census_argument_errors_need_no_gpu():
 
 
 def test_struct_layouts_match_the_header(tmp_path):
-    """The ctypes mirrors of LdsBatch and LdsSideWork (ldsgnn._native) have
+    """The ctypes mirror of LdsBatch (ldsgnn._native) has
     the sizes and field offsets the C compiler gives include/ldsgnn.h."""
     import shutil
     import subprocess
@@ -98,7 +98,7 @@ def test_struct_layouts_match_the_header(tmp_path):
         import pytest
         pytest.skip("no C compiler")
     lines = []
-    for st in (nat.LdsBatch, nat.LdsSideWork):
+    for st in (nat.LdsBatch,):
         lines.append(f'printf("{st.__name__} size %zu\\n", sizeof({st.__name__}));')
         for f, _ in st._fields_:
             lines.append(f'printf("{st.__name__} {f} %zu\\n", offsetof({st.__name__}, {f}));')
@@ -109,7 +109,7 @@ def test_struct_layouts_match_the_header(tmp_path):
     subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
     got = {tuple(line.split()[:2]): int(line.split()[2]) for line in out if line}
-    for st in (nat.LdsBatch, nat.LdsSideWork):
+    for st in (nat.LdsBatch,):
         assert got[(st.__name__, "size")] == ctypes.sizeof(st), st.__name__
         for f, _ in st._fields_:
             assert got[(st.__name__, f)] == getattr(st, f).offset, (st.__name__, f)

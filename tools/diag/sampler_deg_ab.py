@@ -36,7 +36,7 @@ def main():
     nat.call = real
     torch.cuda.synchronize()
     draw = [a for name, a in calls if name == "lds_sample_graphs_multi"][0]
-    fused = draw[:-2] + (0,) + draw[-1:]          # clears its own workspace
+    fused = draw[:-3] + (0,) + draw[-2:]          # clears its own workspace
     bits_only = fused[:13] + (None,) + fused[14:]  # col = NULL
     for label, a in (("fused", fused), ("bits_only", bits_only)):
         for _ in range(50):

@@ -45,7 +45,7 @@ def main():
                  nat.ptr(scal), 1, nat.stream_of(dev))
         nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, seed, tag, 1, nat.ptr(base), 0, graphs, 1,
                  nat.ptr(bits), words, nat.ptr(deg), nat.ptr(row_ptr), nat.ptr(col), cap, nat.ptr(s), nat.ptr(ell),
-                 0, 0, nat.stream_of(dev))
+                 0, 0, 0, nat.stream_of(dev))
 
     def fused():
         nat.call("lds_theta_grad_sgd_draw", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, 1, nat.ptr(theta), n, 0,

@@ -85,7 +85,7 @@ def main():
     print(json.dumps({"what": "memset chain", "bytes": ws_bytes, "us": 1e6 * memset / args.k}), flush=True)
     for i, (name, a) in enumerate(calls):
         if name == "lds_sample_graphs_multi":  # repeated draws: the call clears its workspace (ws_zeroed = 0)
-            a = a[:-2] + (0,) + a[-1:]
+            a = a[:-3] + (0,) + a[-2:]
 
         def chain(name=name, a=a):
             for _ in range(args.k):

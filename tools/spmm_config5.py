@@ -81,14 +81,16 @@ def main(n=20000, f=16, reps=20, high=1.0):
     y_dn = torch.empty((n, f), device=dev)
     ws_dn = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=dev)
 
-    def dense(quantize=1):
+    def dense(quantize=1, grid=0):
         nat.call("lds_spmm_norm_dense", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_dn), f, 0,
-                 nat.ptr(ws_dn), 0, quantize, st)
+                 nat.ptr(ws_dn), grid, quantize, st)
 
     t_bp = time_it(lambda: nat.call("lds_csr_block_ptr", nat.ptr(rp), nat.ptr(col), n, nat.ptr(bptr), st), 3)
     t_row = time_it(row, reps)
     t_blk = time_it(blk, reps)
     t_bit = time_it(bit, reps)
+    t_tile = time_it(lambda: dense(0, -256), reps)  # round 3's tile kernel (product only)
+    y_tile = y_dn.clone()
     t_dn = time_it(dense, reps)
     t_dn_main = time_it(lambda: dense(0), reps)
     # parity: blocked vs row kernel (fp32, different order) and fp64 on sampled rows
@@ -117,6 +119,9 @@ def main(n=20000, f=16, reps=20, high=1.0):
                                 "frac_product": algo / t_dn_main / 1e3 / HBM_PEAK_GBS,
                                 "speedup_vs_blocked": t_blk / t_dn,
                                 "max_rel_vs_row": float((y_dn - y_row).abs().max() / y_row.abs().max()),
+                                "tile_kernel_us_product": t_tile,
+                                "tile_kernel_frac_product": algo / t_tile / 1e3 / HBM_PEAK_GBS,
+                                "equal_to_tile_kernel": bool(torch.equal(y_dn, y_tile)),
                                 "equal_to_bitmask": bool(torch.equal(y_dn, y_bit))},
            "max_rel_blocked_vs_row": rel, "max_rel_vs_fp64_rows": err64,
            "max_rel_bitmask_vs_row": float((y_bit - y_row).abs().max() / y_row.abs().max()),
