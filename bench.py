@@ -53,7 +53,9 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector/MFMA peak
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
 METRIC = "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X"
-PMC_RECORD = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
+# committed rocprofv3 PMC records (2 x FETCH_SIZE + WRITE_SIZE per launch, separate passes) by workload
+PMC_RECORDS = {"cora-lds-S1-tau5": os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"),
+               "synthetic20k-lds-S1-tau5": os.path.join(ROOT, "profiles", "r04_pmc_traffic_config5.json")}
 
 
 def world_info():
@@ -145,9 +147,15 @@ def algo_cost(name, eng, n_calls_per_window):
     nnz = eng.sampled_nnz_mean()
     xnnz = int(eng.xcol.numel())
     act = 4 * 16 * n * S                      # one n × 16 fp32 activation array (all samples)
-    graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)  # row_ptr, col, s, ELL head
+    if eng.bitmask_agg:  # long rows, bitmask aggregation: the kernels read s and Â·Z's split partials, no CSR
+        graph = S * (4 * n + 4 * 16 * n * eng.agg_splits)
+    elif eng.long_rows:  # long rows, column-blocked pre-pass: s and Â·Z
+        graph = S * (4 * n + 4 * 16 * n)
+    else:
+        graph = S * (4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)  # row_ptr, col, s, ELL head
     tri = n * (n + 1) // 2
     P = eng.np
+    words = nat.lib.lds_bitmask_words(n)
     if name in ("lds_theta_grad_sgd", "lds_theta_grad", "lds_theta_grad_ex", "lds_theta_grad_sgd_draw",
                 "lds_theta_grad_direct"):
         # (_draw: the next window's graph draw rides in the epilogue; priced on the θ-grad's flops)
@@ -155,18 +163,19 @@ def algo_cost(name, eng, n_calls_per_window):
         return "mfma", 6.0 * 4.0 * k * tri   # split bf16: six bf16 MFMA products per fp32 product
     if name == "lds_sample_graphs_multi":
         g = eng.tau + 1
-        words = nat.lib.lds_bitmask_words(n)
+        if eng.bitmask_agg:  # bits written, read by the popcount pass, degrees and s written
+            return "hbm", 4 * tri + g * S * (2 * 8 * n * words + 8 * n)
         per = S * (3 * 8 * n * words + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)  # bits w/r/r, CSR, s, ELL
         return "hbm", 4 * tri + g * per      # θ read once per window
     if name == "lds_sample_fill_csr":  # the fill alone: bits read, CSR / s / ELL written
         g = eng.tau + 1
-        words = nat.lib.lds_bitmask_words(n)
+        if eng.bitmask_agg:  # col = NULL: s from the drawn degree counts only
+            return "hbm", g * S * 8 * n
         return "hbm", g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)
     if name == "lds_engine_x_linear":
         return "hbm", S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act
     if name == "lds_engine_fill_x_linear":  # the window fill and the first X product in one launch
         g = eng.tau + 1
-        words = nat.lib.lds_bitmask_words(n)
         return "hbm", (g * S * (8 * n * words + 4 * n + 4 * (n + 1) + 4 * nnz + 4 * n + 8 * ELL_W * n)
                        + S * (4 * (n + 1) + 8 * xnnz + 8 * xnnz) + 4 * 16 * eng.fin + act)
     if name == "lds_aggregate_bitmask_partials":
@@ -196,6 +205,22 @@ def algo_cost(name, eng, n_calls_per_window):
     return "hbm", 0
 
 
+def theta_grad_hbm_bytes(name, eng):
+    """Algorithmic HBM bytes of one θ-grad launch of the window (beside its
+    MFMA flops): θ read and written, dθ written (when kept), the factor
+    columns read once (U, V fp32; the direct form's planes are 3 × bf16), and,
+    for the drawing forms, the next window's bit graphs written."""
+    from ldsgnn import _native as nat
+    n = eng.n
+    tri = n * (n + 1) // 2
+    k = eng.S * eng.ldk if eng.S > 1 else eng.window_columns(eng.tau, eng.c)
+    fac = 2 * n * k * (6 if name == "lds_theta_grad_direct" else 4)
+    out = 8 * tri + (4 * tri if eng.keep_grad else 0) + fac
+    if name in ("lds_theta_grad_sgd_draw", "lds_theta_grad_direct") and eng.prefetch_draw:
+        out += eng.gbatch.count * eng.S * 8 * n * nat.lib.lds_bitmask_words(n)
+    return out
+
+
 def bitagg_hbm_bytes(n):
     """Algorithmic HBM bytes of one lds_aggregate_bitmask call (csrc/bitagg.hip):
     the mask, s and Z once, the int8 digits written once and read once (the
@@ -211,17 +236,17 @@ def bitagg_hbm_bytes(n):
 
 def pmc_traffic(name, args):
     """HBM bytes per launch of an entry point from the committed rocprofv3 PMC
-    record of THIS default workload (tools/gpu_pmc.sh + tools/pmc_summary.py:
+    record of THIS workload (tools/gpu.sh pmc / pmc5 + tools/pmc_summary.py:
     2 x FETCH_SIZE + WRITE_SIZE in separate passes, gfx950 read correction)."""
-    default = (args.dataset == "cora" and args.samples == 1 and args.tau == 5 and args.model == "lds")
-    if not default or not os.path.exists(PMC_RECORD):
+    path = PMC_RECORDS.get(f"{args.dataset}-lds-S{args.samples}-tau{args.tau}")
+    if args.model != "lds" or path is None or not os.path.exists(path):
         return None, None
-    with open(PMC_RECORD) as f:
+    with open(path) as f:
         recs = json.load(f)
     rec = recs.get(name)
     if rec is None:
         return None, None
-    return rec["traffic_bytes"], os.path.relpath(PMC_RECORD, ROOT)
+    return rec["traffic_bytes"], os.path.relpath(path, ROOT)
 
 
 def chain_us(fn, dev, k, reps=3):
@@ -298,6 +323,8 @@ def window_breakdown(eng, reducer, args, device, k=20):
             elif bound == "mfma":
                 row["algorithmic_flop"] = cost
                 row["achieved_tflops"] = cost / (avg * 1e-6) / 1e12
+                row["algorithmic_bytes"] = theta_grad_hbm_bytes(name, eng)
+                row["achieved_GBs"] = row["algorithmic_bytes"] / (avg * 1e-6) / 1e9
             else:
                 row["algorithmic_bytes"] = cost
                 row["achieved_GBs"] = cost / (avg * 1e-6) / 1e9
@@ -317,7 +344,8 @@ def roofline_of(row, args):
         from ldsgnn import ops as ldsops
         roof = {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / BF16_PEAK_TFLOPS, "form": ldsops.theta_grad_form(),
-                "fp32_equiv_tflops": achieved / 6.0}
+                "fp32_equiv_tflops": achieved / 6.0, "hbm_GBs": row.get("achieved_GBs"),
+                "hbm_frac": row["achieved_GBs"] / HBM_PEAK_GBS if "achieved_GBs" in row else None}
     else:
         achieved = row.get("achieved_GBs", 0.0)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -44,6 +44,11 @@ struct U32x4 {
 };
 
 // Philox4x32-10 (Salmon et al., SC'11).  Counter (c0..c3), key (k0, k1).
+// REQUIREMENT: the key must be the same in every lane (it is a kernel argument
+// at every call site): the rounds take it as the SGPR operand ("s") of
+// v_bitop3_b32, so a per-lane key would silently use one lane's.  (Forcing it
+// with readfirstlane here costs 17 more SGPR spills in the θ-grad draw
+// epilogues; the equality tests against the host Philox are the guard.)
 __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {

@@ -1788,12 +1788,10 @@ template <bool SMALL, bool PART, bool DRAW>
 static void launch_dma_inst(int grid, hipStream_t st, const uint16_t* up, const uint16_t* vp, int nt, int k,
                             const float* r, int ldr, int nr, float* theta, int n, float* grad, int mode,
                             const double* lr, int ldrc, float gscale, int per, const DrawArgs& dr) {
-    static bool attr_set = false;  // > 64 KB of dynamic LDS must be enabled per kernel
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_dma_kernel<SMALL, PART, DRAW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDmaLds);
-        attr_set = true;
-    }
+    // > 64 KB of dynamic LDS must be enabled per kernel and device: set on every
+    // launch (a cheap host call); a refusal surfaces as the launch's error
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_dma_kernel<SMALL, PART, DRAW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kDmaLds);
     hipLaunchKernelGGL((theta_grad_dma_kernel<SMALL, PART, DRAW>), dim3(grid), dim3(512), kDmaLds, st, up, vp, nt, k,
                        r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, 8, per, dr);
 }
@@ -1835,12 +1833,9 @@ template <bool SMALL, bool PART, bool DRAW>
 static void launch_w8_inst(int grid, hipStream_t st, const float* u, const float* v, int ld, int k, const float* r,
                            int ldr, int nr, float* theta, int n, float* grad, int mode, const double* lr, int ldrc,
                            float gscale, int per, const DrawArgs& dr) {
-    static bool attr_set = false;  // > 64 KB of dynamic LDS must be enabled per kernel
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_w8_kernel<SMALL, PART, DRAW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kW8Lds);
-        attr_set = true;
-    }
+    // > 64 KB of dynamic LDS, enabled per kernel and device on every launch
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_w8_kernel<SMALL, PART, DRAW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kW8Lds);
     hipLaunchKernelGGL((theta_grad_w8_kernel<SMALL, PART, DRAW>), dim3(grid), dim3(512), kW8Lds, st, u, v, ld, k, r,
                        ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, kGroup, per, dr);
 }
@@ -1903,16 +1898,13 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
     if (form == 8 && !pre && fast) {
         const int per = (nt2 + 7) / 8;
         const bool small = n <= 46340;
-        static bool attr_set[2] = {false, false};
-        if (!attr_set[small]) {  // > 64 KB of dynamic LDS must be enabled per kernel
-            if (small)
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_bf3_pipe_kernel<true>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kPipeLds);
-            else
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_bf3_pipe_kernel<false>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, kPipeLds);
-            attr_set[small] = true;
-        }
+        // > 64 KB of dynamic LDS, enabled per kernel and device on every launch
+        if (small)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_bf3_pipe_kernel<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kPipeLds);
+        else
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_bf3_pipe_kernel<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kPipeLds);
         if (small)
             hipLaunchKernelGGL((theta_grad_bf3_pipe_kernel<true>), dim3(8 * per), dim3(256), kPipeLds, st, u, v, ld, k,
                                r, ldr, nr, theta, n, grad, mode, lr, ldrc, gscale, kGroup, per);

@@ -144,8 +144,17 @@ def knn_graph_dense(x: torch.Tensor, k: int, loop: bool = True, metric: str = "c
       candidate is dropped instead (sklearn.neighbors KNeighborsMixin
       .kneighbors with X=None).  Under "dot" a point's own distance |x|² is
       rarely among the smallest, so its nearest neighbour is skipped.
-    Pinned against the reference's own sklearn calls: tests/golden/knn_cora.npz
-    (cosine) and graph_models.npz (cosine and dot)."""
+    Cosine is pinned against the reference's own sklearn calls
+    (tests/golden/knn_cora.npz, graph_models.npz knn_cosine_).  "dot" is NOT
+    drop-in with the reference: the reference hands np.dot to sklearn as a
+    callable metric, for which sklearn's default search is a BallTree whose
+    pruning assumes a metric (dot "distances" are negative), so its pattern
+    depends on the tree.  This function computes the exact k nearest under
+    the same dissimilarity instead — the reference's call with
+    algorithm="brute", a modified reference call (golden knn_dotbrute_,
+    bit-exact).  Against the reference's own dot golden (knn_dot_, 70 nodes,
+    k = 7) the sampled graph differs in 126 of 4,900 entries
+    (tests/test_graph_models_cpu.py::test_knn_dot_distance_from_reference_balltree)."""
     x = x.detach().float()
     n = x.size(0)
     if metric == "cosine":   # nearest = largest cosine; a point is its own nearest (distance 0)

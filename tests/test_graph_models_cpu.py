@@ -1,12 +1,17 @@
 """Host-side pieces of the embedding / GAE graph models
 that need no GPU: the kNN pattern with the reference's metrics, the dense
 sparsification semantics, the factory's error behaviour."""
+import os
+
+import numpy as np
 import pytest
 import torch
 
 from ldsgnn.models.factory import GraphGenerativeModelFactory
 from ldsgnn.models.sampling import SPARSIFICATION, sparsify
 from ldsgnn.utils.graph import DenseData, knn_graph_dense
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_knn_dot_metric_is_a_distance():
@@ -75,3 +80,25 @@ def test_factory_unknown_model_and_optimizer():
         fac.optimizer(torch.nn.Linear(2, 2))
     with pytest.raises(NotImplementedError):
         GraphGenerativeModelFactory.get_optimizer("rmsprop")
+
+
+def test_knn_dot_distance_from_reference_balltree():
+    """knn_metric="dot" is the exact k nearest under -x·y (the reference's
+    call with sklearn's brute-force search), not the reference's own BallTree
+    pattern.  On the reference goldens' 70 embeddings (k = 7,
+    include_self=False) with the goldens' uniforms: bit-exact against
+    knn_dotbrute_ (the reference code with algorithm="brute"), and the
+    recorded distance from the reference's default call (knn_dot_): 126 of
+    the 4,900 sampled entries differ (100 edges here, 122 there)."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "graph_models.npz"))
+    e = torch.from_numpy(g["emb_e"])
+    p = torch.sigmoid(e @ e.t())
+    knn = knn_graph_dense(e, 7, loop=False, metric="dot")
+
+    def sample(key):  # src/models/sampling.py:19-36, 47-79 on the CPU: knn mask, triu draw, symmetric
+        a = torch.triu(torch.from_numpy(g[key + "u"]) < p * knn, 1)
+        return (a | a.t()).float()
+    assert torch.equal(sample("knn_dotbrute_"), torch.from_numpy(g["knn_dotbrute_sample"]))
+    ours, ref = sample("knn_dot_"), torch.from_numpy(g["knn_dot_sample"])
+    assert int((ours != ref).sum()) == 126
+    assert (int(ours.sum()), int(ref.sum())) == (100, 122)

@@ -11,6 +11,7 @@
 #   bench      the default bench line (Cora, S = 1)          bench_TAG.json
 #   prof       rocprofv3 kernel-trace summary of the bench   prof_TAG/
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the bench   pmc_TAG_{fetch,write}/
+#   pmc5       FETCH_SIZE / WRITE_SIZE passes of the config-5 line pmc5_TAG_{fetch,write}/
 #   config5    synthetic N = 20 000 line + its kernel trace c5_bench_TAG.json, c5_prof_TAG/
 #   c5cpu      the config-5 line with its CPU baseline       c5_cpu_TAG.json
 #   samples    Cora S = 8 / 16, Citeseer S = 16 lines        s_<ds>_<S>_TAG.json
@@ -49,6 +50,13 @@ for step in "$@"; do
             run 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_${tag}_$lc -o run -- \
                 python3 bench.py --no-cpu-baseline --no-breakdown --steps 50 --warmup 10 \
                 > $O/pmc_${tag}_$lc.log 2>&1 || exit $?
+        done ;;
+    pmc5)
+        for c in FETCH_SIZE WRITE_SIZE; do
+            lc=$(echo $c | cut -d_ -f1 | tr 'A-Z' 'a-z')
+            run 400 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc5_${tag}_$lc -o run -- \
+                python3 bench.py --dataset synthetic20k --no-cpu-baseline --no-breakdown --steps 10 --warmup 5 \
+                > $O/pmc5_${tag}_$lc.log 2>&1 || exit $?
         done ;;
     config5)
         run 400 python -u bench.py --dataset synthetic20k --steps 10 --warmup 5 --no-cpu-baseline \

@@ -1,4 +1,4 @@
-"""Per-kernel HBM traffic from the two rocprofv3 PMC passes of tools/gpu_pmc.sh.
+"""Per-kernel HBM traffic from the two rocprofv3 PMC passes of tools/gpu.sh (pmc, pmc5).
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 half the bytes of a wide coalesced read (MI355X_MICROARCH.md, HBM section), so
@@ -24,7 +24,7 @@ ENTRY_KERNELS = {
     # the window's batched draw: graphs looped in the tile kernel (kLoop, kDeg) + the fused fill
     # (the single-graph <false, false, true> draws of the step-0 window are not this entry's launches)
     "lds_sample_graphs_multi": ["lds::sample_tiles_kernel<false, true, true>", "lds::fill_csr_fused_kernel"],
-    "lds_sample_fill_csr": ["lds::fill_csr_fused_kernel"],
+    "lds_sample_fill_csr": ["lds::fill_csr_fused_kernel", "lds::degree_scale_kernel"],
     # θ-grad + SGD; with the next window's draw fused in: the DRAW = true instance
     "lds_theta_grad_sgd": ["theta_grad_bf3_kernel<16, true, false, true, false>", "theta_grad_bf3_t128",
                            "theta_grad_bf3_pipe", "theta_grad_mfma", "theta_grad_w8_kernel<true, false, false>",
@@ -48,6 +48,9 @@ ENTRY_KERNELS = {
     "lds_engine_rev_c": ["rev_c_kernel"],
     "lds_engine_rev_d_reduce": ["rev_d_reduce_kernel"],
     "lds_engine_end_window": ["end_window_kernel"],
+    # config 5 (long rows, bitmask aggregation): the aggregation's prepasses and product, the split W0 products
+    "lds_aggregate_bitmask_partials": ["bitagg_colmax_kernel", "bitagg_quant_kernel", "bitagg_main_kernel"],
+    "lds_engine_xt_partials": ["xt_partials_kernel"],
 }
 
 
