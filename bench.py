@@ -584,6 +584,10 @@ def main():
     ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
                     "the ranks, against rank 0 alone (default 64 when N > 1, off at N = 1)")
     ap.add_argument("--strong-steps", type=int, default=50)
+    ap.add_argument("--exchange", default="auto", choices=["auto", "noop"],
+                    help="noop (one GPU): the N > 1 per-rank path with a no-op reducer in place of the RCCL "
+                         "all-reduce — windows split at the exchange into two replayed graphs, the next window's "
+                         "draw in the SGD pass (DESIGN §5b: the per-rank window of the strong-scaling leg)")
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-launch window breakdown leg")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
@@ -637,6 +641,13 @@ def main():
     if use_engine:
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
         eng, reducer = make_engine(runner, args.tau, world, args.samples)
+        if args.exchange == "noop":
+            if world > 1:
+                raise SystemExit("--exchange noop rehearses the N > 1 path on one GPU")
+
+            def reducer(grad):  # the exchange point, without the collective
+                return None
+            eng.grad_reducer = reducer
         eng.async_draw = bool(args.async_draw)
         if args.xt_pair:
             eng.set_xt_pair(args.xt_pair)
@@ -745,7 +756,7 @@ def main():
                        "windows_per_graph": (args.graph_windows if reducer is None else 1)
                        if use_engine and use_graph else None,
                        "prefetched_draw": prefetched, "async_draw": bool(args.async_draw),
-                       "xt_pair": args.xt_pair},
+                       "xt_pair": args.xt_pair, "exchange": args.exchange if world == 1 else f"{args.backend}-allreduce"},
             "steady_state": steady,
             "strong_scaling": strong,
             "window": window,

@@ -227,15 +227,19 @@ int64_t lds_bitmask_agg_ws_bytes(int n);
  * bits as lds_aggregate_bitmask's y with beta = 0. */
 /* CSR-SpMM for dense sampled graphs (long rows, e.g. BASELINE config 5):
  * y (= or +=) diag(s)·A·diag(s)·z for the 0/1 matrix A given as CSR
- * (row_ptr, col: distinct columns per row, any order; ascending is the fast
- * path), F = 16 features — the
- * operator of lds_spmm_norm.  The column-index stream is read once; each
- * 16-row tile's entries become a bit tile in LDS that the int8 matrix cores
- * multiply with the fixed-point digits of s⊙z (lds_aggregate_bitmask's
+ * (row_ptr, col: distinct columns per row), F = 16 features — the operator
+ * of lds_spmm_norm.  The column-index stream is read once; a workgroup's
+ * rows become bit rows that the int8 matrix cores multiply with the
+ * fixed-point digits of s⊙z (lds_aggregate_bitmask's
  * quantisation: exact integer sums, one rounding per digit at 2^-31 of the
  * column maximum).  n <= lds_spmm_dense_max_n(); col 16-byte aligned; ws:
- * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned; grid 0 = one persistent
- * workgroup per CU.  Three launches (column maxima, digits, the product);
+ * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned.  grid >= 0: the
+ * row-block kernel (bit rows of a workgroup's rows staged in ws), one
+ * workgroup per CU (0) or `grid` workgroups; grid < 0: the round-3 tile
+ * kernel on -grid persistent workgroups.  Columns distinct within a row, any
+ * order (the column-pass variants of lds_spmm_dense_ablation need them
+ * ascending).
+ * Three launches (column maxima, digits, the product);
  * quantize = 0 skips the first two (ws holds the digits of this s, z from an
  * earlier call).
  * Replaces torch.mm(normalize_adjacency_matrix(A), Z) (src/models/layers.py:44,
@@ -244,6 +248,16 @@ int64_t lds_spmm_dense_ws_bytes(int n);
 int lds_spmm_dense_max_n(void);
 int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
                         float* y, int ldy, int beta, void* ws, int grid, int quantize, void* stream);
+/* Variants and timing-only ablations of lds_spmm_norm_dense (tools/spmm_config5.py;
+ * the digits of an earlier call must be in ws).  Products (same results as
+ * lds_spmm_norm_dense): dbg 20 the column-pass kernel, streaming and multiply
+ * waves concurrent, 21 its sequential form, 22 the row-block kernel with bit
+ * slabs in ws (the default).  Ablations (wrong results): 11 / 12 the
+ * concurrent column-pass kernel without its multiply / streaming waves; 1-4
+ * the row-block kernel's streaming phase alone, without its slab stores, its
+ * multiply phase alone, without its slab loads.  Test hook. */
+int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
+                            float* y, int ldy, void* ws, int dbg, void* stream);
 int lds_bitmask_agg_splits(int n);
 int64_t lds_bitmask_agg_part_offset(int n);
 int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, const float* s, int n, const float* z,

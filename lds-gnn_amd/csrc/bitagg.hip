@@ -643,15 +643,14 @@ constexpr int kRbThreads = 64 * kRbWaves;
 constexpr int kRbUnits = 6;                  // 1-KB ring units per wave: three 512-entry steps
 constexpr int kRbRing = kRbUnits / 2;        // steps in a wave's ring
 constexpr int kRbMaxTiles = 6;               // 16-row tiles per workgroup (R <= 96)
-constexpr int kRbStages = 3;                 // phase-B chunk stages in flight
+constexpr int kRbAhead = 4;                  // phase B: chunks of operands in flight per wave (registers)
 constexpr int kRbMaxGrid = 512;
 
 // Scratch rows of the bit slabs for any grid <= kRbMaxGrid: G·T·16 <= n + 17·G.
 int64_t rb_scratch_rows(int n) { return (int64_t)n + 17 * kRbMaxGrid; }
-__host__ __device__ constexpr int rb_stage_bytes(int tiles) { return kChunkBytes + tiles * 1024; }
 int rb_lds_bytes(int chunks, int tiles) {
-    const int a = kRbWaves * kRbUnits * 1024 + kRbWaves * 64 * chunks;      // rings + row buffers
-    const int b = kRbStages * rb_stage_bytes(tiles) + tiles * 16 * kF * 8;  // stages + int64 sums
+    const int a = kRbWaves * kRbUnits * 1024 + kRbWaves * 64 * chunks;  // phase A: rings + row buffers
+    const int b = tiles * 16 * kF * 8;                                  // phase B: the int64 sums
     return a > b ? a : b;
 }
 
@@ -680,7 +679,10 @@ __device__ __forceinline__ void rb_advance(RbStep& s, const int* __restrict__ rp
     }
 }
 
-template <int kTiles>
+// DBG (timing-only ablations, wrong results): 1 phase A only, 2 phase A without
+// the slab stores, 3 phase B only, 4 phase B without the bit-row loads.  The
+// product path is DBG = 0.
+template <int kTiles, int DBG = 0>
 __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
     int chunks, const uint32_t* __restrict__ colmax, const float* __restrict__ s, float* __restrict__ y, int ldy,
@@ -710,41 +712,50 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
     const uint32_t* myring = rb_lds + wave * kRbUnits * 256;
     RbStep is{-1, 0, 0, 0}, ps{-1, 0, 0, 0};
     int kis = 0, kps = 0, cur = 0;  // steps issued / processed; next row to write out
-    // write the wave's bit rows cur .. k - 1 to the slab (the buffer holds row
-    // cur's bits; the rows after it are empty) and clear the buffer
-    auto flush_to = [&](int k) {
-        for (; cur < k; ++cur) {
+    // vector-memory ops this wave issued (loads and stores count together, in
+    // order) and the count after each in-flight step's loads, oldest first:
+    // waiting for the oldest step is vmcnt(ops - q0), so the bit-row stores of
+    // a flush do not hold up the next step's wait
+    int ops = 0, q0 = 0, q1 = 0, q2 = 0;
+    const int row_stores = DBG == 2 || DBG == 5 ? 0 : (rs + 255) / 256;  // store instructions per bit row
+    rb_advance(is, rp, r0, nrows, kend, wave);
+    ps = is;
+    while (DBG != 3 && DBG != 4) {
+        // fill the ring: up to kRbRing steps in flight, the one read next included
+        while (is.k < kend && kis - kps < kRbRing) {
+            const uint32_t unit = (uint32_t)(2 * (kis % kRbRing));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int a = is.p + 256 * h + 4 * lane;
+                const int* src = a + 4 <= nnz ? col + a : col;  // past the array: a dummy block (reloaded below)
+                lds_dma16(src, ring_lds + (unit + h) * 1024u);
+            }
+            ops += 2;
+            const int inflight = kis - kps;
+            q0 = inflight == 0 ? ops : q0;
+            q1 = inflight == 1 ? ops : q1;
+            q2 = inflight == 2 ? ops : q2;
+            ++kis;
+            rb_advance(is, rp, r0, nrows, kend, wave);
+        }
+        if (ps.k >= kend) break;
+        wait_vmcnt(ops - q0);  // step kps landed; every op issued after its loads may stay in flight
+        asm volatile("" ::: "memory");
+        // a new row: write the wave's bit rows cur .. ps.k - 1 to the slab (the
+        // buffer holds row cur's bits, the rows between are empty) and clear it
+        for (; cur < ps.k; ++cur) {
             uint32_t* dst = slab + (int64_t)(wave + 16 * cur) * rs;
             for (int d = 4 * lane; d < rs; d += 256) {
                 uint4* b = reinterpret_cast<uint4*>(rowbuf + d);
-                *reinterpret_cast<uint4*>(dst + d) = *b;
+                if (DBG != 2 && DBG != 5) {
+                    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                    const uint4 bv = *b;
+                    __builtin_nontemporal_store(u4v{bv.x, bv.y, bv.z, bv.w}, reinterpret_cast<u4v*>(dst + d));
+                }
                 *b = make_uint4(0u, 0u, 0u, 0u);
             }
+            ops += row_stores;
         }
-    };
-    auto issue = [&]() {
-        const uint32_t unit = (uint32_t)(2 * (kis % kRbRing));
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int a = is.p + 256 * h + 4 * lane;
-            const int* src = a + 4 <= nnz ? col + a : col;  // past the array: a dummy block (reloaded below)
-            lds_dma16(src, ring_lds + (unit + h) * 1024u);
-        }
-        ++kis;
-        rb_advance(is, rp, r0, nrows, kend, wave);
-    };
-    rb_advance(is, rp, r0, nrows, kend, wave);
-    ps = is;
-    for (int d = 0; d < kRbRing - 1 && is.k < kend; ++d) issue();
-    while (ps.k < kend) {
-        if (is.k < kend) issue();
-        // step kps landed: at most the younger steps (two loads each) in flight
-        const int ahead = kis - kps;
-        if (ahead >= 3) __builtin_amdgcn_s_waitcnt(0x0F74);       // vmcnt(4)
-        else if (ahead == 2) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
-        else __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0)
-        asm volatile("" ::: "memory");
-        if (ps.k != cur) flush_to(ps.k);
         const uint32_t* sl = myring + (2 * (kps % kRbRing)) * 256 + 8 * lane;
         const int4 c0 = *reinterpret_cast<const int4*>(sl);
         const int4 c1 = *reinterpret_cast<const int4*>(sl + 4);
@@ -772,84 +783,122 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
             }
         }
         if (!done) {
+            // the per-entry path (row ends, sparse rows, unsorted columns); entries
+            // in a dummy block past the array's end are reloaded — only in the
+            // array's last step (wave-uniform), so no other step waits on a load
+            // (two copies of the loop: a load under a lane condition makes the
+            // compiler wait vmcnt(0) at the join whether or not it was taken)
+            if (ps.p + kDnStep + 4 > nnz) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int idx = p + e;
-                if (idx >= ps.beg && idx < ps.end) {
-                    const int v = (idx & ~3) + 4 > nnz ? col[idx] : c[e];
-                    atomicOr(rowbuf + (v >> 5), 1u << (v & 31));
+                for (int e = 0; e < 8; ++e) {
+                    const int idx = p + e;
+                    if (idx >= ps.beg && idx < ps.end) {
+                        const int v = (idx & ~3) + 4 > nnz ? col[idx] : c[e];
+                        atomicOr(rowbuf + (v >> 5), 1u << (v & 31));
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int idx = p + e;
+                    if (idx >= ps.beg && idx < ps.end) atomicOr(rowbuf + (c[e] >> 5), 1u << (c[e] & 31));
                 }
             }
         }
+        if constexpr (DBG == 5) {  // ablation: the column-pass kernel's per-step bookkeeping, no effect
+            __shared__ int dbg_state[16];
+            int myx = 0x7FFFFFFF;
+#pragma unroll
+            for (int e = 7; e >= 0; --e)
+                if (p + e >= ps.beg && p + e < ps.end && c[e] >= n) myx = p + e;
+            const int st = __builtin_amdgcn_readfirstlane(dbg_state[wave]);
+            const uint64_t hit = __ballot(myx != 0x7FFFFFFF);
+            const int nx = hit != 0ull ? __builtin_amdgcn_readlane(myx, __builtin_ctzll(hit)) : st + 1;
+            if (lane == 0) dbg_state[wave] = nx;
+        }
         ++kps;
+        q0 = q1;
+        q1 = q2;
         rb_advance(ps, rp, r0, nrows, kend, wave);
     }
-    flush_to(kend);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slab rows are written before any wave stages them
-    __syncthreads();
-
-    // ---- phase B: the block's bit rows × the digits, chunk by chunk --------
-    int8_t* const stage0 = reinterpret_cast<int8_t*>(rb_lds);
-    const int sbytes = rb_stage_bytes(kTiles);
-    unsigned long long* const sums =
-        reinterpret_cast<unsigned long long*>(stage0 + kRbStages * sbytes);  // [kTiles·16][16] int64
-    for (int i = t; i < kTiles * 16 * kF; i += kRbThreads) sums[i] = 0ull;
-    const uint32_t stage_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)rb_lds);
-    // chunk c's stage: 32 digit blocks of 1 KB, then `tiles` blocks of the bit
-    // rows' 64-byte chunk segments (lane l: row 16T + (l >> 2), 16 bytes l & 3)
-    const int nblk = 32 + tiles;
-    auto stage = [&](int c, int buf) {
-        for (int i = wave; i < nblk; i += kRbWaves) {
-            const uint32_t dst = stage_lds + (uint32_t)(buf * sbytes + i * 1024);
-            if (i < 32) {
-                lds_dma16(zq + (int64_t)c * kChunkBytes + i * 1024 + lane * 16, dst);
-            } else {
-                const int T = i - 32;
-                lds_dma16(slab + (int64_t)(16 * T + (lane >> 2)) * rs + 16 * c + 4 * (lane & 3), dst);
+    if (DBG != 3 && DBG != 4) {  // the wave's last bit row(s)
+        for (; cur < kend; ++cur) {
+            uint32_t* dst = slab + (int64_t)(wave + 16 * cur) * rs;
+            for (int d = 4 * lane; d < rs; d += 256) {
+                uint4* b = reinterpret_cast<uint4*>(rowbuf + d);
+                if (DBG != 2 && DBG != 5) *reinterpret_cast<uint4*>(dst + d) = *b;
+                *b = make_uint4(0u, 0u, 0u, 0u);
             }
         }
-    };
-    const int mine = (nblk - 1 - wave) / kRbWaves + 1;  // stage loads this wave issues per chunk (>= 2)
-    const int L = wave & 3, pm = wave >> 2;              // limb; k-steps 2pm, 2pm + 1 (dword pm of each group)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slab rows are written before any wave stages them
+    __syncthreads();
+    if constexpr (DBG == 1 || DBG == 2 || DBG == 5) return;
+
+    // ---- phase B: the block's bit rows × the digits, chunk by chunk --------
+    // Each wave loads what it multiplies straight into registers, kRbAhead
+    // chunks ahead (no LDS stage, no barrier per chunk: LDS-DMA staging of the
+    // digits measured ~26 GB/s per CU here, register loads from L2 ~90): its
+    // limb's two B fragments of the chunk (k-steps 2pm, 2pm + 1) and, per row
+    // tile, the A dword pm of its (row, lane group) from the slab.
+    const int L = wave & 3, pm = wave >> 2;  // limb; k-steps 2pm, 2pm + 1 (dword pm of each group)
     const int r16 = lane & 15, g = lane >> 4;
+    // the blocks start at different chunks (the chunk order is free: exact
+    // integer sums), so the CUs of an XCD do not all read one chunk's digits
+    const int rot = (int)(blockIdx.x % (unsigned)chunks);
+    const v4i* const zv = reinterpret_cast<const v4i*>(zq) + (2 * pm * kLimbs + L) * 64 + lane;  // + chunk·2048
+    const uint32_t* const sa = slab + (int64_t)r16 * rs + 4 * g + pm;                              // + T·16·rs + 16c
+    constexpr int D = kRbAhead;
+    v4i bq[D][2];
+    uint32_t aq[D][kTiles];
+#define LDS_RB_LOAD(cc, BQ, AQ)                                                               \
+    do {                                                                                      \
+        const int c_ = (cc) + rot < chunks ? (cc) + rot : (cc) + rot - chunks;                \
+        const bool ok_ = (cc) < chunks;                                                       \
+        const v4i* z_ = zv + (int64_t)(ok_ ? c_ : 0) * (kChunkBytes / 16);                    \
+        BQ[0] = z_[0];                                                                        \
+        BQ[1] = z_[kLimbs * 64];                                                              \
+        _Pragma("unroll") for (int T = 0; T < kTiles; ++T)                                    \
+            AQ[T] = (DBG == 4 || T >= tiles) ? 0x01010101u                                    \
+                                             : sa[(int64_t)(16 * T) * rs + 16 * (ok_ ? c_ : 0)]; \
+    } while (0)
     v4i acc[kTiles];
 #pragma unroll
     for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
-    for (int c = 0; c < kRbStages - 1 && c < chunks; ++c) stage(c, c);
-    for (int c = 0; c < chunks; ++c) {
-        // chunk c landed (the younger chunk's loads may stay in flight), and every
-        // wave is past chunk c - 1 (whose buffer the next stage call refills)
-        if (c + 1 < chunks) {
-            if (mine >= 3) __builtin_amdgcn_s_waitcnt(0x0F73);  // vmcnt(3)
-            else __builtin_amdgcn_s_waitcnt(0x0F72);            // vmcnt(2)
-        } else {
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-        }
-        __syncthreads();
-        if (c + kRbStages - 1 < chunks) stage(c + kRbStages - 1, (c + kRbStages - 1) % kRbStages);
-        const int8_t* sb = stage0 + (c % kRbStages) * sbytes;
-        const v4i* bs = reinterpret_cast<const v4i*>(sb);
-        const v4i b0 = bs[((2 * pm) * kLimbs + L) * 64 + lane];
-        const v4i b1 = bs[((2 * pm + 1) * kLimbs + L) * 64 + lane];
-        const uint32_t* tb = reinterpret_cast<const uint32_t*>(sb + kChunkBytes);
 #pragma unroll
-        for (int T = 0; T < kTiles; ++T) {
-            if (T < tiles) {
-                const uint32_t w = tb[T * 256 + r16 * 16 + 4 * g + pm];
+    for (int d = 0; d < D - 1; ++d) LDS_RB_LOAD(d, bq[d], aq[d]);
+    for (int c0 = 0; c0 < chunks; c0 += D) {
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int sh = 4 * h;
-                    v4i a;
-                    a.x = (int)((w >> sh) & 0x01010101u);
-                    a.y = (int)((w >> (sh + 1)) & 0x01010101u);
-                    a.z = (int)((w >> (sh + 2)) & 0x01010101u);
-                    a.w = (int)((w >> (sh + 3)) & 0x01010101u);
-                    acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, h ? b1 : b0, acc[T], 0, 0, 0);
+        for (int d = 0; d < D; ++d) {
+            if (c0 + d < chunks) {  // (uniform)
+                LDS_RB_LOAD(c0 + d + D - 1, bq[(d + D - 1) % D], aq[(d + D - 1) % D]);
+#pragma unroll
+                for (int T = 0; T < kTiles; ++T) {
+                    if (T < tiles) {
+                        const uint32_t w = aq[d][T];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int sh = 4 * h;
+                            v4i a;
+                            a.x = (int)((w >> sh) & 0x01010101u);
+                            a.y = (int)((w >> (sh + 1)) & 0x01010101u);
+                            a.z = (int)((w >> (sh + 2)) & 0x01010101u);
+                            a.w = (int)((w >> (sh + 3)) & 0x01010101u);
+                            acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[d][h], acc[T], 0, 0, 0);
+                        }
+                    }
                 }
             }
         }
     }
-    // C/D: col = lane & 15 (feature), row = 4(lane >> 4) + i; limb L weighs 2^(8L)
+#undef LDS_RB_LOAD
+    int8_t* const stage0 = reinterpret_cast<int8_t*>(rb_lds);
+    // C/D: col = lane & 15 (feature), row = 4(lane >> 4) + i; limb L weighs 2^(8L);
+    // the int64 sums live in the (now idle) stage memory
+    unsigned long long* const sums = reinterpret_cast<unsigned long long*>(stage0);  // [kTiles·16][16]
+    __syncthreads();  // every wave's last fragment reads are done
+    for (int i = t; i < kTiles * 16 * kF; i += kRbThreads) sums[i] = 0ull;
+    __syncthreads();
 #pragma unroll
     for (int T = 0; T < kTiles; ++T)
         if (T < tiles)
@@ -859,6 +908,290 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
                           (unsigned long long)((int64_t)acc[T][i] * ((int64_t)1 << (8 * L))));
     __syncthreads();
     for (int o = t; o < nrows * kF; o += kRbThreads) {
+        const int lr = o >> 4, f = o & 15;
+        const int row = r0 + lr;
+        const float r = s[row] * (float)ldexp((double)(int64_t)sums[o], -e_sh[f]);
+        float* out = y + (int64_t)row * ldy + f;
+        *out = beta ? *out + r : r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CSR-SpMM for dense sampled graphs, column-pass form (round 4, the product
+// path of lds_spmm_norm_dense).  Each workgroup owns one contiguous block of
+// rows (R <= kTiles·16) and sweeps the columns in P passes of cpp 512-column
+// chunks, so that the block's bit rows of ONE pass fit in LDS (R × cpp·64 B):
+// nothing of size nnz leaves the CU, and each CU reads s⊙Z's digits once.
+//  - streaming waves stream the block's CSR rows through per-wave rings of
+//    1-KB LDS-DMA units (512-entry steps, three in flight) and set each
+//    entry of the pass's column range in the pass's bit buffer.  A row's
+//    entries are ascending, so a pass ends for a row at its first entry past
+//    the range (the row's position is kept for the next pass; the one step
+//    that straddles the boundary is read again there).  A wave interleaves its
+//    rows round robin, a step of one row in flight at a time, so every load it
+//    issues is one the pass needs;
+//  - multiply waves run the pass's chunks: digits straight from L2 into
+//    registers kRbAhead chunks ahead, the A operand from the bit buffer
+//    (lds_aggregate_bitmask's digits, k order and exact int32 sums).
+// kConc: 8 streaming + 8 multiply waves and two bit buffers (pass p is
+// multiplied while pass p + 1 streams; one barrier per pass); otherwise all 16
+// waves stream, then all 16 multiply (one buffer, two barriers per pass).
+// The waves' int32 sums meet as int64 adds in LDS; y = s_i · 2^-e_f · Σ.
+// Columns must be ascending within each row (the sampler's CSR).
+// ---------------------------------------------------------------------------
+constexpr int kCpUnits = 6;                 // 1-KB ring units per streaming wave (three steps)
+constexpr int kCpRing = kCpUnits / 2;
+
+__host__ __device__ constexpr int cp_stream_waves(bool conc) { return conc ? 8 : 16; }
+int cp_fixed_lds(bool conc) { return cp_stream_waves(conc) * kCpUnits * 1024; }
+// LDS bytes of the pass buffers for tiles row tiles and cpp chunks per pass
+int cp_buf_lds(bool conc, int tiles, int cpp) { return (conc ? 2 : 1) * tiles * 16 * cpp * 64; }
+
+// DBG (timing-only, wrong results): 1 no multiply, 2 no streaming.
+template <int kTiles, bool kConc, int DBG = 0>
+__global__ __launch_bounds__(1024, 1) void csr_colpass_agg_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
+    int chunks, int cpp, const uint32_t* __restrict__ colmax, const float* __restrict__ s, float* __restrict__ y,
+    int ldy, int beta) {
+    constexpr int NS = cp_stream_waves(kConc);  // streaming waves
+    constexpr int MW0 = kConc ? NS : 0;         // first multiply wave
+    constexpr int NM = 16 - MW0;                // multiply waves
+    constexpr int KP = NM == 16 ? 1 : 2;        // dwords (k-step pairs) per multiply wave and chunk
+    constexpr int NBUF = kConc ? 2 : 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t cp_lds[];
+    __shared__ int e_sh[kF];
+    __shared__ int rpos[kTiles * 16], rend[kTiles * 16];  // per local row: next entry, row end
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int r0 = (int)blockIdx.x * rows_per_wg;
+    const int nrows = min(rows_per_wg, n - r0);
+    if (nrows <= 0) return;  // (uniform: the whole workgroup)
+    const int nnz = rp[n];
+    const int tiles = (nrows + 15) / 16;
+    const int rsp = 16 * cpp;               // dwords per bit row of a pass buffer
+    const int bufdw = kTiles * 16 * rsp;    // dwords per pass buffer
+    uint32_t* const bufs = cp_lds + NS * kCpUnits * 256;
+    if (t < 64) {
+        const uint32_t m = colmax_of(colmax, t);
+        if (t < kF) e_sh[t] = col_exponent(m);
+    }
+    for (int i = t; i < kTiles * 16; i += 1024) {
+        rpos[i] = i < nrows ? rp[r0 + i] : 0;
+        rend[i] = i < nrows ? rp[r0 + i + 1] : 0;
+    }
+    for (int d = 4 * t; d < NBUF * bufdw; d += 4096)
+        *reinterpret_cast<uint4*>(bufs + d) = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const int npass = (chunks + cpp - 1) / cpp;
+
+    // ---- streaming waves' state
+    const int kcnt = wave < NS && nrows > wave ? (nrows - 1 - wave) / NS + 1 : 0;  // rows of this wave (<= 12)
+    const uint32_t ring_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)cp_lds) +
+                              (uint32_t)(wave * kCpUnits * 1024);
+    const uint32_t* const myring = cp_lds + wave * kCpUnits * 256;
+    int kis = 0;  // steps issued (ring slot = kis % kCpRing)
+
+    // ---- multiply waves' state
+    const int mw = wave - MW0;
+    const int L = mw & 3, pm0 = (mw >> 2) * KP;  // limb; dwords pm0 .. pm0 + KP - 1 (k-steps 2pm, 2pm + 1)
+    const int r16 = lane & 15, g = lane >> 4;
+    v4i acc[kTiles];
+#pragma unroll
+    for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+
+    for (int pass = 0; pass < npass; ++pass) {
+        const int c0 = pass * cpp, cn = min(cpp, chunks - c0);
+        uint32_t* const buf = bufs + (kConc ? (pass & 1) : 0) * bufdw;
+        if (wave < NS && DBG != 2) {
+            // stream pass `pass`: columns [lo, hi) of this wave's rows into buf
+            const int lo = c0 * kChunk, hi = min(n, (c0 + cn) * kChunk);
+            uint32_t act = 0u;  // rows that may still hold entries of this pass
+            for (int k = 0; k < kcnt; ++k) {
+                const int i = wave + NS * k;
+                if (__builtin_amdgcn_readfirstlane(rpos[i]) < __builtin_amdgcn_readfirstlane(rend[i])) act |= 1u << k;
+            }
+            uint32_t fl = 0u;  // rows with a step in flight
+            int cursor = 0, nf = 0;
+            int fk0 = 0, fa0 = 0, fp0 = 0, fk1 = 0, fa1 = 0, fp1 = 0, fk2 = 0, fa2 = 0, fp2 = 0;  // FIFO, oldest first
+            while (true) {
+                while (nf < kCpRing) {  // issue: the next row (round robin) with no step in flight
+                    const uint32_t elig = act & ~fl;
+                    if (elig == 0u) break;
+                    const uint32_t up = elig & (~0u << cursor);
+                    const int k = __builtin_ctz(up != 0u ? up : elig);
+                    cursor = k + 1 >= kcnt ? 0 : k + 1;
+                    const int i = wave + NS * k;
+                    const int p0 = __builtin_amdgcn_readfirstlane(rpos[i]);
+                    const int a = p0 & ~3;
+                    const uint32_t unit = (uint32_t)(2 * (kis % kCpRing));
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int e = a + 256 * h + 4 * lane;
+                        const int* src = e + 4 <= nnz ? col + e : col;  // past the array: a dummy block
+                        lds_dma16(src, ring_lds + (unit + h) * 1024u);
+                    }
+                    ++kis;
+                    fl |= 1u << k;
+                    if (nf == 0) { fk0 = k; fa0 = a; fp0 = p0; }
+                    else if (nf == 1) { fk1 = k; fa1 = a; fp1 = p0; }
+                    else { fk2 = k; fa2 = a; fp2 = p0; }
+                    ++nf;
+                }
+                if (nf == 0) break;  // the pass is done for this wave
+                wait_vmcnt(2 * (nf - 1));  // the oldest step landed
+                asm volatile("" ::: "memory");
+                const int k = fk0, a = fa0, p0 = fp0;
+                const int i = wave + NS * k;
+                const int end = __builtin_amdgcn_readfirstlane(rend[i]);
+                const uint32_t* sl = myring + (2 * ((kis - nf) % kCpRing)) * 256 + 8 * lane;
+                const int4 q0 = *reinterpret_cast<const int4*>(sl);
+                const int4 q1 = *reinterpret_cast<const int4*>(sl + 4);
+                int c[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+                const int p = a + 8 * lane;
+                const bool tail = a + kDnStep + 4 > nnz;  // (wave-uniform) entries past the array reloaded
+                if (tail) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (p + e < end && (((p + e) & ~3) + 4 > nnz)) c[e] = col[p + e];
+                }
+                uint32_t* const rowb = buf + i * rsp;
+                // first entry of this lane at or past hi (sorted: the row's crossing is the first such entry)
+                int myx = 0x7FFFFFFF;
+#pragma unroll
+                for (int e = 7; e >= 0; --e)
+                    if (p + e >= p0 && p + e < end && c[e] >= hi) myx = p + e;
+                const bool full = a >= p0 && a + kDnStep <= end;  // every entry of the step is the row's
+                bool done = false;
+                if (full && c[7] < hi) {  // (c[7] < hi: all eight are in the pass; ascending)
+                    const uint32_t wf = (uint32_t)(c[0] - lo) >> 5;
+                    const int base = lo + (int)(wf << 5);
+                    uint32_t out = 0u;
+                    uint64_t m = 0;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const uint32_t r = (uint32_t)(c[e] - base);
+                        out |= r >> 6;
+                        m |= 1ull << (r & 63);
+                    }
+                    if (out == 0u) {
+                        dn_or(rowb + wf, (uint32_t)m);
+                        dn_or(rowb + wf + 1, (uint32_t)(m >> 32));
+                        done = true;
+                    }
+                }
+                if (!done) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int v = c[e];
+                        if (p + e >= p0 && p + e < end && v < hi) atomicOr(rowb + ((v - lo) >> 5), 1u << ((v - lo) & 31));
+                    }
+                }
+                // the row goes on in this pass iff no entry reached hi and the step
+                // did not reach the row's end
+                const uint64_t hit = __ballot(myx != 0x7FFFFFFF);
+                int nextpos;
+                bool more;
+                if (hit != 0ull) {
+                    nextpos = __builtin_amdgcn_readlane(myx, __builtin_ctzll(hit));
+                    more = false;
+                } else if (a + kDnStep < end) {
+                    nextpos = a + kDnStep;
+                    more = true;
+                } else {
+                    nextpos = end;
+                    more = false;
+                }
+                if (lane == 0) rpos[i] = nextpos;
+                fl &= ~(1u << k);
+                if (!more) act &= ~(1u << k);
+                fk0 = fk1; fa0 = fa1; fp0 = fp1;
+                fk1 = fk2; fa1 = fa2; fp1 = fp2;
+                --nf;
+            }
+        }
+        __syncthreads();  // pass `pass` is in buf (and, kConc, the multiply waves are done with pass - 1)
+        if (kConc && wave < NS && pass + 1 < npass) {
+            // clear the rows this wave owns in the other buffer (multiplied up to the barrier) for the next pass
+            uint32_t* const nb = bufs + ((pass + 1) & 1) * bufdw;
+            for (int k = 0; k < kcnt; ++k)
+                for (int d = 4 * lane; d < rsp; d += 256)
+                    *reinterpret_cast<uint4*>(nb + (wave + NS * k) * rsp + d) = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (wave >= MW0 && DBG != 1) {
+            // multiply pass `pass`: chunks c0 .. c0 + cn - 1, starting at a block-dependent one
+            const int rot = (int)(blockIdx.x % (unsigned)cn);
+            const v4i* const zv = reinterpret_cast<const v4i*>(zq) + (2 * pm0 * kLimbs + L) * 64 + lane;
+            constexpr int D = kRbAhead;
+            v4i bq[D][2 * KP];
+#define LDS_CP_LOAD(cc, BQ)                                                                   \
+    do {                                                                                      \
+        const int u_ = (cc) < cn ? ((cc) + rot < cn ? (cc) + rot : (cc) + rot - cn) : 0;      \
+        const v4i* z_ = zv + (int64_t)(c0 + u_) * (kChunkBytes / 16);                         \
+        _Pragma("unroll") for (int x = 0; x < 2 * KP; ++x) BQ[x] = z_[x * kLimbs * 64];       \
+    } while (0)
+#pragma unroll
+            for (int d = 0; d < D - 1; ++d) LDS_CP_LOAD(d, bq[d]);
+            for (int cb = 0; cb < cn; cb += D) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const int cc = cb + d;
+                    if (cc < cn) {
+                        LDS_CP_LOAD(cc + D - 1, bq[(d + D - 1) % D]);
+                        const int u = cc + rot < cn ? cc + rot : cc + rot - cn;
+                        const uint32_t* ab = buf + r16 * rsp + u * 16 + 4 * g + pm0;
+#pragma unroll
+                        for (int T = 0; T < kTiles; ++T) {
+                            if (T < tiles) {
+                                uint32_t w[KP];
+                                if constexpr (KP == 2) {
+                                    const uint2 ww = *reinterpret_cast<const uint2*>(ab + T * 16 * rsp);
+                                    w[0] = ww.x;
+                                    w[1] = ww.y;
+                                } else {
+                                    w[0] = ab[T * 16 * rsp];
+                                }
+#pragma unroll
+                                for (int x = 0; x < 2 * KP; ++x) {
+                                    const uint32_t wsel = w[x >> 1];
+                                    const int sh = 4 * (x & 1);
+                                    v4i av;
+                                    av.x = (int)((wsel >> sh) & 0x01010101u);
+                                    av.y = (int)((wsel >> (sh + 1)) & 0x01010101u);
+                                    av.z = (int)((wsel >> (sh + 2)) & 0x01010101u);
+                                    av.w = (int)((wsel >> (sh + 3)) & 0x01010101u);
+                                    acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bq[d][x], acc[T], 0, 0, 0);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+#undef LDS_CP_LOAD
+        }
+        if constexpr (!kConc) {
+            __syncthreads();  // every wave's reads of the buffer are done
+            if (pass + 1 < npass)
+                for (int d = 4 * t; d < bufdw; d += 4096)
+                    *reinterpret_cast<uint4*>(bufs + d) = make_uint4(0u, 0u, 0u, 0u);
+            __syncthreads();
+        }
+    }
+    // the int64 sums in the (idle) ring memory
+    unsigned long long* const sums = reinterpret_cast<unsigned long long*>(cp_lds);  // [kTiles·16][16]
+    __syncthreads();
+    for (int i = t; i < kTiles * 16 * kF; i += 1024) sums[i] = 0ull;
+    __syncthreads();
+    if (wave >= MW0) {
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T)
+            if (T < tiles)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    atomicAdd(sums + (T * 16 + 4 * g + i) * kF + r16,
+                              (unsigned long long)((int64_t)acc[T][i] * ((int64_t)1 << (8 * L))));
+    }
+    __syncthreads();
+    for (int o = t; o < nrows * kF; o += 1024) {
         const int lr = o >> 4, f = o & 15;
         const int row = r0 + lr;
         const float r = s[row] * (float)ldexp((double)(int64_t)sums[o], -e_sh[f]);
@@ -935,6 +1268,8 @@ extern "C" int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, c
 // digit chunks, then the row-block kernel's bit slabs (or the tile kernel's
 // partials, the larger of the two).
 static int64_t dense_scratch_off(int n) { return (int64_t)kMaxBlocks * kF * 4 + (int64_t)chunks_of(n) * kChunkBytes; }
+static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
+                             float* y, int ldy, int beta, void* ws, int grid, int quantize, int dbg, hipStream_t st);
 extern "C" int64_t lds_spmm_dense_ws_bytes(int n) {
     if (n <= 0) return 0;
     const int64_t slabs = rb_scratch_rows(n) * 64 * chunks_of(n);
@@ -959,15 +1294,32 @@ static hipError_t allow_lds(K kernel, int bytes) {
                                bytes);
 }
 
-// grid: > 0 workgroups of the row-block kernel (0: one per CU); < 0: the
+// grid: > 0 workgroups of the product kernel (0: one per CU); < 0: the
 // round-3 tile kernel (csr_dense_agg_kernel) on -grid workgroups (A/B timing).
+// The product kernel (variant): 0 column-pass concurrent, 1 column-pass
+// sequential, 2 row-block with bit slabs.  MI355X, config 5 (n = 20 000,
+// 2·10⁸ entries), µs per call: row-block 223, column-pass sequential 248,
+// concurrent 303, tile kernel 242 (profiles/r04_spmm5_*.json).
+constexpr int kDenseProduct = 2;
 extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                    int ldz, float* y, int ldy, int beta, void* ws, int grid, int quantize,
                                    void* stream) {
+    return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, beta, ws, grid, quantize, 0, (hipStream_t)stream);
+}
+
+// Timing-only ablations of the row-block kernel (tools/spmm_config5.py; wrong
+// results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
+extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
+                                       int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 5) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 22));
+    return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
+}
+
+static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
+                             float* y, int ldy, int beta, void* ws, int grid, int quantize, int dbg, hipStream_t st) {
     LDS_CHECK_ARG(row_ptr && col && s && z && y && ws && n > 0 && n <= kDnMaxChunks * kChunk);
     LDS_CHECK_ARG(ldz >= kF && ldy >= kF);
     LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
-    hipStream_t st = (hipStream_t)stream;
     const Ws w = carve(ws, n);
     const int nc = chunks_of(n);
     if (quantize) {
@@ -998,19 +1350,67 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
     LDS_CHECK_ARG(R <= 16 * kRbMaxTiles);
     g = (n + R - 1) / R;  // every block has rows
     const int tiles = (R + 15) / 16;
-    LDS_CHECK_ARG((int64_t)g * tiles * 16 <= rb_scratch_rows(n));
-    uint32_t* slabs = reinterpret_cast<uint32_t*>(scratch);
-#define LDS_RB_LAUNCH(TT)                                                                                        \
+    // variant: 0 the column-pass kernel, 8 + 8 waves (the product path); 1 the
+    // same, 16 waves streaming then multiplying; 2 the row-block kernel with
+    // bit slabs in global scratch.  dbg (ablations): rowblock 1-4, column-pass
+    // (concurrent) 11 no multiply, 12 no streaming
+    const int variant = dbg >= 20 ? dbg - 20 : dbg == 13 ? 1 : dbg >= 10 ? 0 : dbg > 0 ? 2 : kDenseProduct;
+    if (variant == 2) {
+        LDS_CHECK_ARG((int64_t)g * tiles * 16 <= rb_scratch_rows(n));
+        uint32_t* slabs = reinterpret_cast<uint32_t*>(scratch);
+#define LDS_RB_LAUNCH(TT, DD)                                                                                    \
     do {                                                                                                         \
         const int lds = rb_lds_bytes(nc, TT);                                                                    \
-        const hipError_t e = allow_lds(&csr_rowblock_agg_kernel<TT>, lds);                                       \
+        const hipError_t e = allow_lds(&csr_rowblock_agg_kernel<TT, DD>, lds);                                   \
         if (e != hipSuccess) return (int)e;                                                                      \
-        hipLaunchKernelGGL(csr_rowblock_agg_kernel<TT>, dim3(g), dim3(kRbThreads), lds, st, row_ptr, col, n, R, \
-                           (const int8_t*)w.zq, nc, (const uint32_t*)w.colmax, s, y, ldy, beta, slabs);         \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_rowblock_agg_kernel<TT, DD>), dim3(g), dim3(kRbThreads), lds, st,  \
+                           row_ptr, col, n, R, (const int8_t*)w.zq, nc, (const uint32_t*)w.colmax, s, y, ldy,    \
+                           beta, slabs);                                                                         \
     } while (0)
-    if (tiles <= 2) LDS_RB_LAUNCH(2);
-    else if (tiles <= 4) LDS_RB_LAUNCH(4);
-    else LDS_RB_LAUNCH(6);
+        if (dbg == 1) LDS_RB_LAUNCH(6, 1);
+        else if (dbg == 2) LDS_RB_LAUNCH(6, 2);
+        else if (dbg == 3) LDS_RB_LAUNCH(6, 3);
+        else if (dbg == 4) LDS_RB_LAUNCH(6, 4);
+        else if (dbg == 5) LDS_RB_LAUNCH(6, 5);
+        else if (tiles <= 2) LDS_RB_LAUNCH(2, 0);
+        else if (tiles <= 4) LDS_RB_LAUNCH(4, 0);
+        else LDS_RB_LAUNCH(6, 0);
 #undef LDS_RB_LAUNCH
+        LDS_RETURN_LAST_ERROR();
+    }
+    const bool conc = variant == 0;
+    const int cd = dbg == 11 || dbg == 13 ? 1 : dbg == 12 ? 2 : 0;
+    // chunks per pass: as many as the pass buffers hold next to the rings (LDS
+    // 160 KB, ~2 KB of static arrays), evened out over the passes
+    const int kt = tiles <= 2 ? 2 : tiles <= 3 ? 3 : tiles <= 4 ? 4 : tiles <= 5 ? 5 : 6;
+    const int room = 163840 - 2048 - cp_fixed_lds(conc);
+    int cmax = room / cp_buf_lds(conc, kt, 1);
+    LDS_CHECK_ARG(cmax >= 1);
+    const int passes = (nc + cmax - 1) / cmax;
+    const int cpp = (nc + passes - 1) / passes;
+    const int lds = cp_fixed_lds(conc) + cp_buf_lds(conc, kt, cpp);
+#define LDS_CP_LAUNCH(TT, CC, DD)                                                                                 \
+    do {                                                                                                          \
+        const hipError_t e = allow_lds(&csr_colpass_agg_kernel<TT, CC, DD>, lds);                                 \
+        if (e != hipSuccess) return (int)e;                                                                       \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_colpass_agg_kernel<TT, CC, DD>), dim3(g), dim3(1024), lds, st,      \
+                           row_ptr, col, n, R, (const int8_t*)w.zq, nc, cpp, (const uint32_t*)w.colmax, s, y, ldy, \
+                           beta);                                                                                 \
+    } while (0)
+#define LDS_CP_TILES(CC, DD)                     \
+    do {                                         \
+        if (kt == 2) LDS_CP_LAUNCH(2, CC, DD);   \
+        else if (kt == 3) LDS_CP_LAUNCH(3, CC, DD); \
+        else if (kt == 4) LDS_CP_LAUNCH(4, CC, DD); \
+        else if (kt == 5) LDS_CP_LAUNCH(5, CC, DD); \
+        else LDS_CP_LAUNCH(6, CC, DD);           \
+    } while (0)
+    if (!conc && cd == 1) LDS_CP_LAUNCH(5, false, 1);
+    else if (!conc) LDS_CP_TILES(false, 0);
+    else if (cd == 1) LDS_CP_LAUNCH(5, true, 1);
+    else if (cd == 2) LDS_CP_LAUNCH(5, true, 2);
+    else LDS_CP_TILES(true, 0);
+#undef LDS_CP_TILES
+#undef LDS_CP_LAUNCH
     LDS_RETURN_LAST_ERROR();
 }

@@ -179,7 +179,22 @@ __device__ __forceinline__ T wave_sum(T v) {
 // a count stricter.
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved; the asm sets it before its one use
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (0..15; larger counts
+// wait for 15, which is stricter, never looser).  Kernels that count their own
+// inline-asm loads and stores use it to wait for exactly the op they need.
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    n = __builtin_amdgcn_readfirstlane(n);  // uniform: a scalar branch, not every case under exec masks
+    switch (n < 0 ? 0 : n > 15 ? 15 : n) {
+#define LDS_VMW(N) \
+    case N: __builtin_amdgcn_s_waitcnt(0x0F70 | N); break;
+        LDS_VMW(0) LDS_VMW(1) LDS_VMW(2) LDS_VMW(3) LDS_VMW(4) LDS_VMW(5) LDS_VMW(6) LDS_VMW(7)
+        LDS_VMW(8) LDS_VMW(9) LDS_VMW(10) LDS_VMW(11) LDS_VMW(12) LDS_VMW(13) LDS_VMW(14) LDS_VMW(15)
+#undef LDS_VMW
+    }
+}
+
 __device__ __forceinline__ void lds_dma16(const void* p, uint32_t m0) {
+    m0 = __builtin_amdgcn_readfirstlane(m0);  // wave-uniform by contract; free when already in an SGPR
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0) : "memory", "m0");
 }
 #pragma clang diagnostic pop

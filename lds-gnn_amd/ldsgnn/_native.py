@@ -64,6 +64,7 @@ SIGNATURES = {
     "lds_spmm_dense_ws_bytes": [c_int],
     "lds_spmm_dense_max_n": [],
     "lds_spmm_norm_dense": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, c_int, c_int, P],
+    "lds_spmm_dense_ablation": [P, P, P, c_int, P, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_int, P],

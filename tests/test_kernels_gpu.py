@@ -833,6 +833,16 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     y = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=grid).cpu().double()
     y_other = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=0 if grid < 0 else -256).cpu().double()
     assert torch.equal(y, y_other)
+    ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
+    y0 = torch.empty(n, 16, device=device)  # (quantises z into ws for the variants below)
+    nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n, nat.ptr(zd), 16,
+             nat.ptr(y0), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
+    for dbg in (20, 21, 22):  # the column-pass (both forms) and row-block kernels: the same bits
+        yv = torch.empty(n, 16, device=device)
+        nat.call("lds_spmm_dense_ablation", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n,
+                 nat.ptr(zd), 16, nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
+        torch.cuda.synchronize()
+        assert torch.equal(yv.cpu().double(), y), dbg
     a = graph.normalized_dense().cpu().double()
     ref = a @ z.double()
     scale = (a.abs() @ z.double().abs()).max(0).values.clamp(min=1e-300)
@@ -854,7 +864,9 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
 
 def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     """A general 0/1 CSR: empty rows give 0, a row's columns in any order (the
-    bits are set by OR), long rows straddling the 1024-entry steps."""
+    bits are set by OR), long rows straddling the 512-entry steps; the
+    product kernel (one block per CU, and 14 blocks of 93 rows) and the tile
+    kernel (grid < 0)."""
     n = 1300
     g = torch.Generator().manual_seed(5)
     a = (torch.rand(n, n, generator=g) < 0.45)
@@ -880,7 +892,7 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     z = torch.randn(n, 16, generator=g)
     ref = s.double()[:, None] * (a.double() @ (s.double()[:, None] * z.double()))
     scale = (a.double() @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
-    for grid in (0, 13, -256):  # row-block kernel (one block per CU; 13 blocks of 100 rows), tile kernel
+    for grid in (0, 14, -256):  # product kernel (one block per CU; 14 blocks of 93 rows), tile kernel
         y = _spmm_dense(rp.int().to(device), col.to(device), s.to(device), n, z.to(device), grid=grid).cpu().double()
         assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL, grid
         assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0), grid

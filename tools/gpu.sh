@@ -16,6 +16,7 @@
 #   c5cpu      the config-5 line with its CPU baseline       c5_cpu_TAG.json
 #   samples    Cora S = 8 / 16, Citeseer S = 16 lines        s_<ds>_<S>_TAG.json
 #   scpu       the Citeseer S = 16 line with its CPU baseline s_cpu_TAG.json
+#   perrank    N > 1 per-rank window on one GPU (S = 8, no-op exchange), S = 8 local, T1 (S = 64)
 #   accuracy   LDS τ = 5 fused engine, 10 seeds, Cora + Citeseer acc_<ds>_tau5_TAG.jsonl
 #   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
 #   spmm5      config-5 CSR-SpMM kernels + kernel trace + PMC spmm5_TAG.json, spmm5_prof_TAG/, spmm5_pmc_TAG_*/
@@ -79,6 +80,13 @@ for step in "$@"; do
             run 300 python bench.py --dataset $1 --samples $2 --steps 100 --warmup 10 --no-cpu-baseline \
                 > $O/s_${1}_$2_$tag.json 2> $O/s_${1}_$2_$tag.err || exit $?
         done ;;
+    perrank)  # the N > 1 per-rank window on one GPU (no-op exchange, S = 8) beside T1 (S = 64 alone)
+        run 300 python bench.py --samples 8 --exchange noop --steps 100 --warmup 10 --no-cpu-baseline \
+            > $O/perrank_s8_$tag.json 2> $O/perrank_s8_$tag.err || exit $?
+        run 300 python bench.py --samples 8 --steps 100 --warmup 10 --no-cpu-baseline --no-breakdown \
+            > $O/perrank_s8_local_$tag.json 2> $O/perrank_s8_local_$tag.err || exit $?
+        run 300 python bench.py --samples 64 --steps 50 --warmup 10 --no-cpu-baseline --no-breakdown \
+            > $O/perrank_t1_s64_$tag.json 2> $O/perrank_t1_s64_$tag.err || exit $? ;;
     scpu)
         run 400 python bench.py --dataset citeseer --samples 16 --steps 100 --warmup 10 \
             > $O/s_cpu_$tag.json 2> $O/s_cpu_$tag.err || exit $? ;;

@@ -89,10 +89,30 @@ def main(n=20000, f=16, reps=20, high=1.0):
     t_row = time_it(row, reps)
     t_blk = time_it(blk, reps)
     t_bit = time_it(bit, reps)
+    t_dn = time_it(dense, reps)  # (the digits of this s, z are in ws from here on)
+    y_main = y_dn.clone()
     t_tile = time_it(lambda: dense(0, -256), reps)  # round 3's tile kernel (product only)
+    y_abl0 = torch.empty_like(y_dn)
+    eq_variants = {}
+    for dbg in (20, 21, 22):  # the product variants give the same bits
+        nat.call("lds_spmm_dense_ablation", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_abl0), f,
+                 nat.ptr(ws_dn), dbg, st)
+        eq_variants[dbg] = bool(torch.equal(y_abl0, y_main))
     y_tile = y_dn.clone()
-    t_dn = time_it(dense, reps)
     t_dn_main = time_it(lambda: dense(0), reps)
+    y_abl = torch.empty_like(y_dn)
+    abl = {}
+    for dbg, what in ((20, "column-pass, 8 streaming + 8 multiply waves (product)"),
+                      (21, "column-pass, 16 waves streaming then multiplying (product)"),
+                      (22, "row-block kernel with bit slabs (product)"),
+                      (11, "column-pass concurrent, no multiply"), (12, "column-pass concurrent, no streaming"),
+                      (13, "column-pass sequential, no multiply"),
+                      (1, "row-block: streaming phase alone"), (2, "row-block: streaming without bit-row stores"),
+                      (3, "row-block: multiply phase alone"), (4, "row-block: multiply without bit-row loads"),
+                      (5, "row-block: streaming without stores + column-pass step bookkeeping")):
+        abl[what] = time_it(lambda: nat.call("lds_spmm_dense_ablation", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n,
+                                             nat.ptr(z), f, nat.ptr(y_abl), f, nat.ptr(ws_dn), dbg, st), reps)
+    dense(0)  # the product again (the multiply-only ablation left its slabs in place)
     # parity: blocked vs row kernel (fp32, different order) and fp64 on sampled rows
     rel = float((y_blk - y_row).abs().max() / y_row.abs().max())
     rows = torch.randint(0, n, (32,), generator=g, device=dev)
@@ -121,7 +141,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
                                 "max_rel_vs_row": float((y_dn - y_row).abs().max() / y_row.abs().max()),
                                 "tile_kernel_us_product": t_tile,
                                 "tile_kernel_frac_product": algo / t_tile / 1e3 / HBM_PEAK_GBS,
-                                "equal_to_tile_kernel": bool(torch.equal(y_dn, y_tile)),
+                                "equal_to_tile_kernel": bool(torch.equal(y_main, y_tile)),
+                                "ablations_us": abl, "variants_equal": eq_variants,
                                 "equal_to_bitmask": bool(torch.equal(y_dn, y_bit))},
            "max_rel_blocked_vs_row": rel, "max_rel_vs_fp64_rows": err64,
            "max_rel_bitmask_vs_row": float((y_bit - y_row).abs().max() / y_row.abs().max()),
