@@ -221,8 +221,9 @@ class LdsEngine:
         # long rows (dense θ, BASELINE config 5): the aggregations run as a
         # pre-pass whose Â·Z the fused kernels read instead of aggregating
         # in-kernel — the bitmask aggregation on the int8 matrix cores
-        # (lds_aggregate_bitmask, no CSR is built) or the column-blocked LDS
-        # SpMM over CSR (lds_spmm_norm_blocked, long_rows_kernel="blocked").
+        # (lds_aggregate_bitmask, no CSR is built), the CSR row-block SpMM
+        # (lds_spmm_norm_dense, long_rows_kernel="csr") or the column-blocked
+        # LDS SpMM over CSR (lds_spmm_norm_blocked, long_rows_kernel="blocked").
         # Decided once from θ's expected degree 1 + 2·Σ_{i<j} clamp(θ_ij) / n.
         if long_rows is None:
             tsum = float(theta.clamp(0, 1).double().sum().item())
@@ -238,16 +239,20 @@ class LdsEngine:
         self.two_hop_outer = False
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
-        if long_rows_kernel not in ("bitmask", "blocked"):
-            raise ValueError("long_rows_kernel: 'bitmask' or 'blocked'")
+        if long_rows_kernel not in ("bitmask", "csr", "blocked"):
+            raise ValueError("long_rows_kernel: 'bitmask', 'csr' or 'blocked'")
         self.bitmask_agg = self.long_rows and long_rows_kernel == "bitmask"
+        self.dense_agg = self.long_rows and long_rows_kernel == "csr"
+        if self.dense_agg and n > nat.lib.lds_spmm_dense_max_n():
+            raise NotImplementedError(f"long_rows_kernel='csr': n <= {nat.lib.lds_spmm_dense_max_n()}")
         self.agg_splits = 0  # bitmask aggregation: its partial arrays, summed by the consumers
         # graph buffers: CSR column capacity n² per graph (int32 positions);
         # none when the bitmask aggregation reads the sampled bits directly
         if not self.bitmask_agg and n * n >= (1 << 31):
             raise NotImplementedError("LdsEngine needs n² < 2^31 (int32 CSR positions)")
         self.cap = 0 if self.bitmask_agg else n * n
-        self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) if self.long_rows and not self.bitmask_agg else 0
+        self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) \
+            if self.long_rows and not (self.bitmask_agg or self.dense_agg) else 0
         self.words = nat.lib.lds_bitmask_words(n)
         S = self.S
         self.deg = torch.empty((S, int(nat.lib.lds_sample_ws_ints(n))), dtype=torch.int32, device=dev)
@@ -276,6 +281,8 @@ class LdsEngine:
                 self.agg_ws = torch.empty(int(nat.lib.lds_bitmask_agg_ws_bytes(n)), dtype=torch.uint8, device=dev)
                 self.agg_part_off = int(nat.lib.lds_bitmask_agg_part_offset(n))
                 self.agg_splits = int(nat.lib.lds_bitmask_agg_splits(n))
+            elif self.dense_agg:
+                self.agg_ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=dev)
             else:
                 nb = nat.lib.lds_spmm_block_count(n)
                 self.spmm_part = torch.zeros((nb, n, HID), dtype=torch.float32, device=dev)
@@ -645,21 +652,25 @@ class LdsEngine:
         return 0 if self.bitmask_agg else nat.ptr(col)  # NULL: no CSR (bitmask aggregation)
 
     def _block_ptrs(self, graphs):
-        if self.long_rows and not self.bitmask_agg:
+        if self.bptr_len:
             for g in graphs:
                 nat.call("lds_csr_block_ptr", nat.ptr(g.row_ptr), nat.ptr(g.col), self.n, nat.ptr(g.bptr),
                          self._stream())
 
     def _agg(self, g: _Graph, z: torch.Tensor) -> int:
-        """Long rows: Â·Z into self.agg by the bitmask aggregation or the
-        column-blocked SpMM (the fused kernel then reads it); short rows: 0
-        (aggregate in-kernel)."""
+        """Long rows: Â·Z into self.agg by the bitmask aggregation, the CSR
+        row-block SpMM or the column-blocked SpMM (the fused kernel then reads
+        it); short rows: 0 (aggregate in-kernel)."""
         if not self.long_rows:
             return 0
         if self.bitmask_agg:  # the split partials; the consuming kernel sums them (LdsBatch.agg_splits)
             nat.call("lds_aggregate_bitmask_partials", nat.ptr(g.bits), self.words, nat.ptr(g.s), self.n,
                      nat.ptr(z), HID, nat.ptr(self.agg_ws), self._stream())
             return nat.ptr(self.agg_ws) + self.agg_part_off
+        if self.dense_agg:
+            nat.call("lds_spmm_norm_dense", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z),
+                     HID, nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), 0, 1, self._stream())
+            return nat.ptr(self.agg)
         nat.call("lds_spmm_norm_blocked", nat.ptr(g.bptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z), HID,
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
         return nat.ptr(self.agg)

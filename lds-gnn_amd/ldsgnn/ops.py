@@ -114,14 +114,25 @@ class CsrGraph:
     def spmm(self, z: torch.Tensor, out: Optional[torch.Tensor] = None, beta: int = 0,
              blocked: Optional[bool] = None) -> torch.Tensor:
         """Y = Â·Z; no autograd.  Row-group kernel (lds_spmm_norm), or for long
-        rows at F = 16 the column-blocked kernel (lds_spmm_norm_blocked;
-        `blocked` forces the choice)."""
+        rows at F = 16 the CSR row-block kernel on the int8 matrix cores
+        (lds_spmm_norm_dense; 223 against 414 µs for the column-blocked kernel
+        at BASELINE config 5).  `blocked=True` forces the column-blocked kernel
+        (lds_spmm_norm_blocked), `blocked=False` the row-group kernel."""
         z = _f32c(z, "spmm")
         if z.dim() != 2 or z.size(0) != self.n:
             raise ValueError(f"spmm: Z must be {self.n}×F, got {tuple(z.shape)}")
         f = z.size(1)
         if out is None:
             out = torch.empty((self.n, f), dtype=torch.float32, device=z.device)
+        if blocked is None and f == 16 and self.long_rows() and self.n <= nat.lib.lds_spmm_dense_max_n() \
+                and self.col.data_ptr() % 16 == 0:
+            ws = getattr(self, "_dense_ws", None)
+            if ws is None:
+                ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(self.n)), dtype=torch.uint8, device=z.device)
+                self._dense_ws = ws
+            nat.call("lds_spmm_norm_dense", nat.ptr(self.row_ptr), nat.ptr(self.col), nat.ptr(self.s), self.n,
+                     nat.ptr(z), z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(ws), 0, 1, _stream(z))
+            return out
         use_blocked = (f == 16 and self.long_rows()) if blocked is None else blocked
         if use_blocked:
             if f != 16 or z.stride(0) % 4 or z.data_ptr() % 16:

@@ -5,7 +5,7 @@ oracle cannot run here (N² = 4·10⁸ fp32 per matrix, N³ normalisation):
   * θ-grad assembly (128-tile, XCD-grouped, 32-bit packed-index epilogue —
     the path config 5 takes) vs an fp64 restatement on sampled rows, and the
     64-bit index path (form 7, taken past n = 46 340) on the same inputs;
-  * the bitmask aggregation (int8 MFMA) vs the CSR column-blocked SpMM and
+  * the bitmask aggregation (int8 MFMA) vs the CSR row-block SpMM and
     an fp64 restatement on sampled rows of the same sampled graph;
   * the batched window sampler vs single draws (bit-exact);
   * a long-row engine window (bitmask aggregation pre-pass, no CSR) vs the
@@ -75,7 +75,7 @@ def test_bitmask_aggregation_n20000_vs_csr_and_fp64_rows(device, dense_graph):
     assert graph.nnz() > 1.9e8 and graph.long_rows()
     z = torch.randn(N, 16, generator=torch.Generator().manual_seed(3)).to(device)
     y_bit = graph.spmm_bitmask(z)
-    y_csr = graph.spmm(z)  # column-blocked LDS kernel (long rows)
+    y_csr = graph.spmm(z)  # long rows: the CSR row-block kernel (lds_spmm_norm_dense)
     torch.cuda.synchronize()
     rp = graph.row_ptr.cpu()
     zd = z.double().cpu()

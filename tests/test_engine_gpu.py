@@ -196,16 +196,18 @@ def test_batched_graph_replay_equals_eager():
             assert torch.equal(v, b.get_params(s)[k]), (s, k)
 
 
-@pytest.mark.parametrize("kernel", ["bitmask", "blocked"])
+@pytest.mark.parametrize("kernel", ["bitmask", "csr", "blocked"])
 @pytest.mark.parametrize("dropout", [0.0, 0.5])
 def test_engine_long_rows_match_oracle(dropout, kernel):
     """Long-row mode (config 5's dense θ): every aggregation is a pre-pass
     read by the fused kernels — the bitmask aggregation on the int8 matrix
-    cores (no CSR built) or the column-blocked LDS SpMM.  Dense θ ~ U(0, 1) on
-    300 nodes (≈150 neighbours per row) against the oracle."""
+    cores (no CSR built), the CSR row-block SpMM or the column-blocked LDS
+    SpMM.  Dense θ ~ U(0, 1) on 300 nodes (≈150 neighbours per row) against
+    the oracle."""
     res = run_engine_and_oracle(n=300, f_in=32, classes=5, steps=6, tau=5, dropout=dropout, seed=4,
                                 theta_uniform=1.0, long_rows=True, long_rows_kernel=kernel)
     assert res["engine"].long_rows and res["engine"].bitmask_agg == (kernel == "bitmask")
+    assert res["engine"].dense_agg == (kernel == "csr")
     assert res["theta_changed"] > 0
     assert res["max_loss_err"] < TOL, res
     assert res["max_param_err"] < TOL, res
@@ -213,7 +215,7 @@ def test_engine_long_rows_match_oracle(dropout, kernel):
     assert res["max_theta_err"] < TOL, res
 
 
-@pytest.mark.parametrize("kernel", ["bitmask", "blocked"])
+@pytest.mark.parametrize("kernel", ["bitmask", "csr", "blocked"])
 def test_engine_long_rows_equal_in_kernel_aggregation(kernel):
     """The pre-pass and the in-kernel aggregation give the same window within
     fp32 tolerance at a size with several column blocks / chunks (1300 nodes),

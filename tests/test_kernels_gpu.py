@@ -227,13 +227,16 @@ def test_spmm_blocked_vs_dense(device, n, high):
     z = torch.randn(n, 16, generator=g).to(device)
     y_blk = graph.spmm(z, blocked=True).cpu().double()
     y_row = graph.spmm(z, blocked=False).cpu().double()
+    y_def = graph.spmm(z).cpu().double()  # long rows: the CSR row-block kernel (lds_spmm_norm_dense)
     ref = graph.normalized_dense().cpu().double() @ z.cpu().double()
     scale = ref.abs().max()
     assert float((y_blk - ref).abs().max() / scale) < RTOL
     assert float((y_row - ref).abs().max() / scale) < RTOL
-    out = torch.ones(n, 16, device=device)
-    graph.spmm(z, out=out, beta=1, blocked=True)
-    assert float((out.cpu().double() - ref - 1.0).abs().max() / scale) < RTOL
+    assert float((y_def - ref).abs().max() / scale) < RTOL
+    for blocked in (True, None):
+        out = torch.ones(n, 16, device=device)
+        graph.spmm(z, out=out, beta=1, blocked=blocked)
+        assert float((out.cpu().double() - ref - 1.0).abs().max() / scale) < RTOL, blocked
 
 
 @pytest.mark.parametrize("n,high", [(1, 1.0), (65, 1.0), (700, 1.0), (1500, 1.0), (2600, 0.5), (3000, 0.02)])

@@ -18,6 +18,8 @@
 #   scpu       the Citeseer S = 16 line with its CPU baseline s_cpu_TAG.json
 #   perrank    N > 1 per-rank window on one GPU (S = 8, no-op exchange), S = 8 local, T1 (S = 64)
 #   accuracy   LDS τ = 5 fused engine, 10 seeds, Cora + Citeseer acc_<ds>_tau5_TAG.jsonl
+#   acc20      the same at τ = 20 (report.pdf's setting)          acc_<ds>_tau20_TAG.jsonl
+#   acc5e      Citeseer τ = 5 on the drop-in autograd path, 3 seeds acc_citeseer_tau5_eager_TAG.jsonl
 #   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
 #   spmm5      config-5 CSR-SpMM kernels + kernel trace + PMC spmm5_TAG.json, spmm5_prof_TAG/, spmm5_pmc_TAG_*/
 #   xtpair     W0 products one vs two samples per wave (Citeseer S = 16, Cora S = 16 / 8) xp_<ds>_<S>_<mode>_TAG.json
@@ -95,6 +97,14 @@ for step in "$@"; do
             run 600 python -u tools/accuracy_run.py --dataset $ds --seeds 10 --tau 5 --fused \
                 > $O/acc_${ds}_tau5_$tag.jsonl 2> $O/acc_${ds}_tau5_$tag.err || exit $?
         done ;;
+    acc20)  # the report's setting (tau = 20), 10 seeds, fused engine
+        for ds in cora citeseer; do
+            run 900 python -u tools/accuracy_run.py --dataset $ds --seeds 10 --tau 20 --fused \
+                > $O/acc_${ds}_tau20_$tag.jsonl 2> $O/acc_${ds}_tau20_$tag.err || exit $?
+        done ;;
+    acc5e)  # tau = 5 Citeseer through the drop-in autograd path (not the fused engine), first 3 seeds
+        run 900 python -u tools/accuracy_run.py --dataset citeseer --seeds 3 --tau 5 \
+            > $O/acc_citeseer_tau5_eager_$tag.jsonl 2> $O/acc_citeseer_tau5_eager_$tag.err || exit $? ;;
     multirank)
         run 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29517 bench.py --gpus 2 --backend gloo --steps 50 --warmup 10 --no-cpu-baseline \
