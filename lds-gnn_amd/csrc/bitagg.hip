@@ -1262,6 +1262,364 @@ extern "C" int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, c
     LDS_RETURN_LAST_ERROR();
 }
 
+// ---------------------------------------------------------------------------
+// CSR-SpMM for dense sampled graphs, spill-pass form (round 4; the product
+// path of lds_spmm_norm_dense).  The row-block kernel above writes every bit
+// row to a global slab and reads it back (51 MB each way at config 5, and its
+// multiply phase runs after the stream instead of beside it); the column-pass
+// kernel keeps the bits on chip but re-reads the step that straddles each
+// pass boundary and feeds its streaming waves through LDS rings that leave
+// no room for deep prefetch.  Here each workgroup owns one contiguous block
+// of rows (R <= 96) and sweeps its columns in P passes of cpp 512-column
+// chunks, with three LDS bit buffers (R rows × cpp·64 B each):
+//  * streaming waves 0-7 (wave w: local rows w, w + 8, …) load 1-KB steps
+//    of col (256 entries, one 16-byte load per lane) into a register ring D
+//    steps deep — no LDS ring, so 8·(D − 1) KB stay in flight per CU — and
+//    set each entry's bit in pass p's buffer; entries of pass p + 1 that a
+//    step holds (a row's boundary step, or steps streamed past a row's
+//    predicted pass end) go to pass p + 1's buffer at once ("spill"), so no
+//    step is read twice.  A row's stream in pass p ends at its predicted end
+//    (the row's remaining entries × the pass's share of the remaining
+//    columns + kSpMargin); a row whose boundary lies beyond it is finished
+//    with blocking loads (rare: dense rows are binomial).  Entries past pass
+//    p + 1 (sparse rows only) are left for a later pass to re-read.
+//  * multiply waves 8-15 (limb m & 3, k-steps 4(m >> 2) … + 3 of each chunk)
+//    run pass p − 1's buffer against the digits of its chunks while pass p
+//    streams (lds_aggregate_bitmask's digits, k order and exact int32 sums),
+//    then zero the buffer for pass p + 2's spills.  One barrier per pass.
+// The sums of the multiply waves meet in LDS as int64 adds (exact, order
+// free), then y = s_i · 2^-e_f · Σ.  Columns must ascend within each row
+// (canonical CSR, as every sampler and fill of this package writes it).
+// ---------------------------------------------------------------------------
+constexpr int kSpStream = 8;         // streaming waves 0-7; multiply waves 8-15
+constexpr int kSpThreads = 1024;
+constexpr int kSpStep = 256;         // entries per step: lane l loads p + 4l … + 3
+constexpr int kSpMaxRows = 96;       // rows per workgroup (six 16-row tiles)
+constexpr int kSpMaxGrid = 512;
+constexpr int kSpMargin = 192;       // entries streamed past a row's predicted pass end
+constexpr int kSpStateInts = 3 * kSpMaxRows + 16;  // pos, rend, fin per row; the exponents
+constexpr int kSpDepth = 8;          // 1-KB ring slots per streaming wave (D - 1 steps in flight)
+
+struct SpGeom {
+    int cpp, passes, rowdw;  // chunks per pass, passes, dwords per buffer row (16·cpp + 2: bank spread)
+};
+SpGeom sp_geom(int chunks, int tiles, int depth) {
+    const int rows = 16 * tiles;
+    int cpp = ((163840 - kSpStream * depth * 1024 - 4 * kSpStateInts) / (3 * rows * 4) - 2) / 16;
+    if (cpp > chunks) cpp = chunks;
+    if (cpp < 1) cpp = 1;
+    const int passes = (chunks + cpp - 1) / cpp;
+    cpp = (chunks + passes - 1) / passes;
+    return SpGeom{cpp, passes, 16 * cpp + 2};
+}
+int sp_lds_bytes(int tiles, const SpGeom& g, int depth) {
+    return kSpStream * depth * 1024 + 3 * 16 * tiles * g.rowdw * 4 + 4 * kSpStateInts;
+}
+
+// Entry c (column) of a row in pass p: its bit in pass p's buffer row bp
+// (c < hi), pass p + 1's row bq (c < hq), or past both (returns true).
+__device__ __forceinline__ bool sp_put(int c, int lo, int hi, int hq, uint32_t* bp, uint32_t* bq, bool& spill) {
+    if (c < lo) return false;  // (columns out of order: never written outside the row's buffer)
+    if (c < hi) {
+        atomicOr(bp + ((c - lo) >> 5), 1u << ((c - lo) & 31));
+        return false;
+    }
+    spill = true;
+    if (c < hq) {
+        atomicOr(bq + ((c - hi) >> 5), 1u << ((c - hi) & 31));
+        return false;
+    }
+    return true;
+}
+
+// DBG (timing-only ablations, wrong results): 1 no MFMAs, 2 streaming waves
+// load and count but set no bits.  The product path is DBG = 0.
+template <int kTiles, int D, int DBG = 0>
+__global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
+    const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
+    int chunks, int cpp, int passes, int rowdw, const uint32_t* __restrict__ colmax, const float* __restrict__ s,
+    float* __restrict__ y, int ldy, int beta) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sp_lds_all[];
+    uint32_t* const sp_lds = sp_lds_all + kSpStream * D * 256;  // after the rings: three pass buffers, row state
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int r0 = (int)blockIdx.x * rows_per_wg;
+    const int nrows = min(rows_per_wg, n - r0);
+    if (nrows <= 0) return;  // (uniform: the whole workgroup)
+    const int rowsL = 16 * ((rows_per_wg + 15) / 16);  // buffer rows (the host sized LDS for these)
+    const int bufdw = rowsL * rowdw;
+    int* const pos = reinterpret_cast<int*>(sp_lds + 3 * bufdw);
+    int* const rend = pos + kSpMaxRows;
+    int* const fin = rend + kSpMaxRows;
+    int* const e_sh = fin + kSpMaxRows;
+    const int nnz = rp[n];
+    const int span = cpp * kChunk;  // columns per pass
+    for (int i = t; i < 3 * bufdw; i += kSpThreads) sp_lds[i] = 0u;
+    for (int i = t; i < nrows; i += kSpThreads) {
+        pos[i] = rp[r0 + i];
+        rend[i] = rp[r0 + i + 1];
+        fin[i] = -1;
+    }
+    if (t < 64) {  // per-feature exponents (lds_aggregate_bitmask's quantisation)
+        const uint32_t m = colmax_of(colmax, t);
+        if (t < kF) e_sh[t] = col_exponent(m);
+    }
+    __syncthreads();
+
+    v4i acc[kTiles];
+#pragma unroll
+    for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+
+    if (wave < kSpStream) {
+        // ---- streaming waves -------------------------------------------------
+        const int nrw = nrows > wave ? (nrows - 1 - wave) / kSpStream + 1 : 0;  // this wave's rows
+        const int* const dummy = reinterpret_cast<const int*>(zq) + 4 * lane;    // null steps load here
+        // issue side: pass ip, row ordinal iq, next step ia, the row's stream end
+        int ip = 0, iq = 0, ia = 0, iend = 0, ilow = 0, iup = 0;
+        bool irow = false, ifirst = false;
+        int pending = 0;  // non-null steps in the ring
+        // the ring: a step's data, start, row bounds and packed (row | pass << 8 |
+        // first << 16 | last << 17), -1 for a null step
+        int ma[D], mlo[D], mup[D], mk[D];
+        const uint32_t ring_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)sp_lds_all) +
+                                  (uint32_t)(wave * D * 1024);
+        const uint32_t* const myring = sp_lds_all + wave * D * 256;
+        // process side: the pass the multiply waves wait for; the row's flags
+        int cp = 0, estar = 0x7FFFFFFF;
+        bool bnd = false;
+#define LDS_SP_ISSUE(J)                                                                                      \
+    do {                                                                                                     \
+        int a_ = -1, lo_ = 0, up_ = 0, k_ = -1;                                                              \
+        while (ip < passes) {                                                                                \
+            if (!irow) {                                                                                     \
+                if (iq >= nrw) {                                                                             \
+                    ++ip;                                                                                    \
+                    iq = 0;                                                                                  \
+                    continue;                                                                                \
+                }                                                                                            \
+                const int lr_ = wave + kSpStream * iq;                                                       \
+                if (__builtin_amdgcn_readfirstlane(fin[lr_]) < ip - 1) break; /* previous pass not closed */ \
+                ilow = __builtin_amdgcn_readfirstlane(pos[lr_]);                                             \
+                iup = __builtin_amdgcn_readfirstlane(rend[lr_]);                                             \
+                if (ilow >= iup) { /* the row is done: closed for this pass too */                          \
+                    fin[lr_] = ip;                                                                           \
+                    ++iq;                                                                                    \
+                    continue;                                                                                \
+                }                                                                                            \
+                ia = ilow & ~3;                                                                              \
+                if (ip == passes - 1) {                                                                      \
+                    iend = iup;                                                                              \
+                } else {                                                                                     \
+                    const int lo0_ = ip * span, hi0_ = min(lo0_ + span, n);                                  \
+                    const float fr_ = (float)(hi0_ - lo0_) / (float)(n - lo0_);                              \
+                    iend = min(iup, ilow + (int)((float)(iup - ilow) * fr_) + kSpMargin);                    \
+                }                                                                                            \
+                irow = true;                                                                                 \
+                ifirst = true;                                                                               \
+            }                                                                                                \
+            const bool last_ = ia + kSpStep >= iend;                                                         \
+            a_ = ia;                                                                                         \
+            lo_ = ilow;                                                                                      \
+            up_ = iup;                                                                                       \
+            k_ = (wave + kSpStream * iq) | (ip << 8) | (ifirst ? 1 << 16 : 0) | (last_ ? 1 << 17 : 0);      \
+            ia += kSpStep;                                                                                   \
+            ifirst = false;                                                                                  \
+            if (last_) {                                                                                     \
+                irow = false;                                                                                \
+                ++iq;                                                                                        \
+            }                                                                                                \
+            break;                                                                                           \
+        }                                                                                                    \
+        ma[J] = a_;                                                                                          \
+        mlo[J] = lo_;                                                                                        \
+        mup[J] = up_;                                                                                        \
+        mk[J] = k_;                                                                                          \
+        pending += k_ >= 0 ? 1 : 0;                                                                          \
+        const int aa_ = a_ + 4 * lane;                                                                       \
+        const int* src_ = (a_ >= 0 && aa_ + 4 <= nnz) ? col + aa_ : dummy;                                   \
+        lds_dma16(src_, ring_lds + (uint32_t)(J) * 1024u);                                                   \
+    } while (0)
+#define LDS_SP_PROCESS(J)                                                                                    \
+    do {                                                                                                     \
+        /* slot J's step landed: every iteration issues exactly one DMA, so D - 1 younger ones stay in */    \
+        /* flight (the rare paths' plain loads are waited for where they are used: stricter, never looser) */ \
+        __builtin_amdgcn_s_waitcnt(0x0F70 | (D - 1));                                                        \
+        asm volatile("" ::: "memory");                                                                       \
+        const int k_ = mk[J];                                                                                \
+        if (k_ >= 0) {                                                                                       \
+            --pending;                                                                                       \
+            const int lr_ = k_ & 0xFF, p_ = (k_ >> 8) & 0xFF;                                                \
+            for (; cp < p_; ++cp) { /* pass cp streamed: the multiply waves take it */                      \
+                __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): this wave's bit ORs are done */           \
+                __builtin_amdgcn_s_barrier();                                                                \
+            }                                                                                                \
+            if (k_ & (1 << 16)) {                                                                            \
+                bnd = false;                                                                                 \
+                estar = 0x7FFFFFFF;                                                                          \
+            }                                                                                                \
+            const int lo_ = p_ * span, hi_ = min(lo_ + span, n), hq_ = min(hi_ + span, n);                   \
+            uint32_t* const bp_ = sp_lds + (p_ % 3) * bufdw + lr_ * rowdw;                                   \
+            uint32_t* const bq_ = sp_lds + ((p_ + 1) % 3) * bufdw + lr_ * rowdw;                             \
+            const int a_ = ma[J], rlo_ = mlo[J], rup_ = mup[J];                                              \
+            const int4 v_ = *reinterpret_cast<const int4*>(myring + (J) * 256 + 4 * lane);                   \
+            int c_[4] = {v_.x, v_.y, v_.z, v_.w};                                                            \
+            const int i0_ = a_ + 4 * lane;                                                                   \
+            bool fast_ = false, spill_ = false;                                                              \
+            int myx_ = 0x7FFFFFFF;                                                                           \
+            if (a_ >= rlo_ && a_ + kSpStep <= rup_) { /* interior (uniform): every entry the row's */       \
+                const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
+                fast_ = c_[0] >= lo_ && c_[3] < hi_ && (uint32_t)(c_[3] - lo_) - (w0_ << 5) < 64u;          \
+                if (fast_ && DBG != 2) {                                                                     \
+                    uint64_t m_ = 0;                                                                         \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
+                    dn_or(bp_ + w0_, (uint32_t)m_);                                                          \
+                    dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                              \
+                }                                                                                            \
+            }                                                                                                \
+            if (!fast_ && DBG != 2) {                                                                        \
+                /* per entry; two copies under a uniform branch: only the array's last step reloads the */\
+                /* lanes that read the dummy (a lane-conditional load costs vmcnt(0) on every path) */  \
+                if (a_ + kSpStep > nnz) {                                                               \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+                        const int idx_ = i0_ + e;                                                       \
+                        if (idx_ >= rlo_ && idx_ < rup_ &&                                              \
+                            sp_put(i0_ + 4 > nnz ? col[idx_] : c_[e], lo_, hi_, hq_, bp_, bq_, spill_)) \
+                            myx_ = min(myx_, idx_);                                                     \
+                    }                                                                                   \
+                } else {                                                                                \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+                        const int idx_ = i0_ + e;                                                       \
+                        if (idx_ >= rlo_ && idx_ < rup_ && sp_put(c_[e], lo_, hi_, hq_, bp_, bq_, spill_))\
+                            myx_ = min(myx_, idx_);                                                     \
+                    }                                                                                   \
+                }                                                                                       \
+            }                                                                                                \
+            if (__ballot(spill_) != 0ull) bnd = true;                                                        \
+            {                                                                                                \
+                const uint64_t xm_ = __ballot(myx_ != 0x7FFFFFFF);                                           \
+                if (xm_ != 0ull) estar = min(estar, __builtin_amdgcn_readlane(myx_, __builtin_ctzll(xm_)));  \
+            }                                                                                                \
+            if (k_ & (1 << 17)) { /* the row's last issued step: where pass p + 1 starts */                 \
+                int np_ = min(a_ + kSpStep, rup_);                                                           \
+                if (estar == 0x7FFFFFFF && !bnd && np_ < rup_ && DBG != 2) {                                 \
+                    /* the boundary lies past the predicted end: finish the row with blocking loads */       \
+                    while (np_ < rup_) {                                                                     \
+                        const int b_ = (np_ & ~3) + 4 * lane;                                                \
+                        bool sp2_ = false;                                                                   \
+                        int mx2_ = 0x7FFFFFFF;                                                               \
+                        _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                      \
+                            const int idx_ = b_ + e;                                                         \
+                            if (idx_ >= np_ && idx_ < rup_ &&                                                \
+                                sp_put(col[idx_], lo_, hi_, hq_, bp_, bq_, sp2_))             \
+                                mx2_ = min(mx2_, idx_);                                                      \
+                        }                                                                                    \
+                        np_ = min((np_ & ~3) + kSpStep, rup_);                                               \
+                        const uint64_t xm_ = __ballot(mx2_ != 0x7FFFFFFF);                                   \
+                        if (xm_ != 0ull) estar = min(estar, __builtin_amdgcn_readlane(mx2_, __builtin_ctzll(xm_))); \
+                        if (__ballot(sp2_) != 0ull) break;                                                   \
+                    }                                                                                        \
+                }                                                                                            \
+                if (estar != 0x7FFFFFFF) np_ = estar;                                                        \
+                if (lane == 0) {                                                                             \
+                    pos[lr_] = np_;                                                                          \
+                    fin[lr_] = p_;                                                                           \
+                }                                                                                            \
+            }                                                                                                \
+        }                                                                                                    \
+    } while (0)
+#pragma unroll
+        for (int j = 0; j < D - 1; ++j) LDS_SP_ISSUE(j);
+        while (true) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                LDS_SP_ISSUE((j + D - 1) % D);
+                LDS_SP_PROCESS(j);
+                if (ip >= passes && pending == 0) goto streamed;
+            }
+        }
+#undef LDS_SP_PROCESS
+#undef LDS_SP_ISSUE
+    streamed:
+        for (; cp < passes; ++cp) {  // the last pass (and passes without steps of this wave)
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+        }
+    } else {
+        // ---- multiply waves --------------------------------------------------
+        const int m = wave - kSpStream, L = m & 3, hh = m >> 2;
+        const int r16 = lane & 15, g = lane >> 4;
+        const v4i* const zv = reinterpret_cast<const v4i*>(zq) + (4 * hh * kLimbs + L) * 64 + lane;
+        const int ntiles = (nrows + 15) / 16;
+#define LDS_SP_DIG(CH, DQ)                                                         \
+    do {                                                                           \
+        const v4i* z_ = zv + (int64_t)(CH) * (kChunkBytes / 16);                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) DQ[i] = z_[i * kLimbs * 64]; \
+    } while (0)
+#define LDS_SP_MUL(CC, DQ)                                                                                    \
+    do {                                                                                                      \
+        _Pragma("unroll") for (int T = 0; T < kTiles; ++T) {                                                  \
+            if (T < ntiles) {                                                                                 \
+                const uint2 w_ = *reinterpret_cast<const uint2*>(bp + (16 * T + r16) * rowdw + (CC) * 16 + 4 * g + 2 * hh); \
+                _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
+                    const uint32_t w = (i >> 1) ? w_.y : w_.x;                                                \
+                    const int sh = 4 * (i & 1);                                                               \
+                    v4i a;                                                                                    \
+                    a.x = (int)((w >> sh) & 0x01010101u);                                                     \
+                    a.y = (int)((w >> (sh + 1)) & 0x01010101u);                                               \
+                    a.z = (int)((w >> (sh + 2)) & 0x01010101u);                                               \
+                    a.w = (int)((w >> (sh + 3)) & 0x01010101u);                                               \
+                    if (DBG != 1) acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, DQ[i], acc[T], 0, 0, 0); \
+                    else acc[T] += a;                                                                         \
+                }                                                                                             \
+            }                                                                                                 \
+        }                                                                                                     \
+    } while (0)
+        for (int p = 0; p < passes; ++p) {
+            const int c0 = p * cpp, cn = min(cpp, chunks - c0);
+            v4i da[4], db[4];
+            LDS_SP_DIG(c0, da);  // before the barrier: in flight while pass p finishes streaming
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();  // pass p streamed
+            const uint32_t* const bp = sp_lds + (p % 3) * bufdw;
+            for (int cc = 0; cc < cn; cc += 2) {
+                if (cc + 1 < cn) LDS_SP_DIG(c0 + cc + 1, db);
+                LDS_SP_MUL(cc, da);
+                if (cc + 1 >= cn) break;
+                if (cc + 2 < cn) LDS_SP_DIG(c0 + cc + 2, da);
+                LDS_SP_MUL(cc + 1, db);
+            }
+            // pass p done: clear its buffer for pass p + 3 (whose spills start in pass p + 2)
+            uint32_t* const bz = sp_lds + (p % 3) * bufdw;
+            for (int i = t - 64 * kSpStream; i < bufdw; i += 64 * (16 - kSpStream)) bz[i] = 0u;
+        }
+#undef LDS_SP_MUL
+#undef LDS_SP_DIG
+    }
+    __syncthreads();  // every pass multiplied
+    unsigned long long* const sums = reinterpret_cast<unsigned long long*>(sp_lds);  // [rowsL][16]
+    for (int i = t; i < rowsL * kF; i += kSpThreads) sums[i] = 0ull;
+    __syncthreads();
+    if (wave >= kSpStream) {
+        const int m = wave - kSpStream, L = m & 3;
+        const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T)
+            if (16 * T < nrows)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    atomicAdd(sums + (T * 16 + 4 * g + i) * kF + r16,
+                              (unsigned long long)((int64_t)acc[T][i] * ((int64_t)1 << (8 * L))));
+    }
+    __syncthreads();
+    for (int o = t; o < nrows * kF; o += kSpThreads) {
+        const int lr = o >> 4, f = o & 15;
+        const int row = r0 + lr;
+        const float r = s[row] * (float)ldexp((double)(int64_t)sums[o], -e_sh[f]);
+        float* out = y + (int64_t)row * ldy + f;
+        *out = beta ? *out + r : r;
+    }
+}
+
 // Workspace of lds_spmm_norm_dense: lds_aggregate_bitmask's column maxima and
 // digit chunks, then the row-block kernel's bit slabs (or the tile kernel's
 // partials, the larger of the two).
@@ -1298,7 +1656,7 @@ static hipError_t allow_lds(K kernel, int bytes) {
 // sequential, 2 row-block with bit slabs.  MI355X, config 5 (n = 20 000,
 // 2·10⁸ entries), µs per call: row-block 223, column-pass sequential 248,
 // concurrent 303, tile kernel 242 (profiles/r04_spmm5_*.json).
-constexpr int kDenseProduct = 2;
+constexpr int kDenseProduct = 3;
 extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                    int ldz, float* y, int ldy, int beta, void* ws, int grid, int quantize,
                                    void* stream) {
@@ -1309,7 +1667,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 5) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 22));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 5) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 34));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -1352,7 +1710,33 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
     // same, 16 waves streaming then multiplying; 2 the row-block kernel with
     // bit slabs in global scratch.  dbg (ablations): rowblock 1-4, column-pass
     // (concurrent) 11 no multiply, 12 no streaming
-    const int variant = dbg >= 20 ? dbg - 20 : dbg == 13 ? 1 : dbg >= 10 ? 0 : dbg > 0 ? 2 : kDenseProduct;
+    const int variant = dbg >= 30 ? 3 : dbg >= 20 ? dbg - 20 : dbg == 13 ? 1 : dbg >= 10 ? 0 : dbg > 0 ? 2
+                                                                                                : kDenseProduct;
+    if (variant == 3) {  // the spill-pass kernel; dbg 31 no MFMAs, 32 no bit setting, 33 / 34 ring depth 6 / 12
+        LDS_CHECK_ARG(R <= kSpMaxRows && g <= kSpMaxGrid);
+        const int depth = dbg == 33 ? 6 : dbg == 34 ? 12 : kSpDepth;
+        const SpGeom sg = sp_geom(nc, tiles, depth);
+        const int lds = sp_lds_bytes(tiles, sg, depth);
+        LDS_CHECK_ARG(lds <= 163840);
+#define LDS_SP_LAUNCH(TT, DP, DD)                                                                                  \
+    do {                                                                                                           \
+        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, DP, DD>, lds);                                    \
+        if (e != hipSuccess) return (int)e;                                                                        \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, DP, DD>), dim3(g), dim3(kSpThreads), lds, st,  \
+                           row_ptr, col, n, R, (const int8_t*)w.zq, nc, sg.cpp, sg.passes, sg.rowdw,              \
+                           (const uint32_t*)w.colmax, s, y, ldy, beta);                                           \
+    } while (0)
+        if (dbg == 31) LDS_SP_LAUNCH(6, kSpDepth, 1);
+        else if (dbg == 32) LDS_SP_LAUNCH(6, kSpDepth, 2);
+        else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
+        else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
+        else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
+        else if (tiles <= 4) LDS_SP_LAUNCH(4, kSpDepth, 0);
+        else if (tiles <= 5) LDS_SP_LAUNCH(5, kSpDepth, 0);
+        else LDS_SP_LAUNCH(6, kSpDepth, 0);
+#undef LDS_SP_LAUNCH
+        LDS_RETURN_LAST_ERROR();
+    }
     if (variant == 2) {
         LDS_CHECK_ARG((int64_t)g * tiles * 16 <= rb_scratch_rows(n));
         uint32_t* slabs = reinterpret_cast<uint32_t*>(scratch);

@@ -840,7 +840,7 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     y0 = torch.empty(n, 16, device=device)  # (quantises z into ws for the variants below)
     nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n, nat.ptr(zd), 16,
              nat.ptr(y0), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
-    for dbg in (20, 21, 22):  # the column-pass (both forms) and row-block kernels: the same bits
+    for dbg in (20, 21, 22, 23, 33, 34):  # column-pass (both forms), row-block, spill-pass (ring depths 8, 6, 12)
         yv = torch.empty(n, 16, device=device)
         nat.call("lds_spmm_dense_ablation", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n,
                  nat.ptr(zd), 16, nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
@@ -866,10 +866,11 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
 
 
 def test_spmm_dense_empty_rows_and_unsorted_columns(device):
-    """A general 0/1 CSR: empty rows give 0, a row's columns in any order (the
-    bits are set by OR), long rows straddling the 512-entry steps; the
-    product kernel (one block per CU, and 14 blocks of 93 rows) and the tile
-    kernel (grid < 0)."""
+    """A general 0/1 CSR with rows in any column order (the bits are set by
+    OR), empty rows, long rows straddling the 512-entry steps: the kernels
+    that accept any order — the tile kernel (grid < 0) and the row-block
+    kernel — give 0 for the empty rows and identical bits.  (The product
+    kernel needs ascending columns: test_spmm_dense_spill_pass_row_shapes.)"""
     n = 1300
     g = torch.Generator().manual_seed(5)
     a = (torch.rand(n, n, generator=g) < 0.45)
@@ -895,10 +896,79 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     z = torch.randn(n, 16, generator=g)
     ref = s.double()[:, None] * (a.double() @ (s.double()[:, None] * z.double()))
     scale = (a.double() @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
-    for grid in (0, 14, -256):  # product kernel (one block per CU; 14 blocks of 93 rows), tile kernel
-        y = _spmm_dense(rp.int().to(device), col.to(device), s.to(device), n, z.to(device), grid=grid).cpu().double()
+    rpd, cold, sd, zd = rp.int().to(device), col.to(device), s.to(device), z.to(device)
+    ys = []
+    for grid in (-256, None):  # the tile kernel; the row-block kernel (any column order)
+        if grid is None:
+            ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
+            y0 = torch.empty(n, 16, device=device)  # (the tile kernel quantises z into ws for the hook)
+            nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(y0),
+                     16, 0, nat.ptr(ws), -256, 1, nat.stream_of(device))
+            yv = torch.empty(n, 16, device=device)
+            nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16,
+                     nat.ptr(yv), 16, nat.ptr(ws), 22, nat.stream_of(device))
+            torch.cuda.synchronize()
+            y = yv.cpu().double()
+        else:
+            y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid).cpu().double()
         assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL, grid
         assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0), grid
+        ys.append(y)
+    assert torch.equal(ys[0], ys[1])
+
+
+@pytest.mark.parametrize("grid", [0, 63])
+def test_spmm_dense_spill_pass_row_shapes(device, grid):
+    """The spill-pass product kernel (ascending columns) on rows that take
+    each of its paths, against the row-block kernel (identical bits: exact
+    integer sums) and fp64: rows whose entries crowd the first columns (the
+    stream stops at the predicted pass end before the pass boundary and the
+    row is finished with blocking loads), rows crowding the last columns
+    (every step of the early passes lies past pass p + 1: re-read later),
+    sparse rows whose steps span several passes, empty rows, full rows, and a
+    last row that ends the array off a 16-byte boundary.  grid 63 gives 96-row
+    blocks and three passes at n = 6000."""
+    n = 6000
+    g = torch.Generator().manual_seed(11)
+    dens = torch.rand(n, generator=g) * 0.6
+    a = torch.rand(n, n, generator=g) < dens[:, None]
+    a[0:40, 1000:] = False          # crowd the first columns
+    a[40:80, :4500] = False         # crowd the last columns
+    a[80:120] = torch.rand(40, n, generator=g) < 0.002   # sparse: steps span passes
+    a[120] = False
+    a[121] = True
+    a[200:260:3] = False
+    a[n - 1] = False
+    a[n - 1, 5] = True
+    a[n - 1, 7] = True
+    a[n - 1, 5999] = True           # nnz off a multiple of four (checked below)
+    rows, cols = a.nonzero(as_tuple=True)
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(a.sum(1), 0)
+    if int(rp[-1]) % 4 == 0:
+        a[n - 2, 3] = not bool(a[n - 2, 3])
+        rows, cols = a.nonzero(as_tuple=True)
+        rp[1:] = torch.cumsum(a.sum(1), 0)
+    assert int(rp[-1]) % 4 != 0
+    col = cols.int()
+    s = torch.rand(n, generator=g) + 0.5
+    z = torch.randn(n, 16, generator=g)
+    rpd, cold, sd, zd = rp.int().to(device), col.to(device), s.to(device), z.to(device)
+    y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid)
+    ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
+    y0 = torch.empty(n, 16, device=device)
+    nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(y0), 16, 0,
+             nat.ptr(ws), 0, 1, nat.stream_of(device))
+    yv = torch.empty(n, 16, device=device)
+    nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(yv),
+             16, nat.ptr(ws), 22, nat.stream_of(device))
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), yv.cpu())
+    ad = a.double()
+    ref = s.double()[:, None] * (ad @ (s.double()[:, None] * z.double()))
+    scale = (ad @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
+    assert float(((y.cpu().double() - ref).abs().max(0).values / scale).max()) < RTOL
+    assert torch.all(y[120] == 0)
 
 
 @pytest.mark.parametrize("samples,count,n", [(5, 3, 700), (16, 2, 257)])
