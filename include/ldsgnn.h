@@ -234,13 +234,11 @@ int64_t lds_bitmask_agg_ws_bytes(int n);
  * quantisation: exact integer sums, one rounding per digit at 2^-31 of the
  * column maximum).  n <= lds_spmm_dense_max_n(); col 16-byte aligned; ws:
  * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned.  grid >= 0: the
- * spill-pass kernel (a workgroup's rows swept in column passes, bit rows in
- * LDS, entries past a pass written into the next pass's bits), one workgroup
- * per CU (0) or `grid` workgroups (at most 96 rows each); grid < 0: the
- * round-3 tile kernel on -grid persistent workgroups.  Columns distinct and
- * ascending within each row for grid >= 0 (canonical CSR, as the samplers
- * write it); the tile kernel and the row-block variant of
- * lds_spmm_dense_ablation take any order.
+ * row-block kernel (a workgroup's rows streamed into bit rows staged in ws,
+ * then multiplied once per workgroup), one workgroup per CU (0) or `grid`
+ * workgroups (at most 96 rows each); grid < 0: the round-3 tile kernel on
+ * -grid persistent workgroups.  Columns distinct within a row, any order
+ * (the spill-pass variant of lds_spmm_dense_ablation needs them ascending).
  * Three launches (column maxima, digits, the product);
  * quantize = 0 skips the first two (ws holds the digits of this s, z from an
  * earlier call).
@@ -252,15 +250,19 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
                         float* y, int ldy, int beta, void* ws, int grid, int quantize, void* stream);
 /* Variants and timing-only ablations of lds_spmm_norm_dense (tools/spmm_config5.py;
  * the digits of an earlier call must be in ws).  Products (same results as
- * lds_spmm_norm_dense): dbg 23 the spill-pass kernel (the default), 33 / 34
- * the same with 6 / 12 ring slots per streaming wave (8 by default), 20 the
- * column-pass kernel, streaming and multiply waves concurrent, 21 its
- * sequential form, 22 the row-block kernel with bit slabs in ws (any column
- * order).  Ablations (wrong results): 31 / 32 the spill-pass kernel without
- * MFMAs / without setting bits; 11 / 12 / 13 the column-pass kernel without
- * its multiply / streaming waves; 1-5 the row-block kernel's streaming phase
- * alone, without its slab stores, its multiply phase alone, without its slab
- * loads, streaming with the column-pass step bookkeeping.  Test hook. */
+ * lds_spmm_norm_dense): dbg 22 the row-block kernel with bit slabs in ws
+ * (the default; any column order), 6 the same with digits loaded into
+ * registers, 23 the spill-pass kernel (column passes, bit rows in LDS,
+ * entries past a pass set in the next pass's bits; ascending columns), 33 / 34
+ * the same with 6 / 12 ring slots per streaming wave (8 by default), 35 the
+ * same draining its ring before every step, 20 the column-pass kernel,
+ * streaming and multiply waves concurrent, 21 its sequential form.  Ablations
+ * (wrong results): 31 / 32 the spill-pass kernel without MFMAs / without
+ * setting bits; 11 / 12 / 13 the column-pass kernel without its multiply /
+ * streaming waves; 1-5 the row-block kernel's streaming phase alone, without
+ * its slab stores, its multiply phase alone, without its slab loads,
+ * streaming with the column-pass step bookkeeping; 7 the register-digit
+ * multiply phase alone.  Test hook. */
 int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
                             float* y, int ldy, void* ws, int dbg, void* stream);
 int lds_bitmask_agg_splits(int n);

@@ -643,16 +643,28 @@ constexpr int kRbThreads = 64 * kRbWaves;
 constexpr int kRbUnits = 6;                  // 1-KB ring units per wave: three 512-entry steps
 constexpr int kRbRing = kRbUnits / 2;        // steps in a wave's ring
 constexpr int kRbMaxTiles = 6;               // 16-row tiles per workgroup (R <= 96)
-constexpr int kRbAhead = 4;                  // phase B: chunks of operands in flight per wave (registers)
+constexpr int kRbStages = 3;                 // phase-B chunk stages in flight
+constexpr int kRbAhead = 4;                  // column-pass multiply waves: digit chunks in flight (registers)
 constexpr int kRbMaxGrid = 512;
 
 // Scratch rows of the bit slabs for any grid <= kRbMaxGrid: GÂ·TÂ·16 <= n + 17Â·G.
 int64_t rb_scratch_rows(int n) { return (int64_t)n + 17 * kRbMaxGrid; }
+__host__ __device__ constexpr int rb_stage_bytes(int tiles) { return kChunkBytes + tiles * 1024; }
 int rb_lds_bytes(int chunks, int tiles) {
-    const int a = kRbWaves * kRbUnits * 1024 + kRbWaves * 64 * chunks;  // phase A: rings + row buffers
-    const int b = tiles * 16 * kF * 8;                                  // phase B: the int64 sums
+    const int a = kRbWaves * kRbUnits * 1024 + kRbWaves * 64 * chunks;      // phase A: rings + row buffers
+    const int b = kRbStages * rb_stage_bytes(tiles) + tiles * 16 * kF * 8;  // phase B: stages + int64 sums
     return a > b ? a : b;
 }
+
+// Phase B's digit loads, issued from asm: the compiler's own waits for loads
+// carried around the chunk loop came out as vmcnt(0) on the chunk just issued
+// (no prefetch at all); the kernel counts these with its bit DMAs and waits
+// itself, and rb_bind ties the registers to that wait (nothing reads them
+// earlier).
+__device__ __forceinline__ void rb_gload(v4i& v, const v4i* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void rb_bind(v4i& a, v4i& b) { asm volatile("" : "+v"(a), "+v"(b)); }
 
 // A wave's position in its CSR stream (wave-uniform): its k-th row (local row
 // wave + 16k of the block), entries [p, p + 512) of [beg, end), p â‰¡ 0 mod 4;
@@ -720,7 +732,7 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
     const int row_stores = DBG == 2 || DBG == 5 ? 0 : (rs + 255) / 256;  // store instructions per bit row
     rb_advance(is, rp, r0, nrows, kend, wave);
     ps = is;
-    while (DBG != 3 && DBG != 4) {
+    while (DBG != 3 && DBG != 4 && DBG != 7) {
         // fill the ring: up to kRbRing steps in flight, the one read next included
         while (is.k < kend && kis - kps < kRbRing) {
             const uint32_t unit = (uint32_t)(2 * (kis % kRbRing));
@@ -819,7 +831,7 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
         q1 = q2;
         rb_advance(ps, rp, r0, nrows, kend, wave);
     }
-    if (DBG != 3 && DBG != 4) {  // the wave's last bit row(s)
+    if (DBG != 3 && DBG != 4 && DBG != 7) {  // the wave's last bit row(s)
         for (; cur < kend; ++cur) {
             uint32_t* dst = slab + (int64_t)(wave + 16 * cur) * rs;
             for (int d = 4 * lane; d < rs; d += 256) {
@@ -833,70 +845,165 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
     __syncthreads();
     if constexpr (DBG == 1 || DBG == 2 || DBG == 5) return;
 
-    // ---- phase B: the block's bit rows Ã— the digits, chunk by chunk --------
-    // Each wave loads what it multiplies straight into registers, kRbAhead
-    // chunks ahead (no LDS stage, no barrier per chunk: LDS-DMA staging of the
-    // digits measured ~26 GB/s per CU here, register loads from L2 ~90): its
-    // limb's two B fragments of the chunk (k-steps 2pm, 2pm + 1) and, per row
-    // tile, the A dword pm of its (row, lane group) from the slab.
-    const int L = wave & 3, pm = wave >> 2;  // limb; k-steps 2pm, 2pm + 1 (dword pm of each group)
-    const int r16 = lane & 15, g = lane >> 4;
-    // the blocks start at different chunks (the chunk order is free: exact
-    // integer sums), so the CUs of an XCD do not all read one chunk's digits
-    const int rot = (int)(blockIdx.x % (unsigned)chunks);
-    const v4i* const zv = reinterpret_cast<const v4i*>(zq) + (2 * pm * kLimbs + L) * 64 + lane;  // + chunkÂ·2048
-    const uint32_t* const sa = slab + (int64_t)r16 * rs + 4 * g + pm;                              // + TÂ·16Â·rs + 16c
-    constexpr int D = kRbAhead;
-    v4i bq[D][2];
-    uint32_t aq[D][kTiles];
-#define LDS_RB_LOAD(cc, BQ, AQ)                                                               \
-    do {                                                                                      \
-        const int c_ = (cc) + rot < chunks ? (cc) + rot : (cc) + rot - chunks;                \
-        const bool ok_ = (cc) < chunks;                                                       \
-        const v4i* z_ = zv + (int64_t)(ok_ ? c_ : 0) * (kChunkBytes / 16);                    \
-        BQ[0] = z_[0];                                                                        \
-        BQ[1] = z_[kLimbs * 64];                                                              \
-        _Pragma("unroll") for (int T = 0; T < kTiles; ++T)                                    \
-            AQ[T] = (DBG == 4 || T >= tiles) ? 0x01010101u                                    \
-                                             : sa[(int64_t)(16 * T) * rs + 16 * (ok_ ? c_ : 0)]; \
+    if constexpr (DBG == 6 || DBG == 7) {
+        // ---- phase B, hybrid staging (DBG 6; 7: phase B alone) ---------------
+        // digits straight into registers, S chunks ahead (each wave its limb's
+        // two k-steps: register loads from L2 run ~3.5x the LDS-DMA rate per
+        // CU here); the block's bit-row segments of a chunk (64 B per row) by
+        // LDS-DMA, wave T < tiles one 1-KB block (row tile T) per chunk, S
+        // chunks in flight; one barrier per chunk.  Same chunks, k order and
+        // exact sums as the staged form.
+        constexpr int S = 4;
+        const int L = wave & 3, pm = wave >> 2;
+        const int r16 = lane & 15, g = lane >> 4;
+        const int rot = (int)(blockIdx.x % (unsigned)chunks);
+        unsigned long long* const sums = reinterpret_cast<unsigned long long*>(rb_lds + S * kTiles * 256);
+        for (int i = t; i < kTiles * 16 * kF; i += kRbThreads) sums[i] = 0ull;
+        const uint32_t stage_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)rb_lds);
+        const v4i* const zv = reinterpret_cast<const v4i*>(zq) + (2 * pm * kLimbs + L) * 64 + lane;
+        const bool loader = wave < tiles;
+        const uint32_t* const sseg = slab + (int64_t)(16 * (loader ? wave : 0) + (lane >> 2)) * rs + 4 * (lane & 3);
+        int ops = 0;  // this wave's vector-memory operations, in issue order
+        int qa[S];    // ops right after the loads of the chunk in slot s (its bit DMA, then its digits)
+        v4i bq[S][2];
+        v4i acc[kTiles];
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+#define LDS_RB_ISSUE(CH, SL)                                                                      \
+    do {                                                                                          \
+        const int cc_ = (CH) + rot < chunks ? (CH) + rot : (CH) + rot - chunks;                   \
+        if (loader) {                                                                             \
+            lds_dma16(sseg + 16 * cc_, stage_lds + (uint32_t)(((SL) * kTiles + wave) * 1024));    \
+            ++ops;                                                                                \
+        }                                                                                         \
+        const v4i* z_ = zv + (int64_t)cc_ * (kChunkBytes / 16);                                   \
+        rb_gload(bq[SL][0], z_);                                                                  \
+        rb_gload(bq[SL][1], z_ + kLimbs * 64);                                                    \
+        ops += 2;                                                                                 \
+        qa[SL] = ops;                                                                             \
     } while (0)
-    v4i acc[kTiles];
 #pragma unroll
-    for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+        for (int c = 0; c < S - 1; ++c)
+            if (c < chunks) LDS_RB_ISSUE(c, c);
+        for (int c0 = 0; c0 < chunks; c0 += S) {
 #pragma unroll
-    for (int d = 0; d < D - 1; ++d) LDS_RB_LOAD(d, bq[d], aq[d]);
-    for (int c0 = 0; c0 < chunks; c0 += D) {
+            for (int d = 0; d < S; ++d) {
+                const int c = c0 + d;
+                if (c < chunks) {  // (uniform)
+                    // this wave's loads of chunk c landed (its digits, and its bit
+                    // block, issued before them), then every wave's bit blocks
+                    // (barrier), and every wave is done with chunk c - 1's slot
+                    wait_vmcnt(ops - qa[d]);
+                    rb_bind(bq[d][0], bq[d][1]);
+                    asm volatile("" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    asm volatile("" ::: "memory");
+                    if (c + S - 1 < chunks) LDS_RB_ISSUE(c + S - 1, (d + S - 1) % S);
+                    const uint32_t* const tb = rb_lds + d * kTiles * 256;
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            if (c0 + d < chunks) {  // (uniform)
-                LDS_RB_LOAD(c0 + d + D - 1, bq[(d + D - 1) % D], aq[(d + D - 1) % D]);
+                    for (int T = 0; T < kTiles; ++T) {
+                        if (T < tiles) {
+                            const uint32_t w = tb[T * 256 + r16 * 16 + 4 * g + pm];
 #pragma unroll
-                for (int T = 0; T < kTiles; ++T) {
-                    if (T < tiles) {
-                        const uint32_t w = aq[d][T];
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int sh = 4 * h;
-                            v4i a;
-                            a.x = (int)((w >> sh) & 0x01010101u);
-                            a.y = (int)((w >> (sh + 1)) & 0x01010101u);
-                            a.z = (int)((w >> (sh + 2)) & 0x01010101u);
-                            a.w = (int)((w >> (sh + 3)) & 0x01010101u);
-                            acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[d][h], acc[T], 0, 0, 0);
+                            for (int h = 0; h < 2; ++h) {
+                                const int sh = 4 * h;
+                                v4i a;
+                                a.x = (int)((w >> sh) & 0x01010101u);
+                                a.y = (int)((w >> (sh + 1)) & 0x01010101u);
+                                a.z = (int)((w >> (sh + 2)) & 0x01010101u);
+                                a.w = (int)((w >> (sh + 3)) & 0x01010101u);
+                                acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[d][h], acc[T], 0, 0, 0);
+                            }
                         }
                     }
                 }
             }
         }
+#undef LDS_RB_ISSUE
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T)
+            if (T < tiles)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    atomicAdd(sums + (T * 16 + 4 * g + i) * kF + r16,
+                              (unsigned long long)((int64_t)acc[T][i] * ((int64_t)1 << (8 * L))));
+        __syncthreads();
+        for (int o = t; o < nrows * kF; o += kRbThreads) {
+            const int lr = o >> 4, f = o & 15;
+            const int row = r0 + lr;
+            const float r = s[row] * (float)ldexp((double)(int64_t)sums[o], -e_sh[f]);
+            float* out = y + (int64_t)row * ldy + f;
+            *out = beta ? *out + r : r;
+        }
+        return;
     }
-#undef LDS_RB_LOAD
+
+    // ---- phase B: the block's bit rows Ã— the digits, chunk by chunk --------
+    // Per chunk the digits (32 KB) and the block's bit-row segments (64 B per
+    // row) are staged by LDS-DMA, three chunks in flight, one barrier per chunk.
+    // (Register loads of the slab's A dwords, one 4-byte load per row tile and
+    // lane, measured 287-290 against 223 Âµs per call: 16 lines per load.)
     int8_t* const stage0 = reinterpret_cast<int8_t*>(rb_lds);
-    // C/D: col = lane & 15 (feature), row = 4(lane >> 4) + i; limb L weighs 2^(8L);
-    // the int64 sums live in the (now idle) stage memory
-    unsigned long long* const sums = reinterpret_cast<unsigned long long*>(stage0);  // [kTilesÂ·16][16]
-    __syncthreads();  // every wave's last fragment reads are done
+    const int sbytes = rb_stage_bytes(kTiles);
+    unsigned long long* const sums =
+        reinterpret_cast<unsigned long long*>(stage0 + kRbStages * sbytes);  // [kTilesÂ·16][16] int64
     for (int i = t; i < kTiles * 16 * kF; i += kRbThreads) sums[i] = 0ull;
-    __syncthreads();
+    const uint32_t stage_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)rb_lds);
+    // chunk c's stage: 32 digit blocks of 1 KB, then `tiles` blocks of the bit
+    // rows' 64-byte chunk segments (lane l: row 16T + (l >> 2), 16 bytes l & 3)
+    const int nblk = 32 + tiles;
+    auto stage = [&](int c, int buf) {
+        for (int i = wave; i < nblk; i += kRbWaves) {
+            const uint32_t dst = stage_lds + (uint32_t)(buf * sbytes + i * 1024);
+            if (i < 32) {
+                lds_dma16(zq + (int64_t)c * kChunkBytes + i * 1024 + lane * 16, dst);
+            } else {
+                const int T = i - 32;
+                lds_dma16(slab + (int64_t)(16 * T + (lane >> 2)) * rs + 16 * c + 4 * (lane & 3), dst);
+            }
+        }
+    };
+    const int mine = (nblk - 1 - wave) / kRbWaves + 1;  // stage loads this wave issues per chunk (>= 2)
+    const int L = wave & 3, pm = wave >> 2;              // limb; k-steps 2pm, 2pm + 1 (dword pm of each group)
+    const int r16 = lane & 15, g = lane >> 4;
+    v4i acc[kTiles];
+#pragma unroll
+    for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+    for (int c = 0; c < kRbStages - 1 && c < chunks; ++c) stage(c, c);
+    for (int c = 0; c < chunks; ++c) {
+        // chunk c landed (the younger chunk's loads may stay in flight), and every
+        // wave is past chunk c - 1 (whose buffer the next stage call refills)
+        if (c + 1 < chunks) {
+            if (mine >= 3) __builtin_amdgcn_s_waitcnt(0x0F73);  // vmcnt(3)
+            else __builtin_amdgcn_s_waitcnt(0x0F72);            // vmcnt(2)
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+        __syncthreads();
+        if (c + kRbStages - 1 < chunks) stage(c + kRbStages - 1, (c + kRbStages - 1) % kRbStages);
+        const int8_t* sb = stage0 + (c % kRbStages) * sbytes;
+        const v4i* bs = reinterpret_cast<const v4i*>(sb);
+        const v4i b0 = bs[((2 * pm) * kLimbs + L) * 64 + lane];
+        const v4i b1 = bs[((2 * pm + 1) * kLimbs + L) * 64 + lane];
+        const uint32_t* tb = reinterpret_cast<const uint32_t*>(sb + kChunkBytes);
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T) {
+            if (T < tiles) {
+                const uint32_t w = DBG == 4 ? 0x01010101u : tb[T * 256 + r16 * 16 + 4 * g + pm];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int sh = 4 * h;
+                    v4i a;
+                    a.x = (int)((w >> sh) & 0x01010101u);
+                    a.y = (int)((w >> (sh + 1)) & 0x01010101u);
+                    a.z = (int)((w >> (sh + 2)) & 0x01010101u);
+                    a.w = (int)((w >> (sh + 3)) & 0x01010101u);
+                    acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, h ? b1 : b0, acc[T], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // C/D: col = lane & 15 (feature), row = 4(lane >> 4) + i; limb L weighs 2^(8L)
 #pragma unroll
     for (int T = 0; T < kTiles; ++T)
         if (T < tiles)
@@ -1297,7 +1404,7 @@ constexpr int kSpStep = 256;         // entries per step: lane l loads p + 4l â€
 constexpr int kSpMaxRows = 96;       // rows per workgroup (six 16-row tiles)
 constexpr int kSpMaxGrid = 512;
 constexpr int kSpMargin = 192;       // entries streamed past a row's predicted pass end
-constexpr int kSpStateInts = 3 * kSpMaxRows + 16;  // pos, rend, fin per row; the exponents
+constexpr int kSpStateInts = 20;  // the exponents; the done counters
 constexpr int kSpDepth = 8;          // 1-KB ring slots per streaming wave (D - 1 steps in flight)
 
 struct SpGeom {
@@ -1332,6 +1439,58 @@ __device__ __forceinline__ bool sp_put(int c, int lo, int hi, int hq, uint32_t* 
     return true;
 }
 
+// A streaming wave's bit setting for one step (lane: entries i0 â€¦ i0 + 3 of
+// its row, columns c; the row's entries [rlo, rup); pass p's columns [lo, hi),
+// pass p + 1's [hi, hq)).  Each quad of lanes (16 entries, ~32 columns of a
+// dense row) ORs its pass-p entries into one 64-bit window from its first
+// valid column's word: one pair of LDS ORs per quad instead of per lane (four
+// lanes on one word serialise).  Entries outside the window â€” sparse rows,
+// the next pass's (spill), later passes' (their first index: myx) â€” take the
+// per-entry path.
+__device__ __forceinline__ void sp_set_bits(const int (&c)[4], int i0, int rlo, int rup, int lo, int hi, int hq,
+                                            uint32_t* bp, uint32_t* bq, int lane, bool& spill, int& myx) {
+    bool v[4];
+    int cm = 0x7FFFFFFF;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        v[e] = i0 + e >= rlo && i0 + e < rup;
+        if (v[e] && c[e] >= lo && c[e] < hi) cm = min(cm, c[e]);
+    }
+    cm = min(cm, __builtin_amdgcn_mov_dpp(cm, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+    cm = min(cm, __builtin_amdgcn_mov_dpp(cm, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+    const int wb = cm == 0x7FFFFFFF ? 0 : (cm - lo) >> 5;
+    uint32_t mlo = 0u, mhi = 0u;
+    bool left = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (!v[e]) continue;
+        const uint32_t r = (uint32_t)(c[e] - lo) - (uint32_t)(wb << 5);
+        if (c[e] >= lo && c[e] < hi && r < 64u) {
+            if (r < 32u) mlo |= 1u << r;
+            else mhi |= 1u << (r - 32u);
+        } else {
+            left = true;
+        }
+    }
+    mlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mlo, 0xB1, 0xF, 0xF, false);
+    mhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mhi, 0xB1, 0xF, 0xF, false);
+    mlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mlo, 0x4E, 0xF, 0xF, false);
+    mhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mhi, 0x4E, 0xF, 0xF, false);
+    if ((lane & 3) == 0) {
+        dn_or(bp + wb, mlo);
+        dn_or(bp + wb + 1, mhi);
+    }
+    if (__ballot(left) != 0ull && left) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (!v[e]) continue;
+            const uint32_t r = (uint32_t)(c[e] - lo) - (uint32_t)(wb << 5);
+            if (c[e] >= lo && c[e] < hi && r < 64u) continue;
+            if (sp_put(c[e], lo, hi, hq, bp, bq, spill)) myx = min(myx, i0 + e);
+        }
+    }
+}
+
 // DBG (timing-only ablations, wrong results): 1 no MFMAs, 2 streaming waves
 // load and count but set no bits.  The product path is DBG = 0.
 template <int kTiles, int D, int DBG = 0>
@@ -1348,21 +1507,15 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     if (nrows <= 0) return;  // (uniform: the whole workgroup)
     const int rowsL = 16 * ((rows_per_wg + 15) / 16);  // buffer rows (the host sized LDS for these)
     const int bufdw = rowsL * rowdw;
-    int* const pos = reinterpret_cast<int*>(sp_lds + 3 * bufdw);
-    int* const rend = pos + kSpMaxRows;
-    int* const fin = rend + kSpMaxRows;
-    int* const e_sh = fin + kSpMaxRows;
+    int* const e_sh = reinterpret_cast<int*>(sp_lds + 3 * bufdw);
+    int* const done = e_sh + 16;  // per buffer: multiply waves finished with it
     const int nnz = rp[n];
     const int span = cpp * kChunk;  // columns per pass
     for (int i = t; i < 3 * bufdw; i += kSpThreads) sp_lds[i] = 0u;
-    for (int i = t; i < nrows; i += kSpThreads) {
-        pos[i] = rp[r0 + i];
-        rend[i] = rp[r0 + i + 1];
-        fin[i] = -1;
-    }
     if (t < 64) {  // per-feature exponents (lds_aggregate_bitmask's quantisation)
         const uint32_t m = colmax_of(colmax, t);
         if (t < kF) e_sh[t] = col_exponent(m);
+        if (t < 3) done[t] = 0;
     }
     __syncthreads();
 
@@ -1373,6 +1526,14 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     if (wave < kSpStream) {
         // ---- streaming waves -------------------------------------------------
         const int nrw = nrows > wave ? (nrows - 1 - wave) / kSpStream + 1 : 0;  // this wave's rows
+        // the wave's row q (local row wave + 8q) in lane q's registers: where its
+        // stream resumes (pos), its end (rend), the last pass it closed (fin) â€”
+        // v_readlane / a lane select, no LDS round trip per row
+        int pos = 0, rend = 0, fin = -1;
+        if (lane < nrw) {
+            pos = rp[r0 + wave + kSpStream * lane];
+            rend = rp[r0 + wave + kSpStream * lane + 1];
+        }
         const int* const dummy = reinterpret_cast<const int*>(zq) + 4 * lane;    // null steps load here
         // issue side: pass ip, row ordinal iq, next step ia, the row's stream end
         int ip = 0, iq = 0, ia = 0, iend = 0, ilow = 0, iup = 0;
@@ -1397,12 +1558,11 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     iq = 0;                                                                                  \
                     continue;                                                                                \
                 }                                                                                            \
-                const int lr_ = wave + kSpStream * iq;                                                       \
-                if (__builtin_amdgcn_readfirstlane(fin[lr_]) < ip - 1) break; /* previous pass not closed */ \
-                ilow = __builtin_amdgcn_readfirstlane(pos[lr_]);                                             \
-                iup = __builtin_amdgcn_readfirstlane(rend[lr_]);                                             \
+                if (__builtin_amdgcn_readlane(fin, iq) < ip - 1) break; /* previous pass not closed */       \
+                ilow = __builtin_amdgcn_readlane(pos, iq);                                                    \
+                iup = __builtin_amdgcn_readlane(rend, iq);                                                    \
                 if (ilow >= iup) { /* the row is done: closed for this pass too */                          \
-                    fin[lr_] = ip;                                                                           \
+                    fin = lane == iq ? ip : fin;                                                             \
                     ++iq;                                                                                    \
                     continue;                                                                                \
                 }                                                                                            \
@@ -1443,7 +1603,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     do {                                                                                                     \
         /* slot J's step landed: every iteration issues exactly one DMA, so D - 1 younger ones stay in */    \
         /* flight (the rare paths' plain loads are waited for where they are used: stricter, never looser) */ \
-        __builtin_amdgcn_s_waitcnt(0x0F70 | (D - 1));                                                        \
+        if (DBG == 3) __builtin_amdgcn_s_waitcnt(0x0F70);                                                     \
+        else __builtin_amdgcn_s_waitcnt(0x0F70 | (D - 1));                                                   \
         asm volatile("" ::: "memory");                                                                       \
         const int k_ = mk[J];                                                                                \
         if (k_ >= 0) {                                                                                       \
@@ -1464,36 +1625,20 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             const int4 v_ = *reinterpret_cast<const int4*>(myring + (J) * 256 + 4 * lane);                   \
             int c_[4] = {v_.x, v_.y, v_.z, v_.w};                                                            \
             const int i0_ = a_ + 4 * lane;                                                                   \
-            bool fast_ = false, spill_ = false;                                                              \
-            int myx_ = 0x7FFFFFFF;                                                                           \
-            if (a_ >= rlo_ && a_ + kSpStep <= rup_) { /* interior (uniform): every entry the row's */       \
-                const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
-                fast_ = c_[0] >= lo_ && c_[3] < hi_ && (uint32_t)(c_[3] - lo_) - (w0_ << 5) < 64u;          \
-                if (fast_ && DBG != 2) {                                                                     \
-                    uint64_t m_ = 0;                                                                         \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
-                    dn_or(bp_ + w0_, (uint32_t)m_);                                                          \
-                    dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                              \
-                }                                                                                            \
-            }                                                                                                \
-            if (!fast_ && DBG != 2) {                                                                        \
-                /* per entry; two copies under a uniform branch: only the array's last step reloads the */\
-                /* lanes that read the dummy (a lane-conditional load costs vmcnt(0) on every path) */  \
+            bool spill_ = false;                                                                        \
+            int myx_ = 0x7FFFFFFF;                                                                      \
+            if (DBG != 2) {                                                                             \
                 if (a_ + kSpStep > nnz) {                                                               \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
-                        const int idx_ = i0_ + e;                                                       \
-                        if (idx_ >= rlo_ && idx_ < rup_ &&                                              \
-                            sp_put(i0_ + 4 > nnz ? col[idx_] : c_[e], lo_, hi_, hq_, bp_, bq_, spill_)) \
-                            myx_ = min(myx_, idx_);                                                     \
-                    }                                                                                   \
+                    /* the array's last step: lanes that read the dummy reload their entries (a copy of */\
+                    /* the bit setting of its own: a lane-conditional load made the compiler wait */    \
+                    /* vmcnt(0) wherever the entries are used, in every step) */                        \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)                                       \
+                        if (i0_ + 4 > nnz) c_[e] = i0_ + e < nnz ? col[i0_ + e] : 0;                    \
+                    sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
                 } else {                                                                                \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
-                        const int idx_ = i0_ + e;                                                       \
-                        if (idx_ >= rlo_ && idx_ < rup_ && sp_put(c_[e], lo_, hi_, hq_, bp_, bq_, spill_))\
-                            myx_ = min(myx_, idx_);                                                     \
-                    }                                                                                   \
+                    sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
                 }                                                                                       \
-            }                                                                                                \
+            }                                                                                           \
             if (__ballot(spill_) != 0ull) bnd = true;                                                        \
             {                                                                                                \
                 const uint64_t xm_ = __ballot(myx_ != 0x7FFFFFFF);                                           \
@@ -1520,10 +1665,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     }                                                                                        \
                 }                                                                                            \
                 if (estar != 0x7FFFFFFF) np_ = estar;                                                        \
-                if (lane == 0) {                                                                             \
-                    pos[lr_] = np_;                                                                          \
-                    fin[lr_] = p_;                                                                           \
-                }                                                                                            \
+                pos = lane == (lr_ - wave) / kSpStream ? np_ : pos;                                          \
+                fin = lane == (lr_ - wave) / kSpStream ? p_ : fin;                                           \
             }                                                                                                \
         }                                                                                                    \
     } while (0)
@@ -1588,9 +1731,15 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 if (cc + 2 < cn) LDS_SP_DIG(c0 + cc + 2, da);
                 LDS_SP_MUL(cc + 1, db);
             }
-            // pass p done: clear its buffer for pass p + 3 (whose spills start in pass p + 2)
-            uint32_t* const bz = sp_lds + (p % 3) * bufdw;
-            for (int i = t - 64 * kSpStream; i < bufdw; i += 64 * (16 - kSpStream)) bz[i] = 0u;
+            // pass p done: the last multiply wave to finish with its buffer clears it
+            // for pass p + 3 (whose spills start in pass p + 2, after the next barrier)
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's fragment reads of the buffer returned
+            const int order = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(done + p % 3, 1) : 0);
+            if (order == 16 - kSpStream - 1) {
+                uint4* const bz = reinterpret_cast<uint4*>(sp_lds + (p % 3) * bufdw);
+                for (int i = lane; i < bufdw / 4; i += 64) bz[i] = make_uint4(0u, 0u, 0u, 0u);
+                if (lane == 0) done[p % 3] = 0;
+            }
         }
 #undef LDS_SP_MUL
 #undef LDS_SP_DIG
@@ -1653,10 +1802,11 @@ static hipError_t allow_lds(K kernel, int bytes) {
 // grid: > 0 workgroups of the product kernel (0: one per CU); < 0: the
 // round-3 tile kernel (csr_dense_agg_kernel) on -grid workgroups (A/B timing).
 // The product kernel (variant): 0 column-pass concurrent, 1 column-pass
-// sequential, 2 row-block with bit slabs.  MI355X, config 5 (n = 20 000,
-// 2Â·10â¸ entries), Âµs per call: row-block 223, column-pass sequential 248,
-// concurrent 303, tile kernel 242 (profiles/r04_spmm5_*.json).
-constexpr int kDenseProduct = 3;
+// sequential, 2 row-block with bit slabs, 3 spill-pass.  MI355X, config 5
+// (n = 20 000, 2Â·10â¸ entries), Âµs per call: row-block 223-229, tile kernel
+// 242, column-pass sequential 248, concurrent 297, spill-pass 377
+// (profiles/r04_spmm5_*.json).
+constexpr int kDenseProduct = 2;
 extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                    int ldz, float* y, int ldy, int beta, void* ws, int grid, int quantize,
                                    void* stream) {
@@ -1667,7 +1817,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 5) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 34));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 7) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 35));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -1714,7 +1864,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
                                                                                                 : kDenseProduct;
     if (variant == 3) {  // the spill-pass kernel; dbg 31 no MFMAs, 32 no bit setting, 33 / 34 ring depth 6 / 12
         LDS_CHECK_ARG(R <= kSpMaxRows && g <= kSpMaxGrid);
-        const int depth = dbg == 33 ? 6 : dbg == 34 ? 12 : kSpDepth;
+        const int depth = dbg == 33 ? 6 : dbg == 34 ? 12 : kSpDepth;  // (35: depth 8, drained before every read)
         const SpGeom sg = sp_geom(nc, tiles, depth);
         const int lds = sp_lds_bytes(tiles, sg, depth);
         LDS_CHECK_ARG(lds <= 163840);
@@ -1728,6 +1878,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
     } while (0)
         if (dbg == 31) LDS_SP_LAUNCH(6, kSpDepth, 1);
         else if (dbg == 32) LDS_SP_LAUNCH(6, kSpDepth, 2);
+        else if (dbg == 35) LDS_SP_LAUNCH(6, kSpDepth, 3);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
@@ -1754,6 +1905,10 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 3) LDS_RB_LAUNCH(6, 3);
         else if (dbg == 4) LDS_RB_LAUNCH(6, 4);
         else if (dbg == 5) LDS_RB_LAUNCH(6, 5);
+        else if (dbg == 6 && tiles <= 2) LDS_RB_LAUNCH(2, 6);
+        else if (dbg == 6 && tiles <= 4) LDS_RB_LAUNCH(4, 6);
+        else if (dbg == 6) LDS_RB_LAUNCH(6, 6);
+        else if (dbg == 7) LDS_RB_LAUNCH(6, 7);
         else if (tiles <= 2) LDS_RB_LAUNCH(2, 0);
         else if (tiles <= 4) LDS_RB_LAUNCH(4, 0);
         else LDS_RB_LAUNCH(6, 0);
