@@ -899,21 +899,25 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
                     __builtin_amdgcn_s_barrier();
                     asm volatile("" ::: "memory");
                     if (c + S - 1 < chunks) LDS_RB_ISSUE(c + S - 1, (d + S - 1) % S);
+                    // every tile slot is read and multiplied (no per-tile guard, so the
+                    // reads issue together); slots past `tiles` hold stale bits whose
+                    // sums are never stored
                     const uint32_t* const tb = rb_lds + d * kTiles * 256;
+                    uint32_t wv[kTiles];
+#pragma unroll
+                    for (int T = 0; T < kTiles; ++T) wv[T] = tb[T * 256 + r16 * 16 + 4 * g + pm];
 #pragma unroll
                     for (int T = 0; T < kTiles; ++T) {
-                        if (T < tiles) {
-                            const uint32_t w = tb[T * 256 + r16 * 16 + 4 * g + pm];
+                        const uint32_t w = wv[T];
 #pragma unroll
-                            for (int h = 0; h < 2; ++h) {
-                                const int sh = 4 * h;
-                                v4i a;
-                                a.x = (int)((w >> sh) & 0x01010101u);
-                                a.y = (int)((w >> (sh + 1)) & 0x01010101u);
-                                a.z = (int)((w >> (sh + 2)) & 0x01010101u);
-                                a.w = (int)((w >> (sh + 3)) & 0x01010101u);
-                                acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[d][h], acc[T], 0, 0, 0);
-                            }
+                        for (int h = 0; h < 2; ++h) {
+                            const int sh = 4 * h;
+                            v4i a;
+                            a.x = (int)((w >> sh) & 0x01010101u);
+                            a.y = (int)((w >> (sh + 1)) & 0x01010101u);
+                            a.z = (int)((w >> (sh + 2)) & 0x01010101u);
+                            a.w = (int)((w >> (sh + 3)) & 0x01010101u);
+                            acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bq[d][h], acc[T], 0, 0, 0);
                         }
                     }
                 }
@@ -1909,9 +1913,12 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 6 && tiles <= 4) LDS_RB_LAUNCH(4, 6);
         else if (dbg == 6) LDS_RB_LAUNCH(6, 6);
         else if (dbg == 7) LDS_RB_LAUNCH(6, 7);
-        else if (tiles <= 2) LDS_RB_LAUNCH(2, 0);
-        else if (tiles <= 4) LDS_RB_LAUNCH(4, 0);
-        else LDS_RB_LAUNCH(6, 0);
+        else if (dbg == 22 && tiles <= 2) LDS_RB_LAUNCH(2, 0);  // the LDS-staged multiply phase
+        else if (dbg == 22 && tiles <= 4) LDS_RB_LAUNCH(4, 0);
+        else if (dbg == 22) LDS_RB_LAUNCH(6, 0);
+        else if (tiles <= 2) LDS_RB_LAUNCH(2, 6);  // the product: digits by register loads
+        else if (tiles <= 4) LDS_RB_LAUNCH(4, 6);
+        else LDS_RB_LAUNCH(6, 6);
 #undef LDS_RB_LAUNCH
         LDS_RETURN_LAST_ERROR();
     }

@@ -102,14 +102,14 @@ def main(n=20000, f=16, reps=20, high=1.0):
     t_dn_main = time_it(lambda: dense(0), reps)
     y_abl = torch.empty_like(y_dn)
     abl = {}
-    for dbg, what in ((6, "row-block, hybrid phase B (digits in registers, bits by LDS-DMA)"),
+    for dbg, what in ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
                       (7, "row-block: hybrid multiply phase alone"),
-                      (23, "spill-pass kernel, ring depth 8 (product)"), (33, "spill-pass, ring depth 6"),
+                      (23, "spill-pass kernel, ring depth 8"), (33, "spill-pass, ring depth 6"),
                       (34, "spill-pass, ring depth 12"), (31, "spill-pass, no MFMAs"),
                       (32, "spill-pass, streaming without bit setting"),
-                      (20, "column-pass, 8 streaming + 8 multiply waves (product)"),
-                      (21, "column-pass, 16 waves streaming then multiplying (product)"),
-                      (22, "row-block kernel with bit slabs (product)"),
+                      (20, "column-pass, 8 streaming + 8 multiply waves"),
+                      (21, "column-pass, 16 waves streaming then multiplying"),
+                      (22, "row-block kernel, multiply phase staged by LDS-DMA"),
                       (11, "column-pass concurrent, no multiply"), (12, "column-pass concurrent, no streaming"),
                       (13, "column-pass sequential, no multiply"),
                       (1, "row-block: streaming phase alone"), (2, "row-block: streaming without bit-row stores"),
