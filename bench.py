@@ -328,6 +328,12 @@ def window_breakdown(eng, reducer, args, device, k=20):
             else:
                 row["algorithmic_bytes"] = cost
                 row["achieved_GBs"] = cost / (avg * 1e-6) / 1e9
+        # HBM bytes per launch from the committed rocprofv3 PMC record of this
+        # workload (FETCH_SIZE + WRITE_SIZE, profiles/r04_pmc_traffic*.json)
+        tr, _src = pmc_traffic(name, args)
+        if tr:
+            row["pmc_traffic_bytes"] = tr
+            row["pmc_GBs"] = tr / (avg * 1e-6) / 1e9
         rows.append(row)
     rows.sort(key=lambda r: -r["us_per_window"])
     return rows, len(calls)

@@ -960,33 +960,20 @@ __device__ __forceinline__ void t128_draw(const uint32_t (&thr)[2][2][16], uint3
     }
 }
 
-// PERSIST (forms 11-13, with DRAW): a grid of two blocks per CU, each looping
-// over its XCD's tiles; the blocks of the second half sleep `stagger` ×
-// s_sleep(127) first, so that the two blocks a CU holds run out of phase —
-// one's Philox epilogue (VALU) beside the other's k-loop (MFMA).
-template <bool VEC, bool SMALL = false, bool PRE = false, bool DRAW = false, bool PERSIST = false>
+template <bool VEC, bool SMALL = false, bool PRE = false, bool DRAW = false>
 __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     const float* __restrict__ u, const float* __restrict__ v, int ld, int k,
     const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int vec4, int ldrc,
-    float gscale, int group, int per_xcd, Planes pl, DrawArgs dr = DrawArgs{}, int stagger = 0) {
+    float gscale, int group, int per_xcd, Planes pl, DrawArgs dr = DrawArgs{}) {
     constexpr int kPL = kPL2 + (PRE ? 4 : 0);
     __shared__ __attribute__((aligned(16))) uint32_t lds[12 * kPL];
     __shared__ float Ri[kT2], Rj[kT2];
 
     const int nb = (n + kT2 - 1) / kT2;
     const int ntiles = nb * (nb + 1) / 2;
-    if (PERSIST && stagger > 0 && (int)(blockIdx.x >> 3) >= (int)(gridDim.x >> 4))
-        for (int z = 0; z < stagger; ++z) __builtin_amdgcn_s_sleep(127);
-  for (int it = 0;; ++it) {
     int bi, bj;
-    if (PERSIST) {
-        const int q = (int)(blockIdx.x >> 3) + it * (int)(gridDim.x >> 3);
-        const int L = (blockIdx.x & 7) * per_xcd + q;
-        if (q >= per_xcd || L >= ntiles) break;  // (uniform: the whole block)
-        if (it > 0) __syncthreads();             // the previous tile's LDS reads are done
-        grouped_tile(L, nb, group, bi, bj);
-    } else if (group > 0) {
+    if (group > 0) {
         const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
         if (L >= ntiles) return;  // whole block: no barrier reached
         grouped_tile(L, nb, group, bi, bj);
@@ -1132,8 +1119,6 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     } else {
         t128_epilogue<SMALL>(acc, Ri, Rj, theta, grad, n, mode, lr_dev, gscale, i0, j0, wr, wc, lane);
     }
-    if (!PERSIST) break;
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1884,7 +1869,6 @@ static void launch_theta_grad(int ntiles, hipStream_t st, const float* u, const 
                               const double* lr, int vec4, int ldrc, float gscale, int form,
                               Planes pl = Planes{nullptr, nullptr}) {
     const bool pre = pl.u != nullptr;
-    if (form >= 11) form = 5;  // the persistent forms are draw-only (lds_theta_grad_sgd_draw)
     if (pre && (form == 0 || form == 3)) form = 6;  // pre-split: the 16-wide-chunk 64-tile or the 128-tile forms
     const int nb2 = (n + kT2 - 1) / kT2;
     const int nt2 = nb2 * (nb2 + 1) / 2;
@@ -2050,7 +2034,7 @@ using namespace lds;
 extern "C" int lds_theta_grad(const float* u, const float* v, int ld, int k, const float* r,
                               int ldr, int nr, const float* theta, int n, float* grad,
                               int accumulate, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 13);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
     if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(grad != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
@@ -2079,7 +2063,7 @@ extern "C" int lds_theta_grad_valu(const float* u, const float* v, int ld, int k
 extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k, const float* r,
                                   int ldr, int nr, float* theta, int n, float* grad,
                                   const void* scalars, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 13);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
     if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(theta != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
@@ -2096,7 +2080,7 @@ extern "C" int lds_theta_grad_sgd(const float* u, const float* v, int ld, int k,
 extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, int k, const float* r,
                                         int ldr, int nr, float* theta, int n, float* grad,
                                         const void* scalars, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 13);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
     if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(theta != nullptr && grad != nullptr && scalars != nullptr && n > 0 && k >= 0 && nr >= 0);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
@@ -2112,7 +2096,7 @@ extern "C" int lds_theta_grad_sgd_accum(const float* u, const float* v, int ld, 
 extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                                  int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
                                  int mode, const void* scalars, float gscale, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 13);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
     if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
     LDS_CHECK_ARG(k == 0 || (u != nullptr && v != nullptr && ld >= k));
@@ -2135,7 +2119,7 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
 extern "C" int lds_theta_grad_planes(const uint16_t* up, const uint16_t* vp, int ld, int k, const float* r,
                                      int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad, int mode,
                                      const void* scalars, float gscale, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 13);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
     if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && mode >= 0 && mode <= 3);
     LDS_CHECK_ARG(k == 0 || (up != nullptr && vp != nullptr && ld >= k));
@@ -2180,7 +2164,7 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
                                        uint64_t seed, uint32_t tag, const uint32_t* counter_base,
                                        uint32_t counter_offset, int graphs, uint64_t* bits, int words,
                                        int* deg_ws, int form, void* stream) {
-    LDS_CHECK_ARG(form >= 0 && form <= 13);
+    LDS_CHECK_ARG(form >= 0 && form <= 10);
     if (form == 10) form = 1;  // the direct-staged form needs planes (lds_theta_grad_direct): by shape here
     LDS_CHECK_ARG(u && v && theta && scalars && bits && deg_ws && n > 0 && k >= 0 && ld >= k);
     // the 128-tile draws store two words per (graph, row): whole 128-column word pairs
@@ -2206,20 +2190,6 @@ extern "C" int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, i
     // (Citeseer: 82.8 against 97.4 for the 128-tile, 112 eight-wave), the
     // 128-tile form at large n (2.49 against 2.63 ms at n = 20 000)
     if (form == 1) form = nt2 <= 256 ? 9 : nt2 >= 1024 ? 5 : 6;
-    if (form >= 11 && form <= 13 && n <= 46340) {  // persistent 128-tile, two blocks per CU (stagger by form)
-        int dev = 0, cus = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const int per2 = (nt2 + 7) / 8;
-        int g8 = (2 * (cus > 0 ? cus : 256)) / 8;
-        if (g8 > per2) g8 = per2;
-        const int stagger = form == 11 ? 0 : form == 12 ? 4 : 8;
-        hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true, false, true, true>), dim3(8 * g8), dim3(256), 0,
-                           (hipStream_t)stream, u, v, ld, k, r, ldr, nr, theta, n, grad, 2, lr, 1, 1, 1.0f, kGroup,
-                           per2, Planes{nullptr, nullptr}, dr, stagger);
-        LDS_RETURN_LAST_ERROR();
-    }
-    if (form >= 11) form = 5;
     if (form == 4 || form == 5 || form == 7 || form == 8) {
         const int per2 = (nt2 + 7) / 8;
         if (n <= 46340 && form != 7)

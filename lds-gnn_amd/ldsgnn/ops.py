@@ -437,10 +437,7 @@ def theta_grad(u: torch.Tensor, v: torch.Tensor, r: torch.Tensor, n: int,
 
 THETA_GRAD_FORMS = {"fp32": 0, "bf16x3": 1, "bf16x3-t64k16": 2, "bf16x3-t64k32": 3, "bf16x3-t128": 4,
                     "bf16x3-t128-grouped": 5, "bf16x3-t64k16-grouped": 6, "bf16x3-t128-grouped-i64": 7,
-                    "bf16x3-t128-pipe": 8, "bf16x3-t128-w8": 9, "bf16x3-direct": 10,
-                    # with the fused draw only (lds_theta_grad_sgd_draw; elsewhere the grouped 128-tile):
-                    # persistent 128-tiles, two blocks per CU, the second half started 0 / 4 / 8 sleeps late
-                    "bf16x3-t128-persist": 11, "bf16x3-t128-persist-s4": 12, "bf16x3-t128-persist-s8": 13}
+                    "bf16x3-t128-pipe": 8, "bf16x3-t128-w8": 9, "bf16x3-direct": 10}
 
 
 _theta_form = "bf16x3"

@@ -76,9 +76,9 @@ def test_theta_grad_form_is_a_per_call_argument():
         ops.theta_grad_form("bf16x3")
     with pytest.raises(ValueError):
         ops.theta_grad_form("bf16x4")
-    # a valid call shape with form 14 (past the draw-only 11-13): hipErrorInvalidValue from the form check
+    # a valid call shape with form 11: hipErrorInvalidValue from the form check
     fake = 1 << 20  # never dereferenced: the argument checks run first
-    assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, 14, None) == 1
+    assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, 11, None) == 1
     assert nat.lib.lds_theta_grad(fake, fake, 8, 8, 0, 0, 0, 0, 16, fake, 0, -1, None) == 1
 
 

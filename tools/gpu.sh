@@ -21,7 +21,6 @@
 #   acc20      the same at τ = 20 (report.pdf's setting)          acc_<ds>_tau20_TAG.jsonl
 #   acc5e      Citeseer τ = 5 on the drop-in autograd path, 3 seeds acc_citeseer_tau5_eager_TAG.jsonl
 #   multirank  2 ranks on the card over gloo (N > 1 path)    bench_2rank_gloo_TAG*.log
-#   tgp5       config-5 θ-grad + draw, persistent forms      tgp5_TAG.jsonl
 #   spmmt      the CSR-SpMM kernel tests                     spmmt_TAG.log
 #   spmm5      config-5 CSR-SpMM kernels + kernel trace + PMC spmm5_TAG.json, spmm5_prof_TAG/, spmm5_pmc_TAG_*/
 #   xtpair     W0 products one vs two samples per wave (Citeseer S = 16, Cora S = 16 / 8) xp_<ds>_<S>_<mode>_TAG.json
@@ -114,10 +113,6 @@ for step in "$@"; do
         run 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29518 bench.py --gpus 2 --backend gloo --samples 8 --steps 50 --warmup 10 \
             --no-cpu-baseline > $O/bench_2rank_gloo_s8_$tag.log 2>&1 || exit $? ;;
-    tgp5)  # config-5 theta-grad + draw: grouped 128-tile vs the persistent staggered forms
-        DRAW_FORMS=bf16x3-t64k16-grouped,bf16x3-t128-grouped,bf16x3-t128-persist,bf16x3-t128-persist-s4,bf16x3-t128-persist-s8 \
-            THETA_FORMS=bf16x3-t128-grouped run 300 python -u tools/microbench/tg_draw_ab.py c5 \
-            > $O/tgp5_$tag.jsonl 2> $O/tgp5_$tag.err || exit $? ;;
     spmmt)  # the CSR-SpMM kernel tests alone (kernels + config 5)
         run 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_config5_gpu.py -k "spmm or bitmask" -x -v \
             --timeout 240 --timeout-method thread > $O/spmmt_$tag.log 2>&1 || exit $? ;;
