@@ -1408,7 +1408,7 @@ constexpr int kSpStep = 256;         // entries per step: lane l loads p + 4l â€
 constexpr int kSpMaxRows = 96;       // rows per workgroup (six 16-row tiles)
 constexpr int kSpMaxGrid = 512;
 constexpr int kSpMargin = 192;       // entries streamed past a row's predicted pass end
-constexpr int kSpStateInts = 20;  // the exponents; the done counters
+constexpr int kSpStateInts = 3 * kSpMaxRows + 20;  // pos, rend, fin per row; the exponents; done counters
 constexpr int kSpDepth = 8;          // 1-KB ring slots per streaming wave (D - 1 steps in flight)
 
 struct SpGeom {
@@ -1443,58 +1443,6 @@ __device__ __forceinline__ bool sp_put(int c, int lo, int hi, int hq, uint32_t* 
     return true;
 }
 
-// A streaming wave's bit setting for one step (lane: entries i0 â€¦ i0 + 3 of
-// its row, columns c; the row's entries [rlo, rup); pass p's columns [lo, hi),
-// pass p + 1's [hi, hq)).  Each quad of lanes (16 entries, ~32 columns of a
-// dense row) ORs its pass-p entries into one 64-bit window from its first
-// valid column's word: one pair of LDS ORs per quad instead of per lane (four
-// lanes on one word serialise).  Entries outside the window â€” sparse rows,
-// the next pass's (spill), later passes' (their first index: myx) â€” take the
-// per-entry path.
-__device__ __forceinline__ void sp_set_bits(const int (&c)[4], int i0, int rlo, int rup, int lo, int hi, int hq,
-                                            uint32_t* bp, uint32_t* bq, int lane, bool& spill, int& myx) {
-    bool v[4];
-    int cm = 0x7FFFFFFF;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        v[e] = i0 + e >= rlo && i0 + e < rup;
-        if (v[e] && c[e] >= lo && c[e] < hi) cm = min(cm, c[e]);
-    }
-    cm = min(cm, __builtin_amdgcn_mov_dpp(cm, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-    cm = min(cm, __builtin_amdgcn_mov_dpp(cm, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
-    const int wb = cm == 0x7FFFFFFF ? 0 : (cm - lo) >> 5;
-    uint32_t mlo = 0u, mhi = 0u;
-    bool left = false;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        if (!v[e]) continue;
-        const uint32_t r = (uint32_t)(c[e] - lo) - (uint32_t)(wb << 5);
-        if (c[e] >= lo && c[e] < hi && r < 64u) {
-            if (r < 32u) mlo |= 1u << r;
-            else mhi |= 1u << (r - 32u);
-        } else {
-            left = true;
-        }
-    }
-    mlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mlo, 0xB1, 0xF, 0xF, false);
-    mhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mhi, 0xB1, 0xF, 0xF, false);
-    mlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mlo, 0x4E, 0xF, 0xF, false);
-    mhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mhi, 0x4E, 0xF, 0xF, false);
-    if ((lane & 3) == 0) {
-        dn_or(bp + wb, mlo);
-        dn_or(bp + wb + 1, mhi);
-    }
-    if (__ballot(left) != 0ull && left) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if (!v[e]) continue;
-            const uint32_t r = (uint32_t)(c[e] - lo) - (uint32_t)(wb << 5);
-            if (c[e] >= lo && c[e] < hi && r < 64u) continue;
-            if (sp_put(c[e], lo, hi, hq, bp, bq, spill)) myx = min(myx, i0 + e);
-        }
-    }
-}
-
 // DBG (timing-only ablations, wrong results): 1 no MFMAs, 2 streaming waves
 // load and count but set no bits.  The product path is DBG = 0.
 template <int kTiles, int D, int DBG = 0>
@@ -1511,11 +1459,19 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     if (nrows <= 0) return;  // (uniform: the whole workgroup)
     const int rowsL = 16 * ((rows_per_wg + 15) / 16);  // buffer rows (the host sized LDS for these)
     const int bufdw = rowsL * rowdw;
-    int* const e_sh = reinterpret_cast<int*>(sp_lds + 3 * bufdw);
+    int* const pos = reinterpret_cast<int*>(sp_lds + 3 * bufdw);
+    int* const rend = pos + kSpMaxRows;
+    int* const fin = rend + kSpMaxRows;
+    int* const e_sh = fin + kSpMaxRows;
     int* const done = e_sh + 16;  // per buffer: multiply waves finished with it
     const int nnz = rp[n];
     const int span = cpp * kChunk;  // columns per pass
     for (int i = t; i < 3 * bufdw; i += kSpThreads) sp_lds[i] = 0u;
+    for (int i = t; i < nrows; i += kSpThreads) {
+        pos[i] = rp[r0 + i];
+        rend[i] = rp[r0 + i + 1];
+        fin[i] = -1;
+    }
     if (t < 64) {  // per-feature exponents (lds_aggregate_bitmask's quantisation)
         const uint32_t m = colmax_of(colmax, t);
         if (t < kF) e_sh[t] = col_exponent(m);
@@ -1530,14 +1486,6 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     if (wave < kSpStream) {
         // ---- streaming waves -------------------------------------------------
         const int nrw = nrows > wave ? (nrows - 1 - wave) / kSpStream + 1 : 0;  // this wave's rows
-        // the wave's row q (local row wave + 8q) in lane q's registers: where its
-        // stream resumes (pos), its end (rend), the last pass it closed (fin) â€”
-        // v_readlane / a lane select, no LDS round trip per row
-        int pos = 0, rend = 0, fin = -1;
-        if (lane < nrw) {
-            pos = rp[r0 + wave + kSpStream * lane];
-            rend = rp[r0 + wave + kSpStream * lane + 1];
-        }
         const int* const dummy = reinterpret_cast<const int*>(zq) + 4 * lane;    // null steps load here
         // issue side: pass ip, row ordinal iq, next step ia, the row's stream end
         int ip = 0, iq = 0, ia = 0, iend = 0, ilow = 0, iup = 0;
@@ -1562,11 +1510,12 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     iq = 0;                                                                                  \
                     continue;                                                                                \
                 }                                                                                            \
-                if (__builtin_amdgcn_readlane(fin, iq) < ip - 1) break; /* previous pass not closed */       \
-                ilow = __builtin_amdgcn_readlane(pos, iq);                                                    \
-                iup = __builtin_amdgcn_readlane(rend, iq);                                                    \
+                const int lr_ = wave + kSpStream * iq;                                                       \
+                if (__builtin_amdgcn_readfirstlane(fin[lr_]) < ip - 1) break; /* previous pass not closed */ \
+                ilow = __builtin_amdgcn_readfirstlane(pos[lr_]);                                             \
+                iup = __builtin_amdgcn_readfirstlane(rend[lr_]);                                             \
                 if (ilow >= iup) { /* the row is done: closed for this pass too */                          \
-                    fin = lane == iq ? ip : fin;                                                             \
+                    fin[lr_] = ip;                                                                           \
                     ++iq;                                                                                    \
                     continue;                                                                                \
                 }                                                                                            \
@@ -1629,20 +1578,36 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             const int4 v_ = *reinterpret_cast<const int4*>(myring + (J) * 256 + 4 * lane);                   \
             int c_[4] = {v_.x, v_.y, v_.z, v_.w};                                                            \
             const int i0_ = a_ + 4 * lane;                                                                   \
-            bool spill_ = false;                                                                        \
-            int myx_ = 0x7FFFFFFF;                                                                      \
-            if (DBG != 2) {                                                                             \
+            bool fast_ = false, spill_ = false;                                                              \
+            int myx_ = 0x7FFFFFFF;                                                                           \
+            if (a_ >= rlo_ && a_ + kSpStep <= rup_) { /* interior (uniform): every entry the row's */       \
+                const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
+                fast_ = c_[0] >= lo_ && c_[3] < hi_ && (uint32_t)(c_[3] - lo_) - (w0_ << 5) < 64u;          \
+                if (fast_ && DBG != 2) {                                                                     \
+                    uint64_t m_ = 0;                                                                         \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
+                    dn_or(bp_ + w0_, (uint32_t)m_);                                                          \
+                    dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                              \
+                }                                                                                            \
+            }                                                                                                \
+            if (!fast_ && DBG != 2) {                                                                        \
+                /* per entry; two copies under a uniform branch: only the array's last step reloads the */\
+                /* lanes that read the dummy (a lane-conditional load costs vmcnt(0) on every path) */  \
                 if (a_ + kSpStep > nnz) {                                                               \
-                    /* the array's last step: lanes that read the dummy reload their entries (a copy of */\
-                    /* the bit setting of its own: a lane-conditional load made the compiler wait */    \
-                    /* vmcnt(0) wherever the entries are used, in every step) */                        \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e)                                       \
-                        if (i0_ + 4 > nnz) c_[e] = i0_ + e < nnz ? col[i0_ + e] : 0;                    \
-                    sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+                        const int idx_ = i0_ + e;                                                       \
+                        if (idx_ >= rlo_ && idx_ < rup_ &&                                              \
+                            sp_put(i0_ + 4 > nnz ? col[idx_] : c_[e], lo_, hi_, hq_, bp_, bq_, spill_)) \
+                            myx_ = min(myx_, idx_);                                                     \
+                    }                                                                                   \
                 } else {                                                                                \
-                    sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+                        const int idx_ = i0_ + e;                                                       \
+                        if (idx_ >= rlo_ && idx_ < rup_ && sp_put(c_[e], lo_, hi_, hq_, bp_, bq_, spill_))\
+                            myx_ = min(myx_, idx_);                                                     \
+                    }                                                                                   \
                 }                                                                                       \
-            }                                                                                           \
+            }                                                                                                \
             if (__ballot(spill_) != 0ull) bnd = true;                                                        \
             {                                                                                                \
                 const uint64_t xm_ = __ballot(myx_ != 0x7FFFFFFF);                                           \
@@ -1669,8 +1634,10 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     }                                                                                        \
                 }                                                                                            \
                 if (estar != 0x7FFFFFFF) np_ = estar;                                                        \
-                pos = lane == (lr_ - wave) / kSpStream ? np_ : pos;                                          \
-                fin = lane == (lr_ - wave) / kSpStream ? p_ : fin;                                           \
+                if (lane == 0) {                                                                             \
+                    pos[lr_] = np_;                                                                          \
+                    fin[lr_] = p_;                                                                           \
+                }                                                                                            \
             }                                                                                                \
         }                                                                                                    \
     } while (0)
@@ -1736,7 +1703,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 LDS_SP_MUL(cc + 1, db);
             }
             // pass p done: the last multiply wave to finish with its buffer clears it
-            // for pass p + 3 (whose spills start in pass p + 2, after the next barrier)
+            // for pass p + 3 (whose spills start in pass p + 2, after the next barrier);
+            // clearing it from every wave raced with the slower waves' reads
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's fragment reads of the buffer returned
             const int order = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(done + p % 3, 1) : 0);
             if (order == 16 - kSpStream - 1) {
