@@ -250,9 +250,9 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
                         float* y, int ldy, int beta, void* ws, int grid, int quantize, void* stream);
 /* Variants and timing-only ablations of lds_spmm_norm_dense (tools/spmm_config5.py;
  * the digits of an earlier call must be in ws).  Products (same results as
- * lds_spmm_norm_dense): dbg 22 the row-block kernel with bit slabs in ws
- * (the default; any column order), 6 the same with digits loaded into
- * registers, 23 the spill-pass kernel (column passes, bit rows in LDS,
+ * lds_spmm_norm_dense): dbg 6 the row-block kernel with bit slabs in ws and
+ * its digits loaded into registers (the default; any column order), 22 the
+ * same with the digits staged by LDS-DMA, 23 the spill-pass kernel (column passes, bit rows in LDS,
  * entries past a pass set in the next pass's bits; ascending columns), 33 / 34
  * the same with 6 / 12 ring slots per streaming wave (8 by default), 35 the
  * same draining its ring before every step, 20 the column-pass kernel,
@@ -262,7 +262,8 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
  * streaming waves; 1-5 the row-block kernel's streaming phase alone, without
  * its slab stores, its multiply phase alone, without its slab loads,
  * streaming with the column-pass step bookkeeping; 7 the register-digit
- * multiply phase alone.  Test hook. */
+ * multiply phase alone, 8 the same without its per-chunk barrier.  Test
+ * hook. */
 int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
                             float* y, int ldy, void* ws, int dbg, void* stream);
 int lds_bitmask_agg_splits(int n);

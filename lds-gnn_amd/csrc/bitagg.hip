@@ -732,7 +732,7 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
     const int row_stores = DBG == 2 || DBG == 5 ? 0 : (rs + 255) / 256;  // store instructions per bit row
     rb_advance(is, rp, r0, nrows, kend, wave);
     ps = is;
-    while (DBG != 3 && DBG != 4 && DBG != 7) {
+    while (DBG != 3 && DBG != 4 && DBG != 7 && DBG != 8) {
         // fill the ring: up to kRbRing steps in flight, the one read next included
         while (is.k < kend && kis - kps < kRbRing) {
             const uint32_t unit = (uint32_t)(2 * (kis % kRbRing));
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
         q1 = q2;
         rb_advance(ps, rp, r0, nrows, kend, wave);
     }
-    if (DBG != 3 && DBG != 4 && DBG != 7) {  // the wave's last bit row(s)
+    if (DBG != 3 && DBG != 4 && DBG != 7 && DBG != 8) {  // the wave's last bit row(s)
         for (; cur < kend; ++cur) {
             uint32_t* dst = slab + (int64_t)(wave + 16 * cur) * rs;
             for (int d = 4 * lane; d < rs; d += 256) {
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
     __syncthreads();
     if constexpr (DBG == 1 || DBG == 2 || DBG == 5) return;
 
-    if constexpr (DBG == 6 || DBG == 7) {
+    if constexpr (DBG == 6 || DBG == 7 || DBG == 8) {
         // ---- phase B, hybrid staging (DBG 6; 7: phase B alone) ---------------
         // digits straight into registers, S chunks ahead (each wave its limb's
         // two k-steps: register loads from L2 run ~3.5x the LDS-DMA rate per
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
                     wait_vmcnt(ops - qa[d]);
                     rb_bind(bq[d][0], bq[d][1]);
                     asm volatile("" ::: "memory");
-                    __builtin_amdgcn_s_barrier();
+                    if (DBG != 8) __builtin_amdgcn_s_barrier();  // (8: timing only, no barrier)
                     asm volatile("" ::: "memory");
                     if (c + S - 1 < chunks) LDS_RB_ISSUE(c + S - 1, (d + S - 1) % S);
                     // every tile slot is read and multiplied (no per-tile guard, so the
@@ -1789,7 +1789,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 7) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 35));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 35));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -1881,6 +1881,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 6 && tiles <= 4) LDS_RB_LAUNCH(4, 6);
         else if (dbg == 6) LDS_RB_LAUNCH(6, 6);
         else if (dbg == 7) LDS_RB_LAUNCH(6, 7);
+        else if (dbg == 8) LDS_RB_LAUNCH(6, 8);
         else if (dbg == 22 && tiles <= 2) LDS_RB_LAUNCH(2, 0);  // the LDS-staged multiply phase
         else if (dbg == 22 && tiles <= 4) LDS_RB_LAUNCH(4, 0);
         else if (dbg == 22) LDS_RB_LAUNCH(6, 0);

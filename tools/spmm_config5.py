@@ -104,6 +104,7 @@ def main(n=20000, f=16, reps=20, high=1.0):
     abl = {}
     for dbg, what in ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
                       (7, "row-block: hybrid multiply phase alone"),
+                      (8, "row-block: hybrid multiply phase alone, no per-chunk barrier"),
                       (23, "spill-pass kernel, ring depth 8"), (33, "spill-pass, ring depth 6"),
                       (34, "spill-pass, ring depth 12"), (31, "spill-pass, no MFMAs"),
                       (32, "spill-pass, streaming without bit setting"),
