@@ -255,7 +255,8 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
  * same with the digits staged by LDS-DMA, 23 the spill-pass kernel (column passes, bit rows in LDS,
  * entries past a pass set in the next pass's bits; ascending columns), 33 / 34
  * the same with 6 / 12 ring slots per streaming wave (8 by default), 35 the
- * same draining its ring before every step, 20 the column-pass kernel,
+ * same draining its ring before every step, 36 the same OR-reducing each
+ * lane quad's masks before the LDS ORs, 20 the column-pass kernel,
  * streaming and multiply waves concurrent, 21 its sequential form.  Ablations
  * (wrong results): 31 / 32 the spill-pass kernel without MFMAs / without
  * setting bits; 11 / 12 / 13 the column-pass kernel without its multiply /

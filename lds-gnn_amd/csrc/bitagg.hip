@@ -1443,6 +1443,58 @@ __device__ __forceinline__ bool sp_put(int c, int lo, int hi, int hq, uint32_t* 
     return true;
 }
 
+// A streaming wave's bit setting for one step (lane: entries i0 … i0 + 3 of
+// its row, columns c; the row's entries [rlo, rup); pass p's columns [lo, hi),
+// pass p + 1's [hi, hq)).  Each quad of lanes (16 entries, ~32 columns of a
+// dense row) ORs its pass-p entries into one 64-bit window from its first
+// valid column's word: one pair of LDS ORs per quad instead of per lane (four
+// lanes on one word serialise).  Entries outside the window — sparse rows,
+// the next pass's (spill), later passes' (their first index: myx) — take the
+// per-entry path.
+__device__ __forceinline__ void sp_set_bits(const int (&c)[4], int i0, int rlo, int rup, int lo, int hi, int hq,
+                                            uint32_t* bp, uint32_t* bq, int lane, bool& spill, int& myx) {
+    bool v[4];
+    int cm = 0x7FFFFFFF;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        v[e] = i0 + e >= rlo && i0 + e < rup;
+        if (v[e] && c[e] >= lo && c[e] < hi) cm = min(cm, c[e]);
+    }
+    cm = min(cm, __builtin_amdgcn_mov_dpp(cm, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+    cm = min(cm, __builtin_amdgcn_mov_dpp(cm, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+    const int wb = cm == 0x7FFFFFFF ? 0 : (cm - lo) >> 5;
+    uint32_t mlo = 0u, mhi = 0u;
+    bool left = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        if (!v[e]) continue;
+        const uint32_t r = (uint32_t)(c[e] - lo) - (uint32_t)(wb << 5);
+        if (c[e] >= lo && c[e] < hi && r < 64u) {
+            if (r < 32u) mlo |= 1u << r;
+            else mhi |= 1u << (r - 32u);
+        } else {
+            left = true;
+        }
+    }
+    mlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mlo, 0xB1, 0xF, 0xF, false);
+    mhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mhi, 0xB1, 0xF, 0xF, false);
+    mlo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mlo, 0x4E, 0xF, 0xF, false);
+    mhi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)mhi, 0x4E, 0xF, 0xF, false);
+    if ((lane & 3) == 0) {
+        dn_or(bp + wb, mlo);
+        dn_or(bp + wb + 1, mhi);
+    }
+    if (__ballot(left) != 0ull && left) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (!v[e]) continue;
+            const uint32_t r = (uint32_t)(c[e] - lo) - (uint32_t)(wb << 5);
+            if (c[e] >= lo && c[e] < hi && r < 64u) continue;
+            if (sp_put(c[e], lo, hi, hq, bp, bq, spill)) myx = min(myx, i0 + e);
+        }
+    }
+}
+
 // DBG (timing-only ablations, wrong results): 1 no MFMAs, 2 streaming waves
 // load and count but set no bits.  The product path is DBG = 0.
 template <int kTiles, int D, int DBG = 0>
@@ -1578,8 +1630,18 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             const int4 v_ = *reinterpret_cast<const int4*>(myring + (J) * 256 + 4 * lane);                   \
             int c_[4] = {v_.x, v_.y, v_.z, v_.w};                                                            \
             const int i0_ = a_ + 4 * lane;                                                                   \
-            bool fast_ = false, spill_ = false;                                                              \
-            int myx_ = 0x7FFFFFFF;                                                                           \
+            bool spill_ = false;                                                                        \
+            int myx_ = 0x7FFFFFFF;                                                                      \
+            if (DBG == 4) { /* the quad-reduced bit setting (sp_set_bits) */                            \
+                if (a_ + kSpStep > nnz) {                                                               \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)                                       \
+                        if (i0_ + 4 > nnz) c_[e] = i0_ + e < nnz ? col[i0_ + e] : 0;                    \
+                    sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
+                } else {                                                                                \
+                    sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
+                }                                                                                       \
+            } else {                                                                                    \
+            bool fast_ = false;                                                                              \
             if (a_ >= rlo_ && a_ + kSpStep <= rup_) { /* interior (uniform): every entry the row's */       \
                 const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
                 fast_ = c_[0] >= lo_ && c_[3] < hi_ && (uint32_t)(c_[3] - lo_) - (w0_ << 5) < 64u;          \
@@ -1608,6 +1670,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     }                                                                                   \
                 }                                                                                       \
             }                                                                                                \
+            }                                                                                           \
             if (__ballot(spill_) != 0ull) bnd = true;                                                        \
             {                                                                                                \
                 const uint64_t xm_ = __ballot(myx_ != 0x7FFFFFFF);                                           \
@@ -1789,7 +1852,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 35));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 36));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -1851,6 +1914,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         if (dbg == 31) LDS_SP_LAUNCH(6, kSpDepth, 1);
         else if (dbg == 32) LDS_SP_LAUNCH(6, kSpDepth, 2);
         else if (dbg == 35) LDS_SP_LAUNCH(6, kSpDepth, 3);
+        else if (dbg == 36) LDS_SP_LAUNCH(6, kSpDepth, 4);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);

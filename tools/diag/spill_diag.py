@@ -28,7 +28,7 @@ def run(n, dens, grid, seed):
     z = z.to(dev)
     ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=dev)
     y = {}
-    for name, dbg in (("rowblock", 22), ("spill", 23), ("spill_d6", 33), ("spill_d12", 34), ("spill_vm0", 35), ("rowblock_hybrid", 6)):
+    for name, dbg in (("rowblock", 22), ("spill", 23), ("spill_d6", 33), ("spill_d12", 34), ("spill_vm0", 35), ("rowblock_hybrid", 6), ("spill_quad", 36)):
         out = torch.empty(n, 16, device=dev)
         if dbg == 22:
             nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(s), n, nat.ptr(z), 16, nat.ptr(out),

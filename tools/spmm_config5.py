@@ -94,7 +94,7 @@ def main(n=20000, f=16, reps=20, high=1.0):
     t_tile = time_it(lambda: dense(0, -256), reps)  # round 3's tile kernel (product only)
     y_abl0 = torch.empty_like(y_dn)
     eq_variants = {}
-    for dbg in (20, 21, 22, 23, 33, 34, 6):  # the product variants give the same bits
+    for dbg in (20, 21, 22, 23, 33, 34, 6, 36):  # the product variants give the same bits
         nat.call("lds_spmm_dense_ablation", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_abl0), f,
                  nat.ptr(ws_dn), dbg, st)
         eq_variants[dbg] = bool(torch.equal(y_abl0, y_main))
@@ -105,7 +105,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
     for dbg, what in ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
                       (7, "row-block: hybrid multiply phase alone"),
                       (8, "row-block: hybrid multiply phase alone, no per-chunk barrier"),
-                      (23, "spill-pass kernel, ring depth 8"), (33, "spill-pass, ring depth 6"),
+                      (23, "spill-pass kernel, ring depth 8"), (36, "spill-pass, quad-reduced bit setting"),
+                      (33, "spill-pass, ring depth 6"),
                       (34, "spill-pass, ring depth 12"), (31, "spill-pass, no MFMAs"),
                       (32, "spill-pass, streaming without bit setting"),
                       (20, "column-pass, 8 streaming + 8 multiply waves"),
