@@ -1408,23 +1408,24 @@ constexpr int kSpStep = 256;         // entries per step: lane l loads p + 4l â€
 constexpr int kSpMaxRows = 96;       // rows per workgroup (six 16-row tiles)
 constexpr int kSpMaxGrid = 512;
 constexpr int kSpMargin = 192;       // entries streamed past a row's predicted pass end
-constexpr int kSpStateInts = 3 * kSpMaxRows + 20;  // pos, rend, fin per row; the exponents; done counters
+constexpr int kSpStateInts = 3 * kSpMaxRows + 20 + 12 * 12 * 4;  // pos, rend, fin per row; the exponents;
+                                                                         // done counters; (DBG 8) ring slot records
 constexpr int kSpDepth = 8;          // 1-KB ring slots per streaming wave (D - 1 steps in flight)
 
 struct SpGeom {
     int cpp, passes, rowdw;  // chunks per pass, passes, dwords per buffer row (16Â·cpp + 2: bank spread)
 };
-SpGeom sp_geom(int chunks, int tiles, int depth) {
+SpGeom sp_geom(int chunks, int tiles, int depth, int ns = kSpStream, int slot = 1024) {
     const int rows = 16 * tiles;
-    int cpp = ((163840 - kSpStream * depth * 1024 - 4 * kSpStateInts) / (3 * rows * 4) - 2) / 16;
+    int cpp = ((163840 - ns * depth * slot - 4 * kSpStateInts) / (3 * rows * 4) - 2) / 16;
     if (cpp > chunks) cpp = chunks;
     if (cpp < 1) cpp = 1;
     const int passes = (chunks + cpp - 1) / cpp;
     cpp = (chunks + passes - 1) / passes;
     return SpGeom{cpp, passes, 16 * cpp + 2};
 }
-int sp_lds_bytes(int tiles, const SpGeom& g, int depth) {
-    return kSpStream * depth * 1024 + 3 * 16 * tiles * g.rowdw * 4 + 4 * kSpStateInts;
+int sp_lds_bytes(int tiles, const SpGeom& g, int depth, int ns = kSpStream, int slot = 1024) {
+    return ns * depth * slot + 3 * 16 * tiles * g.rowdw * 4 + 4 * kSpStateInts;
 }
 
 // Entry c (column) of a row in pass p: its bit in pass p's buffer row bp
@@ -1495,15 +1496,79 @@ __device__ __forceinline__ void sp_set_bits(const int (&c)[4], int i0, int rlo, 
     }
 }
 
+// A streaming wave's bit setting for one step without per-entry branches
+// (DBG 5): each lane ORs its entries of pass p into one 64-bit window from
+// its first such entry's word and its entries of pass p + 1 into another, so
+// a row's boundary steps (about a third of all steps at 8 passes) cost about
+// what an interior step costs.  Entries that fit neither window (sparse rows)
+// take single-bit ORs under a wave-uniform guard; entries past pass p + 1
+// only report their first index (myx).  Same bits as sp_put entry by entry.
+__device__ __forceinline__ void sp_set_bits_win(const int (&c)[4], int i0, int rlo, int rup, int lo, int hi, int hq,
+                                                uint32_t* bp, uint32_t* bq, bool& spill, int& myx) {
+    constexpr int kNone = 0x7FFFFFFF;
+    bool vp[4], vq[4];
+    int fp = kNone, fq = kNone;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const bool v = i0 + e >= rlo && i0 + e < rup;
+        vp[e] = v && c[e] >= lo && c[e] < hi;
+        vq[e] = v && c[e] >= hi && c[e] < hq;
+        spill = spill || (v && c[e] >= hi);
+        myx = v && c[e] >= hq ? min(myx, i0 + e) : myx;
+        fp = vp[e] ? min(fp, c[e]) : fp;
+        fq = vq[e] ? min(fq, c[e]) : fq;
+    }
+    // window starts (a lane without entries of a pass: the row's first word, empty mask)
+    const int bp0 = fp == kNone ? lo : lo + ((fp - lo) & ~31);
+    const int bq0 = fq == kNone ? hi : hi + ((fq - hi) & ~31);
+    uint64_t mp = 0, mq = 0;
+    bool misfit = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const uint32_t rp = (uint32_t)(c[e] - bp0), rq = (uint32_t)(c[e] - bq0);
+        mp |= vp[e] && rp < 64u ? 1ull << (rp & 63u) : 0ull;
+        mq |= vq[e] && rq < 64u ? 1ull << (rq & 63u) : 0ull;
+        misfit = misfit || (vp[e] && rp >= 64u) || (vq[e] && rq >= 64u);
+    }
+    uint32_t* const wp = bp + ((bp0 - lo) >> 5);
+    dn_or(wp, (uint32_t)mp);
+    dn_or(wp + 1, (uint32_t)(mp >> 32));
+    if (__ballot(mq != 0ull) != 0ull) {
+        uint32_t* const wq = bq + ((bq0 - hi) >> 5);
+        dn_or(wq, (uint32_t)mq);
+        dn_or(wq + 1, (uint32_t)(mq >> 32));
+    }
+    if (__ballot(misfit) != 0ull) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (vp[e] && (uint32_t)(c[e] - bp0) >= 64u) atomicOr(bp + ((c[e] - lo) >> 5), 1u << ((c[e] - lo) & 31));
+            if (vq[e] && (uint32_t)(c[e] - bq0) >= 64u) atomicOr(bq + ((c[e] - hi) >> 5), 1u << ((c[e] - hi) & 31));
+        }
+    }
+}
+
 // DBG (timing-only ablations, wrong results): 1 no MFMAs, 2 streaming waves
-// load and count but set no bits.  The product path is DBG = 0.
-template <int kTiles, int D, int DBG = 0>
+// load and count but set no bits.  The product path is DBG = 0.  Same
+// results: 3 drains the ring before every read, 4 quad-reduced bit setting
+// (sp_set_bits), 5 windowed bit setting on every step (sp_set_bits_win), 6 each
+// step's columns read from the ring one step ahead of its bit ORs.  Timing
+// only: 7 the interior steps' ORs as plain stores.  8 (same results): the
+// ring loop not unrolled (the slot a runtime index, its records in LDS); 9
+// the interior fast path, sp_set_bits_win for every other step; 10 a second
+// fast path for lanes whose four entries all belong to pass p + 1; 11 as 10
+// and a third for lanes that straddle the pass boundary; 12 as 11 with 2-KB
+// steps (8 entries per lane, two DMAs per step).
+template <int kTiles, int D, int DBG = 0, int NS = kSpStream>
 __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
     int chunks, int cpp, int passes, int rowdw, const uint32_t* __restrict__ colmax, const float* __restrict__ s,
     float* __restrict__ y, int ldy, int beta) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sp_lds_all[];
-    uint32_t* const sp_lds = sp_lds_all + kSpStream * D * 256;  // after the rings: three pass buffers, row state
+    // entries per lane and step: 4 (1-KB steps) or, DBG 12, 8 (2-KB steps, two DMAs)
+    constexpr int kE = DBG == 12 ? 8 : 4;
+    constexpr int kStep = 64 * kE;
+    static_assert((D - 1) * (kE / 4) <= 15, "vmcnt field");
+    uint32_t* const sp_lds = sp_lds_all + NS * D * kStep;  // after the rings: three pass buffers, row state
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int r0 = (int)blockIdx.x * rows_per_wg;
@@ -1516,6 +1581,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     int* const fin = rend + kSpMaxRows;
     int* const e_sh = fin + kSpMaxRows;
     int* const done = e_sh + 16;  // per buffer: multiply waves finished with it
+    int4* const meta = reinterpret_cast<int4*>(done + 4);  // (DBG 8) per wave and slot: start, row bounds, key
     const int nnz = rp[n];
     const int span = cpp * kChunk;  // columns per pass
     for (int i = t; i < 3 * bufdw; i += kSpThreads) sp_lds[i] = 0u;
@@ -1531,13 +1597,20 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     }
     __syncthreads();
 
-    v4i acc[kTiles];
+    // multiply waves: kMW; each runs kLW limbs over kHalves halves of every chunk
+    constexpr int kMW = 16 - NS;
+    constexpr int kLW = kMW == 2 ? 2 : 1;
+    constexpr int kHalves = kMW <= 4 ? 2 : 1;
+    static_assert(kMW == 2 || kMW == 4 || kMW == 8, "8, 4 or 2 multiply waves");
+    v4i acc[kLW][kTiles];
 #pragma unroll
-    for (int T = 0; T < kTiles; ++T) acc[T] = v4i{0, 0, 0, 0};
+    for (int l = 0; l < kLW; ++l)
+#pragma unroll
+        for (int T = 0; T < kTiles; ++T) acc[l][T] = v4i{0, 0, 0, 0};
 
-    if (wave < kSpStream) {
+    if (wave < NS) {
         // ---- streaming waves -------------------------------------------------
-        const int nrw = nrows > wave ? (nrows - 1 - wave) / kSpStream + 1 : 0;  // this wave's rows
+        const int nrw = nrows > wave ? (nrows - 1 - wave) / NS + 1 : 0;  // this wave's rows
         const int* const dummy = reinterpret_cast<const int*>(zq) + 4 * lane;    // null steps load here
         // issue side: pass ip, row ordinal iq, next step ia, the row's stream end
         int ip = 0, iq = 0, ia = 0, iend = 0, ilow = 0, iup = 0;
@@ -1547,10 +1620,11 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         // first << 16 | last << 17), -1 for a null step
         int ma[D], mlo[D], mup[D], mk[D];
         const uint32_t ring_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)sp_lds_all) +
-                                  (uint32_t)(wave * D * 1024);
-        const uint32_t* const myring = sp_lds_all + wave * D * 256;
+                                  (uint32_t)(wave * D * kStep * 4);
+        const uint32_t* const myring = sp_lds_all + wave * D * kStep;
         // process side: the pass the multiply waves wait for; the row's flags
         int cp = 0, estar = 0x7FFFFFFF;
+        int4 nxt_ = int4{0, 0, 0, 0};  // (DBG 6) the next step's columns
         bool bnd = false;
 #define LDS_SP_ISSUE(J)                                                                                      \
     do {                                                                                                     \
@@ -1562,7 +1636,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     iq = 0;                                                                                  \
                     continue;                                                                                \
                 }                                                                                            \
-                const int lr_ = wave + kSpStream * iq;                                                       \
+                const int lr_ = wave + NS * iq;                                                       \
                 if (__builtin_amdgcn_readfirstlane(fin[lr_]) < ip - 1) break; /* previous pass not closed */ \
                 ilow = __builtin_amdgcn_readfirstlane(pos[lr_]);                                             \
                 iup = __builtin_amdgcn_readfirstlane(rend[lr_]);                                             \
@@ -1582,12 +1656,12 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 irow = true;                                                                                 \
                 ifirst = true;                                                                               \
             }                                                                                                \
-            const bool last_ = ia + kSpStep >= iend;                                                         \
+            const bool last_ = ia + kStep >= iend;                                                           \
             a_ = ia;                                                                                         \
             lo_ = ilow;                                                                                      \
             up_ = iup;                                                                                       \
-            k_ = (wave + kSpStream * iq) | (ip << 8) | (ifirst ? 1 << 16 : 0) | (last_ ? 1 << 17 : 0);      \
-            ia += kSpStep;                                                                                   \
+            k_ = (wave + NS * iq) | (ip << 8) | (ifirst ? 1 << 16 : 0) | (last_ ? 1 << 17 : 0);      \
+            ia += kStep;                                                                                     \
             ifirst = false;                                                                                  \
             if (last_) {                                                                                     \
                 irow = false;                                                                                \
@@ -1595,23 +1669,44 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             }                                                                                                \
             break;                                                                                           \
         }                                                                                                    \
-        ma[J] = a_;                                                                                          \
-        mlo[J] = lo_;                                                                                        \
-        mup[J] = up_;                                                                                        \
-        mk[J] = k_;                                                                                          \
+        if constexpr (DBG == 8) {                                                                            \
+            if (lane == 0) meta[wave * D + (J)] = int4{a_, lo_, up_, k_};                                    \
+        } else {                                                                                             \
+            ma[J] = a_;                                                                                      \
+            mlo[J] = lo_;                                                                                    \
+            mup[J] = up_;                                                                                    \
+            mk[J] = k_;                                                                                      \
+        }                                                                                                    \
         pending += k_ >= 0 ? 1 : 0;                                                                          \
-        const int aa_ = a_ + 4 * lane;                                                                       \
-        const int* src_ = (a_ >= 0 && aa_ + 4 <= nnz) ? col + aa_ : dummy;                                   \
-        lds_dma16(src_, ring_lds + (uint32_t)(J) * 1024u);                                                   \
+        _Pragma("unroll") for (int h_ = 0; h_ < kE / 4; ++h_) {                                              \
+            const int aa_ = a_ + 256 * h_ + 4 * lane;                                                        \
+            const int* src_ = (a_ >= 0 && aa_ + 4 <= nnz) ? col + aa_ : dummy;                               \
+            lds_dma16(src_, ring_lds + (uint32_t)(J) * (uint32_t)(4 * kStep) + 1024u * h_);                 \
+        }                                                                                                    \
     } while (0)
 #define LDS_SP_PROCESS(J)                                                                                    \
     do {                                                                                                     \
         /* slot J's step landed: every iteration issues exactly one DMA, so D - 1 younger ones stay in */    \
         /* flight (the rare paths' plain loads are waited for where they are used: stricter, never looser) */ \
         if (DBG == 3) __builtin_amdgcn_s_waitcnt(0x0F70);                                                     \
-        else __builtin_amdgcn_s_waitcnt(0x0F70 | (D - 1));                                                   \
+        else if (DBG == 6) __builtin_amdgcn_s_waitcnt(0x0F70 | (D - 2)); /* slots J and J + 1 landed */       \
+        else __builtin_amdgcn_s_waitcnt(0x0F70 | ((D - 1) * (kE / 4)));                                                 \
         asm volatile("" ::: "memory");                                                                       \
-        const int k_ = mk[J];                                                                                \
+        const int4 cur_ = nxt_; /* DBG 6: slot J, read one step ahead of its bit ORs */                      \
+        if (DBG == 6) nxt_ = *reinterpret_cast<const int4*>(myring + (((J) + 1) % D) * 256 + 4 * lane);      \
+        int k_, ma_, mlo_, mup_;                                                                             \
+        if constexpr (DBG == 8) {                                                                            \
+            const int4 mt_ = meta[wave * D + (J)];                                                           \
+            k_ = __builtin_amdgcn_readfirstlane(mt_.w);                                                      \
+            ma_ = __builtin_amdgcn_readfirstlane(mt_.x);                                                     \
+            mlo_ = __builtin_amdgcn_readfirstlane(mt_.y);                                                    \
+            mup_ = __builtin_amdgcn_readfirstlane(mt_.z);                                                    \
+        } else {                                                                                             \
+            k_ = mk[J];                                                                                      \
+            ma_ = ma[J];                                                                                     \
+            mlo_ = mlo[J];                                                                                   \
+            mup_ = mup[J];                                                                                   \
+        }                                                                                                    \
         if (k_ >= 0) {                                                                                       \
             --pending;                                                                                       \
             const int lr_ = k_ & 0xFF, p_ = (k_ >> 8) & 0xFF;                                                \
@@ -1626,14 +1721,20 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             const int lo_ = p_ * span, hi_ = min(lo_ + span, n), hq_ = min(hi_ + span, n);                   \
             uint32_t* const bp_ = sp_lds + (p_ % 3) * bufdw + lr_ * rowdw;                                   \
             uint32_t* const bq_ = sp_lds + ((p_ + 1) % 3) * bufdw + lr_ * rowdw;                             \
-            const int a_ = ma[J], rlo_ = mlo[J], rup_ = mup[J];                                              \
-            const int4 v_ = *reinterpret_cast<const int4*>(myring + (J) * 256 + 4 * lane);                   \
-            int c_[4] = {v_.x, v_.y, v_.z, v_.w};                                                            \
-            const int i0_ = a_ + 4 * lane;                                                                   \
+            const int a_ = ma_, rlo_ = mlo_, rup_ = mup_;                                                    \
+            int c_[kE];                                                                                      \
+            _Pragma("unroll") for (int h_ = 0; h_ < kE / 4; ++h_) {                                          \
+                const int4 v_ = DBG == 6 ? cur_ : *reinterpret_cast<const int4*>(myring + (J) * kStep + kE * lane + 4 * h_); \
+                c_[4 * h_] = v_.x;                                                                           \
+                c_[4 * h_ + 1] = v_.y;                                                                       \
+                c_[4 * h_ + 2] = v_.z;                                                                       \
+                c_[4 * h_ + 3] = v_.w;                                                                       \
+            }                                                                                                \
+            const int i0_ = a_ + kE * lane;                                                                  \
             bool spill_ = false;                                                                        \
             int myx_ = 0x7FFFFFFF;                                                                      \
-            if (DBG == 4) { /* the quad-reduced bit setting (sp_set_bits) */                            \
-                if (a_ + kSpStep > nnz) {                                                               \
+            if constexpr (DBG == 4) { /* the quad-reduced bit setting (sp_set_bits) */                  \
+                if (a_ + kStep > nnz) {                                                                 \
                     _Pragma("unroll") for (int e = 0; e < 4; ++e)                                       \
                         if (i0_ + 4 > nnz) c_[e] = i0_ + e < nnz ? col[i0_ + e] : 0;                    \
                     sp_set_bits(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, lane, spill_, myx_);      \
@@ -1642,28 +1743,67 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 }                                                                                       \
             } else {                                                                                    \
             bool fast_ = false;                                                                              \
-            if (a_ >= rlo_ && a_ + kSpStep <= rup_) { /* interior (uniform): every entry the row's */       \
+            if (DBG != 5 && a_ >= rlo_ && a_ + kStep <= rup_) { /* interior (uniform): all the row's */   \
                 const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
-                fast_ = c_[0] >= lo_ && c_[3] < hi_ && (uint32_t)(c_[3] - lo_) - (w0_ << 5) < 64u;          \
+                fast_ = c_[0] >= lo_ && c_[kE - 1] < hi_ && (uint32_t)(c_[kE - 1] - lo_) - (w0_ << 5) < 64u; \
                 if (fast_ && DBG != 2) {                                                                     \
                     uint64_t m_ = 0;                                                                         \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
-                    dn_or(bp_ + w0_, (uint32_t)m_);                                                          \
-                    dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                              \
+                    _Pragma("unroll") for (int e = 0; e < kE; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
+                    if (DBG == 7) { /* timing only: plain stores instead of ORs */                           \
+                        bp_[w0_] = (uint32_t)m_;                                                             \
+                        bp_[w0_ + 1] = (uint32_t)(m_ >> 32);                                                 \
+                    } else {                                                                                 \
+                        dn_or(bp_ + w0_, (uint32_t)m_);                                                      \
+                        dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                          \
+                    }                                                                                        \
+                }                                                                                            \
+                if ((DBG == 10 || DBG >= 11) && !fast_) { /* all of pass p + 1 (past the boundary) */       \
+                    const uint32_t q0_ = (uint32_t)(c_[0] - hi_) >> 5;                                       \
+                    if (c_[0] >= hi_ && c_[kE - 1] < hq_ && (uint32_t)(c_[kE - 1] - hi_) - (q0_ << 5) < 64u) { \
+                        uint64_t m_ = 0;                                                                     \
+                        _Pragma("unroll") for (int e = 0; e < kE; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - hi_) - (q0_ << 5)); \
+                        dn_or(bq_ + q0_, (uint32_t)m_);                                                      \
+                        dn_or(bq_ + q0_ + 1, (uint32_t)(m_ >> 32));                                          \
+                        spill_ = true;                                                                       \
+                        fast_ = true;                                                                        \
+                    }                                                                                        \
+                }                                                                                            \
+                if (DBG >= 11 && !fast_ && c_[0] >= lo_ && c_[0] < hi_ && c_[kE - 1] >= hi_ &&               \
+                    c_[kE - 1] < hq_ && (uint32_t)(c_[kE - 1] - hi_) < 64u) { /* straddles the boundary */   \
+                    uint64_t mp_ = 0, mq_ = 0;                                                               \
+                    bool ok_ = true;                                                                         \
+                    _Pragma("unroll") for (int e = 0; e < kE; ++e) {                                         \
+                        const bool in_ = c_[e] < hi_;                                                        \
+                        const uint32_t r_ = in_ ? (uint32_t)(c_[e] - lo_) - (w0_ << 5) : (uint32_t)(c_[e] - hi_); \
+                        ok_ = ok_ && r_ < 64u;                                                               \
+                        const uint64_t b_ = 1ull << (r_ & 63u);                                              \
+                        mp_ |= in_ ? b_ : 0ull;                                                              \
+                        mq_ |= in_ ? 0ull : b_;                                                              \
+                    }                                                                                        \
+                    if (ok_) {                                                                               \
+                        dn_or(bp_ + w0_, (uint32_t)mp_);                                                     \
+                        dn_or(bp_ + w0_ + 1, (uint32_t)(mp_ >> 32));                                         \
+                        dn_or(bq_, (uint32_t)mq_);                                                           \
+                        dn_or(bq_ + 1, (uint32_t)(mq_ >> 32));                                               \
+                        spill_ = true;                                                                       \
+                        fast_ = true;                                                                        \
+                    }                                                                                        \
                 }                                                                                            \
             }                                                                                                \
             if (!fast_ && DBG != 2) {                                                                        \
                 /* per entry; two copies under a uniform branch: only the array's last step reloads the */\
                 /* lanes that read the dummy (a lane-conditional load costs vmcnt(0) on every path) */  \
-                if (a_ + kSpStep > nnz) {                                                               \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+                if (a_ + kStep > nnz) {                                                                 \
+                    _Pragma("unroll") for (int e = 0; e < kE; ++e) {                                    \
                         const int idx_ = i0_ + e;                                                       \
                         if (idx_ >= rlo_ && idx_ < rup_ &&                                              \
-                            sp_put(i0_ + 4 > nnz ? col[idx_] : c_[e], lo_, hi_, hq_, bp_, bq_, spill_)) \
+                            sp_put((idx_ & ~3) + 4 > nnz ? col[idx_] : c_[e], lo_, hi_, hq_, bp_, bq_, spill_)) \
                             myx_ = min(myx_, idx_);                                                     \
                     }                                                                                   \
+                } else if constexpr (DBG == 5 || DBG == 9) {                                            \
+                    sp_set_bits_win(c_, i0_, rlo_, rup_, lo_, hi_, hq_, bp_, bq_, spill_, myx_);        \
                 } else {                                                                                \
-                    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+                    _Pragma("unroll") for (int e = 0; e < kE; ++e) {                                    \
                         const int idx_ = i0_ + e;                                                       \
                         if (idx_ >= rlo_ && idx_ < rup_ && sp_put(c_[e], lo_, hi_, hq_, bp_, bq_, spill_))\
                             myx_ = min(myx_, idx_);                                                     \
@@ -1677,7 +1817,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 if (xm_ != 0ull) estar = min(estar, __builtin_amdgcn_readlane(myx_, __builtin_ctzll(xm_)));  \
             }                                                                                                \
             if (k_ & (1 << 17)) { /* the row's last issued step: where pass p + 1 starts */                 \
-                int np_ = min(a_ + kSpStep, rup_);                                                           \
+                int np_ = min(a_ + kStep, rup_);                                                             \
                 if (estar == 0x7FFFFFFF && !bnd && np_ < rup_ && DBG != 2) {                                 \
                     /* the boundary lies past the predicted end: finish the row with blocking loads */       \
                     while (np_ < rup_) {                                                                     \
@@ -1704,8 +1844,21 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             }                                                                                                \
         }                                                                                                    \
     } while (0)
+        if constexpr (DBG == 8) {  // one copy of the loop body, the slot a runtime index
+            for (int j = 0; j < D - 1; ++j) LDS_SP_ISSUE(j);
+            for (int j = 0;; j = j + 1 == D ? 0 : j + 1) {
+                LDS_SP_ISSUE(j == 0 ? D - 1 : j - 1);
+                LDS_SP_PROCESS(j);
+                if (ip >= passes && pending == 0) goto streamed;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < D - 1; ++j) LDS_SP_ISSUE(j);
+        if (DBG == 6) {  // slot 0 landed: read it ahead
+            __builtin_amdgcn_s_waitcnt(0x0F70 | (D - 2));
+            asm volatile("" ::: "memory");
+            nxt_ = *reinterpret_cast<const int4*>(myring + 4 * lane);
+        }
         while (true) {
 #pragma unroll
             for (int j = 0; j < D; ++j) {
@@ -1723,20 +1876,23 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         }
     } else {
         // ---- multiply waves --------------------------------------------------
-        const int m = wave - kSpStream, L = m & 3, hh = m >> 2;
+        // 8 multiply waves: limb m & 3, k-steps 4(m >> 2) â€¦ + 3 of each chunk; 4
+        // (NS = 12): limb m, both halves of each chunk in turn
+        const int m = wave - NS, L = kLW * (m & 3), hh0 = kHalves == 2 ? 0 : m >> 2;
         const int r16 = lane & 15, g = lane >> 4;
-        const v4i* const zv = reinterpret_cast<const v4i*>(zq) + (4 * hh * kLimbs + L) * 64 + lane;
+        const v4i* const zv = reinterpret_cast<const v4i*>(zq) + L * 64 + lane;
         const int ntiles = (nrows + 15) / 16;
-#define LDS_SP_DIG(CH, DQ)                                                         \
-    do {                                                                           \
-        const v4i* z_ = zv + (int64_t)(CH) * (kChunkBytes / 16);                   \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) DQ[i] = z_[i * kLimbs * 64]; \
+#define LDS_SP_DIG(CH, HH, DQ)                                                                 \
+    do {                                                                                       \
+        const v4i* z_ = zv + (int64_t)(CH) * (kChunkBytes / 16) + 4 * (HH) * kLimbs * 64;      \
+        _Pragma("unroll") for (int l = 0; l < kLW; ++l)                                      \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) DQ[l][i] = z_[i * kLimbs * 64 + l * 64]; \
     } while (0)
-#define LDS_SP_MUL(CC, DQ)                                                                                    \
+#define LDS_SP_MUL(CC, HH, DQ)                                                                                  \
     do {                                                                                                      \
         _Pragma("unroll") for (int T = 0; T < kTiles; ++T) {                                                  \
             if (T < ntiles) {                                                                                 \
-                const uint2 w_ = *reinterpret_cast<const uint2*>(bp + (16 * T + r16) * rowdw + (CC) * 16 + 4 * g + 2 * hh); \
+                const uint2 w_ = *reinterpret_cast<const uint2*>(bp + (16 * T + r16) * rowdw + (CC) * 16 + 4 * g + 2 * (HH)); \
                 _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
                     const uint32_t w = (i >> 1) ? w_.y : w_.x;                                                \
                     const int sh = 4 * (i & 1);                                                               \
@@ -1745,32 +1901,36 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     a.y = (int)((w >> (sh + 1)) & 0x01010101u);                                               \
                     a.z = (int)((w >> (sh + 2)) & 0x01010101u);                                               \
                     a.w = (int)((w >> (sh + 3)) & 0x01010101u);                                               \
-                    if (DBG != 1) acc[T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, DQ[i], acc[T], 0, 0, 0); \
-                    else acc[T] += a;                                                                         \
+                    _Pragma("unroll") for (int l = 0; l < kLW; ++l) {                                         \
+                        if (DBG != 1) acc[l][T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, DQ[l][i], acc[l][T], 0, 0, 0); \
+                        else acc[l][T] += a;                                                                  \
+                    }                                                                                         \
                 }                                                                                             \
             }                                                                                                 \
         }                                                                                                     \
     } while (0)
         for (int p = 0; p < passes; ++p) {
             const int c0 = p * cpp, cn = min(cpp, chunks - c0);
-            v4i da[4], db[4];
-            LDS_SP_DIG(c0, da);  // before the barrier: in flight while pass p finishes streaming
+            v4i da[kLW][4], db[kLW][4];
+            // units u = (chunk, half): chunk u / kHalves, half hh0 + u % kHalves
+            const int un = cn * kHalves;
+            LDS_SP_DIG(c0, hh0, da);  // before the barrier: in flight while pass p finishes streaming
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_s_barrier();  // pass p streamed
             const uint32_t* const bp = sp_lds + (p % 3) * bufdw;
-            for (int cc = 0; cc < cn; cc += 2) {
-                if (cc + 1 < cn) LDS_SP_DIG(c0 + cc + 1, db);
-                LDS_SP_MUL(cc, da);
-                if (cc + 1 >= cn) break;
-                if (cc + 2 < cn) LDS_SP_DIG(c0 + cc + 2, da);
-                LDS_SP_MUL(cc + 1, db);
+            for (int u = 0; u < un; u += 2) {
+                if (u + 1 < un) LDS_SP_DIG(c0 + (u + 1) / kHalves, hh0 + (u + 1) % kHalves, db);
+                LDS_SP_MUL(u / kHalves, hh0 + u % kHalves, da);
+                if (u + 1 >= un) break;
+                if (u + 2 < un) LDS_SP_DIG(c0 + (u + 2) / kHalves, hh0 + (u + 2) % kHalves, da);
+                LDS_SP_MUL((u + 1) / kHalves, hh0 + (u + 1) % kHalves, db);
             }
             // pass p done: the last multiply wave to finish with its buffer clears it
             // for pass p + 3 (whose spills start in pass p + 2, after the next barrier);
             // clearing it from every wave raced with the slower waves' reads
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's fragment reads of the buffer returned
             const int order = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(done + p % 3, 1) : 0);
-            if (order == 16 - kSpStream - 1) {
+            if (order == 16 - NS - 1) {
                 uint4* const bz = reinterpret_cast<uint4*>(sp_lds + (p % 3) * bufdw);
                 for (int i = lane; i < bufdw / 4; i += 64) bz[i] = make_uint4(0u, 0u, 0u, 0u);
                 if (lane == 0) done[p % 3] = 0;
@@ -1783,16 +1943,18 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     unsigned long long* const sums = reinterpret_cast<unsigned long long*>(sp_lds);  // [rowsL][16]
     for (int i = t; i < rowsL * kF; i += kSpThreads) sums[i] = 0ull;
     __syncthreads();
-    if (wave >= kSpStream) {
-        const int m = wave - kSpStream, L = m & 3;
+    if (wave >= NS) {
+        const int m = wave - NS, L0 = kLW * (m & 3);
         const int r16 = lane & 15, g = lane >> 4;
 #pragma unroll
-        for (int T = 0; T < kTiles; ++T)
-            if (16 * T < nrows)
+        for (int l = 0; l < kLW; ++l)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    atomicAdd(sums + (T * 16 + 4 * g + i) * kF + r16,
-                              (unsigned long long)((int64_t)acc[T][i] * ((int64_t)1 << (8 * L))));
+            for (int T = 0; T < kTiles; ++T)
+                if (16 * T < nrows)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        atomicAdd(sums + (T * 16 + 4 * g + i) * kF + r16,
+                                  (unsigned long long)((int64_t)acc[l][T][i] * ((int64_t)1 << (8 * (L0 + l)))));
     }
     __syncthreads();
     for (int o = t; o < nrows * kF; o += kSpThreads) {
@@ -1852,7 +2014,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 36));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 55));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -1899,15 +2061,22 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
                                                                                                 : kDenseProduct;
     if (variant == 3) {  // the spill-pass kernel; dbg 31 no MFMAs, 32 no bit setting, 33 / 34 ring depth 6 / 12
         LDS_CHECK_ARG(R <= kSpMaxRows && g <= kSpMaxGrid);
-        const int depth = dbg == 33 ? 6 : dbg == 34 ? 12 : kSpDepth;  // (35: depth 8, drained before every read)
-        const SpGeom sg = sp_geom(nc, tiles, depth);
-        const int lds = sp_lds_bytes(tiles, sg, depth);
+        // (35: depth 8, drained before every read; 43-47: 12 streaming waves)
+        const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
+                        : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4 : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg == 55 ? 2
+                        : kSpDepth;
+        const int slot = dbg == 54 || dbg == 55 ? 2048 : 1024;  // bytes per ring slot (54 / 55: 2-KB steps)
+        const int ns = (dbg >= 43 && dbg <= 47) || (dbg >= 50 && dbg <= 55 && dbg != 51) ? 12 : dbg == 48 || dbg == 49 || dbg == 51 ? 14 : kSpStream;
+        const SpGeom sg = sp_geom(nc, tiles, depth, ns, slot);
+        const int lds = sp_lds_bytes(tiles, sg, depth, ns, slot);
         LDS_CHECK_ARG(lds <= 163840);
-#define LDS_SP_LAUNCH(TT, DP, DD)                                                                                  \
+#define LDS_SP_LAUNCH(TT, DP, DD) LDS_SP_LAUNCH_NS(TT, DP, DD, kSpStream)
+#define LDS_SP_LAUNCH_NS(TT, DP, DD, NS)                                                                           \
     do {                                                                                                           \
-        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, DP, DD>, lds);                                    \
+        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, DP, DD, NS>, lds);                                \
         if (e != hipSuccess) return (int)e;                                                                        \
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, DP, DD>), dim3(g), dim3(kSpThreads), lds, st,  \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, DP, DD, NS>), dim3(g), dim3(kSpThreads), lds,  \
+                           st,                                                                                     \
                            row_ptr, col, n, R, (const int8_t*)w.zq, nc, sg.cpp, sg.passes, sg.rowdw,              \
                            (const uint32_t*)w.colmax, s, y, ldy, beta);                                           \
     } while (0)
@@ -1915,6 +2084,28 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 32) LDS_SP_LAUNCH(6, kSpDepth, 2);
         else if (dbg == 35) LDS_SP_LAUNCH(6, kSpDepth, 3);
         else if (dbg == 36) LDS_SP_LAUNCH(6, kSpDepth, 4);
+        else if (dbg == 37) LDS_SP_LAUNCH(6, kSpDepth, 5);
+        else if (dbg == 38) LDS_SP_LAUNCH(6, 6, 5);
+        else if (dbg == 39) LDS_SP_LAUNCH(6, kSpDepth, 6);
+        else if (dbg == 40) LDS_SP_LAUNCH(6, kSpDepth, 7);
+        else if (dbg == 41) LDS_SP_LAUNCH(6, kSpDepth, 8);
+        else if (dbg == 42) LDS_SP_LAUNCH(6, 12, 8);
+        else if (dbg == 43) LDS_SP_LAUNCH_NS(6, 5, 0, 12);
+        else if (dbg == 44) LDS_SP_LAUNCH_NS(6, 6, 0, 12);
+        else if (dbg == 45) LDS_SP_LAUNCH_NS(6, 4, 0, 12);
+        else if (dbg == 46) LDS_SP_LAUNCH_NS(6, 5, 9, 12);
+        else if (dbg == 47) LDS_SP_LAUNCH_NS(6, 3, 0, 12);
+        else if (dbg == 48 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 4, 0, 14);
+        else if (dbg == 48) LDS_SP_LAUNCH_NS(6, 4, 0, 14);
+        else if (dbg == 49 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 3, 0, 14);
+        else if (dbg == 49) LDS_SP_LAUNCH_NS(6, 3, 0, 14);
+        else if (dbg == 50) LDS_SP_LAUNCH_NS(6, 4, 10, 12);
+        else if (dbg == 51 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 4, 10, 14);
+        else if (dbg == 51) LDS_SP_LAUNCH_NS(6, 4, 10, 14);
+        else if (dbg == 52) LDS_SP_LAUNCH_NS(6, 4, 11, 12);
+        else if (dbg == 53) LDS_SP_LAUNCH_NS(6, 3, 11, 12);
+        else if (dbg == 54) LDS_SP_LAUNCH_NS(6, 3, 12, 12);
+        else if (dbg == 55) LDS_SP_LAUNCH_NS(6, 2, 12, 12);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
@@ -1922,6 +2113,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (tiles <= 5) LDS_SP_LAUNCH(5, kSpDepth, 0);
         else LDS_SP_LAUNCH(6, kSpDepth, 0);
 #undef LDS_SP_LAUNCH
+#undef LDS_SP_LAUNCH_NS
         LDS_RETURN_LAST_ERROR();
     }
     if (variant == 2) {
