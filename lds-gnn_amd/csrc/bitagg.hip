@@ -1428,6 +1428,26 @@ int sp_lds_bytes(int tiles, const SpGeom& g, int depth, int ns = kSpStream, int 
     return ns * depth * slot + 3 * 16 * tiles * g.rowdw * 4 + 4 * kSpStateInts;
 }
 
+// The product configuration of the spill-pass kernel: 12 streaming + 4
+// multiply waves, 2-KB steps (mode 12: 8 entries per lane, the fast paths for
+// pass p + 1 and for boundary lanes), a ring two steps deep (one in flight:
+// the smaller ring leaves LDS for fewer, wider passes).  Config 5: 178 µs
+// against 375 for round 4's first form (8 + 8 waves, 1-KB steps, depth 8).
+constexpr int kSpProdMode = 12, kSpProdWaves = 12, kSpProdDepth = 2;
+struct SpCfg {
+    int depth, ns, slot;  // ring slots per streaming wave, streaming waves, bytes per slot
+};
+// dbg 0 the product; the variants of lds_spmm_dense_ablation (tools/spmm_config5.py)
+SpCfg sp_cfg(int dbg) {
+    if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 2048};
+    const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
+                    : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
+                    : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
+    const int ns = (dbg >= 43 && dbg <= 47) || dbg == 50 || (dbg >= 52 && dbg <= 55) ? 12
+                 : dbg == 48 || dbg == 49 || dbg == 51 || dbg == 57 ? 14 : kSpStream;
+    return SpCfg{depth, ns, dbg >= 54 && dbg <= 57 ? 2048 : 1024};
+}
+
 // Entry c (column) of a row in pass p: its bit in pass p's buffer row bp
 // (c < hi), pass p + 1's row bq (c < hq), or past both (returns true).
 __device__ __forceinline__ bool sp_put(int c, int lo, int hi, int hq, uint32_t* bp, uint32_t* bq, bool& spill) {
@@ -2003,7 +2023,7 @@ static hipError_t allow_lds(K kernel, int bytes) {
 // (n = 20 000, 2·10⁸ entries), µs per call: row-block 223-229, tile kernel
 // 242, column-pass sequential 248, concurrent 297, spill-pass 377
 // (profiles/r04_spmm5_*.json).
-constexpr int kDenseProduct = 2;
+constexpr int kDenseProduct = 3;
 extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                    int ldz, float* y, int ldy, int beta, void* ws, int grid, int quantize,
                                    void* stream) {
@@ -2014,7 +2034,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 55));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 57));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2059,14 +2079,10 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
     // (concurrent) 11 no multiply, 12 no streaming
     const int variant = dbg >= 30 ? 3 : dbg >= 20 ? dbg - 20 : dbg == 13 ? 1 : dbg >= 10 ? 0 : dbg > 0 ? 2
                                                                                                 : kDenseProduct;
-    if (variant == 3) {  // the spill-pass kernel; dbg 31 no MFMAs, 32 no bit setting, 33 / 34 ring depth 6 / 12
+    if (variant == 3) {  // the spill-pass kernel (the product, dbg 0) and its variants (sp_cfg)
         LDS_CHECK_ARG(R <= kSpMaxRows && g <= kSpMaxGrid);
-        // (35: depth 8, drained before every read; 43-47: 12 streaming waves)
-        const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
-                        : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4 : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg == 55 ? 2
-                        : kSpDepth;
-        const int slot = dbg == 54 || dbg == 55 ? 2048 : 1024;  // bytes per ring slot (54 / 55: 2-KB steps)
-        const int ns = (dbg >= 43 && dbg <= 47) || (dbg >= 50 && dbg <= 55 && dbg != 51) ? 12 : dbg == 48 || dbg == 49 || dbg == 51 ? 14 : kSpStream;
+        const SpCfg cfg = sp_cfg(dbg);
+        const int depth = cfg.depth, ns = cfg.ns, slot = cfg.slot;
         const SpGeom sg = sp_geom(nc, tiles, depth, ns, slot);
         const int lds = sp_lds_bytes(tiles, sg, depth, ns, slot);
         LDS_CHECK_ARG(lds <= 163840);
@@ -2080,7 +2096,11 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
                            row_ptr, col, n, R, (const int8_t*)w.zq, nc, sg.cpp, sg.passes, sg.rowdw,              \
                            (const uint32_t*)w.colmax, s, y, ldy, beta);                                           \
     } while (0)
-        if (dbg == 31) LDS_SP_LAUNCH(6, kSpDepth, 1);
+        if (dbg == 0 && tiles <= 2) LDS_SP_LAUNCH_NS(2, kSpProdDepth, kSpProdMode, kSpProdWaves);
+        else if (dbg == 0 && tiles <= 4) LDS_SP_LAUNCH_NS(4, kSpProdDepth, kSpProdMode, kSpProdWaves);
+        else if (dbg == 0 && tiles <= 5) LDS_SP_LAUNCH_NS(5, kSpProdDepth, kSpProdMode, kSpProdWaves);
+        else if (dbg == 0) LDS_SP_LAUNCH_NS(6, kSpProdDepth, kSpProdMode, kSpProdWaves);
+        else if (dbg == 31) LDS_SP_LAUNCH(6, kSpDepth, 1);
         else if (dbg == 32) LDS_SP_LAUNCH(6, kSpDepth, 2);
         else if (dbg == 35) LDS_SP_LAUNCH(6, kSpDepth, 3);
         else if (dbg == 36) LDS_SP_LAUNCH(6, kSpDepth, 4);
@@ -2106,6 +2126,9 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 53) LDS_SP_LAUNCH_NS(6, 3, 11, 12);
         else if (dbg == 54) LDS_SP_LAUNCH_NS(6, 3, 12, 12);
         else if (dbg == 55) LDS_SP_LAUNCH_NS(6, 2, 12, 12);
+        else if (dbg == 56) LDS_SP_LAUNCH_NS(6, 2, 12, 8);
+        else if (dbg == 57 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 2, 12, 14);
+        else if (dbg == 57) LDS_SP_LAUNCH_NS(6, 2, 12, 14);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);

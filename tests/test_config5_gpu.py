@@ -75,7 +75,7 @@ def test_bitmask_aggregation_n20000_vs_csr_and_fp64_rows(device, dense_graph):
     assert graph.nnz() > 1.9e8 and graph.long_rows()
     z = torch.randn(N, 16, generator=torch.Generator().manual_seed(3)).to(device)
     y_bit = graph.spmm_bitmask(z)
-    y_csr = graph.spmm(z)  # long rows: the CSR row-block kernel (lds_spmm_norm_dense)
+    y_csr = graph.spmm(z)  # long rows: the CSR spill-pass kernel (lds_spmm_norm_dense)
     torch.cuda.synchronize()
     rp = graph.row_ptr.cpu()
     zd = z.double().cpu()

@@ -227,7 +227,7 @@ def test_spmm_blocked_vs_dense(device, n, high):
     z = torch.randn(n, 16, generator=g).to(device)
     y_blk = graph.spmm(z, blocked=True).cpu().double()
     y_row = graph.spmm(z, blocked=False).cpu().double()
-    y_def = graph.spmm(z).cpu().double()  # long rows: the CSR row-block kernel (lds_spmm_norm_dense)
+    y_def = graph.spmm(z).cpu().double()  # long rows: the CSR spill-pass kernel (lds_spmm_norm_dense)
     ref = graph.normalized_dense().cpu().double() @ z.cpu().double()
     scale = ref.abs().max()
     assert float((y_blk - ref).abs().max() / scale) < RTOL
@@ -840,7 +840,9 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     y0 = torch.empty(n, 16, device=device)  # (quantises z into ws for the variants below)
     nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n, nat.ptr(zd), 16,
              nat.ptr(y0), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
-    for dbg in (20, 21, 22, 23, 33, 34, 6):  # column-pass (2 forms), row-block, spill-pass (depth 8, 6, 12), hybrid
+    # column-pass (2 forms), row-block (LDS-DMA digits), spill-pass (1-KB steps, depths 8, 6, 12), hybrid
+    # row-block, spill-pass with 12 streaming waves and 1-KB / 2-KB steps (the product form as a variant: 55)
+    for dbg in (20, 21, 22, 23, 33, 34, 6, 52, 54, 55):
         yv = torch.empty(n, 16, device=device)
         nat.call("lds_spmm_dense_ablation", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n,
                  nat.ptr(zd), 16, nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
@@ -869,9 +871,9 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     """A general 0/1 CSR with rows in any column order (the bits are set by
     OR), empty rows, long rows straddling the 512-entry steps: the kernels
     that accept any order — the tile kernel (grid < 0) and the row-block
-    kernel — give 0 for the empty rows and identical bits.  (The product
-    kernel is the row-block kernel too: grid >= 0 below; the spill-pass
-    variant needs ascending columns: test_spmm_dense_spill_pass_row_shapes.)"""
+    kernel (lds_spmm_dense_ablation dbg 22) — give 0 for the empty rows and
+    identical bits.  (The product, the spill-pass kernel at grid >= 0, needs
+    ascending columns: test_spmm_dense_spill_pass_row_shapes.)"""
     n = 1300
     g = torch.Generator().manual_seed(5)
     a = (torch.rand(n, n, generator=g) < 0.45)
@@ -920,9 +922,11 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
 
 @pytest.mark.parametrize("grid", [0, 63])
 def test_spmm_dense_spill_pass_row_shapes(device, grid):
-    """The spill-pass kernel (lds_spmm_dense_ablation dbg 23; ascending
-    columns) on rows that take each of its paths, against the row-block
-    product (identical bits: exact integer sums) and fp64: rows whose entries crowd the first columns (the
+    """The spill-pass kernel (the product at grid >= 0, and its variants:
+    lds_spmm_dense_ablation dbg 23 / 33 / 34 with 1-KB steps and ring depths
+    8 / 6 / 12, 52 / 54 with 12 streaming waves; ascending columns) on rows
+    that take each of its paths, against the row-block kernel (dbg 6, any
+    column order; identical bits: exact integer sums) and fp64: rows whose entries crowd the first columns (the
     stream stops at the predicted pass end before the pass boundary and the
     row is finished with blocking loads), rows crowding the last columns
     (every step of the early passes lies past pass p + 1: re-read later),
@@ -955,12 +959,12 @@ def test_spmm_dense_spill_pass_row_shapes(device, grid):
     s = torch.rand(n, generator=g) + 0.5
     z = torch.randn(n, 16, generator=g)
     rpd, cold, sd, zd = rp.int().to(device), col.to(device), s.to(device), z.to(device)
-    y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid)  # the product (row-block kernel)
+    y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid)  # the product (spill-pass kernel)
     ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
     y0 = torch.empty(n, 16, device=device)
     nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(y0), 16, 0,
              nat.ptr(ws), grid, 1, nat.stream_of(device))
-    for dbg in (23, 33, 34, 6):  # the spill-pass kernel (ring depths 8, 6, 12), the hybrid row-block
+    for dbg in (23, 33, 34, 52, 54, 55, 6):  # spill-pass variants, the hybrid row-block
         yv = torch.empty(n, 16, device=device)
         nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16,
                  nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
