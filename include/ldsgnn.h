@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 12
+#define LDS_ABI_VERSION 13
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -234,11 +234,16 @@ int64_t lds_bitmask_agg_ws_bytes(int n);
  * quantisation: exact integer sums, one rounding per digit at 2^-31 of the
  * column maximum).  n <= lds_spmm_dense_max_n(); col 16-byte aligned; ws:
  * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned.  grid >= 0: the
- * row-block kernel (a workgroup's rows streamed into bit rows staged in ws,
- * then multiplied once per workgroup), one workgroup per CU (0) or `grid`
- * workgroups (at most 96 rows each); grid < 0: the round-3 tile kernel on
- * -grid persistent workgroups.  Columns distinct within a row, any order
- * (the spill-pass variant of lds_spmm_dense_ablation needs them ascending).
+ * spill-pass kernel (ABI 13; a workgroup's rows, at most 96, swept in column
+ * passes with their bit rows in LDS: 12 waves stream 2-KB steps of col
+ * through registers and set the bits, entries past a pass go straight into
+ * the next pass's bits, 4 waves multiply the previous pass), one workgroup
+ * per CU (0) or `grid` workgroups; columns distinct and ASCENDING within each
+ * row (canonical CSR, as every sampler and fill of this library writes it;
+ * out-of-order columns give wrong sums, never an out-of-bounds access).
+ * grid < 0: the round-3 tile kernel on -grid persistent workgroups, columns
+ * in any order (so is the row-block kernel, lds_spmm_dense_ablation dbg 6 /
+ * 22, the product of ABI 12).
  * Three launches (column maxima, digits, the product);
  * quantize = 0 skips the first two (ws holds the digits of this s, z from an
  * earlier call).
@@ -251,15 +256,24 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
 /* Variants and timing-only ablations of lds_spmm_norm_dense (tools/spmm_config5.py;
  * the digits of an earlier call must be in ws).  Products (same results as
  * lds_spmm_norm_dense): dbg 6 the row-block kernel with bit slabs in ws and
- * its digits loaded into registers (the default; any column order), 22 the
- * same with the digits staged by LDS-DMA, 23 the spill-pass kernel (column passes, bit rows in LDS,
- * entries past a pass set in the next pass's bits; ascending columns), 33 / 34
- * the same with 6 / 12 ring slots per streaming wave (8 by default), 35 the
- * same draining its ring before every step, 36 the same OR-reducing each
- * lane quad's masks before the LDS ORs, 20 the column-pass kernel,
+ * its digits loaded into registers (any column order), 22 the
+ * same with the digits staged by LDS-DMA; the spill-pass kernel (ascending
+ * columns) in the forms that led to the product: 23 8 streaming + 8 multiply
+ * waves, 1-KB steps through an LDS-DMA ring 8 deep, 33 / 34 ring depth 6 / 12,
+ * 35 the ring drained before every step, 36 quad-reduced bit ORs, 37 / 38
+ * windowed bit setting on every step (depth 8 / 6), 39 the ring read one step
+ * ahead, 41 / 42 the ring loop not unrolled (depth 8 / 12), 43-47 12 streaming
+ * + 4 multiply waves (depths 5, 6, 4, 5 with windowed boundary steps, 3),
+ * 48 / 49 14 + 2 (depths 4 / 3), 50 / 51 12 / 14 streaming waves with the
+ * pass p + 1 fast path, 52 / 53 with the boundary-lane fast path too (depths
+ * 4 / 3), 54 / 55 / 56 / 57 2-KB steps (12 waves depth 3 and 2, 8 waves, 14
+ * waves; depth 2), 60 / 61 / 62 2-KB steps through a register ring 3 / 4 / 6
+ * deep (61 = the product); 20 the column-pass kernel,
  * streaming and multiply waves concurrent, 21 its sequential form.  Ablations
  * (wrong results): 31 / 32 the spill-pass kernel without MFMAs / without
- * setting bits; 11 / 12 / 13 the column-pass kernel without its multiply /
+ * setting bits, 40 with plain stores for its interior ORs, 58 / 59 the
+ * 2-KB LDS-ring form (55) without setting bits / without MFMAs;
+ * 11 / 12 / 13 the column-pass kernel without its multiply /
  * streaming waves; 1-5 the row-block kernel's streaming phase alone, without
  * its slab stores, its multiply phase alone, without its slab loads,
  * streaming with the column-pass step bookkeeping; 7 the register-digit

@@ -1429,17 +1429,21 @@ int sp_lds_bytes(int tiles, const SpGeom& g, int depth, int ns = kSpStream, int 
 }
 
 // The product configuration of the spill-pass kernel: 12 streaming + 4
-// multiply waves, 2-KB steps (mode 12: 8 entries per lane, the fast paths for
-// pass p + 1 and for boundary lanes), a ring two steps deep (one in flight:
-// the smaller ring leaves LDS for fewer, wider passes).  Config 5: 178 µs
-// against 375 for round 4's first form (8 + 8 waves, 1-KB steps, depth 8).
-constexpr int kSpProdMode = 12, kSpProdWaves = 12, kSpProdDepth = 2;
+// multiply waves, 2-KB steps (8 entries per lane, the fast paths for pass
+// p + 1 and for boundary lanes) and the ring in registers, four steps deep
+// (mode 15: asm loads with counted waits; no LDS ring, so the whole LDS
+// holds the pass buffers: 4 passes at config 5).  Config 5: 170 µs against
+// 178 with a 2-slot LDS ring (mode 12, 6 passes) and 375 for round 4's first
+// form (8 + 8 waves, 1-KB steps, an LDS ring 8 deep).
+constexpr int kSpProdMode = 15, kSpProdWaves = 12, kSpProdDepth = 4;
 struct SpCfg {
     int depth, ns, slot;  // ring slots per streaming wave, streaming waves, bytes per slot
 };
 // dbg 0 the product; the variants of lds_spmm_dense_ablation (tools/spmm_config5.py)
 SpCfg sp_cfg(int dbg) {
-    if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 2048};
+    if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
+    if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
+    if (dbg >= 60 && dbg <= 62) return SpCfg{dbg == 60 ? 3 : dbg == 61 ? 4 : 6, 12, 0};  // register ring: no LDS
     const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
                     : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
                     : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
@@ -1585,10 +1589,13 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     float* __restrict__ y, int ldy, int beta) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sp_lds_all[];
     // entries per lane and step: 4 (1-KB steps) or, DBG 12, 8 (2-KB steps, two DMAs)
-    constexpr int kE = DBG == 12 ? 8 : 4;
+    constexpr int kE = DBG >= 12 ? 8 : 4;
+    constexpr bool kNoBits = DBG == 2 || DBG == 13;  // timing only: no bit setting
+    constexpr bool kRegRing = DBG == 15;  // the ring in registers (asm loads, counted waits): no LDS ring
+    constexpr bool kNoMfma = DBG == 1 || DBG == 14;  // timing only: no matrix-core products
     constexpr int kStep = 64 * kE;
     static_assert((D - 1) * (kE / 4) <= 15, "vmcnt field");
-    uint32_t* const sp_lds = sp_lds_all + NS * D * kStep;  // after the rings: three pass buffers, row state
+    uint32_t* const sp_lds = sp_lds_all + (kRegRing ? 0 : NS * D * kStep);  // after the rings: pass buffers, row state
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int r0 = (int)blockIdx.x * rows_per_wg;
@@ -1639,6 +1646,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         // the ring: a step's data, start, row bounds and packed (row | pass << 8 |
         // first << 16 | last << 17), -1 for a null step
         int ma[D], mlo[D], mup[D], mk[D];
+        v4i rg[D][kE / 4];  // (kRegRing) the ring's columns
         const uint32_t ring_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)sp_lds_all) +
                                   (uint32_t)(wave * D * kStep * 4);
         const uint32_t* const myring = sp_lds_all + wave * D * kStep;
@@ -1699,9 +1707,10 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         }                                                                                                    \
         pending += k_ >= 0 ? 1 : 0;                                                                          \
         _Pragma("unroll") for (int h_ = 0; h_ < kE / 4; ++h_) {                                              \
-            const int aa_ = a_ + 256 * h_ + 4 * lane;                                                        \
+            const int aa_ = a_ + (kRegRing ? kE * lane + 4 * h_ : 256 * h_ + 4 * lane);                       \
             const int* src_ = (a_ >= 0 && aa_ + 4 <= nnz) ? col + aa_ : dummy;                               \
-            lds_dma16(src_, ring_lds + (uint32_t)(J) * (uint32_t)(4 * kStep) + 1024u * h_);                 \
+            if constexpr (kRegRing) rb_gload(rg[J][h_], reinterpret_cast<const v4i*>(src_));                  \
+            else lds_dma16(src_, ring_lds + (uint32_t)(J) * (uint32_t)(4 * kStep) + 1024u * h_);             \
         }                                                                                                    \
     } while (0)
 #define LDS_SP_PROCESS(J)                                                                                    \
@@ -1743,8 +1752,12 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             uint32_t* const bq_ = sp_lds + ((p_ + 1) % 3) * bufdw + lr_ * rowdw;                             \
             const int a_ = ma_, rlo_ = mlo_, rup_ = mup_;                                                    \
             int c_[kE];                                                                                      \
+            if constexpr (kRegRing) {                                                                        \
+                if constexpr (kE == 8) rb_bind(rg[J][0], rg[J][1]);                                          \
+            }                                                                                                \
             _Pragma("unroll") for (int h_ = 0; h_ < kE / 4; ++h_) {                                          \
-                const int4 v_ = DBG == 6 ? cur_ : *reinterpret_cast<const int4*>(myring + (J) * kStep + kE * lane + 4 * h_); \
+                const int4 v_ = kRegRing ? int4{rg[J][h_][0], rg[J][h_][1], rg[J][h_][2], rg[J][h_][3]}      \
+                              : DBG == 6 ? cur_ : *reinterpret_cast<const int4*>(myring + (J) * kStep + kE * lane + 4 * h_); \
                 c_[4 * h_] = v_.x;                                                                           \
                 c_[4 * h_ + 1] = v_.y;                                                                       \
                 c_[4 * h_ + 2] = v_.z;                                                                       \
@@ -1766,7 +1779,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             if (DBG != 5 && a_ >= rlo_ && a_ + kStep <= rup_) { /* interior (uniform): all the row's */   \
                 const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
                 fast_ = c_[0] >= lo_ && c_[kE - 1] < hi_ && (uint32_t)(c_[kE - 1] - lo_) - (w0_ << 5) < 64u; \
-                if (fast_ && DBG != 2) {                                                                     \
+                if (fast_ && !kNoBits) {                                                                    \
                     uint64_t m_ = 0;                                                                         \
                     _Pragma("unroll") for (int e = 0; e < kE; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
                     if (DBG == 7) { /* timing only: plain stores instead of ORs */                           \
@@ -1777,7 +1790,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                         dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                          \
                     }                                                                                        \
                 }                                                                                            \
-                if ((DBG == 10 || DBG >= 11) && !fast_) { /* all of pass p + 1 (past the boundary) */       \
+                if ((DBG == 10 || DBG >= 11) && !kNoBits && !fast_) { /* all of pass p + 1 (past the boundary) */       \
                     const uint32_t q0_ = (uint32_t)(c_[0] - hi_) >> 5;                                       \
                     if (c_[0] >= hi_ && c_[kE - 1] < hq_ && (uint32_t)(c_[kE - 1] - hi_) - (q0_ << 5) < 64u) { \
                         uint64_t m_ = 0;                                                                     \
@@ -1788,7 +1801,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                         fast_ = true;                                                                        \
                     }                                                                                        \
                 }                                                                                            \
-                if (DBG >= 11 && !fast_ && c_[0] >= lo_ && c_[0] < hi_ && c_[kE - 1] >= hi_ &&               \
+                if (DBG >= 11 && !kNoBits && !fast_ && c_[0] >= lo_ && c_[0] < hi_ && c_[kE - 1] >= hi_ &&               \
                     c_[kE - 1] < hq_ && (uint32_t)(c_[kE - 1] - hi_) < 64u) { /* straddles the boundary */   \
                     uint64_t mp_ = 0, mq_ = 0;                                                               \
                     bool ok_ = true;                                                                         \
@@ -1810,7 +1823,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     }                                                                                        \
                 }                                                                                            \
             }                                                                                                \
-            if (!fast_ && DBG != 2) {                                                                        \
+            if (!fast_ && !kNoBits) {                                                                       \
                 /* per entry; two copies under a uniform branch: only the array's last step reloads the */\
                 /* lanes that read the dummy (a lane-conditional load costs vmcnt(0) on every path) */  \
                 if (a_ + kStep > nnz) {                                                                 \
@@ -1838,7 +1851,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             }                                                                                                \
             if (k_ & (1 << 17)) { /* the row's last issued step: where pass p + 1 starts */                 \
                 int np_ = min(a_ + kStep, rup_);                                                             \
-                if (estar == 0x7FFFFFFF && !bnd && np_ < rup_ && DBG != 2) {                                 \
+                if (estar == 0x7FFFFFFF && !bnd && np_ < rup_ && !kNoBits) {                               \
                     /* the boundary lies past the predicted end: finish the row with blocking loads */       \
                     while (np_ < rup_) {                                                                     \
                         const int b_ = (np_ & ~3) + 4 * lane;                                                \
@@ -1922,7 +1935,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     a.z = (int)((w >> (sh + 2)) & 0x01010101u);                                               \
                     a.w = (int)((w >> (sh + 3)) & 0x01010101u);                                               \
                     _Pragma("unroll") for (int l = 0; l < kLW; ++l) {                                         \
-                        if (DBG != 1) acc[l][T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, DQ[l][i], acc[l][T], 0, 0, 0); \
+                        if (!kNoMfma) acc[l][T] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, DQ[l][i], acc[l][T], 0, 0, 0); \
                         else acc[l][T] += a;                                                                  \
                     }                                                                                         \
                 }                                                                                             \
@@ -2034,7 +2047,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 57));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 62));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2129,6 +2142,11 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 56) LDS_SP_LAUNCH_NS(6, 2, 12, 8);
         else if (dbg == 57 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 2, 12, 14);
         else if (dbg == 57) LDS_SP_LAUNCH_NS(6, 2, 12, 14);
+        else if (dbg == 58) LDS_SP_LAUNCH_NS(6, 2, 13, 12);
+        else if (dbg == 59) LDS_SP_LAUNCH_NS(6, 2, 14, 12);
+        else if (dbg == 60) LDS_SP_LAUNCH_NS(6, 3, 15, 12);
+        else if (dbg == 61) LDS_SP_LAUNCH_NS(6, 4, 15, 12);
+        else if (dbg == 62) LDS_SP_LAUNCH_NS(6, 6, 15, 12);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);

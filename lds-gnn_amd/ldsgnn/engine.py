@@ -221,7 +221,7 @@ class LdsEngine:
         # long rows (dense θ, BASELINE config 5): the aggregations run as a
         # pre-pass whose Â·Z the fused kernels read instead of aggregating
         # in-kernel — the bitmask aggregation on the int8 matrix cores
-        # (lds_aggregate_bitmask, no CSR is built), the CSR row-block SpMM
+        # (lds_aggregate_bitmask, no CSR is built), the CSR spill-pass SpMM
         # (lds_spmm_norm_dense, long_rows_kernel="csr") or the column-blocked
         # LDS SpMM over CSR (lds_spmm_norm_blocked, long_rows_kernel="blocked").
         # Decided once from θ's expected degree 1 + 2·Σ_{i<j} clamp(θ_ij) / n.
@@ -659,7 +659,7 @@ class LdsEngine:
 
     def _agg(self, g: _Graph, z: torch.Tensor) -> int:
         """Long rows: Â·Z into self.agg by the bitmask aggregation, the CSR
-        row-block SpMM or the column-blocked SpMM (the fused kernel then reads
+        spill-pass SpMM or the column-blocked SpMM (the fused kernel then reads
         it); short rows: 0 (aggregate in-kernel)."""
         if not self.long_rows:
             return 0

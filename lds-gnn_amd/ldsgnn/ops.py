@@ -114,9 +114,9 @@ class CsrGraph:
     def spmm(self, z: torch.Tensor, out: Optional[torch.Tensor] = None, beta: int = 0,
              blocked: Optional[bool] = None) -> torch.Tensor:
         """Y = Â·Z; no autograd.  Row-group kernel (lds_spmm_norm), or for long
-        rows at F = 16 the CSR row-block kernel on the int8 matrix cores
-        (lds_spmm_norm_dense; 223 against 414 µs for the column-blocked kernel
-        at BASELINE config 5).  `blocked=True` forces the column-blocked kernel
+        rows at F = 16 the CSR spill-pass kernel on the int8 matrix cores
+        (lds_spmm_norm_dense; 170 against 414 µs for the column-blocked kernel
+        at BASELINE config 5; needs the ascending columns this class holds).  `blocked=True` forces the column-blocked kernel
         (lds_spmm_norm_blocked), `blocked=False` the row-group kernel."""
         z = _f32c(z, "spmm")
         if z.dim() != 2 or z.size(0) != self.n:

@@ -124,7 +124,11 @@ for step in "$@"; do
             lc=$(echo $c | cut -d_ -f1 | tr 'A-Z' 'a-z')
             run 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/spmm5_pmc_${tag}_$lc -o run -- \
                 python3 tools/spmm_config5.py > $O/spmm5_pmc_${tag}_$lc.log 2>&1 || exit $?
-        done ;;
+        done
+        # instruction mix and issue stalls per kernel (one pass: 8 SQ counters)
+        run 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
+            SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_WAVES --kernel-trace --output-format csv \
+            -d $O/spmm5_sq_$tag -o run -- python3 tools/spmm_config5.py > $O/spmm5_sq_$tag.log 2>&1 || exit $? ;;
     *)
         echo "unknown step $step" >&2
         exit 2 ;;
