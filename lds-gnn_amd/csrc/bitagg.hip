@@ -1430,12 +1430,15 @@ int sp_lds_bytes(int tiles, const SpGeom& g, int depth, int ns = kSpStream, int 
 
 // The product configuration of the spill-pass kernel: 12 streaming + 4
 // multiply waves, 2-KB steps (8 entries per lane, the fast paths for pass
-// p + 1 and for boundary lanes) and the ring in registers, four steps deep
-// (mode 15: asm loads with counted waits; no LDS ring, so the whole LDS
-// holds the pass buffers: 4 passes at config 5).  Config 5: 170 µs against
-// 178 with a 2-slot LDS ring (mode 12, 6 passes) and 375 for round 4's first
-// form (8 + 8 waves, 1-KB steps, an LDS ring 8 deep).
-constexpr int kSpProdMode = 15, kSpProdWaves = 12, kSpProdDepth = 4;
+// p + 1 and for boundary lanes), the ring in registers, four steps deep (asm
+// loads with counted waits; no LDS ring, so the whole LDS holds the pass
+// buffers: 4 passes at config 5), and a step's pass bounds and bit-row
+// pointers reused while its (row, pass) repeats (mode 17).  Config 5: 165 µs,
+// against 171 without the reuse (mode 15), 178 with a 2-slot LDS ring (mode
+// 12, 6 passes) and 375 for round 4's first form (8 + 8 waves, 1-KB steps, an
+// LDS ring 8 deep): the streaming waves are bound by the instructions they
+// issue per step, not by HBM.
+constexpr int kSpProdMode = 17, kSpProdWaves = 12, kSpProdDepth = 4;
 struct SpCfg {
     int depth, ns, slot;  // ring slots per streaming wave, streaming waves, bytes per slot
 };
@@ -1443,7 +1446,7 @@ struct SpCfg {
 SpCfg sp_cfg(int dbg) {
     if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
     if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
-    if (dbg >= 60 && dbg <= 62) return SpCfg{dbg == 60 ? 3 : dbg == 61 ? 4 : 6, 12, 0};  // register ring: no LDS
+    if (dbg >= 60 && dbg <= 64) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, 12, 0};  // register ring: no LDS
     const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
                     : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
                     : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
@@ -1591,7 +1594,9 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     // entries per lane and step: 4 (1-KB steps) or, DBG 12, 8 (2-KB steps, two DMAs)
     constexpr int kE = DBG >= 12 ? 8 : 4;
     constexpr bool kNoBits = DBG == 2 || DBG == 13;  // timing only: no bit setting
-    constexpr bool kRegRing = DBG == 15;  // the ring in registers (asm loads, counted waits): no LDS ring
+    constexpr bool kRegRing = DBG == 15 || DBG == 16 || DBG == 17;  // the ring in registers (asm loads, counted waits): no LDS ring
+    constexpr bool kDynRows = DBG == 16;  // rows taken per pass from an LDS counter, not wave + NS·i
+    constexpr bool kKeyCache = DBG == 17;  // a step's pass bounds and bit rows reused while (row, pass) repeats
     constexpr bool kNoMfma = DBG == 1 || DBG == 14;  // timing only: no matrix-core products
     constexpr int kStep = 64 * kE;
     static_assert((D - 1) * (kE / 4) <= 15, "vmcnt field");
@@ -1609,9 +1614,12 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     int* const e_sh = fin + kSpMaxRows;
     int* const done = e_sh + 16;  // per buffer: multiply waves finished with it
     int4* const meta = reinterpret_cast<int4*>(done + 4);  // (DBG 8) per wave and slot: start, row bounds, key
+    int* const nxt = done + 4;  // (kDynRows) per pass: rows taken so far (the meta area: passes <= 576)
     const int nnz = rp[n];
     const int span = cpp * kChunk;  // columns per pass
     for (int i = t; i < 3 * bufdw; i += kSpThreads) sp_lds[i] = 0u;
+    if constexpr (kDynRows)
+        for (int i = t; i < passes; i += kSpThreads) nxt[i] = 0;
     for (int i = t; i < nrows; i += kSpThreads) {
         pos[i] = rp[r0 + i];
         rend[i] = rp[r0 + i + 1];
@@ -1641,6 +1649,9 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         const int* const dummy = reinterpret_cast<const int*>(zq) + 4 * lane;    // null steps load here
         // issue side: pass ip, row ordinal iq, next step ia, the row's stream end
         int ip = 0, iq = 0, ia = 0, iend = 0, ilow = 0, iup = 0;
+        int ilr = -1, spins = 0;  // (kDynRows) the row taken for pass ip, -1 none; wait steps so far
+        int pk = -1, plo = 0, phi = 0, phq = 0;  // (kKeyCache) (row | pass << 8) of the last step, its bounds
+        uint32_t *pbp = sp_lds, *pbq = sp_lds;  // and bit rows
         bool irow = false, ifirst = false;
         int pending = 0;  // non-null steps in the ring
         // the ring: a step's data, start, row bounds and packed (row | pass << 8 |
@@ -1659,18 +1670,35 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         int a_ = -1, lo_ = 0, up_ = 0, k_ = -1;                                                              \
         while (ip < passes) {                                                                                \
             if (!irow) {                                                                                     \
-                if (iq >= nrw) {                                                                             \
+                if constexpr (kDynRows) {                                                                    \
+                    if (ilr < 0) { /* take the next row of pass ip */                                        \
+                        int g_ = 0;                                                                          \
+                        if (lane == 0) g_ = atomicAdd(nxt + ip, 1);                                          \
+                        g_ = __builtin_amdgcn_readfirstlane(g_);                                             \
+                        if (g_ >= nrows) {                                                                   \
+                            ++ip;                                                                            \
+                            continue;                                                                        \
+                        }                                                                                    \
+                        ilr = g_;                                                                            \
+                    }                                                                                        \
+                } else if (iq >= nrw) {                                                                      \
                     ++ip;                                                                                    \
                     iq = 0;                                                                                  \
                     continue;                                                                                \
                 }                                                                                            \
-                const int lr_ = wave + NS * iq;                                                       \
-                if (__builtin_amdgcn_readfirstlane(fin[lr_]) < ip - 1) break; /* previous pass not closed */ \
+                const int lr_ = kDynRows ? ilr : wave + NS * iq;                                             \
+                /* previous pass not closed (kDynRows: a bound on the wait, so that no logic error can */   \
+                /* leave waves spinning on the GPU; never reached when the barriers below are right) */       \
+                if (__builtin_amdgcn_readfirstlane(fin[lr_]) < ip - 1 && (!kDynRows || ++spins < (1 << 20))) {  \
+                    if constexpr (kDynRows) k_ = -2 - ip; /* a wait step: passes < ip are this wave's past */  \
+                    break;                                                                                   \
+                }                                                                                            \
                 ilow = __builtin_amdgcn_readfirstlane(pos[lr_]);                                             \
                 iup = __builtin_amdgcn_readfirstlane(rend[lr_]);                                             \
                 if (ilow >= iup) { /* the row is done: closed for this pass too */                          \
                     fin[lr_] = ip;                                                                           \
                     ++iq;                                                                                    \
+                    ilr = -1;                                                                                \
                     continue;                                                                                \
                 }                                                                                            \
                 ia = ilow & ~3;                                                                              \
@@ -1688,12 +1716,13 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             a_ = ia;                                                                                         \
             lo_ = ilow;                                                                                      \
             up_ = iup;                                                                                       \
-            k_ = (wave + NS * iq) | (ip << 8) | (ifirst ? 1 << 16 : 0) | (last_ ? 1 << 17 : 0);      \
+            k_ = (kDynRows ? ilr : wave + NS * iq) | (ip << 8) | (ifirst ? 1 << 16 : 0) | (last_ ? 1 << 17 : 0); \
             ia += kStep;                                                                                     \
             ifirst = false;                                                                                  \
             if (last_) {                                                                                     \
                 irow = false;                                                                                \
                 ++iq;                                                                                        \
+                ilr = -1;                                                                                    \
             }                                                                                                \
             break;                                                                                           \
         }                                                                                                    \
@@ -1736,6 +1765,14 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             mlo_ = mlo[J];                                                                                   \
             mup_ = mup[J];                                                                                   \
         }                                                                                                    \
+        if (kDynRows && k_ <= -2) {                                                                          \
+            /* a wait step issued at pass -2 - k_: every step of the earlier passes is processed, so arrive */ \
+            /* at their barriers (the row's previous pass may belong to a wave waiting at one of them) */    \
+            for (; cp < -2 - k_; ++cp) {                                                                     \
+                __builtin_amdgcn_s_waitcnt(0xC07F);                                                          \
+                __builtin_amdgcn_s_barrier();                                                                \
+            }                                                                                                \
+        }                                                                                                    \
         if (k_ >= 0) {                                                                                       \
             --pending;                                                                                       \
             const int lr_ = k_ & 0xFF, p_ = (k_ >> 8) & 0xFF;                                                \
@@ -1747,9 +1784,17 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 bnd = false;                                                                                 \
                 estar = 0x7FFFFFFF;                                                                          \
             }                                                                                                \
-            const int lo_ = p_ * span, hi_ = min(lo_ + span, n), hq_ = min(hi_ + span, n);                   \
-            uint32_t* const bp_ = sp_lds + (p_ % 3) * bufdw + lr_ * rowdw;                                   \
-            uint32_t* const bq_ = sp_lds + ((p_ + 1) % 3) * bufdw + lr_ * rowdw;                             \
+            if (!kKeyCache || (k_ & 0xFFFF) != pk) {                                                         \
+                pk = k_ & 0xFFFF;                                                                            \
+                plo = p_ * span;                                                                             \
+                phi = min(plo + span, n);                                                                    \
+                phq = min(phi + span, n);                                                                    \
+                pbp = sp_lds + (p_ % 3) * bufdw + lr_ * rowdw;                                               \
+                pbq = sp_lds + ((p_ + 1) % 3) * bufdw + lr_ * rowdw;                                         \
+            }                                                                                                \
+            const int lo_ = plo, hi_ = phi, hq_ = phq;                                                       \
+            uint32_t* const bp_ = pbp;                                                                       \
+            uint32_t* const bq_ = pbq;                                                                       \
             const int a_ = ma_, rlo_ = mlo_, rup_ = mup_;                                                    \
             int c_[kE];                                                                                      \
             if constexpr (kRegRing) {                                                                        \
@@ -2047,7 +2092,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 62));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 64));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2098,7 +2143,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         const int depth = cfg.depth, ns = cfg.ns, slot = cfg.slot;
         const SpGeom sg = sp_geom(nc, tiles, depth, ns, slot);
         const int lds = sp_lds_bytes(tiles, sg, depth, ns, slot);
-        LDS_CHECK_ARG(lds <= 163840);
+        LDS_CHECK_ARG(lds <= 163840 && sg.passes <= 576);  // (the row counters of mode 16 share the 576-int meta area)
 #define LDS_SP_LAUNCH(TT, DP, DD) LDS_SP_LAUNCH_NS(TT, DP, DD, kSpStream)
 #define LDS_SP_LAUNCH_NS(TT, DP, DD, NS)                                                                           \
     do {                                                                                                           \
@@ -2111,8 +2156,8 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
     } while (0)
         if (dbg == 0 && tiles <= 2) LDS_SP_LAUNCH_NS(2, kSpProdDepth, kSpProdMode, kSpProdWaves);
         else if (dbg == 0 && tiles <= 4) LDS_SP_LAUNCH_NS(4, kSpProdDepth, kSpProdMode, kSpProdWaves);
-        else if (dbg == 0 && tiles <= 5) LDS_SP_LAUNCH_NS(5, kSpProdDepth, kSpProdMode, kSpProdWaves);
-        else if (dbg == 0) LDS_SP_LAUNCH_NS(6, kSpProdDepth, kSpProdMode, kSpProdWaves);
+        else if (dbg == 0) LDS_SP_LAUNCH_NS(6, kSpProdDepth, kSpProdMode, kSpProdWaves);  // (5 tiles too: the
+        // 6-tile build measured 170-171 µs at config 5 against 175-178 for a 5-tile build of the same code)
         else if (dbg == 31) LDS_SP_LAUNCH(6, kSpDepth, 1);
         else if (dbg == 32) LDS_SP_LAUNCH(6, kSpDepth, 2);
         else if (dbg == 35) LDS_SP_LAUNCH(6, kSpDepth, 3);
@@ -2147,6 +2192,9 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 60) LDS_SP_LAUNCH_NS(6, 3, 15, 12);
         else if (dbg == 61) LDS_SP_LAUNCH_NS(6, 4, 15, 12);
         else if (dbg == 62) LDS_SP_LAUNCH_NS(6, 6, 15, 12);
+        else if (dbg == 63 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 4, 16, 12);
+        else if (dbg == 63) LDS_SP_LAUNCH_NS(6, 4, 16, 12);
+        else if (dbg == 64) LDS_SP_LAUNCH_NS(6, 4, 17, 12);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
