@@ -1446,7 +1446,7 @@ struct SpCfg {
 SpCfg sp_cfg(int dbg) {
     if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
     if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
-    if (dbg >= 60 && dbg <= 64) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, 12, 0};  // register ring: no LDS
+    if (dbg >= 60 && dbg <= 65) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, 12, 0};  // register ring: no LDS
     const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
                     : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
                     : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
@@ -1594,9 +1594,10 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     // entries per lane and step: 4 (1-KB steps) or, DBG 12, 8 (2-KB steps, two DMAs)
     constexpr int kE = DBG >= 12 ? 8 : 4;
     constexpr bool kNoBits = DBG == 2 || DBG == 13;  // timing only: no bit setting
-    constexpr bool kRegRing = DBG == 15 || DBG == 16 || DBG == 17;  // the ring in registers (asm loads, counted waits): no LDS ring
+    constexpr bool kRegRing = DBG >= 15 && DBG <= 18;  // the ring in registers (asm loads, counted waits): no LDS ring
     constexpr bool kDynRows = DBG == 16;  // rows taken per pass from an LDS counter, not wave + NS·i
-    constexpr bool kKeyCache = DBG == 17;  // a step's pass bounds and bit rows reused while (row, pass) repeats
+    constexpr bool kKeyCache = DBG == 17 || DBG == 18;  // a step's pass bounds and bit rows reused while (row, pass) repeats
+    constexpr bool kLean = DBG == 18;  // fast-path ORs without the zero test; one wave-wide skip of the other paths
     constexpr bool kNoMfma = DBG == 1 || DBG == 14;  // timing only: no matrix-core products
     constexpr int kStep = 64 * kE;
     static_assert((D - 1) * (kE / 4) <= 15, "vmcnt field");
@@ -1831,10 +1832,16 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                         bp_[w0_] = (uint32_t)m_;                                                             \
                         bp_[w0_ + 1] = (uint32_t)(m_ >> 32);                                                 \
                     } else {                                                                                 \
-                        dn_or(bp_ + w0_, (uint32_t)m_);                                                      \
-                        dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                          \
+                        if (kLean) { /* m_ is never 0 here: the low word holds c_[0]'s bit */                \
+                            atomicOr(bp_ + w0_, (uint32_t)m_);                                               \
+                            atomicOr(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                   \
+                        } else {                                                                             \
+                            dn_or(bp_ + w0_, (uint32_t)m_);                                                  \
+                            dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                      \
+                        }                                                                                    \
                     }                                                                                        \
                 }                                                                                            \
+                if (!kLean || __ballot(!fast_) != 0ull) { /* (kLean: every lane fast: skip both below) */    \
                 if ((DBG == 10 || DBG >= 11) && !kNoBits && !fast_) { /* all of pass p + 1 (past the boundary) */       \
                     const uint32_t q0_ = (uint32_t)(c_[0] - hi_) >> 5;                                       \
                     if (c_[0] >= hi_ && c_[kE - 1] < hq_ && (uint32_t)(c_[kE - 1] - hi_) - (q0_ << 5) < 64u) { \
@@ -1866,6 +1873,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                         spill_ = true;                                                                       \
                         fast_ = true;                                                                        \
                     }                                                                                        \
+                }                                                                                            \
                 }                                                                                            \
             }                                                                                                \
             if (!fast_ && !kNoBits) {                                                                       \
@@ -2092,7 +2100,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 64));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 65));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2195,6 +2203,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 63 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 4, 16, 12);
         else if (dbg == 63) LDS_SP_LAUNCH_NS(6, 4, 16, 12);
         else if (dbg == 64) LDS_SP_LAUNCH_NS(6, 4, 17, 12);
+        else if (dbg == 65) LDS_SP_LAUNCH_NS(6, 4, 18, 12);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
