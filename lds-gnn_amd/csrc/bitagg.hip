@@ -1446,7 +1446,7 @@ struct SpCfg {
 SpCfg sp_cfg(int dbg) {
     if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
     if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
-    if (dbg >= 60 && dbg <= 65) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, 12, 0};  // register ring: no LDS
+    if (dbg >= 60 && dbg <= 66) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, 12, 0};  // register ring: no LDS
     const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
                     : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
                     : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
@@ -1594,9 +1594,10 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     // entries per lane and step: 4 (1-KB steps) or, DBG 12, 8 (2-KB steps, two DMAs)
     constexpr int kE = DBG >= 12 ? 8 : 4;
     constexpr bool kNoBits = DBG == 2 || DBG == 13;  // timing only: no bit setting
-    constexpr bool kRegRing = DBG >= 15 && DBG <= 18;  // the ring in registers (asm loads, counted waits): no LDS ring
+    constexpr bool kRegRing = DBG >= 15 && DBG <= 19;  // the ring in registers (asm loads, counted waits): no LDS ring
     constexpr bool kDynRows = DBG == 16;  // rows taken per pass from an LDS counter, not wave + NS·i
-    constexpr bool kKeyCache = DBG == 17 || DBG == 18;  // a step's pass bounds and bit rows reused while (row, pass) repeats
+    constexpr bool kKeyCache = DBG >= 17 && DBG <= 19;  // a step's pass bounds and bit rows reused while (row, pass) repeats
+    constexpr bool kOneBallot = DBG == 19;  // one ballot for the spill and past-pass flags of a step
     constexpr bool kLean = DBG == 18;  // fast-path ORs without the zero test; one wave-wide skip of the other paths
     constexpr bool kNoMfma = DBG == 1 || DBG == 14;  // timing only: no matrix-core products
     constexpr int kStep = 64 * kE;
@@ -1897,8 +1898,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 }                                                                                       \
             }                                                                                                \
             }                                                                                           \
-            if (__ballot(spill_) != 0ull) bnd = true;                                                        \
-            {                                                                                                \
+            if (!kOneBallot || __ballot(spill_ || myx_ != 0x7FFFFFFF) != 0ull) { /* (most steps: neither) */ \
+                if (__ballot(spill_) != 0ull) bnd = true;                                                    \
                 const uint64_t xm_ = __ballot(myx_ != 0x7FFFFFFF);                                           \
                 if (xm_ != 0ull) estar = min(estar, __builtin_amdgcn_readlane(myx_, __builtin_ctzll(xm_)));  \
             }                                                                                                \
@@ -2100,7 +2101,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 65));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 66));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2204,6 +2205,7 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 63) LDS_SP_LAUNCH_NS(6, 4, 16, 12);
         else if (dbg == 64) LDS_SP_LAUNCH_NS(6, 4, 17, 12);
         else if (dbg == 65) LDS_SP_LAUNCH_NS(6, 4, 18, 12);
+        else if (dbg == 66) LDS_SP_LAUNCH_NS(6, 4, 19, 12);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
