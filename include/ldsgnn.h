@@ -269,7 +269,9 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
  * 4 / 3), 54 / 55 / 56 / 57 2-KB steps (12 waves depth 3 and 2, 8 waves, 14
  * waves; depth 2), 60 / 61 / 62 2-KB steps through a register ring 3 / 4 / 6
  * deep, 63 the same taking rows per pass from an LDS counter, 64 reusing a
- * step's pass bounds while its (row, pass) repeats (= the product); 20 the column-pass kernel,
+ * step's pass bounds while its (row, pass) repeats (= the product), 65 / 66
+ * the product form with unconditional fast-path ORs / one ballot for a step's
+ * flags; 20 the column-pass kernel,
  * streaming and multiply waves concurrent, 21 its sequential form.  Ablations
  * (wrong results): 31 / 32 the spill-pass kernel without MFMAs / without
  * setting bits, 40 with plain stores for its interior ORs, 58 / 59 the
