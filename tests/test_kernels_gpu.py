@@ -924,7 +924,9 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
 def test_spmm_dense_spill_pass_row_shapes(device, grid):
     """The spill-pass kernel (the product at grid >= 0, and its variants:
     lds_spmm_dense_ablation dbg 23 / 33 / 34 with 1-KB steps and ring depths
-    8 / 6 / 12, 52 / 54 with 12 streaming waves; ascending columns) on rows
+    8 / 6 / 12, 52 / 54 / 55 with 12 streaming waves, 61 the register ring
+    without the cached pass constants, 63 rows taken from a counter (its wait
+    steps and their barriers), 65 / 66 the lean forms; ascending columns) on rows
     that take each of its paths, against the row-block kernel (dbg 6, any
     column order; identical bits: exact integer sums) and fp64: rows whose entries crowd the first columns (the
     stream stops at the predicted pass end before the pass boundary and the
@@ -964,7 +966,7 @@ def test_spmm_dense_spill_pass_row_shapes(device, grid):
     y0 = torch.empty(n, 16, device=device)
     nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(y0), 16, 0,
              nat.ptr(ws), grid, 1, nat.stream_of(device))
-    for dbg in (23, 33, 34, 52, 54, 55, 6):  # spill-pass variants, the hybrid row-block
+    for dbg in (23, 33, 34, 52, 54, 55, 61, 63, 65, 66, 6):  # spill-pass variants, the hybrid row-block
         yv = torch.empty(n, 16, device=device)
         nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16,
                  nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
