@@ -1446,7 +1446,7 @@ struct SpCfg {
 SpCfg sp_cfg(int dbg) {
     if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
     if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
-    if (dbg >= 60 && dbg <= 66) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, 12, 0};  // register ring: no LDS
+    if (dbg >= 60 && dbg <= 67) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, dbg == 67 ? 14 : 12, 0};  // register ring: no LDS
     const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
                     : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
                     : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
@@ -2101,7 +2101,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 66));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 67));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2206,6 +2206,8 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 64) LDS_SP_LAUNCH_NS(6, 4, 17, 12);
         else if (dbg == 65) LDS_SP_LAUNCH_NS(6, 4, 18, 12);
         else if (dbg == 66) LDS_SP_LAUNCH_NS(6, 4, 19, 12);
+        else if (dbg == 67 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 4, 17, 14);
+        else if (dbg == 67) LDS_SP_LAUNCH_NS(6, 4, 17, 14);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);
