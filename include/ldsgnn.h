@@ -271,7 +271,8 @@ int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int 
  * deep, 63 the same taking rows per pass from an LDS counter, 64 reusing a
  * step's pass bounds while its (row, pass) repeats (= the product), 65 / 66
  * the product form with unconditional fast-path ORs / one ballot for a step's
- * flags, 67 the product form with 14 streaming + 2 multiply waves; 20 the
+ * flags, 67 the product form with 14 streaming + 2 multiply waves, 68 / 69
+ * with 3-KB steps (depth 3 / 4); 20 the
  * column-pass kernel,
  * streaming and multiply waves concurrent, 21 its sequential form.  Ablations
  * (wrong results): 31 / 32 the spill-pass kernel without MFMAs / without

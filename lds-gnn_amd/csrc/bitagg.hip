@@ -1446,7 +1446,7 @@ struct SpCfg {
 SpCfg sp_cfg(int dbg) {
     if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
     if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
-    if (dbg >= 60 && dbg <= 67) return SpCfg{dbg == 60 ? 3 : dbg == 62 ? 6 : 4, dbg == 67 ? 14 : 12, 0};  // register ring: no LDS
+    if (dbg >= 60 && dbg <= 69) return SpCfg{dbg == 60 || dbg == 68 ? 3 : dbg == 62 ? 6 : 4, dbg == 67 ? 14 : 12, 0};  // register ring: no LDS
     const int depth = dbg == 33 || dbg == 38 || dbg == 44 ? 6 : dbg == 34 || dbg == 42 ? 12
                     : dbg == 43 || dbg == 46 ? 5 : dbg == 45 || dbg == 48 || (dbg >= 50 && dbg <= 52) ? 4
                     : dbg == 47 || dbg == 49 || dbg == 53 || dbg == 54 ? 3 : dbg >= 55 && dbg <= 57 ? 2 : kSpDepth;
@@ -1592,11 +1592,11 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     float* __restrict__ y, int ldy, int beta) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sp_lds_all[];
     // entries per lane and step: 4 (1-KB steps) or, DBG 12, 8 (2-KB steps, two DMAs)
-    constexpr int kE = DBG >= 12 ? 8 : 4;
+    constexpr int kE = DBG == 20 ? 12 : DBG >= 12 ? 8 : 4;  // (20: 3-KB steps)
     constexpr bool kNoBits = DBG == 2 || DBG == 13;  // timing only: no bit setting
-    constexpr bool kRegRing = DBG >= 15 && DBG <= 19;  // the ring in registers (asm loads, counted waits): no LDS ring
+    constexpr bool kRegRing = DBG >= 15 && DBG <= 20;  // the ring in registers (asm loads, counted waits): no LDS ring
     constexpr bool kDynRows = DBG == 16;  // rows taken per pass from an LDS counter, not wave + NS·i
-    constexpr bool kKeyCache = DBG >= 17 && DBG <= 19;  // a step's pass bounds and bit rows reused while (row, pass) repeats
+    constexpr bool kKeyCache = DBG >= 17 && DBG <= 20;  // a step's pass bounds and bit rows reused while (row, pass) repeats
     constexpr bool kOneBallot = DBG == 19;  // one ballot for the spill and past-pass flags of a step
     constexpr bool kLean = DBG == 18;  // fast-path ORs without the zero test; one wave-wide skip of the other paths
     constexpr bool kNoMfma = DBG == 1 || DBG == 14;  // timing only: no matrix-core products
@@ -1801,6 +1801,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             int c_[kE];                                                                                      \
             if constexpr (kRegRing) {                                                                        \
                 if constexpr (kE == 8) rb_bind(rg[J][0], rg[J][1]);                                          \
+                if constexpr (kE == 12) asm volatile("" : "+v"(rg[J][0]), "+v"(rg[J][1]), "+v"(rg[J][2]));   \
             }                                                                                                \
             _Pragma("unroll") for (int h_ = 0; h_ < kE / 4; ++h_) {                                          \
                 const int4 v_ = kRegRing ? int4{rg[J][h_][0], rg[J][h_][1], rg[J][h_][2], rg[J][h_][3]}      \
@@ -2101,7 +2102,7 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
 // results): dbg 1 phase A only, 2 phase A without slab stores, 3 phase B only.
 extern "C" int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z,
                                        int ldz, float* y, int ldy, void* ws, int dbg, void* stream) {
-    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 67));
+    LDS_CHECK_ARG((dbg >= 1 && dbg <= 8) || (dbg >= 11 && dbg <= 13) || (dbg >= 20 && dbg <= 23) || (dbg >= 31 && dbg <= 69));
     return spmm_dense_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
@@ -2208,6 +2209,8 @@ static int spmm_dense_launch(const int* row_ptr, const int* col, const float* s,
         else if (dbg == 66) LDS_SP_LAUNCH_NS(6, 4, 19, 12);
         else if (dbg == 67 && tiles <= 5) LDS_SP_LAUNCH_NS(5, 4, 17, 14);
         else if (dbg == 67) LDS_SP_LAUNCH_NS(6, 4, 17, 14);
+        else if (dbg == 68) LDS_SP_LAUNCH_NS(6, 3, 20, 12);
+        else if (dbg == 69) LDS_SP_LAUNCH_NS(6, 4, 20, 12);
         else if (dbg == 33) LDS_SP_LAUNCH(6, 6, 0);
         else if (dbg == 34) LDS_SP_LAUNCH(6, 12, 0);
         else if (tiles <= 2) LDS_SP_LAUNCH(2, kSpDepth, 0);

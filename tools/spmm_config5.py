@@ -94,7 +94,7 @@ def main(n=20000, f=16, reps=20, high=1.0):
     t_tile = time_it(lambda: dense(0, -256), reps)  # round 3's tile kernel (product only)
     y_abl0 = torch.empty_like(y_dn)
     eq_variants = {}
-    for dbg in (20, 21, 22, 23, 33, 34, 6, 36, 37, 38, 39, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 60, 61, 62, 63, 64, 65, 66, 67):  # the product variants give the same bits
+    for dbg in (20, 21, 22, 23, 33, 34, 6, 36, 37, 38, 39, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69):  # the product variants give the same bits
         nat.call("lds_spmm_dense_ablation", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_abl0), f,
                  nat.ptr(ws_dn), dbg, st)
         eq_variants[dbg] = bool(torch.equal(y_abl0, y_main))
@@ -133,6 +133,7 @@ def main(n=20000, f=16, reps=20, high=1.0):
                       (65, "spill-pass, product form with lean fast-path ORs and one wave-wide skip"),
                       (66, "spill-pass, product form with one ballot for the step flags"),
                       (67, "spill-pass, product form with 14 streaming + 2 multiply waves"),
+                      (68, "spill-pass, product form with 3-KB steps, depth 3"), (69, "spill-pass, product form with 3-KB steps, depth 4"),
                       (33, "spill-pass, ring depth 6"),
                       (34, "spill-pass, ring depth 12"), (31, "spill-pass, no MFMAs"),
                       (32, "spill-pass, streaming without bit setting"),
