@@ -272,48 +272,109 @@ def chain_us(fn, dev, k, reps=3):
     return 1000.0 * a.elapsed_time(b) / (reps * k)
 
 
-def window_breakdown(eng, reducer, args, device, k=20):
+def _window_state(eng):
+    """The device tensors one τ-window reads before it writes them (and
+    changes): the scalars (counters, error word), θ, the prefetched graphs'
+    bits and degree counts, the window-start weights / Adam state and the Adam
+    table.  Everything else a window reads it wrote itself first."""
+    ts = [eng.scalars, eng.theta, eng.gbatch.bits, eng.gbatch.deg, eng.w[0], eng.m[0], eng.v[0], eng.adam_tab]
+    if eng._deg_next is not None:
+        ts.append(eng._deg_next)
+    return ts
+
+
+def window_breakdown(eng, reducer, args, device, k=20, reps=10, rounds=5):
     """Where one τ-window's GPU time goes.  The C-ABI calls of one eager
-    window are recorded; each recorded call is then replayed as a chain of k
-    dependent copies of itself from one HIP graph (HIP events around the
-    replays, on the launch stream), so a launch's time is its own duration plus
-    the dependent-launch gap it pays inside the real window too — not the
-    event-per-launch skew of timing small kernels eagerly.  Per entry point:
-    launches and µs per window, the average launch, its algorithmic cost and
-    rate.  Runs after every timed leg: the chains re-apply θ / Adam updates,
-    so the engine's state is not used afterwards."""
+    window are recorded.  Two measurements per entry point:
+
+      * in-window (the table's us_per_window / avg_us): HIP graphs of the
+        window's first j calls, j = 0 … all, each preceded by the same
+        restore of the window-start state (kernel copies: θ, the prefetched
+        bits and degree counts, scalars, the window-start weights), are
+        replayed (HIP events on the replay stream, median of `rounds` rounds
+        of `reps` replays); call j's cost is T(j) − T(j − 1): its own duration
+        plus the dependent-launch gap it pays in the real sequence, on the
+        window's real state.  The entries sum to the replayed window.
+      * isolated (chain_avg_us): the call replayed as a dependent chain of k
+        copies of itself from one HIP graph (round 2-4's method; a call whose
+        inputs its own copies disturb — e.g. the fill of prefetched graphs —
+        reads differently there).
+
+    Per entry point: launches and µs per window, the average launch, its
+    algorithmic cost and rate.  Runs after every timed leg: the replays
+    re-apply θ / Adam updates, so the engine's state is not used afterwards."""
     from ldsgnn import _native as nat
     calls = []
     real = nat.call
 
     def rec(name, *a):
-        # with the window's degree counts as this call found them: a chain of
-        # a drawing launch (the θ-grad epilogue) accumulates into them 20 times
-        # over, and a later chain must not fill from those inflated counts
-        # (round 3's bench_sp1 fault, DESIGN §7c)
+        # with the window's degree counts as this call found them (the chain
+        # leg: a chain of a drawing launch accumulates into them k times over)
         calls.append((name, a, eng.gbatch.deg.clone()))
         real(name, *a)
 
+    state = [t.clone() for t in _window_state(eng)]
     nat.call = rec
     try:
         run_engine_windows(eng, reducer, 1, args.tau, False)
     finally:
         nat.call = real
     torch.cuda.synchronize()
-    per = {}
+    live = _window_state(eng)
+
+    def restore():  # kernel copies (x · 1 is exact for every dtype here): no memcpy node in the graphs
+        for dst, src in zip(live, state):
+            torch.mul(src, 1, out=dst)
+
+    cur = torch.cuda.current_stream(device)
+
+    def prefix_graph(j):
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream(device=device)
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            with torch.cuda.graph(g, stream=st):
+                restore()
+                for name, a, _ in calls[:j]:
+                    real(name, *(a[:-1] + (nat.stream_of(device),)))
+        cur.wait_stream(st)
+        return g
+
+    graphs = [prefix_graph(j) for j in range(len(calls) + 1)]
+    st = torch.cuda.Stream(device=device)
+    samples = [[] for _ in graphs]
+    for _ in range(rounds):
+        for j, g in enumerate(graphs):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                g.replay()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                for _ in range(reps):
+                    g.replay()
+                b.record(st)
+            b.synchronize()
+            samples[j].append(1000.0 * a.elapsed_time(b) / reps)
+    t = [float(np.median(x)) for x in samples]
+    restore()
+    torch.cuda.synchronize()
+    inwin = {}
+    for j, (name, _, _) in enumerate(calls):
+        inwin.setdefault(name, []).append(t[j + 1] - t[j])
+    chain = {}
     for name, a, deg in calls:
         if name == "lds_sample_graphs_multi":  # repeated draws clear their own workspace (ws_zeroed = 0)
             a = a[:-3] + (0,) + a[-2:]
         eng.gbatch.deg.copy_(deg)
-        us = chain_us(lambda st, name=name, a=a: real(name, *(a[:-1] + (st,))), device, k)
-        per.setdefault(name, []).append(us)
+        us = chain_us(lambda s_, name=name, a=a: real(name, *(a[:-1] + (s_,))), device, k)
+        chain.setdefault(name, []).append(us)
     rows = []
-    for name, ts in per.items():
+    for name, ts in inwin.items():
         calls_w = len(ts)
         avg = sum(ts) / calls_w
         bound, cost = algo_cost(name, eng, calls_w)
         row = {"entry": name, "launches_per_window": calls_w, "us_per_window": sum(ts), "avg_us": avg,
-               "bound": bound}
+               "chain_avg_us": sum(chain[name]) / len(chain[name]), "bound": bound}
         if cost:
             if bound == "mfma_i8":
                 row["algorithmic_int8_ops"] = cost
@@ -336,7 +397,7 @@ def window_breakdown(eng, reducer, args, device, k=20):
             row["pmc_GBs"] = tr / (avg * 1e-6) / 1e9
         rows.append(row)
     rows.sort(key=lambda r: -r["us_per_window"])
-    return rows, len(calls)
+    return rows, len(calls), {"restore_us": t[0], "window_us": t[-1] - t[0]}
 
 
 def roofline_of(row, args):
@@ -457,9 +518,13 @@ def strong_scaling_leg(args, world, rank, device, barrier_sync):
         eng, reducer = make_engine(runner, args.tau, reducer_world, S)
         eng.inner_step()
         eng.hyper_step(grad_reducer=reducer)
-        # T1 replays whole groups of windows per graph as the N = 1 line does
-        eng.capture_window(args.tau, grad_reducer=reducer, windows=args.graph_windows if reducer is None else 1,
-                           prefetch=not args.no_prefetch_draw)  # (T1, S_total samples, no exchange: not eligible)
+        # T1 replays whole groups of windows per graph as the N = 1 line does, and
+        # so does TN when the all-reduce is captured into the window graph
+        cap = reducer is not None and args.capture_exchange
+        eng.capture_window(args.tau, grad_reducer=reducer,
+                           windows=args.graph_windows if (reducer is None or cap) else 1,
+                           prefetch=not args.no_prefetch_draw,
+                           capture_exchange=cap if reducer is not None else None)
         eng.replay(1)
         if reducer_world > 1:
             barrier_sync()
@@ -590,10 +655,13 @@ def main():
     ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
                     "the ranks, against rank 0 alone (default 64 when N > 1, off at N = 1)")
     ap.add_argument("--strong-steps", type=int, default=50)
-    ap.add_argument("--exchange", default="auto", choices=["auto", "noop"],
-                    help="noop (one GPU): the N > 1 per-rank path with a no-op reducer in place of the RCCL "
-                         "all-reduce — windows split at the exchange into two replayed graphs, the next window's "
-                         "draw in the SGD pass (DESIGN §5b: the per-rank window of the strong-scaling leg)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "split", "noop", "noop-captured", "rccl1"],
+                    help="auto: N > 1 captures the RCCL all-reduce into the window graph when every rank's "
+                         "capture probe succeeds (ldsgnn.replicas.collective_capture_probe), else splits; split: "
+                         "N > 1 with the round-4 two graphs per window around an eager all-reduce; one GPU: "
+                         "noop = the N > 1 per-rank path with a no-op reducer (split graphs), noop-captured = "
+                         "the same reducer captured into the window graph, rccl1 = a world-size-1 nccl (RCCL) "
+                         "group and its real all-reduce captured into the window graph (DESIGN §5b)")
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-launch window breakdown leg")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
@@ -615,6 +683,13 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.backend)
+    elif args.exchange == "rccl1":  # a world-size-1 RCCL group on this GPU (the collective's launches, N = 1)
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=device)
     if args.strong_total is None:
         args.strong_total = 64 if world > 1 and args.model == "lds" and args.path == "engine" else 0
 
@@ -647,13 +722,31 @@ def main():
     if use_engine:
         assert args.steps % args.tau == 0 and args.warmup % args.tau == 0, "steps, warmup: multiples of tau"
         eng, reducer = make_engine(runner, args.tau, world, args.samples)
-        if args.exchange == "noop":
+        exchange_label = args.exchange if world == 1 else None
+        capture_exchange = False
+        if args.exchange in ("noop", "noop-captured", "rccl1"):
             if world > 1:
-                raise SystemExit("--exchange noop rehearses the N > 1 path on one GPU")
+                raise SystemExit(f"--exchange {args.exchange} rehearses the N > 1 path on one GPU")
+            if args.exchange == "rccl1":
+                from ldsgnn.replicas import collective_capture_probe, exchange_capturable
 
-            def reducer(grad):  # the exchange point, without the collective
-                return None
+                def reducer(grad):  # the N > 1 all-reduce mean, on the world-size-1 group
+                    dist.all_reduce(grad, op=dist.ReduceOp.SUM)
+                    grad.div_(dist.get_world_size())
+                reducer.capturable = exchange_capturable
+                capture_exchange = collective_capture_probe(device)
+                exchange_label = "nccl-allreduce-ws1-" + ("captured" if capture_exchange else "split")
+            else:
+                def reducer(grad):  # the exchange point, without the collective
+                    return None
+                capture_exchange = args.exchange == "noop-captured"
             eng.grad_reducer = reducer
+        elif world > 1 and args.exchange == "auto" and args.backend == "nccl":
+            from ldsgnn.replicas import collective_capture_probe
+            capture_exchange = collective_capture_probe(device)
+        if world > 1:
+            exchange_label = f"{args.backend}-allreduce-" + ("captured" if capture_exchange else "split")
+        args.capture_exchange = capture_exchange  # (the strong-scaling leg's TN captures the same way)
         eng.async_draw = bool(args.async_draw)
         if args.xt_pair:
             eng.set_xt_pair(args.xt_pair)
@@ -663,10 +756,14 @@ def main():
         if param_theta:  # the model's outer step runs eagerly between graph A and graph B
             reducer = eng.outer_update
         use_graph = not args.eager and eng.theta_fn is None  # per-draw θ (GAE proposal dropout): eager windows
-        if use_graph:  # N>1: split at the all-reduce (graph A, RCCL, graph B)
+        # N > 1: the all-reduce captured into the window graph (whole groups of
+        # windows per replay, as N = 1), or split at it (graph A, RCCL, graph B)
+        whole = reducer is None or capture_exchange
+        if use_graph:
             eng.capture_window(args.tau, grad_reducer=reducer,
-                               windows=args.graph_windows if reducer is None else 1,
-                               prefetch=not args.no_prefetch_draw)
+                               windows=args.graph_windows if whole else 1,
+                               prefetch=not args.no_prefetch_draw,
+                               capture_exchange=capture_exchange if reducer is not None else None)
         run_engine_windows(eng, reducer, args.warmup // args.tau, args.tau, use_graph)
     else:
         step = run_steps(runner, 0, args.warmup, args.tau)
@@ -716,12 +813,15 @@ def main():
     nnz = eng.sampled_nnz_mean() if use_engine else None
     roof, window = None, None
     if use_engine and not args.no_breakdown:
-        rows, ncalls = window_breakdown(eng, reducer, args, device)
+        rows, ncalls, pre = window_breakdown(eng, reducer, args, device)
         total = sum(r["us_per_window"] for r in rows)
         wall_win = 1000.0 * (steady["ms_per_step"] if steady else 1000.0 * elapsed / args.steps) * args.tau
-        window = {"method": "per-call dependent chains (20 copies, one HIP graph, HIP events on the launch stream)",
+        window = {"method": "in-window marginal cost: HIP graphs of the window's first j calls (after a restore of "
+                            "the window-start state) replayed, call j = T(j) - T(j-1), median of 5 x 10 replays; "
+                            "chain_avg_us: the call alone as a dependent chain of 20 copies",
                   "launch_calls_per_window": ncalls,
                   "sum_of_launch_us_per_window": total,
+                  "prefix_window_us": pre["window_us"], "restore_us": pre["restore_us"],
                   "replayed_window_us": wall_win,
                   "entries": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
                               for r in rows]}
@@ -759,10 +859,10 @@ def main():
                        "tau": args.tau, "samples_per_rank": args.samples, "parallelism": f"replicas{world}",
                        "theta_grad_form": form_name, "sampled_nnz": nnz,
                        "replicas_in_sync": in_sync, "graph_model": args.graph_model,
-                       "windows_per_graph": (args.graph_windows if reducer is None else 1)
+                       "windows_per_graph": (args.graph_windows if whole else 1)
                        if use_engine and use_graph else None,
                        "prefetched_draw": prefetched, "async_draw": bool(args.async_draw),
-                       "xt_pair": args.xt_pair, "exchange": args.exchange if world == 1 else f"{args.backend}-allreduce"},
+                       "xt_pair": args.xt_pair, "exchange": exchange_label if use_engine else None},
             "steady_state": steady,
             "strong_scaling": strong,
             "window": window,
@@ -770,7 +870,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

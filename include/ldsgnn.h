@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 13
+#define LDS_ABI_VERSION 14
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -54,6 +54,14 @@ const char* lds_error_string(int err);
  *     entries are written with the row's own index (valid, never outside the
  *     graph) instead of being left as whatever col held. */
 #define LDS_DEVERR_FILL_DEGREE 1u
+/*   LDS_DEVERR_CSR_COLUMNS (ABI 14) — lds_spmm_norm_dense's spill-pass kernel
+ *     (grid >= 0) met a row whose column order it could not aggregate
+ *     faithfully (a column that belongs to a column pass it had already
+ *     multiplied: the row's columns are not ascending) or a column outside
+ *     [0, n).  The result is then wrong and must not be used; rows out of
+ *     order only within the window the kernel places exactly give exact
+ *     results without the flag. */
+#define LDS_DEVERR_CSR_COLUMNS 2u
 
 /* Number of uint64 words per bitmask row for n nodes (ceil(n/64) rounded up
  * to an even count so every row starts 16-byte aligned). Host-only. */
@@ -233,59 +241,29 @@ int64_t lds_bitmask_agg_ws_bytes(int n);
  * fixed-point digits of s⊙z (lds_aggregate_bitmask's
  * quantisation: exact integer sums, one rounding per digit at 2^-31 of the
  * column maximum).  n <= lds_spmm_dense_max_n(); col 16-byte aligned; ws:
- * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned.  grid >= 0: the
- * spill-pass kernel (ABI 13; a workgroup's rows, at most 96, swept in column
- * passes with their bit rows in LDS: 12 waves stream 2-KB steps of col
- * through registers and set the bits, entries past a pass go straight into
- * the next pass's bits, 4 waves multiply the previous pass), one workgroup
- * per CU (0) or `grid` workgroups; columns distinct and ASCENDING within each
- * row (canonical CSR, as every sampler and fill of this library writes it;
- * out-of-order columns give wrong sums, never an out-of-bounds access).
- * grid < 0: the round-3 tile kernel on -grid persistent workgroups, columns
- * in any order (so is the row-block kernel, lds_spmm_dense_ablation dbg 6 /
- * 22, the product of ABI 12).
- * Three launches (column maxima, digits, the product);
- * quantize = 0 skips the first two (ws holds the digits of this s, z from an
- * earlier call).
+ * lds_spmm_dense_ws_bytes(n) bytes, 16-byte aligned.
+ *   grid >= 0: the spill-pass kernel (a workgroup's rows, at most 96, swept
+ *     in column passes with their bit rows in LDS: 12 waves stream 2-KB steps
+ *     of col through registers and set the bits, entries past a pass go
+ *     straight into the next pass's bits, 4 waves multiply the previous
+ *     pass), one workgroup per CU (0) or `grid` workgroups.  Columns must be
+ *     ASCENDING within each row (canonical CSR, as every sampler and fill of
+ *     this library writes it).  err (required): the device error word; a row
+ *     whose column order the kernel cannot aggregate faithfully, or a column
+ *     outside [0, n), sets LDS_DEVERR_CSR_COLUMNS there (the result is then
+ *     wrong; ABI 14 — ABI 13 dropped such entries silently).
+ *   grid < 0: the round-3 tile kernel on -grid persistent workgroups, columns
+ *     in any order (err unused, may be NULL).
+ * Three launches (column maxima, digits, the product); quantize = 0 skips
+ * the first two (ws holds the digits of this s, z from an earlier call).
  * Replaces torch.mm(normalize_adjacency_matrix(A), Z) (src/models/layers.py:44,
- * src/utils/graph.py:136-153). */
+ * src/utils/graph.py:136-153).  (The non-product forms rounds 3-4 measured
+ * live in the tools-only tools/variants/libldsgnn_variants.so.) */
 int64_t lds_spmm_dense_ws_bytes(int n);
 int lds_spmm_dense_max_n(void);
 int lds_spmm_norm_dense(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
-                        float* y, int ldy, int beta, void* ws, int grid, int quantize, void* stream);
-/* Variants and timing-only ablations of lds_spmm_norm_dense (tools/spmm_config5.py;
- * the digits of an earlier call must be in ws).  Products (same results as
- * lds_spmm_norm_dense): dbg 6 the row-block kernel with bit slabs in ws and
- * its digits loaded into registers (any column order), 22 the
- * same with the digits staged by LDS-DMA; the spill-pass kernel (ascending
- * columns) in the forms that led to the product: 23 8 streaming + 8 multiply
- * waves, 1-KB steps through an LDS-DMA ring 8 deep, 33 / 34 ring depth 6 / 12,
- * 35 the ring drained before every step, 36 quad-reduced bit ORs, 37 / 38
- * windowed bit setting on every step (depth 8 / 6), 39 the ring read one step
- * ahead, 41 / 42 the ring loop not unrolled (depth 8 / 12), 43-47 12 streaming
- * + 4 multiply waves (depths 5, 6, 4, 5 with windowed boundary steps, 3),
- * 48 / 49 14 + 2 (depths 4 / 3), 50 / 51 12 / 14 streaming waves with the
- * pass p + 1 fast path, 52 / 53 with the boundary-lane fast path too (depths
- * 4 / 3), 54 / 55 / 56 / 57 2-KB steps (12 waves depth 3 and 2, 8 waves, 14
- * waves; depth 2), 60 / 61 / 62 2-KB steps through a register ring 3 / 4 / 6
- * deep, 63 the same taking rows per pass from an LDS counter, 64 reusing a
- * step's pass bounds while its (row, pass) repeats (= the product), 65 / 66
- * the product form with unconditional fast-path ORs / one ballot for a step's
- * flags, 67 the product form with 14 streaming + 2 multiply waves, 68 / 69
- * with 3-KB steps (depth 3 / 4); 20 the
- * column-pass kernel,
- * streaming and multiply waves concurrent, 21 its sequential form.  Ablations
- * (wrong results): 31 / 32 the spill-pass kernel without MFMAs / without
- * setting bits, 40 with plain stores for its interior ORs, 58 / 59 the
- * 2-KB LDS-ring form (55) without setting bits / without MFMAs;
- * 11 / 12 / 13 the column-pass kernel without its multiply /
- * streaming waves; 1-5 the row-block kernel's streaming phase alone, without
- * its slab stores, its multiply phase alone, without its slab loads,
- * streaming with the column-pass step bookkeeping; 7 the register-digit
- * multiply phase alone, 8 the same without its per-chunk barrier.  Test
- * hook. */
-int lds_spmm_dense_ablation(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
-                            float* y, int ldy, void* ws, int dbg, void* stream);
+                        float* y, int ldy, int beta, void* ws, int grid, int quantize, uint32_t* err,
+                        void* stream);
 int lds_bitmask_agg_splits(int n);
 int64_t lds_bitmask_agg_part_offset(int n);
 int lds_aggregate_bitmask_partials(const uint64_t* bits, int words, const float* s, int n, const float* z,

@@ -19,7 +19,9 @@ constexpr int kDenseRowFill = 1024;
 // One row of the fused fill with a whole wave (rows of kDenseRowFill or more
 // entries, or a wave that holds one): ascending columns into col from
 // position pre, the first 64 into head.
-// Returns the entries the row's bits hold (written from pre on, up to capacity).
+// Returns the entries the row's bits hold (written from pre on, below `capacity`:
+// callers pass min(col capacity, pre + the row's degree count), so a row whose
+// bits hold more entries than its count never writes into the next row's slots).
 __device__ __forceinline__ int64_t fill_row_wave(const uint64_t* __restrict__ rb_bits, int nbw, int64_t pre, int deg,
                                                  int* __restrict__ col, int64_t capacity, int* __restrict__ head) {
     const int lane = wave_lane();
@@ -77,8 +79,9 @@ __device__ __forceinline__ int64_t fill_row_wave(const uint64_t* __restrict__ rb
 // valid index: wrong weights, never an address outside the graph) and the
 // device error word gets kDevErrFillDegree, which the host reads and raises
 // (include/ldsgnn.h "Device error word").  got > deg (counts short of the
-// bits) spills into the next row's slots, still with valid indices; flagged
-// the same way.  lane / lanes: this row's threads (16 or 64).
+// bits) is flagged too; the fill wrote only the row's own [pre, pre + deg)
+// slots, so the next row's columns stay intact.  lane / lanes: this row's
+// threads (16 or 64).
 __device__ __forceinline__ void fill_degree_guard(int64_t pre, int64_t got, int deg, int row, int* __restrict__ col,
                                                   int64_t capacity, int lane, int lanes, uint32_t* __restrict__ err) {
     if (got == (int64_t)deg) return;
@@ -156,6 +159,7 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
     }
     if (__ballot(live && deg >= kDenseRowFill) == 0) {
         int64_t base = pre;
+        const int64_t lim = min(capacity, (int64_t)pre + deg);  // this row's slots only
         for (int w0 = 0; w0 < nbw; w0 += 16) {  // uniform: every group walks the same word count
             const int w = w0 + h;
             uint64_t word = w0 == 0 ? word0 : ((live && w < nbw) ? rb_bits[w] : 0ull);
@@ -165,7 +169,7 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
             while (word) {
                 const int bit = __ffsll((unsigned long long)word) - 1;
                 const int j = w * 64 + bit;
-                if (pos < capacity) col[pos] = j;
+                if (pos < lim) col[pos] = j;
                 if (pos - pre < kEllWidth) head[k][pos - pre] = j;
                 ++pos;
                 word &= word - 1;
@@ -180,7 +184,8 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
             if (rq >= n) break;
             const int64_t pq = (int64_t)bpre + dblk[kq];
             const int dq = dacc[rq];
-            const int64_t got = fill_row_wave(bits + (int64_t)rq * words, nbw, pq, dq, col, capacity, head[kq]);
+            const int64_t got = fill_row_wave(bits + (int64_t)rq * words, nbw, pq, dq, col,
+                                              min(capacity, pq + dq), head[kq]);
             fill_degree_guard(pq, got, dq, rq, col, capacity, lane, 64, err);
         }
     }

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -63,8 +63,7 @@ SIGNATURES = {
     "lds_aggregate_bitmask_partials": [P, c_int, P, c_int, P, c_int, P, P],
     "lds_spmm_dense_ws_bytes": [c_int],
     "lds_spmm_dense_max_n": [],
-    "lds_spmm_norm_dense": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, c_int, c_int, P],
-    "lds_spmm_dense_ablation": [P, P, P, c_int, P, c_int, P, c_int, P, c_int, P],
+    "lds_spmm_norm_dense": [P, P, P, c_int, P, c_int, P, c_int, c_int, P, c_int, c_int, P, P],
     "lds_theta_grad": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, c_int, P],
     "lds_theta_grad_valu": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, c_int, P],
     "lds_theta_grad_sgd": [P, P, c_int, c_int, P, c_int, c_int, P, c_int, P, P, c_int, P],
@@ -138,10 +137,14 @@ class DeviceError(RuntimeError):
 
 
 DEVERR_FILL_DEGREE = 1  # LDS_DEVERR_FILL_DEGREE
+DEVERR_CSR_COLUMNS = 2  # LDS_DEVERR_CSR_COLUMNS (ABI 14)
 
 _DEVERR_TEXT = {DEVERR_FILL_DEGREE: "a CSR fill found a row whose degree count differs from its drawn bits "
                                     "(degree workspace not zero on entry, or counts of another draw); its "
-                                    "slots past the drawn entries hold the row's own index"}
+                                    "slots past the drawn entries hold the row's own index",
+                DEVERR_CSR_COLUMNS: "the dense CSR-SpMM (lds_spmm_norm_dense) met a row whose columns are not "
+                                    "ascending in a way that changes its sum, or a column outside [0, n): the "
+                                    "aggregation is wrong"}
 
 
 def raise_device_error(word: int, what: str) -> None:
@@ -249,15 +252,32 @@ def new_graph() -> "torch.cuda.CUDAGraph":
 UPLOAD_GRAPHS = True
 
 
-def seal_graph(graph: "torch.cuda.CUDAGraph", what: str) -> "torch.cuda.CUDAGraph":
+# ... and, in a window that captures the replicas' exchange (an RCCL
+# collective), the event nodes a collective library may add to order its own
+# stream against the capture
+_GRAPH_NODE_OK_EXCHANGE = {**_GRAPH_NODE_OK, 6: "event wait", 7: "event record"}
+
+
+def graph_census(graph: "torch.cuda.CUDAGraph") -> dict:
+    """{node type name: count} of a captured (not yet instantiated) graph."""
+    counts = (ctypes.c_int * 16)()
+    call("lds_graph_node_census", graph.raw_cuda_graph(), ctypes.addressof(counts), 16)
+    names = {**_GRAPH_NODE_NAMES, **_GRAPH_NODE_OK}
+    return {names.get(t, f"type {t}"): c for t, c in enumerate(counts) if c}
+
+
+def seal_graph(graph: "torch.cuda.CUDAGraph", what: str, exchange: bool = False) -> "torch.cuda.CUDAGraph":
     """Refuse a captured graph that holds anything but kernel (and empty)
     nodes, then instantiate it.  A memset node in a replayed step graph
     faulted the GPU in round 2; every clear the engine needs is a
     kernel, and this keeps any other node type from entering a capture: the
-    failure is a host-side error at capture time, never a GPU fault."""
+    failure is a host-side error at capture time, never a GPU fault.
+    `exchange`: the capture holds the replicas' collective, whose event
+    nodes are allowed too (never a memset or memcpy)."""
     counts = (ctypes.c_int * 16)()
     call("lds_graph_node_census", graph.raw_cuda_graph(), ctypes.addressof(counts), 16)
-    bad = {_GRAPH_NODE_NAMES.get(t, f"type {t}"): c for t, c in enumerate(counts) if c and t not in _GRAPH_NODE_OK}
+    ok = _GRAPH_NODE_OK_EXCHANGE if exchange else _GRAPH_NODE_OK
+    bad = {_GRAPH_NODE_NAMES.get(t, f"type {t}"): c for t, c in enumerate(counts) if c and t not in ok}
     if bad:
         raise RuntimeError(f"captured {what} holds non-kernel graph nodes {bad}: refusing to replay it")
     graph.instantiate()

@@ -248,9 +248,13 @@ class LdsEngine:
         self.agg_splits = 0  # bitmask aggregation: its partial arrays, summed by the consumers
         # graph buffers: CSR column capacity n² per graph (int32 positions);
         # none when the bitmask aggregation reads the sampled bits directly
-        if not self.bitmask_agg and n * n >= (1 << 31):
+        # (the per-graph column stride rounded up to 4 ints: every graph's col
+        # then starts 16-byte aligned, as lds_spmm_norm_dense requires, also
+        # for odd n)
+        cap = (n * n + 3) & ~3
+        if not self.bitmask_agg and cap >= (1 << 31):
             raise NotImplementedError("LdsEngine needs n² < 2^31 (int32 CSR positions)")
-        self.cap = 0 if self.bitmask_agg else n * n
+        self.cap = 0 if self.bitmask_agg else cap
         self.bptr_len = n * (nat.lib.lds_spmm_block_count(n) + 1) \
             if self.long_rows and not (self.bitmask_agg or self.dense_agg) else 0
         self.words = nat.lib.lds_bitmask_words(n)
@@ -669,7 +673,7 @@ class LdsEngine:
             return nat.ptr(self.agg_ws) + self.agg_part_off
         if self.dense_agg:
             nat.call("lds_spmm_norm_dense", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z),
-                     HID, nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), 0, 1, self._stream())
+                     HID, nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), 0, 1, self._err_ptr(), self._stream())
             return nat.ptr(self.agg)
         nat.call("lds_spmm_norm_blocked", nat.ptr(g.bptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z), HID,
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())
@@ -1357,7 +1361,8 @@ class LdsEngine:
             self.inner_step(presampled=batch)
         return self.hyper_step(grad_reducer=grad_reducer, presampled=batch)
 
-    def capture_window(self, tau: int, grad_reducer=None, windows: int = 1, prefetch: bool = False):
+    def capture_window(self, tau: int, grad_reducer=None, windows: int = 1, prefetch: bool = False,
+                       capture_exchange: Optional[bool] = None):
         """Record run_window(tau) as HIP graphs (state must be at a window
         start).  Replays advance RNG counters, Adam step and lr on device.
 
@@ -1379,7 +1384,12 @@ class LdsEngine:
         (replicas over RCCL) the window is
         split at the exchange: graph A runs up to dθ, `grad_reducer(grad)`
         runs eagerly between the replays (the collective stays outside the
-        captured work), graph B applies SGD + clamp and the detach."""
+        captured work), graph B applies SGD + clamp and the detach.
+        `capture_exchange` (default: the reducer's own `capturable` attribute,
+        which ldsgnn.replicas sets for the RCCL all-reduce): the exchange is
+        captured INTO the window graph (an RCCL collective is a kernel node),
+        so the window is one graph again and `windows` > 1 groups replay as
+        at N = 1."""
         assert self.t == 0 and self.pending_graph == 0 and self.pending_fwd == 0
         if self.theta_fn is not None:
             raise NotImplementedError("per-draw θ (GAE proposal dropout) computes θ of each draw on the host "
@@ -1398,15 +1408,21 @@ class LdsEngine:
         self._enter_window_state(self.prefetch_draw, tau)
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        if grad_reducer is None:
+        if capture_exchange is None:
+            cap = getattr(grad_reducer, "capturable", False)
+            capture_exchange = bool(cap() if callable(cap) else cap)
+        if grad_reducer is None or capture_exchange:
             graphs = []
             for w in sorted({1, windows}):
                 graph = nat.new_graph()
                 with torch.cuda.stream(s):
-                    with torch.cuda.graph(graph, stream=s):
+                    # (thread-local capture errors: a collective library's own
+                    # threads may touch the runtime while the window is captured)
+                    with torch.cuda.graph(graph, stream=s, capture_error_mode="thread_local"):
                         for _ in range(w):
-                            self.run_window(tau)
-                graphs.append((w, nat.seal_graph(graph, f"{w}-window group")))
+                            self.run_window(tau, grad_reducer=grad_reducer)
+                graphs.append((w, nat.seal_graph(graph, f"{w}-window group",
+                                                 exchange=grad_reducer is not None)))
             torch.cuda.current_stream(self.dev).wait_stream(s)
             self._graph_capture = (tuple(graphs), tau, None, self.prefetch_draw)
             return graphs[0][1]

@@ -62,6 +62,8 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
                 grad.copy_(model.probs.grad)
                 model.probs.grad = grad
 
+        # graph-capturable exactly when the trainer's reducer is (RCCL all-reduce)
+        reduce_engine_grad.capturable = getattr(reducer, "capturable", False)
         eng.grad_reducer = reduce_engine_grad
     return eng
 

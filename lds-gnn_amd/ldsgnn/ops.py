@@ -115,8 +115,10 @@ class CsrGraph:
              blocked: Optional[bool] = None) -> torch.Tensor:
         """Y = Â·Z; no autograd.  Row-group kernel (lds_spmm_norm), or for long
         rows at F = 16 the CSR spill-pass kernel on the int8 matrix cores
-        (lds_spmm_norm_dense; 170 against 414 µs for the column-blocked kernel
-        at BASELINE config 5; needs the ascending columns this class holds).  `blocked=True` forces the column-blocked kernel
+        (lds_spmm_norm_dense; 165-168 against 414 µs for the column-blocked kernel
+        at BASELINE config 5; needs the ascending columns this class holds: a
+        CSR whose column order the kernel cannot aggregate faithfully raises
+        ldsgnn._native.DeviceError on the graph's first call).  `blocked=True` forces the column-blocked kernel
         (lds_spmm_norm_blocked), `blocked=False` the row-group kernel."""
         z = _f32c(z, "spmm")
         if z.dim() != 2 or z.size(0) != self.n:
@@ -130,8 +132,18 @@ class CsrGraph:
             if ws is None:
                 ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(self.n)), dtype=torch.uint8, device=z.device)
                 self._dense_ws = ws
+                self._dense_err = torch.zeros(1, dtype=torch.int32, device=z.device)
             nat.call("lds_spmm_norm_dense", nat.ptr(self.row_ptr), nat.ptr(self.col), nat.ptr(self.s), self.n,
-                     nat.ptr(z), z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(ws), 0, 1, _stream(z))
+                     nat.ptr(z), z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(ws), 0, 1,
+                     nat.ptr(self._dense_err), _stream(z))
+            # the kernel flags a column order it cannot aggregate faithfully (a
+            # property of this CSR: checked on the graph's first call, one sync)
+            if not getattr(self, "_dense_checked", False) and not torch.cuda.is_current_stream_capturing():
+                word = int(self._dense_err.item())
+                if word:
+                    self._dense_err.zero_()
+                    nat.raise_device_error(word, "CsrGraph.spmm (lds_spmm_norm_dense)")
+                self._dense_checked = True
             return out
         use_blocked = (f == 16 and self.long_rows()) if blocked is None else blocked
         if use_blocked:

@@ -175,16 +175,18 @@ def test_spmm_dense_n20000_vs_bitmask_csr_and_fp64_rows(device, dense_graph):
     graph = dense_graph
     z = torch.randn(N, 16, generator=torch.Generator().manual_seed(3)).to(device)
     ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(N)), dtype=torch.uint8, device=device)
+    err = torch.zeros(1, dtype=torch.int32, device=device)
     outs = []
     for _ in range(2):
         y = torch.empty(N, 16, device=device)
         nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), N, nat.ptr(z),
-                 16, nat.ptr(y), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
+                 16, nat.ptr(y), 16, 0, nat.ptr(ws), 0, 1, nat.ptr(err), nat.stream_of(device))
         outs.append(y)
     y_tile = torch.empty(N, 16, device=device)  # the round-3 tile kernel (grid < 0): the same exact sums
     nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), N, nat.ptr(z),
-             16, nat.ptr(y_tile), 16, 0, nat.ptr(ws), -256, 1, nat.stream_of(device))
+             16, nat.ptr(y_tile), 16, 0, nat.ptr(ws), -256, 1, 0, nat.stream_of(device))
     torch.cuda.synchronize()
+    assert int(err.item()) == 0  # the sampler's canonical CSR: no column-order flag
     assert torch.equal(outs[0], outs[1])
     assert torch.equal(outs[0], y_tile)
     y = outs[0]

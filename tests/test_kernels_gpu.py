@@ -429,7 +429,9 @@ def test_fill_guard_pads_inflated_degrees(device):
     writes the drawn columns, pads each row's remaining slots with the row
     index (col was garbage before), leaves no CSR position outside [0, n) and
     sets LDS_DEVERR_FILL_DEGREE in the error word; a consistent call leaves
-    the word alone.  Both fill forms: 16-lane rows and whole-wave dense rows."""
+    the word alone.  Counts short of the bits (one less per row) are flagged
+    and every row writes only its own slots.  Both fill forms: 16-lane rows
+    and whole-wave dense rows."""
     for n, dense in ((300, 0.3), (1500, 0.9)):
         g = torch.Generator().manual_seed(n)
         theta = (torch.rand(n * (n + 1) // 2, generator=g) * dense).to(device)
@@ -444,7 +446,7 @@ def test_fill_guard_pads_inflated_degrees(device):
         err = torch.zeros(1, dtype=torch.int32, device=device)
         cap = n * n
         outs = []
-        for extra in (0, 5):
+        for extra in (0, 5, -1):
             ws = torch.full((wsi,), extra, dtype=torch.int32, device=device)
             col = torch.full((cap,), 0x7FFFFFFF, dtype=torch.int32, device=device)
             nat.call("lds_sample_graphs_multi", nat.ptr(theta), n, 11, tag_for(TAG_GRAPH, 0), 1, nat.ptr(base), 0,
@@ -454,7 +456,7 @@ def test_fill_guard_pads_inflated_degrees(device):
             assert int(err.item()) == (1 if extra else 0), (n, extra)
             err.zero_()
             outs.append((rp.clone().long().cpu(), col.cpu(), ws[:n].long().cpu()))
-        (rp0, col0, d0), (rp1, col1, d1) = outs
+        (rp0, col0, d0), (rp1, col1, d1), (rp2, col2, d2) = outs
         assert torch.equal(d1, d0 + 5)
         nnz = int(rp1[n])
         assert nnz == int(d0.sum()) + 5 * n
@@ -464,6 +466,12 @@ def test_fill_guard_pads_inflated_degrees(device):
             k = int(d0[r])
             assert torch.equal(got[:k], col0[int(rp0[r]):int(rp0[r + 1])]), r
             assert bool((got[k:] == r).all()), r
+        # counts one short of the bits (flagged above): every row keeps to its own
+        # slots — its first deg - 1 columns, ascending — never the next row's
+        assert torch.equal(d2, d0 - 1)
+        for r in range(n):
+            got = col2[int(rp2[r]):int(rp2[r + 1])]
+            assert torch.equal(got, col0[int(rp0[r]):int(rp0[r + 1]) - 1]), r
 
 
 
@@ -801,14 +809,25 @@ def test_theta_grad_direct_draw_equals_sgd_draw(device, n, k, graphs):
             assert torch.equal(a, b)
 
 
-def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, grid=0):
+def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, grid=0, expect_err=0):
+    """lds_spmm_norm_dense into `out` (or a new n × 16); the device error word
+    must read `expect_err` afterwards."""
     dev = z.device
     ws = torch.full((int(nat.lib.lds_spmm_dense_ws_bytes(n)),), 0x5A, dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
     y = out if out is not None else torch.empty(n, ldy, device=dev)
     nat.call("lds_spmm_norm_dense", nat.ptr(graph_rp), nat.ptr(graph_col), nat.ptr(s), n, nat.ptr(z), ldz,
-             nat.ptr(y), ldy, beta, nat.ptr(ws), grid, 1, nat.stream_of(dev))
+             nat.ptr(y), ldy, beta, nat.ptr(ws), grid, 1, nat.ptr(err), nat.stream_of(dev))
     torch.cuda.synchronize()
+    assert int(err.item()) == expect_err, (int(err.item()), expect_err)
     return y
+
+
+def _csr_of_dense(a):
+    rows, cols = a.nonzero(as_tuple=True)
+    rp = torch.zeros(a.size(0) + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(a.sum(1), 0)
+    return rp, cols.int()
 
 
 @pytest.mark.parametrize("n,high,grid", [(1, 1.0, 0), (17, 1.0, 0), (700, 1.0, 0), (1500, 1.0, 3), (1500, 1.0, -3),
@@ -817,13 +836,13 @@ def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, 
 def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     """lds_spmm_norm_dense (CSR streamed into LDS bit rows, int8 matrix-core
     product) vs the dense fp64 product, the bitmask aggregation (same digits:
-    identical bits where that takes one split) and the CSR row kernel: ragged
-    n, dense and sparse rows (the sparse fallback of the bit setting), grids
-    that force the most rows per block (the row-block kernel, grid > 0) or a
-    persistent grid smaller than the tile count (the tile kernel, grid < 0),
-    columns of extreme scale.  The row-block and tile kernels give the same
-    bits (exact integer sums, same final arithmetic).  Per-column tolerance
-    1e-5 of max_i Σ_k |Â_ik z_kf|."""
+    identical bits where that takes one split) and the other product kernel
+    (spill-pass at grid >= 0, the tile kernel at grid < 0: identical bits,
+    exact integer sums): ragged n, dense and sparse rows (the sparse fallback
+    of the bit setting), grids that force the most rows per block or a
+    persistent grid smaller than the tile count (the tile kernel), columns of
+    extreme scale; the error word stays 0 on the sampler's canonical CSR.
+    Per-column tolerance 1e-5 of max_i Σ_k |Â_ik z_kf|."""
     g = torch.Generator().manual_seed(n + 29)
     theta = torch.rand(n * (n + 1) // 2, generator=g) * high
     graph = ops.sample_graph_from_triu(theta.to(device), n, generator=Generator(n + 1), track_grad=False)
@@ -836,18 +855,6 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     y = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=grid).cpu().double()
     y_other = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=0 if grid < 0 else -256).cpu().double()
     assert torch.equal(y, y_other)
-    ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
-    y0 = torch.empty(n, 16, device=device)  # (quantises z into ws for the variants below)
-    nat.call("lds_spmm_norm_dense", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n, nat.ptr(zd), 16,
-             nat.ptr(y0), 16, 0, nat.ptr(ws), 0, 1, nat.stream_of(device))
-    # column-pass (2 forms), row-block (LDS-DMA digits), spill-pass (1-KB steps, depths 8, 6, 12), hybrid
-    # row-block, spill-pass with 12 streaming waves and 1-KB / 2-KB steps (the product form as a variant: 55)
-    for dbg in (20, 21, 22, 23, 33, 34, 6, 52, 54, 55):
-        yv = torch.empty(n, 16, device=device)
-        nat.call("lds_spmm_dense_ablation", nat.ptr(graph.row_ptr), nat.ptr(graph.col), nat.ptr(graph.s), n,
-                 nat.ptr(zd), 16, nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
-        torch.cuda.synchronize()
-        assert torch.equal(yv.cpu().double(), y), dbg
     a = graph.normalized_dense().cpu().double()
     ref = a @ z.double()
     scale = (a.abs() @ z.double().abs()).max(0).values.clamp(min=1e-300)
@@ -869,21 +876,20 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
 
 def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     """A general 0/1 CSR with rows in any column order (the bits are set by
-    OR), empty rows, long rows straddling the 512-entry steps: the kernels
-    that accept any order — the tile kernel (grid < 0) and the row-block
-    kernel (lds_spmm_dense_ablation dbg 22) — give 0 for the empty rows and
-    identical bits.  (The product, the spill-pass kernel at grid >= 0, needs
-    ascending columns: test_spmm_dense_spill_pass_row_shapes.)"""
+    OR), empty rows, long rows straddling the 512-entry steps.  The tile
+    kernel (grid < 0) accepts any order; the spill-pass kernel (grid >= 0)
+    places every column exactly when its geometry has one column pass, as
+    here (n = 1300: three chunks in one pass), so both give the sums of the
+    same CSR with its rows sorted, bit for bit, 0 for the empty rows, and no
+    error.  (Several passes: test_spmm_dense_unsorted_columns_flag_or_exact.)"""
     n = 1300
     g = torch.Generator().manual_seed(5)
     a = (torch.rand(n, n, generator=g) < 0.45)
     a[7] = False
     a[500:520] = False
     a[n - 1] = False
-    rows, cols = a.nonzero(as_tuple=True)
-    rp = torch.zeros(n + 1, dtype=torch.int64)
-    rp[1:] = torch.cumsum(a.sum(1), 0)
-    col = cols.clone().int()
+    rp, col_sorted = _csr_of_dense(a)
+    col = col_sorted.clone()
     for i in (3, 900):  # reverse two rows' column order
         b, e = int(rp[i]), int(rp[i + 1])
         col[b:e] = col[b:e].flip(0)
@@ -900,41 +906,101 @@ def test_spmm_dense_empty_rows_and_unsorted_columns(device):
     ref = s.double()[:, None] * (a.double() @ (s.double()[:, None] * z.double()))
     scale = (a.double() @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
     rpd, cold, sd, zd = rp.int().to(device), col.to(device), s.to(device), z.to(device)
+    y_sorted = _spmm_dense(rpd, col_sorted.to(device), sd, n, zd, grid=0).cpu().double()
     ys = []
-    for grid in (-256, None):  # the tile kernel; the row-block kernel (any column order)
-        if grid is None:
-            ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
-            y0 = torch.empty(n, 16, device=device)  # (the tile kernel quantises z into ws for the hook)
-            nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(y0),
-                     16, 0, nat.ptr(ws), -256, 1, nat.stream_of(device))
-            yv = torch.empty(n, 16, device=device)
-            nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16,
-                     nat.ptr(yv), 16, nat.ptr(ws), 22, nat.stream_of(device))
-            torch.cuda.synchronize()
-            y = yv.cpu().double()
-        else:
-            y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid).cpu().double()
+    for grid in (-256, 0):  # the tile kernel; the spill-pass kernel in one pass
+        y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid).cpu().double()
         assert float(((y - ref).abs().max(0).values / scale).max()) < RTOL, grid
         assert torch.all(y[7] == 0) and torch.all(y[500:520] == 0) and torch.all(y[n - 1] == 0), grid
+        assert torch.equal(y, y_sorted), grid
         ys.append(y)
-    assert torch.equal(ys[0], ys[1])
+
+
+def test_spmm_dense_unsorted_columns_flag_or_exact(device):
+    """The spill-pass kernel with several column passes (n = 9000, grid 94:
+    96-row blocks, three passes of six chunks) on CSRs whose rows are out of
+    order: every
+    call either gives exactly the sums of the sorted CSR with the error word
+    0, or sets LDS_DEVERR_CSR_COLUMNS — never a silent wrong result.  Reversed
+    and shuffled rows must be flagged (their first entries belong to the last
+    pass); swaps of neighbouring entries inside a lane's 64-column window are
+    placed exactly.  A column >= n is flagged too.  The host wrapper
+    (CsrGraph.spmm) raises DeviceError on the flag."""
+    n, grid = 9000, 94
+    g = torch.Generator().manual_seed(17)
+    a = torch.rand(n, n, generator=g) < 0.3
+    rp, col_sorted = _csr_of_dense(a)
+    del a
+    s = torch.rand(n, generator=g) + 0.5
+    z = torch.randn(n, 16, generator=g)
+    rpd, sd, zd = rp.int().to(device), s.to(device), z.to(device)
+    y_sorted = _spmm_dense(rpd, col_sorted.to(device), sd, n, zd, grid=grid).cpu()
+
+    def run(col):
+        y = torch.empty(n, 16, device=device)
+        ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
+        err = torch.zeros(1, dtype=torch.int32, device=device)
+        nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(col.to(device)), nat.ptr(sd), n, nat.ptr(zd), 16,
+                 nat.ptr(y), 16, 0, nat.ptr(ws), grid, 1, nat.ptr(err), nat.stream_of(device))
+        torch.cuda.synchronize()
+        return int(err.item()), y.cpu()
+
+    def row(c, i):
+        return slice(int(rp[i]), int(rp[i + 1]))
+
+    cases = {}
+    col = col_sorted.clone()  # one reversed row
+    col[row(col, 2500)] = col[row(col, 2500)].flip(0)
+    cases["reversed"] = (col, True)
+    col = col_sorted.clone()  # shuffled rows
+    for i in (0, 95, 96, n - 1):
+        r = row(col, i)
+        col[r] = col[r][torch.randperm(r.stop - r.start, generator=g)]
+    cases["shuffled"] = (col, True)
+    col = col_sorted.clone()  # the last entry (pass 3) moved to the row's front: re-streamed in pass 2
+    r = row(col, 1234)
+    col[r] = torch.cat([col[r][-1:], col[r][:-1]])
+    cases["last_first"] = (col, True)
+    col = col_sorted.clone()  # an entry of the next pass moved to the front: spilled there exactly
+    r = row(col, 4321)
+    k = int((col[r] >= 3072).nonzero()[0])  # the row's first entry of pass 2
+    col[r] = torch.cat([col[r][k:k + 1], col[r][:k], col[r][k + 1:]])
+    cases["next_pass_first"] = (col, False)
+    col = col_sorted.clone()  # swaps of neighbours (within one lane's eight entries) all over
+    for i in range(0, n, 37):
+        r = row(col, i)
+        k = r.start + 3
+        col[k], col[k + 1] = col[k + 1].clone(), col[k].clone()
+    cases["neighbour_swaps"] = (col, None)
+    col = col_sorted.clone()  # a column past n
+    col[int(rp[4000 + 1]) - 1] = n + 5
+    cases["past_n"] = (col, True)
+    for name, (c, must_flag) in cases.items():
+        word, y = run(c)
+        assert word in (0, nat.DEVERR_CSR_COLUMNS), (name, word)
+        if must_flag is not None:
+            assert word == (nat.DEVERR_CSR_COLUMNS if must_flag else 0), name
+        if word == 0:
+            assert torch.equal(y, y_sorted), name
+    # the drop-in wrapper raises on the flag
+    graph = ops.CsrGraph(n, rpd, cases["past_n"][0].to(device), sd, (rpd[1:] - rpd[:-1]).int())
+    with pytest.raises(nat.DeviceError, match="lds_spmm_norm_dense"):
+        graph.spmm(zd)
 
 
 @pytest.mark.parametrize("grid", [0, 63])
 def test_spmm_dense_spill_pass_row_shapes(device, grid):
-    """The spill-pass kernel (the product at grid >= 0, and its variants:
-    lds_spmm_dense_ablation dbg 23 / 33 / 34 with 1-KB steps and ring depths
-    8 / 6 / 12, 52 / 54 / 55 with 12 streaming waves, 61 the register ring
-    without the cached pass constants, 63 rows taken from a counter (its wait
-    steps and their barriers), 65 / 66 the lean forms; ascending columns) on rows
-    that take each of its paths, against the row-block kernel (dbg 6, any
-    column order; identical bits: exact integer sums) and fp64: rows whose entries crowd the first columns (the
-    stream stops at the predicted pass end before the pass boundary and the
-    row is finished with blocking loads), rows crowding the last columns
-    (every step of the early passes lies past pass p + 1: re-read later),
-    sparse rows whose steps span several passes, empty rows, full rows, and a
-    last row that ends the array off a 16-byte boundary.  grid 63 gives 96-row
-    blocks and three passes at n = 6000."""
+    """The spill-pass kernel (the product at grid >= 0; ascending columns) on
+    rows that take each of its paths, against the tile kernel (grid < 0, any
+    column order; identical bits: exact integer sums) and fp64: rows whose
+    entries crowd the first columns (the stream stops at the predicted pass
+    end before the pass boundary and the row is finished with blocking
+    loads), rows crowding the last columns (every step of the early passes
+    lies past pass p + 1: re-read later), sparse rows whose steps span
+    several passes, empty rows, full rows, and a last row that ends the array
+    off a 16-byte boundary; no error on these canonical rows.  grid 63 gives
+    96-row blocks and two passes of six chunks at n = 6000.  (The round-4 variants of the
+    kernel: tests/test_spmm_variants_gpu.py.)"""
     n = 6000
     g = torch.Generator().manual_seed(11)
     dens = torch.rand(n, generator=g) * 0.6
@@ -949,29 +1015,17 @@ def test_spmm_dense_spill_pass_row_shapes(device, grid):
     a[n - 1, 5] = True
     a[n - 1, 7] = True
     a[n - 1, 5999] = True           # nnz off a multiple of four (checked below)
-    rows, cols = a.nonzero(as_tuple=True)
-    rp = torch.zeros(n + 1, dtype=torch.int64)
-    rp[1:] = torch.cumsum(a.sum(1), 0)
+    rp, col = _csr_of_dense(a)
     if int(rp[-1]) % 4 == 0:
         a[n - 2, 3] = not bool(a[n - 2, 3])
-        rows, cols = a.nonzero(as_tuple=True)
-        rp[1:] = torch.cumsum(a.sum(1), 0)
+        rp, col = _csr_of_dense(a)
     assert int(rp[-1]) % 4 != 0
-    col = cols.int()
     s = torch.rand(n, generator=g) + 0.5
     z = torch.randn(n, 16, generator=g)
     rpd, cold, sd, zd = rp.int().to(device), col.to(device), s.to(device), z.to(device)
     y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid)  # the product (spill-pass kernel)
-    ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=device)
-    y0 = torch.empty(n, 16, device=device)
-    nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16, nat.ptr(y0), 16, 0,
-             nat.ptr(ws), grid, 1, nat.stream_of(device))
-    for dbg in (23, 33, 34, 52, 54, 55, 61, 63, 65, 66, 6):  # spill-pass variants, the hybrid row-block
-        yv = torch.empty(n, 16, device=device)
-        nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(sd), n, nat.ptr(zd), 16,
-                 nat.ptr(yv), 16, nat.ptr(ws), dbg, nat.stream_of(device))
-        torch.cuda.synchronize()
-        assert torch.equal(y.cpu(), yv.cpu()), dbg
+    y_tile = _spmm_dense(rpd, cold, sd, n, zd, grid=-256)
+    assert torch.equal(y.cpu(), y_tile.cpu())
     ad = a.double()
     ref = s.double()[:, None] * (ad @ (s.double()[:, None] * z.double()))
     scale = (ad @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()

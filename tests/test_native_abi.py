@@ -113,3 +113,84 @@ def test_struct_layouts_match_the_header(tmp_path):
         assert got[(st.__name__, "size")] == ctypes.sizeof(st), st.__name__
         for f, _ in st._fields_:
             assert got[(st.__name__, f)] == getattr(st, f).offset, (st.__name__, f)
+
+
+def _exported_lds_symbols(path):
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return sorted({line.split()[-1] for line in out.splitlines() if line.split() and line.split()[-1].startswith("lds_")})
+
+
+def test_library_exports_only_declared_entry_points():
+    """libldsgnn.so exports exactly the header's entry points (plus
+    lds_error_string): no ablation or variant entry point that returns wrong
+    results ships in the product library (those live in the tools-only
+    tools/variants/libldsgnn_variants.so)."""
+    import ldsgnn._native as nat
+    exported = set(_exported_lds_symbols(nat.LIB_PATH))
+    assert exported == set(declared_symbols()) | {"lds_error_string"}, \
+        sorted(exported ^ (set(declared_symbols()) | {"lds_error_string"}))
+    assert "lds_spmm_dense_ablation" not in exported
+
+
+def test_variants_library_is_tools_only():
+    """The variants library (built by __graft_entry__.build() for the
+    ablation tools) exports its two tools entry points and nothing of the
+    product's API."""
+    import pytest
+    path = os.path.join(ROOT, "tools", "variants", "libldsgnn_variants.so")
+    if not os.path.exists(path):
+        pytest.skip("tools/variants not built")
+    assert _exported_lds_symbols(path) == ["lds_variants_spmm_dense", "lds_variants_ws_bytes"]
+
+
+def test_dense_spmm_requires_an_error_word():
+    """lds_spmm_norm_dense (ABI 14) rejects the spill-pass kernel (grid >= 0)
+    without a device error word before any launch."""
+    import ldsgnn._native as nat
+    fake = 1 << 20  # never dereferenced: the argument checks run first
+    assert nat.lib.lds_spmm_norm_dense(fake, fake, fake, 100, fake, 16, fake, 16, 0, fake, 0, 1, None, None) == 1
+
+
+def _kernel_metadata(lib_path, tmp_path):
+    """{kernel symbol: (private segment bytes, VGPR spills)} of every gfx950
+    code object in a built library (llvm-objdump --offloading + the
+    code-object notes)."""
+    import glob
+    import shutil
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        import pytest
+        pytest.skip("no llvm-readelf")
+    lib = tmp_path / os.path.basename(lib_path)
+    shutil.copy(lib_path, lib)
+    subprocess.run([os.path.join(llvm, "llvm-objdump"), "--offloading", str(lib)], check=True, capture_output=True,
+                   cwd=tmp_path)
+    meta = {}
+    for co in glob.glob(str(lib) + ".*gfx950"):
+        notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
+                               text=True).stdout
+        for entry in notes.split("\n  - ")[1:]:
+            kv = dict(re.findall(r"^\s+\.([a-z_]+):\s+(\S+)$", entry, flags=re.M))
+            if "name" in kv and "private_segment_fixed_size" in kv:
+                meta[kv["name"]] = (int(kv["private_segment_fixed_size"]), int(kv.get("vgpr_spill_count", 0)))
+    return meta
+
+
+def test_register_ring_kernels_have_no_scratch(tmp_path):
+    """The spill-pass CSR-SpMM loads its column ring from inline asm
+    (global_load_dwordx4 + counted s_waitcnt + a binding asm): if the compiler
+    ever spilled or copied a ring register between the load and the wait, the
+    kernel would read stale columns silently.  So every instantiation must
+    compile without scratch (private segment 0, no VGPR spills); a compiler
+    or flag change that adds spills fails here, at build time, instead of
+    giving wrong sums."""
+    import ldsgnn._native as nat
+    meta = _kernel_metadata(nat.LIB_PATH, tmp_path)
+    ring = {k: v for k, v in meta.items() if "csr_spill_agg_kernel" in k}
+    assert len(ring) == 3, sorted(ring)
+    for k, (private, spills) in ring.items():
+        assert private == 0 and spills == 0, (k, private, spills)

@@ -13,6 +13,9 @@ import torch  # noqa: E402
 import ldsgnn  # noqa: E402,F401
 from ldsgnn import _native as nat  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "tools", "variants"))
+import variants  # noqa: E402  (the tools-only variants library)
+
 
 def run(n, dens, grid, seed):
     dev = torch.device("cuda:0")
@@ -26,15 +29,16 @@ def run(n, dens, grid, seed):
     z = torch.zeros(n, 16)
     z[torch.arange(n), torch.arange(n) % 16] = 1.0
     z = z.to(dev)
-    ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=dev)
+    ws = torch.empty(variants.ws_bytes(n), dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
     y = {}
     for name, dbg in (("rowblock", 22), ("spill", 23), ("spill_d6", 33), ("spill_d12", 34), ("spill_vm0", 35), ("rowblock_hybrid", 6), ("spill_quad", 36), ("spill_win", 37), ("spill_win_d6", 38), ("spill_ahead", 39), ("spill_rolled", 41), ("spill_rolled_d12", 42), ("spill_ns12_d5", 43), ("spill_ns12_d6", 44), ("ns12_d4", 45), ("ns12_d5_win", 46), ("ns12_d3", 47), ("ns14_d4", 48), ("ns14_d3", 49), ("ns12_d4_fq", 50), ("ns14_d4_fq", 51), ("ns12_d4_fs", 52), ("ns12_d3_fs", 53), ("e8_d3", 54), ("e8_d2", 55), ("e8_d2_ns8", 56), ("e8_d2_ns14", 57), ("reg3", 60), ("reg4", 61), ("reg6", 62), ("reg4_dyn", 63), ("reg4_cache", 64), ("reg4_lean", 65), ("reg4_ballot", 66), ("reg4_ns14", 67), ("e12_d3", 68), ("e12_d4", 69)):
         out = torch.empty(n, 16, device=dev)
         if dbg == 22:
             nat.call("lds_spmm_norm_dense", nat.ptr(rpd), nat.ptr(cold), nat.ptr(s), n, nat.ptr(z), 16, nat.ptr(out),
-                     16, 0, nat.ptr(ws), -256, 1, nat.stream_of(dev))
-        nat.call("lds_spmm_dense_ablation", nat.ptr(rpd), nat.ptr(cold), nat.ptr(s), n, nat.ptr(z), 16, nat.ptr(out),
-                 16, nat.ptr(ws), dbg, nat.stream_of(dev))
+                     16, 0, nat.ptr(ws), -256, 1, nat.ptr(err), nat.stream_of(dev))
+        variants.spmm_dense(nat.ptr(rpd), nat.ptr(cold), nat.ptr(s), n, nat.ptr(z), 16, nat.ptr(out),
+                            16, nat.ptr(ws), dbg, nat.stream_of(dev))
         torch.cuda.synchronize()
         y[name] = out.cpu().round().long()
     ref = torch.zeros(n, 16, dtype=torch.long)

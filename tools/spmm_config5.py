@@ -17,6 +17,9 @@ import ldsgnn  # noqa: E402
 from ldsgnn import _native as nat  # noqa: E402
 from ldsgnn.rng import TAG_GRAPH, tag_for  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "tools", "variants"))
+import variants  # noqa: E402  (the tools-only variants library)
+
 HBM_PEAK_GBS = 8000.0
 
 
@@ -79,11 +82,12 @@ def main(n=20000, f=16, reps=20, high=1.0):
                  nat.ptr(ws), st)
 
     y_dn = torch.empty((n, f), device=dev)
-    ws_dn = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(n)), dtype=torch.uint8, device=dev)
+    ws_dn = torch.empty(variants.ws_bytes(n), dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def dense(quantize=1, grid=0):
         nat.call("lds_spmm_norm_dense", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_dn), f, 0,
-                 nat.ptr(ws_dn), grid, quantize, st)
+                 nat.ptr(ws_dn), grid, quantize, nat.ptr(err), st)
 
     t_bp = time_it(lambda: nat.call("lds_csr_block_ptr", nat.ptr(rp), nat.ptr(col), n, nat.ptr(bptr), st), 3)
     t_row = time_it(row, reps)
@@ -95,8 +99,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
     y_abl0 = torch.empty_like(y_dn)
     eq_variants = {}
     for dbg in (20, 21, 22, 23, 33, 34, 6, 36, 37, 38, 39, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69):  # the product variants give the same bits
-        nat.call("lds_spmm_dense_ablation", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_abl0), f,
-                 nat.ptr(ws_dn), dbg, st)
+        variants.spmm_dense(nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_abl0), f,
+                            nat.ptr(ws_dn), dbg, st)
         eq_variants[dbg] = bool(torch.equal(y_abl0, y_main))
     y_tile = y_dn.clone()
     t_dn_main = time_it(lambda: dense(0), reps)
@@ -145,8 +149,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
                       (1, "row-block: streaming phase alone"), (2, "row-block: streaming without bit-row stores"),
                       (3, "row-block: multiply phase alone"), (4, "row-block: multiply without bit-row loads"),
                       (5, "row-block: streaming without stores + column-pass step bookkeeping")):
-        abl[what] = time_it(lambda: nat.call("lds_spmm_dense_ablation", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n,
-                                             nat.ptr(z), f, nat.ptr(y_abl), f, nat.ptr(ws_dn), dbg, st), reps)
+        abl[what] = time_it(lambda: variants.spmm_dense(nat.ptr(rp), nat.ptr(col), nat.ptr(s), n,
+                                                        nat.ptr(z), f, nat.ptr(y_abl), f, nat.ptr(ws_dn), dbg, st), reps)
     dense(0)  # the product again (the multiply-only ablation left its slabs in place)
     # parity: blocked vs row kernel (fp32, different order) and fp64 on sampled rows
     rel = float((y_blk - y_row).abs().max() / y_row.abs().max())
@@ -178,7 +182,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
                                 "tile_kernel_frac_product": algo / t_tile / 1e3 / HBM_PEAK_GBS,
                                 "equal_to_tile_kernel": bool(torch.equal(y_main, y_tile)),
                                 "ablations_us": abl, "variants_equal": eq_variants,
-                                "equal_to_bitmask": bool(torch.equal(y_dn, y_bit))},
+                                "equal_to_bitmask": bool(torch.equal(y_dn, y_bit)),
+                                "error_word": int(err.item())},
            "max_rel_blocked_vs_row": rel, "max_rel_vs_fp64_rows": err64,
            "max_rel_bitmask_vs_row": float((y_bit - y_row).abs().max() / y_row.abs().max()),
            "max_rel_bitmask_vs_fp64_rows": err64_bit}
