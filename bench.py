@@ -662,6 +662,10 @@ def main():
                          "noop = the N > 1 per-rank path with a no-op reducer (split graphs), noop-captured = "
                          "the same reducer captured into the window graph, rccl1 = a world-size-1 nccl (RCCL) "
                          "group and its real all-reduce captured into the window graph (DESIGN §5b)")
+    ap.add_argument("--keep-theta-grad", type=int, default=1, choices=[0, 1],
+                    help="engine, N = 1: 1 writes dθ to θ.grad beside the fused SGD update (the drop-in "
+                         "trainer's state after its backward); 0 consumes it in the update's registers only "
+                         "(θ.grad left None) — the same θ bit for bit")
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-launch window breakdown leg")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
@@ -748,6 +752,9 @@ def main():
             exchange_label = f"{args.backend}-allreduce-" + ("captured" if capture_exchange else "split")
         args.capture_exchange = capture_exchange  # (the strong-scaling leg's TN captures the same way)
         eng.async_draw = bool(args.async_draw)
+        if not args.keep_theta_grad:  # θ.grad not materialised (the fused update consumes dθ)
+            eng.keep_grad = False
+            runner.outer_trainer.model.probs.grad = None
         if args.xt_pair:
             eng.set_xt_pair(args.xt_pair)
         # step 0 is its own window (hyper step at step 0, src/trainers/bilevel.py:70-71)
@@ -862,6 +869,7 @@ def main():
                        "windows_per_graph": (args.graph_windows if whole else 1)
                        if use_engine and use_graph else None,
                        "prefetched_draw": prefetched, "async_draw": bool(args.async_draw),
+                       "theta_grad_written": bool(args.keep_theta_grad) if use_engine else True,
                        "xt_pair": args.xt_pair, "exchange": exchange_label if use_engine else None},
             "steady_state": steady,
             "strong_scaling": strong,

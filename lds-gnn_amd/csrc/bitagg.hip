@@ -647,7 +647,11 @@ __device__ __forceinline__ uint32_t sp_offsets(const int (&c)[kSpE], int base, u
     return o;
 }
 
-template <int kTiles>
+// kCheck (err != NULL): the windowed paths test every column and the error
+// word is set as described above; without it (the caller guarantees
+// ascending columns in [0, n), as for every CSR this library builds) they test
+// a lane's first and last column only, as the round-4 product did.
+template <int kTiles, bool kCheck>
 __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
     int chunks, int cpp, int passes, int rowdw, const uint32_t* __restrict__ colmax, const float* __restrict__ s,
@@ -801,9 +805,13 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                 const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
                 const int base_ = lo_ + (int)(w0_ << 5);                                                     \
                 uint32_t r_[kSpE];                                                                           \
-                const uint32_t o_ = sp_offsets(c_, base_, r_);                                               \
-                /* all eight in [base, base + 64) and below the pass end */                                 \
-                fast_ = c_[0] >= lo_ && o_ < 64u && base_ + (int)o_ < hi_;                                   \
+                if constexpr (kCheck) { /* all eight in [base, base + 64) and below the pass end */         \
+                    const uint32_t o_ = sp_offsets(c_, base_, r_);                                           \
+                    fast_ = c_[0] >= lo_ && o_ < 64u && base_ + (int)o_ < hi_;                               \
+                } else { /* ascending: the first and the last bound the lane */                              \
+                    _Pragma("unroll") for (int e = 0; e < kSpE; ++e) r_[e] = (uint32_t)(c_[e] - base_);      \
+                    fast_ = c_[0] >= lo_ && c_[kSpE - 1] < hi_ && r_[kSpE - 1] < 64u;                        \
+                }                                                                                            \
                 if (fast_) {                                                                                 \
                     uint64_t m_ = 0;                                                                         \
                     _Pragma("unroll") for (int e = 0; e < kSpE; ++e) m_ |= 1ull << r_[e];                    \
@@ -818,8 +826,15 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     const uint32_t q0_ = (uint32_t)(c_[0] - hi_) >> 5;                                       \
                     const int qbase_ = hi_ + (int)(q0_ << 5);                                                \
                     uint32_t rq_[kSpE];                                                                      \
-                    const uint32_t oq_ = sp_offsets(c_, qbase_, rq_);                                        \
-                    if (c_[0] >= hi_ && oq_ < 64u && qbase_ + (int)oq_ < hq_) {                              \
+                    bool pq_;                                                                                \
+                    if constexpr (kCheck) {                                                                  \
+                        const uint32_t oq_ = sp_offsets(c_, qbase_, rq_);                                    \
+                        pq_ = c_[0] >= hi_ && oq_ < 64u && qbase_ + (int)oq_ < hq_;                          \
+                    } else {                                                                                 \
+                        _Pragma("unroll") for (int e = 0; e < kSpE; ++e) rq_[e] = (uint32_t)(c_[e] - qbase_); \
+                        pq_ = c_[0] >= hi_ && c_[kSpE - 1] < hq_ && rq_[kSpE - 1] < 64u;                     \
+                    }                                                                                        \
+                    if (pq_) {                                                                               \
                         uint64_t m_ = 0;                                                                     \
                         _Pragma("unroll") for (int e = 0; e < kSpE; ++e) m_ |= 1ull << rq_[e];               \
                         dn_or(bq_ + q0_, (uint32_t)m_);                                                      \
@@ -924,7 +939,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_s_barrier();
         }
-        if (__ballot(bad) != 0ull && lane == 0) atomicOr(err, kDevErrCsrColumns);
+        if constexpr (kCheck)
+            if (__ballot(bad) != 0ull && lane == 0) atomicOr(err, kDevErrCsrColumns);
     } else {
         // ---- multiply waves --------------------------------------------------
         // wave 12 + m: limb m, both k-halves of every chunk of the pass
@@ -1094,7 +1110,6 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
     LDS_CHECK_ARG(row_ptr && col && s && z && y && ws && n > 0 && n <= kDnMaxChunks * kChunk);
     LDS_CHECK_ARG(ldz >= kF && ldy >= kF);
     LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
-    LDS_CHECK_ARG(grid < 0 || err != nullptr);
     hipStream_t st = (hipStream_t)stream;
     const Ws w = carve(ws, n);
     const int nc = chunks_of(n);
@@ -1127,18 +1142,26 @@ extern "C" int lds_spmm_norm_dense(const int* row_ptr, const int* col, const flo
     const SpGeom sg = sp_geom(nc, tiles);
     const int lds = sp_lds_bytes(tiles, sg);
     LDS_CHECK_ARG(lds <= 163840 && sg.passes <= 255);  // (the pass is an 8-bit field of a ring record)
-#define LDS_SP_LAUNCH(TT)                                                                                      \
+#define LDS_SP_LAUNCH1(TT, CK)                                                                                 \
     do {                                                                                                       \
-        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT>, lds);                                        \
+        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, CK>, lds);                                    \
         if (e != hipSuccess) return (int)e;                                                                    \
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT>), dim3(g), dim3(kSpThreads), lds, st, row_ptr, \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, CK>), dim3(g), dim3(kSpThreads), lds, st, row_ptr, \
                            col, n, R, (const int8_t*)w.zq, nc, sg.cpp, sg.passes, sg.rowdw,                    \
                            (const uint32_t*)w.colmax, s, y, ldy, beta, err);                                   \
     } while (0)
     // (5 tiles run the 6-tile build: 170-171 µs at config 5 against 175-178 for a 5-tile build of the same code)
+#define LDS_SP_LAUNCH(TT)                    \
+    do {                                     \
+        if (err != nullptr)                  \
+            LDS_SP_LAUNCH1(TT, true);        \
+        else                                 \
+            LDS_SP_LAUNCH1(TT, false);       \
+    } while (0)
     if (tiles <= 2) LDS_SP_LAUNCH(2);
     else if (tiles <= 4) LDS_SP_LAUNCH(4);
     else LDS_SP_LAUNCH(6);
 #undef LDS_SP_LAUNCH
+#undef LDS_SP_LAUNCH1
     LDS_RETURN_LAST_ERROR();
 }

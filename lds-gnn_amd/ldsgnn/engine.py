@@ -673,7 +673,8 @@ class LdsEngine:
             return nat.ptr(self.agg_ws) + self.agg_part_off
         if self.dense_agg:
             nat.call("lds_spmm_norm_dense", nat.ptr(g.row_ptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z),
-                     HID, nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), 0, 1, self._err_ptr(), self._stream())
+                     HID, nat.ptr(self.agg), HID, 0, nat.ptr(self.agg_ws), 0, 1, 0, self._stream())  # (the
+            # engine's own fill: canonical columns, the unchecked form)
             return nat.ptr(self.agg)
         nat.call("lds_spmm_norm_blocked", nat.ptr(g.bptr), nat.ptr(g.col), nat.ptr(g.s), self.n, nat.ptr(z), HID,
                  nat.ptr(self.agg), HID, 0, nat.ptr(self.spmm_part), self._stream())

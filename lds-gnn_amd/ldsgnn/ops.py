@@ -59,6 +59,10 @@ class CsrGraph:
     uint64 stored as int64) — the layouts of include/ldsgnn.h.
     """
 
+    # columns ascending and distinct in [0, n) by construction (set by the
+    # library's own samplers / fills; a caller-built CSR is checked)
+    canonical_columns = False
+
     def __init__(self, n: int, row_ptr: torch.Tensor, col: torch.Tensor, s: torch.Tensor,
                  deg: torch.Tensor, bits: Optional[torch.Tensor] = None):
         self.n = n
@@ -133,12 +137,16 @@ class CsrGraph:
                 ws = torch.empty(int(nat.lib.lds_spmm_dense_ws_bytes(self.n)), dtype=torch.uint8, device=z.device)
                 self._dense_ws = ws
                 self._dense_err = torch.zeros(1, dtype=torch.int32, device=z.device)
+            # a graph this library sampled has canonical columns (the unchecked
+            # form); any other CSR runs the checked form, which flags a column
+            # order it cannot aggregate faithfully (a property of the CSR:
+            # read on the graph's first call, one sync)
+            checked = not self.canonical_columns
             nat.call("lds_spmm_norm_dense", nat.ptr(self.row_ptr), nat.ptr(self.col), nat.ptr(self.s), self.n,
                      nat.ptr(z), z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(ws), 0, 1,
-                     nat.ptr(self._dense_err), _stream(z))
-            # the kernel flags a column order it cannot aggregate faithfully (a
-            # property of this CSR: checked on the graph's first call, one sync)
-            if not getattr(self, "_dense_checked", False) and not torch.cuda.is_current_stream_capturing():
+                     nat.ptr(self._dense_err) if checked else 0, _stream(z))
+            if checked and not getattr(self, "_dense_checked", False) and \
+                    not torch.cuda.is_current_stream_capturing():
                 word = int(self._dense_err.item())
                 if word:
                     self._dense_err.zero_()
@@ -204,6 +212,8 @@ class _TokenChunk:
 
 class SampledGraph(CsrGraph):
     """A graph drawn from θ.  Gradients flow to θ through the token chunks."""
+
+    canonical_columns = True  # the sampler's fill writes each row's columns ascending
 
     def __init__(self, n, row_ptr, col, s, deg, bits, theta: Optional[torch.Tensor]):
         super().__init__(n, row_ptr, col, s, deg, bits)

@@ -203,3 +203,46 @@ def test_spmm_dense_n20000_vs_bitmask_csr_and_fp64_rows(device, dense_graph):
     colscale = (y_csr.abs().max(0).values.double() + 1e-30)
     assert float(((y.double() - y_csr.double()).abs().max(0).values / colscale).max()) < TOL
     assert float(((y.double() - y_bit.double()).abs().max(0).values / colscale).max()) < TOL
+
+
+@pytest.mark.parametrize("kernel", ["bitmask", "csr"])
+def test_long_row_outer_only_n20000_at_north_star_tolerance(device, kernel):
+    """Config 5 at full size, the long-row kernels' θ-gradient at the
+    north-star 1e-5 × max|dθ| (the well-conditioned construction of the
+    config-2 golden hypergrad_cora_wellcond): dropout-free, a hyper step whose
+    window has no inner step (every aggregation of the outer graph's forward
+    and backward on the long-row kernel: the bitmask aggregation or the CSR
+    spill-pass SpMM), against the short-row engine (in-kernel CSR
+    aggregation) from the same state, on every 997th entry of dθ; θ after it
+    within 1e-5."""
+    from ldsgnn.data.workloads import load_workload
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.rng import Generator as Gen
+    from ldsgnn.utils.graph import get_triu_values
+    from oracle import lds_oracle as O
+    data = load_workload("synthetic20k", seed=1, device=device)
+    theta0 = get_triu_values(data.dense_adj).contiguous()
+    del data.dense_adj
+    torch.cuda.empty_cache()
+    opt = data.val_mask.clone()
+    opt[torch.nonzero(opt).squeeze(1)[::2]] = False
+    res = []
+    for long_rows in (True, False):
+        torch.manual_seed(4)
+        params = {k: v.to(device) for k, v in O.init_params(data.num_features, 16, data.num_classes).items()}
+        eng = LdsEngine(data.x, data.y, data.train_mask, opt, theta0.clone(), data.num_classes, dropout=0.0,
+                        outer_lr=0.1, lr_decay=0.99, tau=2, generator=Gen(13, 0), params=params,
+                        long_rows=long_rows, long_rows_kernel=kernel)
+        assert eng.long_rows == long_rows
+        eng.hyper_step()  # θ₀'s outer graph only (no inner step in the window)
+        torch.cuda.synchronize()
+        res.append(dict(loss=eng.outer_metrics()[0], grad=eng.grad[::997].cpu(), theta=eng.theta[::997].cpu()))
+        del eng
+        torch.cuda.empty_cache()
+    a, b = res
+    assert abs(a["loss"] - b["loss"]) <= TOL * abs(b["loss"])
+    gs = float(b["grad"].abs().max())
+    err = float((a["grad"] - b["grad"]).abs().max())
+    print(f"config 5 [{kernel}] outer-only dθ error / max|dθ|: {err / gs:.2e}")
+    assert err <= 1e-5 * gs, (kernel, err / gs)
+    assert torch.allclose(a["theta"], b["theta"], rtol=TOL, atol=1e-6)

@@ -764,3 +764,64 @@ def test_xt_adam_sample_pairs_bit_identical():
                                       seed=7, replica0=2)["engine"]
     with pytest.raises(ValueError):
         c.set_xt_pair(2)
+
+
+def test_keep_grad_off_gives_the_same_theta():
+    """keep_grad = False (bench.py --keep-theta-grad 0): the fused update
+    consumes dθ without writing θ.grad; θ, weights and scalars stay
+    bit-identical to the engine that writes it, in captured four-window
+    groups with prefetched draws (the bench's configuration)."""
+    a = run_engine_and_oracle(n=300, f_in=40, classes=5, steps=1, tau=5, dropout=0.5, seed=21)["engine"]
+    b = run_engine_and_oracle(n=300, f_in=40, classes=5, steps=1, tau=5, dropout=0.5, seed=21)["engine"]
+    b.keep_grad = False
+    b.grad.fill_(7.0)
+    for e in (a, b):
+        e.capture_window(5, windows=4, prefetch=True)
+        e.replay(9)
+    torch.cuda.synchronize()
+    assert torch.equal(a.theta, b.theta)
+    assert bool((b.grad == 7.0).all())  # never written
+    assert not torch.equal(a.grad, b.grad)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+    assert a.scalars_host() == b.scalars_host()
+
+
+@pytest.mark.parametrize("kernel", ["bitmask", "csr", "blocked"])
+def test_engine_long_rows_wellconditioned_at_north_star_tolerance(kernel):
+    """The long-row aggregation kernels' θ-gradient at the north-star 1e-5,
+    separated from the conditioning of Adam windows (the construction of the
+    config-2 golden hypergrad_cora_wellcond): dropout-free, dense θ ~ U(0, 1)
+    on 300 nodes, against the oracle.  (1) A hyper step whose window has no
+    inner step — NLL on the opt mask through one sampled outer graph, with
+    every aggregation of its forward and backward on the long-row kernel —
+    has no Adam step between θ and the loss: every entry of dθ within 1e-5 ×
+    max|dθ|.  (2) A whole dropout-free τ = 5 window: dθ within 1e-5 in L2
+    (‖Δ‖₂ / ‖dθ‖₂), its max entry reported.  θ after each step within 1e-5."""
+    res = run_engine_and_oracle(n=300, f_in=32, classes=5, steps=1, tau=5, dropout=0.0, seed=4,
+                                theta_uniform=1.0, long_rows=True, long_rows_kernel=kernel)
+    eng, oracle = res["engine"], res["oracle"]
+    assert eng.long_rows and eng.dense_agg == (kernel == "csr") and eng.bitmask_agg == (kernel == "bitmask")
+
+    def grad_errs():
+        og = oracle.hyper_step()[2]
+        eg = eng.grad.detach().cpu()
+        mx = float(og.abs().max())
+        return (float((eg - og).abs().max()) / mx, float((eg - og).norm() / og.norm()),
+                float((eng.theta.cpu() - oracle.theta.detach()).abs().max()))
+
+    eng.hyper_step()  # a window with no inner step: the outer graph's path only
+    torch.cuda.synchronize()
+    outer_max, outer_l2, th = grad_errs()
+    assert outer_max <= 1e-5, (kernel, outer_max, outer_l2)
+    assert th < TOL
+    for _ in range(5):
+        eng.inner_step()
+        oracle.inner_step(oracle.sample())
+    eng.hyper_step()
+    torch.cuda.synchronize()
+    win_max, win_l2, th = grad_errs()
+    print(f"long rows [{kernel}] dθ error / max|dθ|: outer-only {outer_max:.2e}, window {win_max:.2e} "
+          f"(L2 {win_l2:.2e})")
+    assert win_l2 <= 1e-5, (kernel, win_max, win_l2)
+    assert th < TOL

@@ -809,15 +809,16 @@ def test_theta_grad_direct_draw_equals_sgd_draw(device, n, k, graphs):
             assert torch.equal(a, b)
 
 
-def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, grid=0, expect_err=0):
-    """lds_spmm_norm_dense into `out` (or a new n × 16); the device error word
-    must read `expect_err` afterwards."""
+def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, grid=0, expect_err=0, checked=True):
+    """lds_spmm_norm_dense into `out` (or a new n × 16); the checked form
+    (an error word) must read `expect_err` afterwards; checked=False runs the
+    unchecked form (err = NULL: canonical columns promised)."""
     dev = z.device
     ws = torch.full((int(nat.lib.lds_spmm_dense_ws_bytes(n)),), 0x5A, dtype=torch.uint8, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     y = out if out is not None else torch.empty(n, ldy, device=dev)
     nat.call("lds_spmm_norm_dense", nat.ptr(graph_rp), nat.ptr(graph_col), nat.ptr(s), n, nat.ptr(z), ldz,
-             nat.ptr(y), ldy, beta, nat.ptr(ws), grid, 1, nat.ptr(err), nat.stream_of(dev))
+             nat.ptr(y), ldy, beta, nat.ptr(ws), grid, 1, nat.ptr(err) if checked else 0, nat.stream_of(dev))
     torch.cuda.synchronize()
     assert int(err.item()) == expect_err, (int(err.item()), expect_err)
     return y
@@ -855,6 +856,8 @@ def test_spmm_dense_csr_vs_bitmask_and_fp64(device, n, high, grid):
     y = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=grid).cpu().double()
     y_other = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=0 if grid < 0 else -256).cpu().double()
     assert torch.equal(y, y_other)
+    y_unchecked = _spmm_dense(graph.row_ptr, graph.col, graph.s, n, zd, grid=max(grid, 0), checked=False)
+    assert torch.equal(y_unchecked.cpu().double(), y if grid >= 0 else y_other)
     a = graph.normalized_dense().cpu().double()
     ref = a @ z.double()
     scale = (a.abs() @ z.double().abs()).max(0).values.clamp(min=1e-300)
@@ -1023,9 +1026,10 @@ def test_spmm_dense_spill_pass_row_shapes(device, grid):
     s = torch.rand(n, generator=g) + 0.5
     z = torch.randn(n, 16, generator=g)
     rpd, cold, sd, zd = rp.int().to(device), col.to(device), s.to(device), z.to(device)
-    y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid)  # the product (spill-pass kernel)
+    y = _spmm_dense(rpd, cold, sd, n, zd, grid=grid)  # the product (spill-pass kernel), checked
     y_tile = _spmm_dense(rpd, cold, sd, n, zd, grid=-256)
     assert torch.equal(y.cpu(), y_tile.cpu())
+    assert torch.equal(_spmm_dense(rpd, cold, sd, n, zd, grid=grid, checked=False).cpu(), y.cpu())  # unchecked
     ad = a.double()
     ref = s.double()[:, None] * (ad @ (s.double()[:, None] * z.double()))
     scale = (ad @ (s.double()[:, None] * z.double()).abs()).max(0).values * s.max()
