@@ -2030,19 +2030,24 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     xval = boff<kB>(xval, bt.xval);
     d = boff<kB>(d, bt.act);
     bkeys<kB>(keys, bt);
-    if (fin_args.partials != nullptr && blockIdx.x == gridDim.x - 1) {
+    // the final reduction is block 0: dispatched first, so its chain of
+    // partial-sum round trips overlaps the column blocks (as the last block it
+    // started after every other block of its sample had been dispatched)
+    const int fb = fin_args.partials != nullptr ? 1 : 0;
+    if (fb && blockIdx.x == 0) {
         final_block_1024<kB ? 16 : 64>(fin_args, adam, sc);
         return;
     }
+    const int bx = (int)blockIdx.x - fb;
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
-    const bool heavy = (int)blockIdx.x < n_heavy;
+    const bool heavy = bx < n_heavy;
     // with the column heads (xtinfo[slot] = {f, p0, nnz}, slot = position in
     // `order`) one load gives the column, its range and its first 64 rows;
     // without them: order[slot] -> xcp[f] -> entries, two dependent loads first
     int f, beg, end, slot;
     if (heavy) {
-        slot = blockIdx.x;
+        slot = bx;
         int cb, ce;
         if (xtinfo != nullptr) {
             const int4 inf = xtinfo[slot];
@@ -2058,7 +2063,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
         beg = min(ce, cb + wave * seg);
         end = min(ce, beg + seg);
     } else {
-        slot = n_heavy + ((int)blockIdx.x - n_heavy) * 16 + wave;
+        slot = n_heavy + (bx - n_heavy) * 16 + wave;
         if (slot >= fin) return;  // light blocks never reach a barrier
         if (xtinfo != nullptr) {
             const int4 inf = xtinfo[slot];
@@ -2136,7 +2141,7 @@ __device__ __forceinline__ void sample_views(FinalArgs& f, AdamArgs& a, const Ba
 // xt_adam_kernel<true> over pairs of samples (LdsBatch.xt_pair): grid.y =
 // samples / 2, a wave takes one column for samples 2y and 2y + 1
 // (x_wave_dot_head_pair: one index walk, the same sums), lanes 0-15 and 32-47
-// complete the two W0 entries' Adam; the last two blocks run the samples'
+// complete the two W0 entries' Adam; the first two blocks run the samples'
 // final reductions.  Light columns only (no heavy-column plan), column heads,
 // no split partials, train = 0 (the stored Xd).
 __global__ __launch_bounds__(1024) void xt_adam_pair_kernel(
@@ -2144,14 +2149,15 @@ __global__ __launch_bounds__(1024) void xt_adam_pair_kernel(
     const EngineScalars* __restrict__ sc, FinalArgs fin_args, AdamArgs adam, const int4* __restrict__ xtinfo,
     const int* __restrict__ xthead, Batch bt) {
     const int s0 = 2 * (int)blockIdx.y;
-    if (fin_args.partials != nullptr && (int)blockIdx.x >= (int)gridDim.x - 2) {
-        sample_views(fin_args, adam, bt, s0 + (int)blockIdx.x - ((int)gridDim.x - 2));
+    const int fb = fin_args.partials != nullptr ? 2 : 0;  // the two final blocks first (as xt_adam_kernel)
+    if ((int)blockIdx.x < fb) {
+        sample_views(fin_args, adam, bt, s0 + (int)blockIdx.x);
         final_block_1024<16>(fin_args, adam, sc);
         return;
     }
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
-    const int slot = (int)blockIdx.x * 16 + wave;
+    const int slot = ((int)blockIdx.x - fb) * 16 + wave;
     if (slot >= fin) return;  // light blocks never reach a barrier
     sample_views(fin_args, adam, bt, s0 + (lane >> 5));
     const int4 inf = xtinfo[slot];

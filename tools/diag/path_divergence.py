@@ -45,6 +45,9 @@ def build(dataset, seed, device):
     return data, inner, outer
 
 
+_last_graph = [None]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="citeseer")
@@ -55,34 +58,60 @@ def main():
     dev = torch.device("cuda:0")
     data, inner_d, outer_d = build(args.dataset, args.seed, dev)
     runner = BilevelProblemRunner(inner_d, outer_d, data)
-    gen_d = ldsgnn.rng.default_generator
+    orig_sample = outer_d.sample
+
+    def sample_and_keep():
+        g = orig_sample()
+        _last_graph[0] = g
+        return g
+    outer_d.sample = sample_and_keep
+    # the drop-in path keeps a private copy of the generator state after its
+    # build; the second build reseeds the default generator for the engine
+    gen_d = ldsgnn.rng.Generator()
+    gen_d.set_state(ldsgnn.rng.default_generator.get_state())
+    inner_d.model.generator = gen_d
+    outer_d.model.generator = gen_d
     _, inner_e, outer_e = build(args.dataset, args.seed, dev)
     eng = engine_from_trainers(inner_e, outer_e, tau=args.tau, generator=ldsgnn.rng.default_generator)
-    # the two builds each reseeded the default generator; the drop-in trainers
-    # keep theirs through the model's generator attribute where they have one
     out = {"dataset": args.dataset, "seed": args.seed, "tau": args.tau, "steps": args.steps,
            "theta0_equal": bool(torch.equal(outer_d.model.probs.data, eng.theta))}
-    first_draw_diff, hyper = None, []
+    hyper, loss_diff, graph_diffs = [], [], []
     n = data.num_nodes
     for step in range(args.steps):
-        runner.outer_trainer.train()
-        g = runner.outer_trainer.sample()
-        md = runner.inner_trainer.train_step(g)
+        md = runner.inner_opt_step()
         t = eng.t
         eng.inner_step()
-        nnz_e = int(eng.slots[t].g.row_ptr[0, n].item())
-        if first_draw_diff is None and g.nnz() != nnz_e:
-            first_draw_diff = {"step": step, "nnz_dropin": g.nnz(), "nnz_engine": nnz_e}
+        eng._flush_fill()
+        if len(graph_diffs) < 8:
+            ge = eng.slots[t].g
+            nnz_e = int(ge.row_ptr[0, n].item())
+            g = _last_graph[0]
+            if g is not None:
+                same = g.nnz() == nnz_e and torch.equal(g.row_ptr.int(), ge.row_ptr[0].int()) and \
+                    torch.equal(g.col[:nnz_e].int(), ge.col[0, :nnz_e].int())
+                if not same:
+                    graph_diffs.append({"step": step, "nnz_dropin": g.nnz(), "nnz_engine": nnz_e})
+        le = eng.inner_metrics(t)[0]
+        loss_diff.append(abs(float(md.loss) - le) / max(abs(le), 1e-30))
         if step % args.tau == 0:
-            runner.hyper_opt_step(step)
+            mo = runner.hyper_opt_step(step)
             eng.hyper_step()
-            le = eng.inner_metrics(t)[0]
+            lo = eng.outer_metrics()[0]
             dth = float((outer_d.model.probs.data - eng.theta).abs().max())
-            hyper.append({"step": step, "max_dtheta": dth, "inner_loss_diff": abs(float(md.loss) - le)})
-    out["first_draw_difference"] = first_draw_diff
+            hyper.append({"step": step, "max_dtheta": dth, "inner_loss_rel_diff": loss_diff[-1],
+                          "outer_loss_rel_diff": abs(float(mo.loss) - lo) / max(abs(lo), 1e-30)})
+        if step % 200 == 0:
+            print(f"step {step}", file=sys.stderr, flush=True)
+    out["graph_differences"] = graph_diffs
+    for thr in (1e-6, 1e-4, 1e-2):
+        out[f"first_step_inner_loss_rel_diff_above_{thr:g}"] = next(
+            (i for i, d in enumerate(loss_diff) if d > thr), None)
     for thr in (1e-6, 1e-5, 1e-4, 1e-3, 1e-2):
         hit = next((h["step"] for h in hyper if h["max_dtheta"] > thr), None)
         out[f"first_hyper_step_dtheta_above_{thr:g}"] = hit
+    if graph_diffs:
+        s0 = graph_diffs[0]["step"]
+        out["hyper_around_first_graph_difference"] = [h for h in hyper if s0 - 3 * args.tau <= h["step"] <= s0 + 3 * args.tau]
     out["hyper"] = hyper[:: max(1, len(hyper) // 40)]
     print(json.dumps(out))
 
