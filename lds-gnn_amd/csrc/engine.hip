@@ -171,19 +171,29 @@ __device__ __forceinline__ float agg_row(const int* __restrict__ rp, const int* 
 // ---------------------------------------------------------------------------
 // Row plan of the aggregating kernels (include/ldsgnn.h LdsBatch): the first
 // ceil(n / W) blocks give each row one wave (W waves per block); a row the
-// plan marks heavy is skipped there and runs on a block of its own appended
-// after them, its W waves taking the row's entries 64 at a time, W·64 apart,
-// their sums combined through LDS in wave order (every wave of the block ends
-// with the row's value; wave 0 stores).  On the kNN-initialised Cora θ₀ the 17
-// rows of more than 64 entries (up to 175) otherwise set every launch's time:
-// 4.3 -> 3.4 µs per aggregation launch (tools/microbench/aggbench.py).
+// plan marks heavy is skipped there and runs on a block of its own (logical
+// blocks ceil(n / W) …), its W waves taking the row's entries 64 at a time,
+// W·64 apart, their sums combined through LDS in wave order (every wave of the
+// block ends with the row's value; wave 0 stores).  On the kNN-initialised
+// Cora θ₀ the 17 rows of more than 64 entries (up to 175) otherwise set every
+// launch's time: 4.3 -> 3.4 µs per aggregation launch
+// (tools/microbench/aggbench.py).  The heavy blocks are the grid's FIRST
+// physical blocks (plan_block): dispatched first, their longer walks start
+// while the light blocks are still being dispatched.  Everything a block
+// writes is indexed by its logical number, so the order changes no result.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int plan_block(int nlight, int nh) {
+    const int p = (int)blockIdx.x;
+    return p < nh ? nlight + p : p - nh;
+}
+
 struct RowSel {
     int row;          // -1: no row for this wave
     int first, end;   // this wave's first CSR entry, the row's end
     int step;         // entry stride between this wave's steps
     bool heavy;       // a heavy-row block (all its waves share the row)
     bool lead;        // this wave stores the row's results
+    int blk;          // the logical block (plan_block)
     int2 e;           // light rows: this lane's ELL head entry {j, s_j}
 };
 
@@ -196,13 +206,15 @@ __device__ __forceinline__ RowSel select_row(int n, const int* __restrict__ rp, 
     r.e = make_int2(0, 0);
     const int wave = wave_id();
     const int nlight = (n + W - 1) / W;
-    r.heavy = (int)blockIdx.x >= nlight;
+    const int blk = plan_block(nlight, bt.nh);
+    r.blk = blk;
+    r.heavy = blk >= nlight;
     r.step = r.heavy ? 64 * W : 64;
     int row;
     if (r.heavy) {
-        row = bt.heavy[(int)blockIdx.x - nlight];
+        row = bt.heavy[blk - nlight];
     } else {
-        row = (int)blockIdx.x * W + wave;
+        row = blk * W + wave;
         if (row >= n) {
             r.row = -1;
             r.lead = false;
@@ -1684,7 +1696,7 @@ constexpr int kAdamTabMax = 256;  // step offsets covered by one Adam table
 // cross-lane broadcasts (the 16-lane-row form needed 64 shuffles per row).
 __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1, float bh1, float av2,
                                                   float bh2, float x1, float x2, float l, float q,
-                                                  float* __restrict__ partials) {
+                                                  float* __restrict__ partials, int blk) {
     __shared__ float vec[16][6][HID];
     __shared__ float sca[16][2];
     const int lane = threadIdx.x & 63;
@@ -1719,7 +1731,7 @@ __device__ __forceinline__ void block_reduce_1024(int c_n, bool valid, float av1
 #pragma unroll
         for (int r = 0; r < 16; ++r) t += sca[r][e - 288];
     }
-    partials[(int64_t)blockIdx.x * kRedLen + e] = t;
+    partials[(int64_t)blk * kRedLen + e] = t;
 }
 
 // dH0 = Â dY0 (+ outer factor (dY0, H0)); block partials of
@@ -1775,7 +1787,7 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     if (valid && g0) dh0[ix] = g;
     if (U != nullptr && valid && g0)  // outer graph, use 1: G = dY0, Z = H0, Y = Y0, ÂG = dH0
         emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_dy0, o_h0, o_y0, g);
-    block_reduce_1024(c, valid && g0, a1, b1, 0.f, 0.f, g, a1, lr, qr, partials);
+    block_reduce_1024(c, valid && g0, a1, b1, 0.f, 0.f, g, a1, lr, qr, partials, rsel.blk);
 }
 
 // H0bar = Â Y0bar (+ factor use 1); block partials of
@@ -1830,7 +1842,7 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
         emit_factor_pre(U, V, ldk, R, rprev, foff, HID, row, lane, si, o_y0bar, o_h0, o_y0, ag);
         h0bar[ix] = ag;
     }
-    block_reduce_1024(c, valid && g0, a1, b1, a2, b2, ag, a2, 0.f, 0.f, partials);
+    block_reduce_1024(c, valid && g0, a1, b1, a2, b2, ag, a2, 0.f, 0.f, partials, rsel.blk);
 }
 
 // Sum the block partials (fixed order) into the flat parameter-shaped buffer

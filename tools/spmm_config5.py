@@ -85,9 +85,9 @@ def main(n=20000, f=16, reps=20, high=1.0):
     ws_dn = torch.empty(variants.ws_bytes(n), dtype=torch.uint8, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
 
-    def dense(quantize=1, grid=0):
+    def dense(quantize=1, grid=0, checked=True):
         nat.call("lds_spmm_norm_dense", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), f, nat.ptr(y_dn), f, 0,
-                 nat.ptr(ws_dn), grid, quantize, nat.ptr(err), st)
+                 nat.ptr(ws_dn), grid, quantize, nat.ptr(err) if checked else 0, st)
 
     t_bp = time_it(lambda: nat.call("lds_csr_block_ptr", nat.ptr(rp), nat.ptr(col), n, nat.ptr(bptr), st), 3)
     t_row = time_it(row, reps)
@@ -104,9 +104,15 @@ def main(n=20000, f=16, reps=20, high=1.0):
         eq_variants[dbg] = bool(torch.equal(y_abl0, y_main))
     y_tile = y_dn.clone()
     t_dn_main = time_it(lambda: dense(0), reps)
+    # the unchecked form (err = NULL: the caller vouches for canonical columns,
+    # as the engine and SampledGraph do): the call and the product
+    t_dn_u = time_it(lambda: dense(1, 0, False), reps)
+    t_dn_main_u = time_it(lambda: dense(0, 0, False), reps)
+    eq_unchecked = bool(torch.equal(y_dn, y_main))
     y_abl = torch.empty_like(y_dn)
     abl = {}
-    for dbg, what in ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
+    quick = bool(os.environ.get("SPMM5_QUICK"))  # product timings only, no ablations
+    for dbg, what in () if quick else ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
                       (7, "row-block: hybrid multiply phase alone"),
                       (8, "row-block: hybrid multiply phase alone, no per-chunk barrier"),
                       (23, "spill-pass kernel, ring depth 8"), (36, "spill-pass, quad-reduced bit setting"),
@@ -176,6 +182,10 @@ def main(n=20000, f=16, reps=20, high=1.0):
                                 "frac_call": algo / t_dn / 1e3 / HBM_PEAK_GBS, "avg_us_product": t_dn_main,
                                 "achieved_GBs_product": algo / t_dn_main / 1e3,
                                 "frac_product": algo / t_dn_main / 1e3 / HBM_PEAK_GBS,
+                                "unchecked": {"avg_us_call": t_dn_u, "frac_call": algo / t_dn_u / 1e3 / HBM_PEAK_GBS,
+                                              "avg_us_product": t_dn_main_u,
+                                              "frac_product": algo / t_dn_main_u / 1e3 / HBM_PEAK_GBS,
+                                              "equal_to_checked": eq_unchecked},
                                 "speedup_vs_blocked": t_blk / t_dn,
                                 "max_rel_vs_row": float((y_dn - y_row).abs().max() / y_row.abs().max()),
                                 "tile_kernel_us_product": t_tile,
