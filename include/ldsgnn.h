@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 14
+#define LDS_ABI_VERSION 15
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -708,7 +708,11 @@ int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int 
  * each (n_heavy = 0 with xt_part).  xtinfo != NULL: per plan slot s,
  * xtinfo[s] = {column, p0, nnz, 0} (int4) replaces order[s] -> xcp loads,
  * and xthead[s] (64 ints, NULL allowed) holds the light column's first 64
- * row indices (values from xval[p0 + e]). */
+ * row indices (values from xval[p0 + e]).  ABI 15: after the heavy slots,
+ * n_single slots run one column per wave, the next n_pair (columns of at most
+ * 32 entries) two per wave and the rest (at most 16 entries) four per wave —
+ * the same sums; n_single = fin - n_heavy, n_pair = 0 is the one-per-wave
+ * plan, the only one allowed without xthead, with xt_part or with train. */
 int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int fin,
                        const float* d, float* out, int accumulate, uint64_t seed,
                        uint32_t tag_x, const void* scalars, int fwd_off, int train, float keep,
@@ -718,7 +722,8 @@ int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* xval, int f
                        float* v1, float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                        const double* hyper, const float* adam_tab, int n_wd, int step_off,
                        const float* xt_part, int xt_splits, const int* order, int n_heavy,
-                       const int* xtinfo, const int* xthead, const LdsBatch* batch, void* stream);
+                       const int* xtinfo, const int* xthead, int n_single, int n_pair,
+                       const LdsBatch* batch, void* stream);
 /* Long X columns (dense X, config 5): Xdᵀ d over `splits` entry ranges of every
  * column, one wave each; part[s][p][f][16] per replica sample s (stride
  * splits·fin·16).  Feeds lds_engine_xt_adam's xt_part. */

@@ -125,6 +125,20 @@ __device__ __forceinline__ void bkeys(Keys& k, const Batch& bt) {
     }
 }
 
+// The same with the sample given (the row-plan kernels: plan_pos).
+template <bool kB, typename T>
+__device__ __forceinline__ T* boffs(int smp, T* p, int64_t stride) {
+    if constexpr (!kB) return p;
+    return p == nullptr ? p : p + (int64_t)smp * stride;
+}
+template <bool kB>
+__device__ __forceinline__ void bkeys_s(int smp, Keys& k, const Batch& bt) {
+    if constexpr (kB) {
+        k.tag_x += smp * bt.tag;
+        k.tag_h += smp * bt.tag;
+    }
+}
+
 __device__ __forceinline__ float u_at(const Keys& k, uint32_t tag, uint32_t ctr, int row, int col) {
     const U32x4 o = philox4x32_10(U32x4{(uint32_t)col, (uint32_t)(row >> 2), tag, ctr}, k.k0, k.k1);
     const uint32_t w = (row & 3) == 0 ? o.x : (row & 3) == 1 ? o.y : (row & 3) == 2 ? o.z : o.w;
@@ -187,6 +201,18 @@ __device__ __forceinline__ int plan_block(int nlight, int nh) {
     return p < nh ? nlight + p : p - nh;
 }
 
+// (sample, logical block) of a row-plan launch (grid nlight + nh by samples):
+// sample blockIdx.y, heavy blocks first within it.  (Dispatching the heavy
+// blocks of every sample ahead of all light blocks measured slower at S = 8:
+// 0.279 against 0.271 ms per step.)
+struct PlanPos {
+    int smp, blk;
+};
+template <bool kB, int W>
+__device__ __forceinline__ PlanPos plan_pos(int n, const Batch& bt) {
+    return PlanPos{kB ? (int)blockIdx.y : 0, plan_block((n + W - 1) / W, bt.nh)};
+}
+
 struct RowSel {
     int row;          // -1: no row for this wave
     int first, end;   // this wave's first CSR entry, the row's end
@@ -200,13 +226,12 @@ struct RowSel {
 // The ELL head, row_ptr and the plan flag of a light row load together (the
 // head's address must not wait for the flag).
 template <int W, bool kAgg>
-__device__ __forceinline__ RowSel select_row(int n, const int* __restrict__ rp, const int2* __restrict__ ell,
+__device__ __forceinline__ RowSel select_row(int blk, int n, const int* __restrict__ rp, const int2* __restrict__ ell,
                                              const Batch& bt) {
     RowSel r;
     r.e = make_int2(0, 0);
     const int wave = wave_id();
     const int nlight = (n + W - 1) / W;
-    const int blk = plan_block(nlight, bt.nh);
     r.blk = blk;
     r.heavy = blk >= nlight;
     r.step = r.heavy ? 64 * W : 64;
@@ -517,6 +542,32 @@ __device__ __forceinline__ float x_wave_dot_head_pair(int p0, int nnz, const int
     return xor16_add(acc[0]) + xor16_add(acc[1]);
 }
 
+// A SHORT X column (at most 32 entries) on part of a wave: the column's
+// 16-lane groups take its head entries 16·qc … 16·qc + 15 (qc = the group's
+// place in the column: 0 for a column of a group, 0 / 1 for a column of two
+// groups), exactly as groups qc of x_wave_dot_head<true, 2> do; the caller
+// adds the groups of a two-group column with xor16_add.  Groups past a
+// column's entries contribute nothing there either, so the sums are the same
+// bits (up to the sign of a zero sum).  train = 0 (the stored Xd).
+__device__ __forceinline__ float x_group_dot_head(int qc, int p0, int nnz, const int* __restrict__ head,
+                                                  const float* __restrict__ val, const float* __restrict__ src) {
+    const int lane = threadIdx.x & (HID - 1);
+    float acc = 0.f;
+    const int e = 16 * qc + lane;
+    const int j = head[e];
+    const float x = e < nnz ? val[p0 + e] : 0.f;
+    if (16 * qc < nnz) {  // group-uniform
+        float sk[HID];
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+        LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(x), sk[K], acc);
+        LDS_R16(LDS_F)
+#undef LDS_F
+    }
+    return acc;
+}
+
 template <bool kCsc>
 __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const int* __restrict__ idx,
                                             const float* __restrict__ val, int r,
@@ -653,22 +704,23 @@ __global__ __launch_bounds__(256) void fwd_layer1_kernel(
     const float* __restrict__ h0, float* __restrict__ y0, float* __restrict__ h1d, float* __restrict__ h2,
     GcnW w, int c, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    h0 = boff<kB>(h0, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    h1d = boff<kB>(h1d, bt.act);
-    h2 = boff<kB>(h2, bt.act);
-    dmask = boff<kB>(dmask, bt.act);
-    w.w1 = boff<kB>(w.w1, bt.par);
-    w.b1 = boff<kB>(w.b1, bt.par);
-    bkeys<kB>(keys, bt);
-    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    h0 = boffs<kB>(pp.smp, h0, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    h1d = boffs<kB>(pp.smp, h1d, bt.act);
+    h2 = boffs<kB>(pp.smp, h2, bt.act);
+    dmask = boffs<kB>(pp.smp, dmask, bt.act);
+    w.w1 = boffs<kB>(pp.smp, w.w1, bt.par);
+    w.b1 = boffs<kB>(pp.smp, w.b1, bt.par);
+    bkeys_s<kB>(pp.smp, keys, bt);
+    const RowSel rsel = select_row<4, kAgg>(pp.blk, n, rp, ell, bt);
     // the row's own operands (dropout draw, W1, b1) ahead of the aggregation
     float dk = 1.f, b1l = 0.f, w1v[HID];
     if (rsel.lead) {
@@ -705,20 +757,21 @@ __global__ __launch_bounds__(256) void fwd_layer2_kernel(
     const float* __restrict__ h2, float* __restrict__ o_out, float* __restrict__ p_out,
     float* __restrict__ d_o, const int* __restrict__ label, const uint8_t* __restrict__ mask,
     float inv_count, float* __restrict__ lossrow, float* __restrict__ corrrow, int c, const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    h2 = boff<kB>(h2, bt.act);
-    o_out = boff<kB>(o_out, bt.act);
-    p_out = boff<kB>(p_out, bt.act);
-    d_o = boff<kB>(d_o, bt.act);
-    lossrow = boff<kB>(lossrow, bt.row);
-    corrrow = boff<kB>(corrrow, bt.row);
-    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    h2 = boffs<kB>(pp.smp, h2, bt.act);
+    o_out = boffs<kB>(pp.smp, o_out, bt.act);
+    p_out = boffs<kB>(pp.smp, p_out, bt.act);
+    d_o = boffs<kB>(pp.smp, d_o, bt.act);
+    lossrow = boffs<kB>(pp.smp, lossrow, bt.row);
+    corrrow = boffs<kB>(pp.smp, corrrow, bt.row);
+    const RowSel rsel = select_row<4, kAgg>(pp.blk, n, rp, ell, bt);
     const float o = agg_value<4, kAgg>(rsel, col, s, ell, h2, agg, bt, n);
     if (!rsel.lead) return;
     const int row = rsel.row;
@@ -757,26 +810,27 @@ __global__ __launch_bounds__(256) void bwd_layer2_kernel(
     int train, float keep, float scale, const float* __restrict__ o_in, const float* __restrict__ h2,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth,
     int r_assign, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    d_o = boff<kB>(d_o, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    dy0 = boff<kB>(dy0, bt.act);
-    o_in = boff<kB>(o_in, bt.act);
-    h2 = boff<kB>(h2, bt.act);
-    dmask = boff<kB>(dmask, bt.act);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    w.w1 = boff<kB>(w.w1, bt.par);
-    bkeys<kB>(keys, bt);
-    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    d_o = boffs<kB>(pp.smp, d_o, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    dy0 = boffs<kB>(pp.smp, dy0, bt.act);
+    o_in = boffs<kB>(pp.smp, o_in, bt.act);
+    h2 = boffs<kB>(pp.smp, h2, bt.act);
+    dmask = boffs<kB>(pp.smp, dmask, bt.act);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    w.w1 = boffs<kB>(pp.smp, w.w1, bt.par);
+    bkeys_s<kB>(pp.smp, keys, bt);
+    const RowSel rsel = select_row<4, kAgg>(pp.blk, n, rp, ell, bt);
     const float g2 = agg_value<4, kAgg>(rsel, col, s, ell, d_o, agg, bt, n);  // zero past c (dO is)
     if (!rsel.lead) return;
     const int row = rsel.row;
@@ -1003,31 +1057,32 @@ __global__ __launch_bounds__(256) void rev_a_kernel(
     Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff,
     const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    dh0bar = boff<kB>(dh0bar, bt.act);
-    dy0 = boff<kB>(dy0, bt.act);
-    dh0 = boff<kB>(dh0, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    h1d = boff<kB>(h1d, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    dh1dbar = boff<kB>(dh1dbar, bt.act);
-    dh2bar = boff<kB>(dh2bar, bt.act);
-    h1dbar = boff<kB>(h1dbar, bt.act);
-    dmask = boff<kB>(dmask, bt.act);
-    w.w1 = boff<kB>(w.w1, bt.par);
-    gw1bar = boff<kB>(gw1bar, bt.par);
-    gb1bar = boff<kB>(gb1bar, bt.par);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    bkeys<kB>(keys, bt);
-    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    dh0bar = boffs<kB>(pp.smp, dh0bar, bt.act);
+    dy0 = boffs<kB>(pp.smp, dy0, bt.act);
+    dh0 = boffs<kB>(pp.smp, dh0, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    h1d = boffs<kB>(pp.smp, h1d, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    dh1dbar = boffs<kB>(pp.smp, dh1dbar, bt.act);
+    dh2bar = boffs<kB>(pp.smp, dh2bar, bt.act);
+    h1dbar = boffs<kB>(pp.smp, h1dbar, bt.act);
+    dmask = boffs<kB>(pp.smp, dmask, bt.act);
+    w.w1 = boffs<kB>(pp.smp, w.w1, bt.par);
+    gw1bar = boffs<kB>(pp.smp, gw1bar, bt.par);
+    gb1bar = boffs<kB>(pp.smp, gb1bar, bt.par);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    bkeys_s<kB>(pp.smp, keys, bt);
+    const RowSel rsel = select_row<4, kAgg>(pp.blk, n, rp, ell, bt);
     // the row's own operands ahead of the aggregation (their loads overlap it)
     const int row = rsel.row;
     const int ix = row * HID + lane;
@@ -1081,22 +1136,23 @@ __global__ __launch_bounds__(256) void rev_b_kernel(
     const float* __restrict__ p, const uint8_t* __restrict__ mask, float inv_count, int c,
     float* __restrict__ obar, float* __restrict__ U, float* __restrict__ V, int ldk,
     float* __restrict__ R, int foff, int cw, const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    dh2bar = boff<kB>(dh2bar, bt.act);
-    d_o = boff<kB>(d_o, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    p = boff<kB>(p, bt.act);
-    obar = boff<kB>(obar, bt.act);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    dh2bar = boffs<kB>(pp.smp, dh2bar, bt.act);
+    d_o = boffs<kB>(pp.smp, d_o, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    p = boffs<kB>(pp.smp, p, bt.act);
+    obar = boffs<kB>(pp.smp, obar, bt.act);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    const RowSel rsel = select_row<4, kAgg>(pp.blk, n, rp, ell, bt);
     const float ag = agg_value<4, kAgg>(rsel, col, s, ell, dh2bar, agg, bt, n);  // dObar
     if (!rsel.lead) return;
     const int row = rsel.row;
@@ -1120,27 +1176,28 @@ __global__ __launch_bounds__(256) void rev_c_kernel(
     float* __restrict__ h2bar, float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc,
     int fwd_off, int train, float keep, float scale, float* __restrict__ U, float* __restrict__ V,
     int ldk, float* __restrict__ R, int foff, int cw, const float* __restrict__ dmask, const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    obar = boff<kB>(obar, bt.act);
-    h2 = boff<kB>(h2, bt.act);
-    o = boff<kB>(o, bt.act);
-    h1dbar_part = boff<kB>(h1dbar_part, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    h2bar = boff<kB>(h2bar, bt.act);
-    y0bar = boff<kB>(y0bar, bt.act);
-    dmask = boff<kB>(dmask, bt.act);
-    w.w1 = boff<kB>(w.w1, bt.par);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    bkeys<kB>(keys, bt);
-    const RowSel rsel = select_row<4, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    obar = boffs<kB>(pp.smp, obar, bt.act);
+    h2 = boffs<kB>(pp.smp, h2, bt.act);
+    o = boffs<kB>(pp.smp, o, bt.act);
+    h1dbar_part = boffs<kB>(pp.smp, h1dbar_part, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    h2bar = boffs<kB>(pp.smp, h2bar, bt.act);
+    y0bar = boffs<kB>(pp.smp, y0bar, bt.act);
+    dmask = boffs<kB>(pp.smp, dmask, bt.act);
+    w.w1 = boffs<kB>(pp.smp, w.w1, bt.par);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    bkeys_s<kB>(pp.smp, keys, bt);
+    const RowSel rsel = select_row<4, kAgg>(pp.blk, n, rp, ell, bt);
     const float ag = agg_value<4, kAgg>(rsel, col, s, ell, obar, agg, bt, n);  // H2bar (zero past c)
     if (!rsel.lead) return;
     const int row = rsel.row;
@@ -1389,28 +1446,29 @@ __global__ __launch_bounds__(256) void fwd2_bwd2_kernel(
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff, int fwidth, int r_assign,
     const float* __restrict__ dmask, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    h2 = boff<kB>(h2, bt.act);
-    o_out = boff<kB>(o_out, bt.act);
-    p_out = boff<kB>(p_out, bt.act);
-    d_o = boff<kB>(d_o, bt.act);
-    lossrow = boff<kB>(lossrow, bt.row);
-    corrrow = boff<kB>(corrrow, bt.row);
-    y0 = boff<kB>(y0, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    dy0 = boff<kB>(dy0, bt.act);
-    dmask = boff<kB>(dmask, bt.act);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    w.w1 = boff<kB>(w.w1, bt.par);
-    bkeys<kB>(keys, bt);
-    const RowSel rsel = select_row<4, false>(n, rp, ell, bt);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    h2 = boffs<kB>(pp.smp, h2, bt.act);
+    o_out = boffs<kB>(pp.smp, o_out, bt.act);
+    p_out = boffs<kB>(pp.smp, p_out, bt.act);
+    d_o = boffs<kB>(pp.smp, d_o, bt.act);
+    lossrow = boffs<kB>(pp.smp, lossrow, bt.row);
+    corrrow = boffs<kB>(pp.smp, corrrow, bt.row);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    dy0 = boffs<kB>(pp.smp, dy0, bt.act);
+    dmask = boffs<kB>(pp.smp, dmask, bt.act);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    w.w1 = boffs<kB>(pp.smp, w.w1, bt.par);
+    bkeys_s<kB>(pp.smp, keys, bt);
+    const RowSel rsel = select_row<4, false>(pp.blk, n, rp, ell, bt);
     const int row = rsel.row;
     // the lead's own-row operands, loaded ahead of the two-hop walk
     const int ix = row * HID + lane;
@@ -1490,29 +1548,30 @@ __global__ __launch_bounds__(256) void rev_bc_kernel(
     float* __restrict__ y0bar, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep,
     float scale, float* __restrict__ U, float* __restrict__ V, int ldk, float* __restrict__ R, int foff_b,
     int foff_c, int cw, const float* __restrict__ dmask, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 4>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    dh2bar = boff<kB>(dh2bar, bt.act);
-    d_o = boff<kB>(d_o, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    p = boff<kB>(p, bt.act);
-    h2 = boff<kB>(h2, bt.act);
-    o = boff<kB>(o, bt.act);
-    h1dbar_part = boff<kB>(h1dbar_part, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    h2bar = boff<kB>(h2bar, bt.act);
-    y0bar = boff<kB>(y0bar, bt.act);
-    dmask = boff<kB>(dmask, bt.act);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    w.w1 = boff<kB>(w.w1, bt.par);
-    bkeys<kB>(keys, bt);
-    const RowSel rsel = select_row<4, false>(n, rp, ell, bt);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    dh2bar = boffs<kB>(pp.smp, dh2bar, bt.act);
+    d_o = boffs<kB>(pp.smp, d_o, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    p = boffs<kB>(pp.smp, p, bt.act);
+    h2 = boffs<kB>(pp.smp, h2, bt.act);
+    o = boffs<kB>(pp.smp, o, bt.act);
+    h1dbar_part = boffs<kB>(pp.smp, h1dbar_part, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    h2bar = boffs<kB>(pp.smp, h2bar, bt.act);
+    y0bar = boffs<kB>(pp.smp, y0bar, bt.act);
+    dmask = boffs<kB>(pp.smp, dmask, bt.act);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    w.w1 = boffs<kB>(pp.smp, w.w1, bt.par);
+    bkeys_s<kB>(pp.smp, keys, bt);
+    const RowSel rsel = select_row<4, false>(pp.blk, n, rp, ell, bt);
     const int row = rsel.row;
     // the lead's own-row operands, loaded ahead of the two-hop walk
     const int ix = row * HID + lane;
@@ -1745,26 +1804,27 @@ __global__ __launch_bounds__(1024) void bwd1_reduce_kernel(
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ h1d,
     const float* __restrict__ lossrow, const float* __restrict__ corrrow, int c, float* __restrict__ partials,
     const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 16>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores and reduces; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    dy0 = boff<kB>(dy0, bt.act);
-    dh0 = boff<kB>(dh0, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    h0 = boff<kB>(h0, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    h1d = boff<kB>(h1d, bt.act);
-    lossrow = boff<kB>(lossrow, bt.row);
-    corrrow = boff<kB>(corrrow, bt.row);
-    partials = boff<kB>(partials, bt.part);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    const RowSel rsel = select_row<16, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    dy0 = boffs<kB>(pp.smp, dy0, bt.act);
+    dh0 = boffs<kB>(pp.smp, dh0, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    h0 = boffs<kB>(pp.smp, h0, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    h1d = boffs<kB>(pp.smp, h1d, bt.act);
+    lossrow = boffs<kB>(pp.smp, lossrow, bt.row);
+    corrrow = boffs<kB>(pp.smp, corrrow, bt.row);
+    partials = boffs<kB>(pp.smp, partials, bt.part);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    const RowSel rsel = select_row<16, kAgg>(pp.blk, n, rp, ell, bt);
     const bool valid = rsel.lead;
     const int row = rsel.row;
     const int ix = row * HID + lane;
@@ -1801,26 +1861,27 @@ __global__ __launch_bounds__(1024) void rev_d_reduce_kernel(
     float* __restrict__ R, int foff, const float* __restrict__ dh2, const float* __restrict__ dh1dbar,
     const float* __restrict__ h2bar, const float* __restrict__ h1d, int c, float* __restrict__ partials,
     const float* __restrict__ agg, Batch bt) {
+    const PlanPos pp = plan_pos<kB, 16>(n, bt);
     const int lane = threadIdx.x & (HID - 1);
     const bool g0 = (threadIdx.x & 63) < HID;  // group 0 stores and reduces; groups 1-3 hold copies
-    if constexpr (kAgg) agg = boff<kB>(agg, bt.act);
-    rp = boff<kB>(rp, bt.rp);
-    col = boff<kB>(col, bt.col);
-    s = boff<kB>(s, bt.row);
-    ell = boff<kB>(ell, bt.ell2);
-    y0bar = boff<kB>(y0bar, bt.act);
-    h0 = boff<kB>(h0, bt.act);
-    y0 = boff<kB>(y0, bt.act);
-    h0bar = boff<kB>(h0bar, bt.act);
-    dh2 = boff<kB>(dh2, bt.act);
-    dh1dbar = boff<kB>(dh1dbar, bt.act);
-    h2bar = boff<kB>(h2bar, bt.act);
-    h1d = boff<kB>(h1d, bt.act);
-    partials = boff<kB>(partials, bt.part);
-    U = boff<kB>(U, bt.uv);
-    V = boff<kB>(V, bt.uv);
-    R = boff<kB>(R, bt.row);
-    const RowSel rsel = select_row<16, kAgg>(n, rp, ell, bt);
+    if constexpr (kAgg) agg = boffs<kB>(pp.smp, agg, bt.act);
+    rp = boffs<kB>(pp.smp, rp, bt.rp);
+    col = boffs<kB>(pp.smp, col, bt.col);
+    s = boffs<kB>(pp.smp, s, bt.row);
+    ell = boffs<kB>(pp.smp, ell, bt.ell2);
+    y0bar = boffs<kB>(pp.smp, y0bar, bt.act);
+    h0 = boffs<kB>(pp.smp, h0, bt.act);
+    y0 = boffs<kB>(pp.smp, y0, bt.act);
+    h0bar = boffs<kB>(pp.smp, h0bar, bt.act);
+    dh2 = boffs<kB>(pp.smp, dh2, bt.act);
+    dh1dbar = boffs<kB>(pp.smp, dh1dbar, bt.act);
+    h2bar = boffs<kB>(pp.smp, h2bar, bt.act);
+    h1d = boffs<kB>(pp.smp, h1d, bt.act);
+    partials = boffs<kB>(pp.smp, partials, bt.part);
+    U = boffs<kB>(pp.smp, U, bt.uv);
+    V = boffs<kB>(pp.smp, V, bt.uv);
+    R = boffs<kB>(pp.smp, R, bt.row);
+    const RowSel rsel = select_row<16, kAgg>(pp.blk, n, rp, ell, bt);
     const bool valid = rsel.lead;
     const int row = rsel.row;
     const int ix = row * HID + lane;
@@ -2015,8 +2076,11 @@ __global__ __launch_bounds__(256) void xt_partials_kernel(
 // launch's time.  The column plan (built once per X by the host,
 // LdsEngine._xt_plan) lists the `n_heavy` columns longer than 128 entries first:
 // each gets a 1024-thread block whose 16 waves take consecutive 64-aligned
-// entry ranges, their partial sums combined through LDS in wave order; the
-// remaining columns go 16 per block, one wave each.
+// entry ranges, their partial sums combined through LDS in wave order; then
+// n_single columns one wave each, n_pair columns of 17-32 entries two per
+// wave (32 lanes each) and the rest, columns of at most 16 entries, four per
+// wave (a 16-lane group each): fewer waves for the same sums (Cora: 68 heavy,
+// 329 / 255 / 781 columns; 1,741 waves instead of 2,453 per sample).
 
 template <bool kB>
 __global__ __launch_bounds__(1024) void xt_adam_kernel(
@@ -2024,7 +2088,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const float* __restrict__ d, Keys keys, const EngineScalars* __restrict__ sc, int fwd_off, int train,
     float keep, float scale, FinalArgs fin_args, AdamArgs adam, const float* __restrict__ xt_part,
     int xt_splits, const int* __restrict__ order, int n_heavy, const int4* __restrict__ xtinfo,
-    const int* __restrict__ xthead, Batch bt) {
+    const int* __restrict__ xthead, int n_single, int n_pair, Batch bt) {
     fin_args.partials = boff<kB>(fin_args.partials, bt.part);
     fin_args.dst = boff<kB>(fin_args.dst, bt.par);
     fin_args.metrics = boff<kB>(fin_args.metrics, bt.met);
@@ -2054,6 +2118,41 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
     const bool heavy = bx < n_heavy;
+    {
+        // light waves past the single-column ones: two or four short columns
+        const int lw = (bx - n_heavy) * 16 + wave;  // light wave number
+        const int w2 = n_single + (n_pair + 1) / 2;  // first four-column wave
+        if (!heavy && lw >= n_single) {
+            const int base = n_heavy + n_single;
+            const bool four = lw >= w2;
+            const int qc = four ? 0 : (lane >> 4) & 1;
+            const int slot = four ? base + n_pair + 4 * (lw - w2) + (lane >> 4)
+                                  : base + 2 * (lw - n_single) + (lane >> 5);
+            const int send = four ? fin : base + n_pair;
+            if (__ballot(slot < send) == 0ull) return;  // light waves never reach a barrier
+            const bool live = slot < send;
+            const int4 inf = xtinfo[live ? slot : base];
+            const int idx = inf.x * HID + (lane & (HID - 1));
+            const bool owner = live && qc == 0;
+            AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
+            float prev = 0.f;
+            if (owner) {
+                o = adam_load(adam, idx);
+                if (fin_args.accumulate) prev = fin_args.dst[idx];
+            }
+            float step_size, c2;
+            adam_step_consts(adam, sc, step_size, c2);
+            float acc = x_group_dot_head(qc, inf.y, live ? inf.z : 0, xthead + (int64_t)(live ? slot : base) * 64,
+                                         xval, d);
+            if (!four) acc = xor16_add(acc);  // the column's two groups, as groups_sum adds them
+            if (owner) {
+                const float val = fin_args.accumulate ? prev + acc : acc;
+                fin_args.dst[idx] = val;
+                adam_apply(adam, idx, val, o, step_size, c2);
+            }
+            return;
+        }
+    }
     // with the column heads (xtinfo[slot] = {f, p0, nnz}, slot = position in
     // `order`) one load gives the column, its range and its first 64 rows;
     // without them: order[slot] -> xcp[f] -> entries, two dependent loads first
@@ -2703,7 +2802,8 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                                   float* gp, float* wbar, float* mbar, float* vbar, float* gbar,
                                   const double* hyper, const float* adam_tab, int n_wd, int step_off,
                                   const float* xt_part, int xt_splits, const int* order, int n_heavy,
-                                  const int* xtinfo, const int* xthead, const LdsBatch* batch, void* stream) {
+                                  const int* xtinfo, const int* xthead, int n_single, int n_pair,
+                                  const LdsBatch* batch, void* stream) {
     LDS_CHECK_ARG(xcp && xrow && xval && d && out && scalars && order && fin > 0 && batch_ok(batch));
     LDS_CHECK_ARG(xthead == nullptr || xtinfo != nullptr);
     LDS_CHECK_ARG(n_heavy >= 0 && n_heavy <= fin && (xt_part == nullptr || n_heavy == 0));
@@ -2729,10 +2829,16 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                            xval, fin, d, (const EngineScalars*)scalars, f, a, (const int4*)xtinfo, xthead, bt);
         LDS_RETURN_LAST_ERROR();
     }
-    const int blocks = n_heavy + (fin - n_heavy + 15) / 16 + (partials != nullptr ? 1 : 0);
+    // light waves: n_single one-column waves, then n_pair columns two per
+    // wave, then the rest four per wave (these need the heads, train = 0)
+    LDS_CHECK_ARG(n_single >= 0 && n_pair >= 0 && n_heavy + n_single + n_pair <= fin);
+    LDS_CHECK_ARG(n_heavy + n_single == fin || (xthead != nullptr && xt_part == nullptr && train == 0));
+    const int n_four = fin - n_heavy - n_single - n_pair;
+    const int lwaves = n_single + (n_pair + 1) / 2 + (n_four + 3) / 4;
+    const int blocks = n_heavy + (lwaves + 15) / 16 + (partials != nullptr ? 1 : 0);
     LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(1024), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
-                       a, xt_part, xt_splits, order, n_heavy, (const int4*)xtinfo, xthead, bt);
+                       a, xt_part, xt_splits, order, n_heavy, (const int4*)xtinfo, xthead, n_single, n_pair, bt);
     LDS_RETURN_LAST_ERROR();
 }
 

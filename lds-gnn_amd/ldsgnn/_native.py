@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -113,7 +113,7 @@ SIGNATURES = {
     "lds_engine_xt_adam": [P, P, P, c_int, P, P, c_int, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float,
                            P, c_int, c_int, c_int, c_int, c_int, P,
                            c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, P, c_int, P, c_int, P, P,
-                           P, P],
+                           c_int, c_int, P, P],
     "lds_engine_xt_partials": [P, P, P, c_int, P, c_uint64, c_uint32, P, c_int, c_int, c_float, c_float, c_int, P,
                                P, P],
     "lds_engine_fwd2_bwd2": [P, P, P, P, c_int, P, c_int, P, P, P, P, P, c_float, P, P, c_int, P, P, P, P,

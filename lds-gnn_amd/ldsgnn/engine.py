@@ -750,8 +750,17 @@ class LdsEngine:
         heavy = (lens > 128) if self.xt_splits <= 1 and self.S <= 8 and getattr(self, "xt_pair", 0) != 2 \
             else torch.zeros_like(lens, dtype=torch.bool)
         idx = torch.arange(self.fin, device=self.dev)
-        self.xt_order = torch.cat([idx[heavy], idx[~heavy]]).to(torch.int32).contiguous()
+        if self.xt_splits <= 1:
+            # the other columns by length: > 32 entries one wave each, 17-32
+            # two per wave, <= 16 four per wave (same sums, fewer waves)
+            one = ~heavy & (lens > 32)
+            two = ~heavy & (lens > 16) & (lens <= 32)
+            four = ~heavy & (lens <= 16)
+        else:
+            one, two, four = ~heavy, torch.zeros_like(heavy), torch.zeros_like(heavy)
+        self.xt_order = torch.cat([idx[heavy], idx[one], idx[two], idx[four]]).to(torch.int32).contiguous()
         self.xt_heavy = int(heavy.sum())
+        self.xt_n1, self.xt_n2 = int(one.sum()), int(two.sum())
         # column heads by plan slot (lds_engine_xt_adam xtinfo / xthead)
         f = self.xt_order.long()
         p0 = self.xcp[f].long()
@@ -849,7 +858,7 @@ class LdsEngine:
                  self.fin, nat.ptr(sl.dh0), nat.ptr(gout), 0, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
                  self.off_b1, nat.ptr(metrics_row), *adam, adam_t, *self._xt_split(xcsc, sl.dh0, fwd_off),
-                 nat.ptr(self.xtinfo), nat.ptr(self.xthead), self.btx, st)
+                 nat.ptr(self.xtinfo), nat.ptr(self.xthead), self.xt_n1, self.xt_n2, self.btx, st)
 
     # ----------------------------------------------------------------- steps
     def _sample_batch(self, count: int):
@@ -1295,7 +1304,7 @@ class LdsEngine:
                  nat.ptr(self.h0bar), nat.ptr(self.wbar), 1, self.seed, self.tag_x, nat.ptr(self.scalars), fwd_off,
                  0, self.keep, self.scale, nat.ptr(self.partials), self.nred, c, self.off_b0, self.off_w1,
                  self.off_b1, 0, *adam, t - 1, *self._xt_split(xcsc, self.h0bar, fwd_off), nat.ptr(self.xtinfo),
-                 nat.ptr(self.xthead), self.btx, st)
+                 nat.ptr(self.xthead), self.xt_n1, self.xt_n2, self.btx, st)
 
     # ------------------------------------------------------------- graphs
     # ------------------------------------------------------ per-step graphs

@@ -215,6 +215,21 @@ def test_engine_long_rows_match_oracle(dropout, kernel):
     assert res["max_theta_err"] < TOL, res
 
 
+@pytest.mark.parametrize("kernel", ["csr", "bitmask"])
+def test_engine_long_rows_odd_n(kernel):
+    """Odd n: n·n is not a multiple of 4, so the window's per-graph column
+    arrays must be padded to keep every graph's col 16-byte aligned for the
+    dense CSR-SpMM (the engine rounds its per-graph capacity up to 4 ints)."""
+    res = run_engine_and_oracle(n=301, f_in=32, classes=5, steps=6, tau=5, dropout=0.5, seed=5,
+                                theta_uniform=1.0, long_rows=True, long_rows_kernel=kernel)
+    assert res["engine"].cap % 4 == 0
+    assert res["theta_changed"] > 0
+    assert res["max_loss_err"] < TOL, res
+    assert res["max_param_err"] < TOL, res
+    assert res["max_grad_rel"] < 1e-4, res
+    assert res["max_theta_err"] < TOL, res
+
+
 @pytest.mark.parametrize("kernel", ["bitmask", "csr", "blocked"])
 def test_engine_long_rows_equal_in_kernel_aggregation(kernel):
     """The pre-pass and the in-kernel aggregation give the same window within

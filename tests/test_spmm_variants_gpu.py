@@ -65,3 +65,45 @@ def test_variants_equal_the_product(device, variants, n, shape, grid_codes):
                             nat.ptr(ws), dbg, st)
         torch.cuda.synchronize()
         assert torch.equal(yv.cpu(), y.cpu()), dbg
+
+
+def test_product_buffer_clear_with_a_delayed_multiply_wave(device, variants):
+    """Timing-independent check of the spill-pass kernel's buffer protocol
+    (the race of round 4: buffers cleared by every multiply wave while a
+    slower one still read them).  The PRODUCT kernel (csrc/spill.hpp), built
+    with multiply wave 12 sleeping after every pass barrier, so that it is the
+    last to finish each buffer, must give the undelayed product's exact sums.
+    n = 16384 on 171 workgroups (96 rows each) is 4 column passes, so every
+    pass buffer is cleared and filled again (pass 3 reuses pass 0's)."""
+    from ldsgnn import _native as nat
+    n, grid = 16384, 171
+    g = torch.Generator(device=device).manual_seed(7)
+    dens = torch.rand(n, generator=g, device=device) * 0.08
+    a = torch.rand(n, n, generator=g, device=device) < dens[:, None]
+    rows, cols = a.nonzero(as_tuple=True)
+    rp = torch.zeros(n + 1, dtype=torch.int32, device=device)
+    rp[1:] = torch.cumsum(a.sum(1), 0).int()
+    col = torch.empty(((cols.numel() + 3) // 4) * 4, dtype=torch.int32, device=device)
+    col[:cols.numel()] = cols.int()
+    del a, rows, cols
+    s = torch.rand(n, generator=g, device=device) + 0.5
+    z = torch.randn(n, 16, generator=g, device=device)
+    ws = torch.empty(variants.ws_bytes(n), dtype=torch.uint8, device=device)
+    err = torch.zeros(1, dtype=torch.int32, device=device)
+    st = nat.stream_of(device)
+    y = torch.empty(n, 16, device=device)
+    nat.call("lds_spmm_norm_dense", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), 16, nat.ptr(y), 16, 0,
+             nat.ptr(ws), grid, 1, nat.ptr(err), st)  # (leaves the digits of s, z in ws)
+    y_tile = torch.empty(n, 16, device=device)
+    nat.call("lds_spmm_norm_dense", nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(z), 16, nat.ptr(y_tile), 16,
+             0, nat.ptr(ws), -256, 0, 0, st)  # the tile kernel: any order, no pass buffers
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(y, y_tile)
+    for delay in (1, 4):
+        yd = torch.full((n, 16), float("nan"), device=device)
+        variants.spmm_dense_delayed(nat.ptr(rp), nat.ptr(col), nat.ptr(s), n, nat.ptr(yd), 16, nat.ptr(ws), grid,
+                                    delay, nat.ptr(err), st)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        assert torch.equal(yd, y), delay

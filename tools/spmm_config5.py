@@ -112,7 +112,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
     y_abl = torch.empty_like(y_dn)
     abl = {}
     quick = bool(os.environ.get("SPMM5_QUICK"))  # product timings only, no ablations
-    for dbg, what in () if quick else ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
+    only = {int(c) for c in os.environ.get("SPMM5_ABL", "").split(",") if c}  # time just these codes
+    for dbg, what in () if quick and not only else ((6, "row-block kernel, digits by register loads, bits by LDS-DMA (product)"),
                       (7, "row-block: hybrid multiply phase alone"),
                       (8, "row-block: hybrid multiply phase alone, no per-chunk barrier"),
                       (23, "spill-pass kernel, ring depth 8"), (36, "spill-pass, quad-reduced bit setting"),
@@ -155,6 +156,8 @@ def main(n=20000, f=16, reps=20, high=1.0):
                       (1, "row-block: streaming phase alone"), (2, "row-block: streaming without bit-row stores"),
                       (3, "row-block: multiply phase alone"), (4, "row-block: multiply without bit-row loads"),
                       (5, "row-block: streaming without stores + column-pass step bookkeeping")):
+        if only and dbg not in only:
+            continue
         abl[what] = time_it(lambda: variants.spmm_dense(nat.ptr(rp), nat.ptr(col), nat.ptr(s), n,
                                                         nat.ptr(z), f, nat.ptr(y_abl), f, nat.ptr(ws_dn), dbg, st), reps)
     dense(0)  # the product again (the multiply-only ablation left its slabs in place)

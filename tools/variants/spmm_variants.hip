@@ -13,13 +13,14 @@
 //
 // Build: make -C tools/variants  ->  tools/variants/libldsgnn_variants.so
 #include "../../lds-gnn_amd/csrc/bitagg.hpp"
+#include "../../lds-gnn_amd/csrc/spill.hpp"  // the product kernel, for its delayed test build
 
 namespace lds_variants {
 using namespace lds;
 
 // ---------------------------------------------------------------------------
 // CSR-SpMM for dense sampled graphs, row-block form (round 4; the product
-// path of lds_spmm_norm_dense).  csr_dense_agg_kernel above multiplies each
+// of lds_spmm_norm_dense until the spill-pass kernel replaced it).  csr_dense_agg_kernel above multiplies each
 // 16-row bit tile as soon as it is streamed, so every tile reads all of s⊙Z's
 // digits (1.3 MB at N = 20 000) from L2: 1.6 GB per call, twice the index
 // stream, on the same CUs — and the two streams serialise (its ablations:
@@ -431,8 +432,8 @@ __global__ __launch_bounds__(kRbThreads, 1) void csr_rowblock_agg_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// CSR-SpMM for dense sampled graphs, column-pass form (round 4, the product
-// path of lds_spmm_norm_dense).  Each workgroup owns one contiguous block of
+// CSR-SpMM for dense sampled graphs, column-pass form (round 4, a candidate
+// for lds_spmm_norm_dense, never the product).  Each workgroup owns one contiguous block of
 // rows (R <= kTiles·16) and sweeps the columns in P passes of cpp 512-column
 // chunks, so that the block's bit rows of ONE pass fit in LDS (R × cpp·64 B):
 // nothing of size nnz leaves the CU, and each CU reads s⊙Z's digits once.
@@ -715,8 +716,8 @@ __global__ __launch_bounds__(1024, 1) void csr_colpass_agg_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// CSR-SpMM for dense sampled graphs, spill-pass form (round 4; the product
-// path of lds_spmm_norm_dense).  The row-block kernel above writes every bit
+// CSR-SpMM for dense sampled graphs, spill-pass form (round 4; its frozen
+// configurations, the product's ancestors).  The row-block kernel above writes every bit
 // row to a global slab and reads it back (51 MB each way at config 5, and its
 // multiply phase runs after the stream instead of beside it); the column-pass
 // kernel keeps the bits on chip but re-reads the step that straddles each
@@ -783,7 +784,7 @@ constexpr int kSpProdMode = 17, kSpProdWaves = 12, kSpProdDepth = 4;
 struct SpCfg {
     int depth, ns, slot;  // ring slots per streaming wave, streaming waves, bytes per slot
 };
-// dbg 0 the product; the variants of lds_spmm_dense_ablation (tools/spmm_config5.py)
+// the spill-pass configurations by dbg code (tools/spmm_config5.py; 64 = the round-4 product form)
 SpCfg sp_cfg(int dbg) {
     if (dbg == 0) return SpCfg{kSpProdDepth, kSpProdWaves, 0};  // (the register ring takes no LDS)
     if (dbg == 58 || dbg == 59) return SpCfg{2, 12, 2048};
@@ -1427,6 +1428,24 @@ LDS_VAR_EXPORT int lds_variants_spmm_dense(const int* row_ptr, const int* col, c
     return variants_launch(row_ptr, col, s, n, z, ldz, y, ldy, 0, ws, 0, 0, dbg, (hipStream_t)stream);
 }
 
+// The PRODUCT spill-pass kernel (lds-gnn_amd/csrc/spill.hpp, the code
+// lds_spmm_norm_dense runs), built with a test delay: multiply wave 12 sleeps
+// `delay` × 127 × 64 cycles after every pass barrier (delay 1 or 4), so it
+// finishes each pass buffer last and the buffer clear must wait for it.  Exact
+// sums (equal to the undelayed product) whatever the delay is the
+// timing-independent check of the last-finisher clear.  err as in
+// lds_spmm_norm_dense; the digits of s, z must be in ws.
+LDS_VAR_EXPORT int lds_variants_spmm_dense_delayed(const int* row_ptr, const int* col, const float* s, int n,
+                                                   float* y, int ldy, void* ws, int grid, int delay, uint32_t* err,
+                                                   void* stream) {
+    LDS_CHECK_ARG(row_ptr && col && s && y && ws && n > 0 && n <= kDnMaxChunks * kChunk && ldy >= kF);
+    LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
+    LDS_CHECK_ARG(delay == 1 || delay == 4);
+    const Ws w = carve(ws, n);
+    if (delay == 1) return lds::spill::sp_launch<1>(row_ptr, col, s, n, w, y, ldy, 0, grid, err, (hipStream_t)stream);
+    return lds::spill::sp_launch<4>(row_ptr, col, s, n, w, y, ldy, 0, grid, err, (hipStream_t)stream);
+}
+
 static int variants_launch(const int* row_ptr, const int* col, const float* s, int n, const float* z, int ldz,
                              float* y, int ldy, int beta, void* ws, int grid, int quantize, int dbg, hipStream_t st) {
     LDS_CHECK_ARG(row_ptr && col && s && z && y && ws && n > 0 && n <= kDnMaxChunks * kChunk);
@@ -1445,13 +1464,13 @@ static int variants_launch(const int* row_ptr, const int* col, const float* s, i
     LDS_CHECK_ARG(R <= 16 * kRbMaxTiles);
     g = (n + R - 1) / R;  // every block has rows
     const int tiles = (R + 15) / 16;
-    // variant: 0 the column-pass kernel, 8 + 8 waves (the product path); 1 the
+    // variant: 0 the column-pass kernel, 8 + 8 waves (a round-4 candidate); 1 the
     // same, 16 waves streaming then multiplying; 2 the row-block kernel with
     // bit slabs in global scratch.  dbg (ablations): rowblock 1-4, column-pass
     // (concurrent) 11 no multiply, 12 no streaming
     const int variant = dbg >= 30 ? 3 : dbg >= 20 ? dbg - 20 : dbg == 13 ? 1 : dbg >= 10 ? 0 : dbg > 0 ? 2
                                                                                                 : 3;
-    if (variant == 3) {  // the spill-pass kernel (the product, dbg 0) and its variants (sp_cfg)
+    if (variant == 3) {  // the round-4 spill-pass kernels (dbg 64 = the round-4 product form) (sp_cfg)
         LDS_CHECK_ARG(R <= kSpMaxRows && g <= kSpMaxGrid);
         const SpCfg cfg = sp_cfg(dbg);
         const int depth = cfg.depth, ns = cfg.ns, slot = cfg.slot;
@@ -1550,7 +1569,7 @@ static int variants_launch(const int* row_ptr, const int* col, const float* s, i
         else if (dbg == 22 && tiles <= 2) LDS_RB_LAUNCH(2, 0);  // the LDS-staged multiply phase
         else if (dbg == 22 && tiles <= 4) LDS_RB_LAUNCH(4, 0);
         else if (dbg == 22) LDS_RB_LAUNCH(6, 0);
-        else if (tiles <= 2) LDS_RB_LAUNCH(2, 6);  // the product: digits by register loads
+        else if (tiles <= 2) LDS_RB_LAUNCH(2, 6);  // dbg 6: digits by register loads (the round-4 row-block product)
         else if (tiles <= 4) LDS_RB_LAUNCH(4, 6);
         else LDS_RB_LAUNCH(6, 6);
 #undef LDS_RB_LAUNCH

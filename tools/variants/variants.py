@@ -31,6 +31,8 @@ def lib():
         _lib.lds_variants_ws_bytes.restype = ctypes.c_int64
         _lib.lds_variants_spmm_dense.argtypes = [P, P, P, c_int, P, c_int, P, c_int, P, c_int, P]
         _lib.lds_variants_spmm_dense.restype = c_int
+        _lib.lds_variants_spmm_dense_delayed.argtypes = [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P]
+        _lib.lds_variants_spmm_dense_delayed.restype = c_int
     return _lib
 
 
@@ -44,3 +46,10 @@ def spmm_dense(rp, col, s, n, z, ldz, y, ldy, ws, dbg, stream):
     an lds_spmm_norm_dense call on the same workspace."""
     nat.check(lib().lds_variants_spmm_dense(rp, col, s, n, z, ldz, y, ldy, ws, dbg, stream),
               f"lds_variants_spmm_dense({dbg})")
+
+
+def spmm_dense_delayed(rp, col, s, n, y, ldy, ws, grid, delay, err, stream):
+    """The product spill-pass kernel with multiply wave 12 delayed after every
+    pass barrier (delay 1 or 4): the timing-independent buffer-clear check."""
+    nat.check(lib().lds_variants_spmm_dense_delayed(rp, col, s, n, y, ldy, ws, grid, delay, err, stream),
+              f"lds_variants_spmm_dense_delayed({delay})")
