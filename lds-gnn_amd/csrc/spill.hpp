@@ -280,16 +280,13 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             const int i0_ = a_ + kSpE * lane;                                                                \
             bool spill_ = false, fast_ = false;                                                              \
             int myx_ = kSpNone;                                                                              \
-            if (a_ >= rlo_ && a_ + kStep <= rup_) { /* interior (uniform): every entry is the row's */       \
+            if (kCheck && a_ >= rlo_ && a_ + kStep <= rup_) { /* interior (uniform): every entry is the row's */       \
                 const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
                 const int base_ = lo_ + (int)(w0_ << 5);                                                     \
                 uint32_t r_[kSpE];                                                                           \
-                if constexpr (kCheck) { /* all eight in [base, base + 64) and below the pass end */         \
+                { /* all eight in [base, base + 64) and below the pass end */                                \
                     const uint32_t o_ = sp_offsets(c_, base_, r_);                                           \
                     fast_ = c_[0] >= lo_ && o_ < 64u && base_ + (int)o_ < hi_;                               \
-                } else { /* ascending: the first and the last bound the lane */                              \
-                    _Pragma("unroll") for (int e = 0; e < kSpE; ++e) r_[e] = (uint32_t)(c_[e] - base_);      \
-                    fast_ = c_[0] >= lo_ && c_[kSpE - 1] < hi_ && r_[kSpE - 1] < 64u;                        \
                 }                                                                                            \
                 if (fast_) {                                                                                 \
                     uint64_t m_ = 0;                                                                         \
@@ -306,12 +303,9 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     const int qbase_ = hi_ + (int)(q0_ << 5);                                                \
                     uint32_t rq_[kSpE];                                                                      \
                     bool pq_;                                                                                \
-                    if constexpr (kCheck) {                                                                  \
+                    {                                                                                        \
                         const uint32_t oq_ = sp_offsets(c_, qbase_, rq_);                                    \
                         pq_ = c_[0] >= hi_ && oq_ < 64u && qbase_ + (int)oq_ < hq_;                          \
-                    } else {                                                                                 \
-                        _Pragma("unroll") for (int e = 0; e < kSpE; ++e) rq_[e] = (uint32_t)(c_[e] - qbase_); \
-                        pq_ = c_[0] >= hi_ && c_[kSpE - 1] < hq_ && rq_[kSpE - 1] < 64u;                     \
                     }                                                                                        \
                     if (pq_) {                                                                               \
                         uint64_t m_ = 0;                                                                     \
@@ -345,6 +339,50 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     }                                                                                        \
                 }                                                                                            \
             }                                                                                                \
+            /* unchecked (ascending columns vouched for by the caller): the round-4 product's */            \
+            /* expressions, verbatim — the same code the compiler scheduled at 164.8 µs (config 5) */        \
+            if (!kCheck && a_ >= rlo_ && a_ + kStep <= rup_) {                                               \
+                const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
+                fast_ = c_[0] >= lo_ && c_[kSpE - 1] < hi_ && (uint32_t)(c_[kSpE - 1] - lo_) - (w0_ << 5) < 64u; \
+                if (fast_) {                                                                                 \
+                    uint64_t m_ = 0;                                                                         \
+                    _Pragma("unroll") for (int e = 0; e < kSpE; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - lo_) - (w0_ << 5)); \
+                    dn_or(bp_ + w0_, (uint32_t)m_);                                                          \
+                    dn_or(bp_ + w0_ + 1, (uint32_t)(m_ >> 32));                                              \
+                }                                                                                            \
+                if (!fast_) {                                                                                \
+                    const uint32_t q0_ = (uint32_t)(c_[0] - hi_) >> 5;                                       \
+                    if (c_[0] >= hi_ && c_[kSpE - 1] < hq_ && (uint32_t)(c_[kSpE - 1] - hi_) - (q0_ << 5) < 64u) { \
+                        uint64_t m_ = 0;                                                                     \
+                        _Pragma("unroll") for (int e = 0; e < kSpE; ++e) m_ |= 1ull << ((uint32_t)(c_[e] - hi_) - (q0_ << 5)); \
+                        dn_or(bq_ + q0_, (uint32_t)m_);                                                      \
+                        dn_or(bq_ + q0_ + 1, (uint32_t)(m_ >> 32));                                          \
+                        spill_ = true;                                                                       \
+                        fast_ = true;                                                                        \
+                    }                                                                                        \
+                }                                                                                            \
+                if (!fast_ && c_[0] >= lo_ && c_[0] < hi_ && c_[kSpE - 1] >= hi_ && c_[kSpE - 1] < hq_ &&    \
+                    (uint32_t)(c_[kSpE - 1] - hi_) < 64u) { /* straddles the boundary */                     \
+                    uint64_t mp_ = 0, mq_ = 0;                                                               \
+                    bool ok_ = true;                                                                         \
+                    _Pragma("unroll") for (int e = 0; e < kSpE; ++e) {                                       \
+                        const bool in_ = c_[e] < hi_;                                                        \
+                        const uint32_t rr_ = in_ ? (uint32_t)(c_[e] - lo_) - (w0_ << 5) : (uint32_t)(c_[e] - hi_); \
+                        ok_ = ok_ && rr_ < 64u;                                                              \
+                        const uint64_t b_ = 1ull << (rr_ & 63u);                                             \
+                        mp_ |= in_ ? b_ : 0ull;                                                              \
+                        mq_ |= in_ ? 0ull : b_;                                                              \
+                    }                                                                                        \
+                    if (ok_) {                                                                               \
+                        dn_or(bp_ + w0_, (uint32_t)mp_);                                                     \
+                        dn_or(bp_ + w0_ + 1, (uint32_t)(mp_ >> 32));                                         \
+                        dn_or(bq_, (uint32_t)mq_);                                                           \
+                        dn_or(bq_ + 1, (uint32_t)(mq_ >> 32));                                               \
+                        spill_ = true;                                                                       \
+                        fast_ = true;                                                                        \
+                    }                                                                                        \
+                }                                                                                            \
+            }                                                                                                \
             if (!fast_) {                                                                                    \
                 /* per entry; two copies under a uniform branch: only the array's last step reloads the */   \
                 /* lanes that read the dummy (a lane-conditional load costs vmcnt(0) on every path) */       \
@@ -352,7 +390,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     _Pragma("unroll") for (int e = 0; e < kSpE; ++e) {                                       \
                         const int idx_ = i0_ + e;                                                            \
                         if (idx_ >= rlo_ && idx_ < rup_ &&                                                   \
-                            sp_put((idx_ & ~3) + 4 > nnz ? sp_ld(col + idx_) : c_[e], lo_, hi_, hq_, bp_, bq_, spill_, bad)) \
+                            sp_put((idx_ & ~3) + 4 > nnz ? (kCheck ? sp_ld(col + idx_) : col[idx_]) : c_[e], lo_, hi_, hq_, bp_, bq_, spill_, bad)) \
                             myx_ = min(myx_, idx_);                                                          \
                     }                                                                                        \
                 } else {                                                                                     \
@@ -376,7 +414,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                         int mx2_ = kSpNone;                                                                  \
                         _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                      \
                             const int idx_ = b_ + e;                                                         \
-                            if (idx_ >= np_ && idx_ < rup_ && sp_put(sp_ld(col + idx_), lo_, hi_, hq_, bp_, bq_, sp2_, bad)) \
+                            if (idx_ >= np_ && idx_ < rup_ && sp_put(kCheck ? sp_ld(col + idx_) : col[idx_], lo_, hi_, hq_, bp_, bq_, sp2_, bad)) \
                                 mx2_ = min(mx2_, idx_);                                                      \
                         }                                                                                    \
                         np_ = min((np_ & ~3) + 256, rup_);                                                   \
@@ -396,11 +434,13 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             }                                                                                                \
         }                                                                                                    \
     } while (0)
-        // every plain load of the prologue has landed before the ring starts: the
-        // compiler's wait analysis does not see the ring's asm loads, so a
-        // prologue load still counted as outstanding would make it wait (vmcnt
-        // 1-2) wherever the ring later reuses that load's registers
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        // checked build: every plain load of the prologue has landed before the
+        // ring starts (the compiler's wait analysis does not see the ring's asm
+        // loads, so a prologue load still counted as outstanding made it wait
+        // vmcnt 1-2 wherever the ring later reused that load's registers); the
+        // unchecked build keeps the round-4 product's code, which the compiler
+        // schedules without those waits
+        if constexpr (kCheck) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll
         for (int j = 0; j < D - 1; ++j) LDS_SP_ISSUE(j);
         while (true) {
