@@ -662,10 +662,11 @@ def main():
                          "noop = the N > 1 per-rank path with a no-op reducer (split graphs), noop-captured = "
                          "the same reducer captured into the window graph, rccl1 = a world-size-1 nccl (RCCL) "
                          "group and its real all-reduce captured into the window graph (DESIGN §5b)")
-    ap.add_argument("--keep-theta-grad", type=int, default=1, choices=[0, 1],
-                    help="engine, N = 1: 1 writes dθ to θ.grad beside the fused SGD update (the drop-in "
-                         "trainer's state after its backward); 0 consumes it in the update's registers only "
-                         "(θ.grad left None) — the same θ bit for bit")
+    ap.add_argument("--keep-theta-grad", type=int, default=0, choices=[0, 1],
+                    help="engine, no exchange: 1 writes dθ to θ.grad beside the fused SGD update (the drop-in "
+                         "trainer's state after its backward, what FusedBilevelRunner keeps); 0 (default: the "
+                         "bench has no θ.grad consumer) consumes it in the update's registers only — the same θ "
+                         "bit for bit.  With an exchange dθ is always written (the all-reduce's input)")
     ap.add_argument("--eager", action="store_true", help="engine: launch windows eagerly (no HIP graph)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-launch window breakdown leg")
     ap.add_argument("--backend", default="nccl", help="process group backend for N>1 (nccl = RCCL; gloo only "
@@ -869,7 +870,8 @@ def main():
                        "windows_per_graph": (args.graph_windows if whole else 1)
                        if use_engine and use_graph else None,
                        "prefetched_draw": prefetched, "async_draw": bool(args.async_draw),
-                       "theta_grad_written": bool(args.keep_theta_grad) if use_engine else True,
+                       "theta_grad_written": bool(args.keep_theta_grad) or reducer is not None
+                       if use_engine else True,
                        "xt_pair": args.xt_pair, "exchange": exchange_label if use_engine else None},
             "steady_state": steady,
             "strong_scaling": strong,
