@@ -788,6 +788,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * args.samples * args.steps / elapsed
+    if use_engine:
+        # the timed windows' device error word (a fill whose degree counts and
+        # bits disagree, a CSR the SpMM cannot use, ...): raise, never report
+        eng.check_device_error()
 
     # steady state: the same replays over a longer stretch (>= ~0.2 s), reported beside `value`
     steady = None
