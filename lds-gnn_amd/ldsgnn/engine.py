@@ -933,14 +933,14 @@ class LdsEngine:
         (lds_theta_grad_direct: the factor producers write split-bf16 planes,
         the θ-grad kernel stages them by direct global -> LDS loads): one
         sample, a full window (its columns are the same every window, so no
-        stale plane columns), dθ fused with SGD (no exchange, no model outer
-        step, no per-draw θ), and the form "bf16x3-direct" or the by-shape
+        stale plane columns), no model outer step, no per-draw θ, and the form "bf16x3-direct" or the by-shape
         default where the 128-tile grid is at most one tile per CU (Cora-sized
         graphs; MI355X: 55.0 vs 62.4 µs with the next window's draw,
-        profiles/r03_theta_direct_forms.jsonl).  Same result bits as the
-        fp32-operand forms."""
+        profiles/r03_theta_direct_forms.jsonl).  With an exchange (round 5) it
+        assembles dθ alone (mode 0) and the SGD + draw follow the reducer.
+        Same result bits as the fp32-operand forms."""
         form = self._form_name()
-        if not self.uv_planes or self.S != 1 or T != self.tau or grad_reducer is not None:
+        if not self.uv_planes or self.S != 1 or T != self.tau:
             return False
         if self.outer_update is not None or self.theta_fn is not None or self.split_theta_grad:
             return False
@@ -1096,8 +1096,13 @@ class LdsEngine:
                          1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
                          nat.ptr(self.scalars), self._form(), st)
         else:  # replicas: dθ, all-reduce (mean), then the identical update everywhere
-            nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
-                     nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, self._form(), st)
+            if self._planes_now:  # the direct-staged form, dθ only (mode 0; no draw: that follows the exchange)
+                nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1, 1,
+                         nat.ptr(self.theta), n, nat.ptr(self.grad), 0, nat.ptr(self.scalars), 1.0, self.seed,
+                         self.tag_graph, nat.ptr(self.scalars), self.pending_graph, 0, 0, self.words, 0, st)
+            else:
+                nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
+                         nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, self._form(), st)
             grad_reducer(self.grad)  # with outer_update: the model's optimizer step, which rewrites θ
             if self.outer_update is None:
                 drew = self._sgd_step(T, k0, presampled)
