@@ -44,7 +44,7 @@ def main():
     for k in (1, 2, 6):
         def fill(k=k):
             nat.call("lds_sample_fill_csr", nat.ptr(bits), n, words, nat.ptr(deg), k, nat.ptr(rp), nat.ptr(col), cap,
-                     nat.ptr(s), nat.ptr(ell), 0, nat.ptr(err), st)
+                     nat.ptr(s), nat.ptr(ell), 0, nat.ptr(err), nat.stream_of(dev))  # (the capture stream)
         out[f"fill_{k}_graphs_us"] = chain_us(fill, dev)
     print(json.dumps(out), flush=True)
 
