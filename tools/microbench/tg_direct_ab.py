@@ -4,7 +4,7 @@ while staging) and the by-shape default, at the engine's shapes: identical θ /
 dθ / bits / degrees, then µs per launch as a dependent chain of 20 copies in
 one HIP graph (HIP events on the launch stream), with and without the next
 window's draw; the plane split (lds_split_planes_t128, U and V) timed alone.
-Usage (GPU box): python tools/microbench/tg_direct_ab.py [cora|s16|c5|all]"""
+Usage (GPU box): python tools/microbench/tg_direct_ab.py [cora|s16|c5|graphs|all]"""
 import json
 import os
 import sys
@@ -102,6 +102,9 @@ def main():
     if which in ("s16", "all"):
         run("cora-S16", 2708, 4224, 0)
         run("citeseer-S16", 3327, 4224, 0)
+    if which == "graphs":  # the draw's cost per graph count (graph 0 only: the split prefetch)
+        for gr in (1, 2, 6):
+            run(f"cora-S1-g{gr}", 2708, 264, gr)
     if which in ("c5", "all"):
         run("synthetic20k-S1", 20000, 264, 6)
 
