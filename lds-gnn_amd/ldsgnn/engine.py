@@ -1096,14 +1096,19 @@ class LdsEngine:
                          1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
                          nat.ptr(self.scalars), self._form(), st)
         else:  # replicas: dθ, all-reduce (mean), then the identical update everywhere
+            pre = self._prescale(grad_reducer) if self._planes_now else None
             if self._planes_now:  # the direct-staged form, dθ only (mode 0; no draw: that follows the exchange)
                 nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1, 1,
-                         nat.ptr(self.theta), n, nat.ptr(self.grad), 0, nat.ptr(self.scalars), 1.0, self.seed,
-                         self.tag_graph, nat.ptr(self.scalars), self.pending_graph, 0, 0, self.words, 0, st)
+                         nat.ptr(self.theta), n, nat.ptr(self.grad), 0, nat.ptr(self.scalars),
+                         1.0 / pre if pre else 1.0, self.seed, self.tag_graph, nat.ptr(self.scalars),
+                         self.pending_graph, 0, 0, self.words, 0, st)
             else:
                 nat.call("lds_theta_grad", nat.ptr(self.U), nat.ptr(self.V), self.ldk, k0, nat.ptr(self.R), 1, 1,
                          nat.ptr(self.theta), n, nat.ptr(self.grad), 1 if split else 0, self._form(), st)
-            grad_reducer(self.grad)  # with outer_update: the model's optimizer step, which rewrites θ
+            if pre:  # dθ already scaled by 1/world: the exchange is the all-reduce SUM alone
+                grad_reducer(self.grad, prescaled=True)
+            else:
+                grad_reducer(self.grad)  # with outer_update: the model's optimizer step, which rewrites θ
             if self.outer_update is None:
                 drew = self._sgd_step(T, k0, presampled)
         # detach: the window restarts from the latest weights / Adam state
@@ -1148,15 +1153,31 @@ class LdsEngine:
             self.V.view(n, S, self.ldk)[:, :, k0:].zero_()
         P = nat.ptr
         gs = float(np.float32(1.0) / np.float32(S))
+        pre = self._prescale(grad_reducer) if grad_reducer is not None else None
+        if pre:  # × 2^-k: exact, the same bits as dividing the summed dθ by world
+            gs = float(np.float32(gs) / np.float32(pre))
         if grad_reducer is None:
             nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
                      P(self.theta), n, P(self.grad) if self.keep_grad else 0, 2, P(self.scalars), gs, self._form(), st)
         else:
             nat.call("lds_theta_grad_ex", P(self.U), P(self.V), self.ldu, self.ldu, P(self.R), 1, n, S,
                      P(self.theta), n, P(self.grad), 0, 0, gs, self._form(), st)
-            grad_reducer(self.grad)
+            if pre:
+                grad_reducer(self.grad, prescaled=True)
+            else:
+                grad_reducer(self.grad)
             return self._sgd_step(self.tau if presampled else -1, k0, presampled)
         return False
+
+    @staticmethod
+    def _prescale(grad_reducer):
+        """World size w when `grad_reducer` takes a dθ the assembly scaled by
+        1/w (its `prescale` attribute, ldsgnn.fused for replicas.allreduce_mean
+        over a power-of-two world): the exchange is then the all-reduce SUM
+        alone, with no division pass over θ.grad.  None: an ordinary reducer."""
+        f = getattr(grad_reducer, "prescale", None)
+        w = f() if callable(f) else f
+        return int(w) if w else None
 
     def _theta_chunk(self, col0: int, k: int, accumulate: int):
         """grad (=|+=) U[:, col0:col0+k] V[...]ᵀ + V U ᵀ on the side stream, after

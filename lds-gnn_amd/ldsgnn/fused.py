@@ -7,6 +7,7 @@ updates the graph model's θ in place and continues the trainers' RNG stream.
 """
 from __future__ import annotations
 
+from . import replicas as _replicas
 from . import rng as _rng
 from .engine import LdsEngine
 
@@ -52,7 +53,12 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
     if outer.grad_reducer is not None:
         reducer, model = outer.grad_reducer, gm
 
-        def reduce_engine_grad(grad):
+        def reduce_engine_grad(grad, prescaled=False):
+            # prescaled (the engine assembled dθ / world, see `prescale`): the
+            # mean is the all-reduce SUM alone, no division pass over θ.grad
+            if prescaled:
+                _replicas.allreduce_sum_(grad)
+                return
             # re-bind on every call: a zero_grad(set_to_none=True) in between
             # would otherwise leave θ.grad None, the reducer would skip it and
             # each rank would apply only its own dθ
@@ -64,6 +70,10 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
 
         # graph-capturable exactly when the trainer's reducer is (RCCL all-reduce)
         reduce_engine_grad.capturable = getattr(reducer, "capturable", False)
+        # the package's all-reduce mean: the engine may scale dθ by 1/world in
+        # the assembly (a power-of-two world: the same bits as sum-then-divide)
+        if reducer is _replicas.allreduce_mean:
+            reduce_engine_grad.prescale = _replicas.mean_prescale
         eng.grad_reducer = reduce_engine_grad
     return eng
 

@@ -48,6 +48,25 @@ def allreduce_mean(model: torch.nn.Module) -> None:
 allreduce_mean.capturable = exchange_capturable
 
 
+def mean_prescale():
+    """World size when the mean over ranks may be taken as a SUM of
+    gradients each rank has already scaled by 1/world: a process group of
+    more than one rank whose size is a power of two (scaling by 2^-k commutes
+    with fp32 rounding, so Σ_r (g_r / world) is bit for bit (Σ_r g_r) / world,
+    barring subnormals).  None otherwise (sum, then divide)."""
+    if not _group_up():
+        return None
+    world = dist.get_world_size()
+    return world if world > 1 and world & (world - 1) == 0 else None
+
+
+def allreduce_sum_(grad: torch.Tensor) -> None:
+    """The exchange of a prescaled gradient (mean_prescale): one all-reduce
+    SUM, no division pass over θ.grad."""
+    if _group_up() and dist.get_world_size() > 1:
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM)
+
+
 def allreduce_mean_always(model: torch.nn.Module) -> None:
     """allreduce_mean that runs the collective at world size 1 too (the
     world-size-1 RCCL rehearsal on one GPU: the same launches as N > 1)."""

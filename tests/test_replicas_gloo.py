@@ -44,3 +44,37 @@ def test_two_replicas_average_and_stay_in_sync():
     theta = torch.rand(55)
     want = (theta - 0.1 * (g0 + g1) / 2).clamp(0, 1)
     assert torch.allclose(out[0], out[1], atol=0) and torch.allclose(out[0], want, atol=1e-7)
+
+
+def _prescale_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ldsgnn.replicas import allreduce_mean, allreduce_sum_, mean_prescale
+    g = torch.Generator().manual_seed(200 + rank)
+    grad = torch.randn(4099, generator=g) * torch.logspace(-20, 20, 4099)
+    model = torch.nn.Module()
+    model.theta = torch.nn.Parameter(torch.zeros(4099))
+    model.theta.grad = grad.clone()
+    allreduce_mean(model)                     # SUM, then ÷ world
+    w = mean_prescale()
+    pre = grad * (1.0 / w)                    # what the engine's assembly writes (gscale = 1/world)
+    allreduce_sum_(pre)                       # SUM alone
+    out[rank] = (w, model.theta.grad.clone(), pre)
+    dist.destroy_process_group()
+
+
+def test_prescaled_sum_equals_mean_bit_for_bit():
+    """The engine's prescaled exchange (dθ assembled × 1/world, then one
+    all-reduce SUM: LdsEngine._prescale, ldsgnn.fused) gives the bits of
+    allreduce_mean's SUM-then-divide for a power-of-two world."""
+    from ldsgnn.replicas import mean_prescale
+    assert mean_prescale() is None  # no process group: no prescaling
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_prescale_worker, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        w, mean, pre = out[r]
+        assert w == world
+        assert torch.equal(mean, pre)
