@@ -374,12 +374,12 @@ int lds_theta_grad_direct(const uint16_t* up, const uint16_t* vp, int k, const f
  * kernel (ABI 16): one block per CU walks its 128 × 128 tiles; eight waves
  * run the k-loop over the block's chunk stream without a break between
  * tiles and hand each finished tile's accumulators to the block's slots in
- * `handoff` (global memory, L2-resident), four waves run the previous
+ * `handoff` (global memory, L2-resident), eight waves run the previous
  * tile's epilogue (θ update, Philox draw, bit rows, degree counts) on the
- * VALU meanwhile.  Taken at two or more tiles per block (large n) when the
- * epilogue's 2·graphs + 3 units fit the ceil(k/16) chunk intervals of a
- * tile; otherwise, or with handoff == NULL / too small, the call runs
- * lds_theta_grad_direct (mode 2).  Same result bits either way.
+ * VALU meanwhile; the two kinds of waves synchronise through LDS counters,
+ * so neither waits for the other's steps.  Taken at two or more tiles per
+ * block (large n); otherwise, or with handoff == NULL / too small, the call
+ * runs lds_theta_grad_direct (mode 2).  Same result bits either way.
  * handoff: >= lds_theta_grad_ws_floats() floats, 16-byte aligned, contents
  * unused between calls.  Replaces, fused: src/trainers/outer.py:77-81 and
  * src/models/sampling.py:68 (as lds_theta_grad_direct). */

@@ -1830,23 +1830,23 @@ static void launch_dma(hipStream_t st, const uint16_t* up, const uint16_t* vp, i
 //    a break between tiles (the LDS-DMA ring continues into the next tile's
 //    chunks) and hand each finished tile's raw accumulators to a per-block
 //    slot in global memory (L2; two slots, alternating);
-//  * waves 8-11 (E) run the previous tile's epilogue meanwhile — w8_epilogue's
-//    arithmetic for the two sub-tiles (wr, e) of wave e, then the draw graph
-//    by graph — on the VALU while the matrix pipe multiplies (separate pipes:
+//  * waves 8-15 (E) run the previous tile's epilogue meanwhile — w8_epilogue's
+//    arithmetic for the sub-tile of M wave e, then the draw graph by graph —
+//    on the VALU while the matrix pipe multiplies (separate pipes:
 //    MI355X_MICROARCH.md "Wave scheduling").
-// Both kinds run the same sequence of s_barriers: one per chunk of the stream
-// (the ring's), nch more at the end; E cuts its work for a tile into units
-// spread over the nch barrier intervals that follow the tile's hand-off.
+// The two kinds never share an s_barrier: LDS counters carry the k-loop's
+// chunk barrier (M only), the hand-off (tile ready / slot free) and the
+// epilogue's own barrier (E only), so neither waits for the other's steps.
 // Same chunks, same MFMA order per accumulator and the same epilogue
 // arithmetic and Philox counters as form 10: identical θ, dθ, bits, degrees.
 // ---------------------------------------------------------------------------
 constexpr int kWsM = 8;                                // MFMA waves (form 10's 2 × 4 sub-tiles)
-constexpr int kWsE = 4;                                // epilogue waves: wave 8 + e owns sub-tiles (0, e), (1, e)
+constexpr int kWsE = 8;                                // epilogue waves: wave 8 + e owns M wave e's sub-tile
 constexpr int kWsThreads = 64 * (kWsM + kWsE);
 constexpr int kWsSlot = kWsM * 64 * 32;                // floats per hand-off slot (the 8 waves' accumulators)
 constexpr int kWsHandoff = 2 * kWsSlot;                // floats per block
 constexpr int kWsGraphLds = kT2 * 4 * 4 + 2 * kT2 * 8; // bytes per graph buffer: row segments + column words
-constexpr int kWsLds = kDmaLds + 2 * kWsGraphLds + 2 * 2 * kT2 * 4;  // the ring, two graph buffers, R sums ×2
+constexpr int kWsLds = kDmaLds + 2 * kWsGraphLds + 2 * 2 * kT2 * 4 + 16;  // ring, graph buffers, R sums ×2, counters
 
 // The hand-off slot's values: plain 16-byte loads.  The slot is written and
 // read by waves of one workgroup (one CU's L1, write-through: no cache
@@ -1866,6 +1866,28 @@ __device__ __forceinline__ void ws_ld16(uint32_t* v, const float* p) {
 #ifndef LDS_WS_ABL
 #define LDS_WS_ABL 0  // timing-only ablations of the persistent form (experiment builds only)
 #endif
+
+// The two kinds of waves synchronise through monotonic LDS counters, never a
+// shared s_barrier (which would tie every k-loop chunk to the slowest
+// epilogue step: measured 3.2 ms against 1.76 for the k-loop alone at
+// n = 20 000): one wave per group of eight adds 1, the others wait for a
+// target.  Every wait is bounded (a broken protocol gives wrong results, never
+// a hung GPU).
+__device__ __forceinline__ void ws_signal(uint32_t* c) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ws_signal_relaxed(uint32_t* c) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <bool kAcquire = true>
+__device__ __forceinline__ void ws_wait(uint32_t* c, uint32_t target) {
+    for (int it = 0; it < (1 << 20); ++it) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(c, kAcquire ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (v >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
 
 template <bool SMALL>
 __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
@@ -1888,8 +1910,22 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
     const int64_t nn = n;
     float* const slots = handoff + (int64_t)blockIdx.x * kWsHandoff;
     auto tile_of = [&](int ti, int& bi, int& bj) { grouped_tile(L0 + q + bpx * ti, nb, group, bi, bj); };
-    const int nbar = (T + 1) * nch;  // barriers after the first one, the same count in both kinds of waves
+    // LDS counters: k-loop chunk barrier, tiles handed off, tiles whose slot
+    // the epilogue no longer reads, epilogue barrier
+    uint32_t* const ctr = lds_dyn + (kWsLds - 16) / 4;
+    if (t < 4) ctr[t] = 0u;  // (the first __syncthreads below publishes them)
 
+    if (wave < kWsM && LDS_WS_ABL == 3) {  // (timing only: the epilogue waves alone, zero accumulators)
+        __syncthreads();
+        for (int ti = 0; ti < T; ++ti) {
+            if (ti >= 2) ws_wait(&ctr[2], (uint32_t)kWsM * (ti - 1));
+            float* const sl = slots + (ti & 1) * kWsSlot + (wave * 64 + lane) * 32;
+            for (int q = 0; q < 32; q += 4) *reinterpret_cast<float4*>(sl + q) = make_float4(0.f, 0.f, 0.f, 0.f);
+            __builtin_amdgcn_s_waitcnt(0x0070);
+            ws_signal(&ctr[1]);
+        }
+        return;
+    }
     if (wave < kWsM) {
         // ---- M: form 10's k-loop over the block's chunk stream -------------
         const int wr = wave >> 2, wc = wave & 3;
@@ -1959,19 +1995,25 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
             const int c = gc % nch;
             read_half(gc, 1, h1);
             mfmas(h0);
-            // chunk gc + 1 landed (this wave's loads; the barrier: every wave's) and
-            // this wave's reads of chunk gc returned; at a tile's first chunk also
-            // the previous tile's hand-off stores (issued after the last fill)
-            if (c == 0 && gc > 0) __builtin_amdgcn_s_waitcnt(0x0070);     // vmcnt(0) lgkmcnt(0)
-            else if (gc + 2 < G) __builtin_amdgcn_s_waitcnt(0x0076);      // vmcnt(6) lgkmcnt(0)
-            else __builtin_amdgcn_s_waitcnt(0x0070);                      // vmcnt(0) lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (gc + 3 < G) fill(gc + 3);
-            if (gc + 1 < G) read_half(gc + 1, 0, h0);
+            if (gc + 1 < G) {
+                // chunk gc + 1 landed (this wave's loads; the counter: every
+                // wave's) and this wave's reads of chunk gc returned, so its
+                // buffer may take chunk gc + 3
+                if (gc + 2 < G) __builtin_amdgcn_s_waitcnt(0x0076);  // vmcnt(6) lgkmcnt(0)
+                else __builtin_amdgcn_s_waitcnt(0x0070);             // vmcnt(0) lgkmcnt(0)
+                ws_signal_relaxed(&ctr[0]);
+                // (relaxed: an acquire would wait for the ring's loads in flight;
+                // the stage reads below depend on the loop's exit)
+                ws_wait<false>(&ctr[0], (uint32_t)kWsM * (gc + 1));
+                asm volatile("" ::: "memory");
+                if (gc + 3 < G) fill(gc + 3);
+                read_half(gc + 1, 0, h0);
+            }
             mfmas(h1);
             if (c == nch - 1) {  // tile done: its accumulators to slot (tile & 1), lane-major
-                float* const sl = slots + ((gc / nch) & 1) * kWsSlot + (wave * 64 + lane) * 32;
+                const int ti = gc / nch;
+                if (ti >= 2) ws_wait(&ctr[2], (uint32_t)kWsM * (ti - 1));  // tile ti - 2 left the slot
+                float* const sl = slots + (ti & 1) * kWsSlot + (wave * 64 + lane) * 32;
 #pragma unroll
                 for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -1982,74 +2024,71 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
                 for (int m = 0; m < 2; ++m)
 #pragma unroll
                     for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the stores (and the ring's loads) done
+                ws_signal(&ctr[1]);                  // tile ti handed off
             }
         }
-        // the last tile's stores, then the E waves' remaining intervals
-        __builtin_amdgcn_s_waitcnt(0x0070);
-        for (int b = G; b < nbar; ++b) __builtin_amdgcn_s_barrier();
         return;
     }
 
     // ---- E: the epilogue of tile ti during the nch intervals after its hand-off
-    // Units of a tile, one per interval (the host checks 2·graphs + 5 <= nch):
-    // four updates (sub-tile wr, accumulator m), 2·graphs draws (graph g,
-    // sub-tile wr), the last graph's store.  Every unit's memory operands are
-    // loaded by the unit before it (the E waves are one per SIMD: an exposed
-    // round trip per unit would set the pace of the k-loop waves): the
-    // accumulators, θ and R sums of an update, the thresholds of a draw (kept
-    // in the hand-off slot, over the consumed accumulators).
-    const int e = wave - kWsM;  // = wc of both sub-tiles
+    // Units of a tile, one per interval (the host checks graphs + 3 <= nch):
+    // two updates (accumulator m of the wave's sub-tile), one draw per graph
+    // (both halves of the tile: all eight waves), the last graph's store.  A
+    // unit's memory operands are loaded by the unit before it (the accumulators
+    // and θ of the second update, the thresholds, kept in the hand-off slot
+    // over the consumed accumulators), and the R sums of the next tile go to
+    // LDS one tile ahead: an exposed round trip per unit would set the pace of
+    // the k-loop waves.
+    const int e = wave - kWsM;  // the M wave whose sub-tile this wave finishes
+    const int wr = e >> 2, wc = e & 3;
     const int te = t - 64 * kWsM;
-    const int jl = e * 32 + (lane & 31);
+    const int jl = wc * 32 + (lane & 31);
     const float lr = (float)(*lr_dev);
     const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
     uint32_t* const gbuf = lds_dyn + kDmaLds / 4;  // two graph buffers
     const int G = dr.graphs;
-    const int nu = 4 + (G > 0 ? 2 * G + 1 : 0);
     int i0 = 0, j0 = 0;
-    __syncthreads();  // the first barrier
-    auto row_of = [&](int wr, int m, int ee) { return wr * 64 + m * 32 + (ee & 3) + 8 * (ee >> 2) + 4 * (lane >> 5); };
-    // this lane's 16 values of accumulator m of sub-tile wr in tile ti's slot
-    auto slot_of = [&](int ti, int wr, int m) { return slots + (ti & 1) * kWsSlot + ((wr * 4 + e) * 64 + lane) * 32 + m * 16; };
-    // operands in flight between two units: two update sets (A / B, each the
-    // accumulators, θ and row R sums of one accumulator) and the thresholds of
-    // both sub-tiles, which stay in registers for all graphs
+    __syncthreads();  // the first barrier (the counters are zero)
+    auto row_of = [&](int m, int ee) { return wr * 64 + m * 32 + (ee & 3) + 8 * (ee >> 2) + 4 * (lane >> 5); };
+    // this lane's 16 values of accumulator m in tile ti's slot
+    auto slot_of = [&](int ti, int m) { return slots + (ti & 1) * kWsSlot + (e * 64 + lane) * 32 + m * 16; };
     struct Upd {
         uint32_t v[16];
         float th[16];
     };
     Upd ua, ub;
-    uint32_t t0a[16], t0b[16], t1a[16], t1b[16];  // thresholds: sub-tile 0 (m 0, 1), sub-tile 1 (m 0, 1)
     // the R sums of a tile's rows (I) and columns (J), double-buffered by tile
     float* const rbuf = reinterpret_cast<float*>(lds_dyn + (kDmaLds + 2 * kWsGraphLds) / 4);
     auto load_r = [&](int ti) {
+        if (te >= 2 * kT2) return;
         int bi, bj;
         tile_of(ti, bi, bj);
         const int row = (te < kT2 ? bi * kT2 : bj * kT2) + (te & (kT2 - 1));
         rbuf[(ti & 1) * 2 * kT2 + te] = row < n ? row_r_sum(r, (int64_t)row * ldr, ldrc, nr) : 0.f;
     };
-    auto issue_update = [&](int ti, int wr, int m, Upd& d) {
-        ws_ld16(d.v, slot_of(ti, wr, m));
+    auto issue_update = [&](int ti, int m, Upd& d) {
+        ws_ld16(d.v, slot_of(ti, m));
         const int j = j0 + jl;
 #pragma unroll
         for (int ee = 0; ee < 16; ++ee) {
-            const int i = i0 + row_of(wr, m, ee);
+            const int i = i0 + row_of(m, ee);
             const bool in = i < n && j < n && j >= i;
             d.th[ee] = in ? theta[in ? tri_at_t<SMALL>(i, j, nn) : 0] : 0.f;
         }
     };
-    // w8_epilogue's update (mode 2) of accumulator m of sub-tile wr (operands
-    // from issue_update): θ (and dθ) stored, the draw's thresholds written
-    // over the consumed accumulators
-    auto finish_update = [&](int ti, int wr, int m, const Upd& d) {
-        float* const sl = slot_of(ti, wr, m);
+    // w8_epilogue's update (mode 2) of accumulator m (operands from
+    // issue_update): θ (and dθ) stored, the draw's thresholds written over the
+    // consumed accumulators
+    auto finish_update = [&](int ti, int m, const Upd& d) {
+        float* const sl = slot_of(ti, m);
         const int j = j0 + jl;
         const float* const Rt = rbuf + (ti & 1) * 2 * kT2;
         const float rj = Rt[kT2 + jl];
         uint32_t thr[16];
 #pragma unroll
         for (int ee = 0; ee < 16; ++ee) {
-            const int li = row_of(wr, m, ee);
+            const int li = row_of(m, ee);
             const int i = i0 + li;
             thr[ee] = 0u;
             if (i >= n || j >= n || j < i) continue;
@@ -2071,9 +2110,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
                 *reinterpret_cast<u32x4*>(sl + 4 * e4) = u32x4{thr[4 * e4], thr[4 * e4 + 1], thr[4 * e4 + 2], thr[4 * e4 + 3]};
         }
     };
-    // graph g of sub-tile wr (its thresholds t0v / t1v): Philox words,
-    // ballots -> row segments / column words of buffer g & 1
-    auto draw_sub = [&](int g, int wr, const uint32_t (&t0v)[16], const uint32_t (&t1v)[16]) {
+    // graph g of the wave's sub-tile: Philox words, ballots -> row segments /
+    // column words of buffer g & 1 (w8_epilogue's draw)
+    auto draw_sub = [&](int ti, int g) {
         uint32_t* const rwb = gbuf + (g & 1) * (kWsGraphLds / 4);
         uint64_t* const cwb = reinterpret_cast<uint64_t*>(rwb + kT2 * 4);
         const uint32_t ctr = dr.counter + cb + (uint32_t)g;
@@ -2081,6 +2120,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
         uint64_t colw = 0;
 #pragma unroll 1
         for (int m = 0; m < 2; ++m) {
+            // the thresholds (L2: the slot), in flight beside the Philox rounds
+            uint32_t th[16];
+            ws_ld16(th, slot_of(ti, m));
             uint32_t x[16];
             const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;
 #pragma unroll
@@ -2094,8 +2136,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
             uint32_t mylo = 0, myhi = 0;
 #pragma unroll
             for (int ee = 0; ee < 16; ++ee) {
-                const uint32_t th = m == 0 ? t0v[ee] : t1v[ee];
-                const bool bit = (x[ee] >> 8) < th;
+                const bool bit = (x[ee] >> 8) < th[ee];
                 const uint64_t w = __ballot(bit);
                 mylo = lane == ee ? (uint32_t)w : mylo;
                 myhi = lane == ee ? (uint32_t)(w >> 32) : myhi;
@@ -2103,19 +2144,22 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
             }
             if (lane < 16) {
                 const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
-                rwb[rr * 4 + e] = mylo;
-                rwb[(rr + 4) * 4 + e] = myhi;
+                rwb[rr * 4 + wc] = mylo;
+                rwb[(rr + 4) * 4 + wc] = myhi;
             }
         }
         colw |= __shfl_xor(colw, 32);
-        if (lane < 32) cwb[wr * 128 + e * 32 + lane] = colw;
+        if (lane < 32) cwb[wr * 128 + wc * 32 + lane] = colw;
     };
     // graph g's words and degrees: one (row, two words) item per E thread
     auto store_graph = [&](int g) {
+        int tt = te;
+        asm volatile("" : "+v"(tt));  // (addresses rebuilt here, not kept live across the graph loop)
+        if (tt >= 2 * kT2) return;
         const uint32_t* const rwb = gbuf + (g & 1) * (kWsGraphLds / 4);
         const uint64_t* const cwb = reinterpret_cast<const uint64_t*>(rwb + kT2 * 4);
         const bool diag = i0 == j0;
-        const int part1 = te >> 7, x = te & 127;
+        const int part1 = tt >> 7, x = tt & 127;
         if (diag && part1) return;
         const int row = (part1 ? j0 : i0) + x;
         if (row >= n) return;
@@ -2143,66 +2187,54 @@ __global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
         const int pc = __popcll(w0) + __popcll(w1);
         if (pc != 0) atomicAdd(&da[row], pc);
     };
-    // the same barrier count as the M waves: nch intervals while they compute
-    // the first tile, then nch per tile (units 0 .. nu - 1, then idle ones)
-    auto bar = [&]() {
-        __builtin_amdgcn_s_barrier();
+    // the epilogue waves' own barrier, over their LDS work only (a release
+    // would also wait for the graph words' global stores and degree atomics in
+    // flight)
+    uint32_t ebars = 0;
+    auto ebar = [&]() {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS reads / writes done
+        ws_signal_relaxed(&ctr[3]);
+        ++ebars;
+        ws_wait<false>(&ctr[3], (uint32_t)kWsE * ebars);
         asm volatile("" ::: "memory");
     };
-    for (int b = 0; b < nch; ++b) {
-        bar();
-        if (b == 0) load_r(0);  // (read from the tile's first unit on, nch - 1 barriers later)
-    }
+    load_r(0);
+    const bool draw = G > 0 && LDS_WS_ABL != 2;
     for (int ti = 0; ti < T; ++ti) {
-        // straight-line units, one per interval: each issues the next unit's
-        // loads before its own work (the E waves are one per SIMD: an exposed
-        // round trip per unit would set the k-loop waves' pace); stores drain
-        // on their own, except the thresholds, which a later unit reads back
-        bar();  // the tile's accumulators are in its slot now
+        ws_wait(&ctr[1], (uint32_t)kWsM * (ti + 1));  // the tile's accumulators are in its slot
+        if (LDS_WS_ABL == 1) {  // (timing only: the k-loop waves alone)
+            ws_signal(&ctr[2]);
+            continue;
+        }
+        ebar();  // (the R sums of the tile, and every read of the previous tile's graph buffers, done)
         {
             int bi, bj;
             tile_of(ti, bi, bj);
             i0 = bi * kT2;
             j0 = bj * kT2;
         }
-        issue_update(ti, 0, 0, ua);
-        issue_update(ti, 0, 1, ub);
-        finish_update(ti, 0, 0, ua);
-        bar();
-        issue_update(ti, 1, 0, ua);
-        finish_update(ti, 0, 1, ub);
-        bar();
-        issue_update(ti, 1, 1, ub);
-        finish_update(ti, 1, 0, ua);
-        bar();
-        const bool draw = G > 0 && LDS_WS_ABL != 2;
-        if (draw) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sub-tile 0's thresholds stored
-            ws_ld16(t0a, slot_of(ti, 0, 0));
-            ws_ld16(t0b, slot_of(ti, 0, 1));
-        }
-        finish_update(ti, 1, 1, ub);
+        issue_update(ti, 0, ua);
+        issue_update(ti, 1, ub);
+        finish_update(ti, 0, ua);
+        finish_update(ti, 1, ub);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the thresholds stored
         if (ti + 1 < T) load_r(ti + 1);  // the other buffer: read after the next tile's first barrier
-        if (G > 0) {
-            for (int v = 0; v < 2 * G; ++v) {  // graph v / 2, sub-tile v % 2
-                bar();
-                if (!draw) continue;
-                if (v == 0) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // sub-tile 1's thresholds stored
-                    ws_ld16(t1a, slot_of(ti, 1, 0));
-                    ws_ld16(t1b, slot_of(ti, 1, 1));
-                }
-                const int g = v >> 1;
-                if ((v & 1) == 0 && g > 0) store_graph(g - 1);
-                if (v & 1) draw_sub(g, 1, t1a, t1b);
-                else draw_sub(g, 0, t0a, t0b);
+        if (draw) {
+            draw_sub(ti, 0);
+            for (int g = 1; g < G; ++g) {
+                ebar();
+                store_graph(g - 1);
+                draw_sub(ti, g);
             }
-            bar();
-            if (draw) store_graph(G - 1);
+            ebar();
+            store_graph(G - 1);
         }
-        for (int k = nu; k < nch; ++k) bar();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every read of the slot returned
+        ws_signal(&ctr[2]);                                // the slot may take tile ti + 2
     }
 }
+
+
 
 
 static int ws_cus() {
@@ -2219,15 +2251,13 @@ static int ws_bpx(int ntiles) {
     return per_xcd < cap ? per_xcd : cap;
 }
 
-// The persistent form applies (mode 2, any draw): the epilogue's units fit the
-// intervals of a tile's chunk stream, and the grid has at least two tiles per
-// block (one tile per CU: form 10 itself, which has no second tile to overlap).
-static bool ws_applies(int n, int k, int graphs) {
+// The persistent form applies (mode 2, any draw) when the grid has at least
+// two tiles per block (one tile per CU: form 10 itself, which has no second
+// tile to overlap).
+static bool ws_applies(int n, int k) {
     const int nb = (n + kT2 - 1) / kT2;
     const int ntiles = nb * (nb + 1) / 2;
-    const int nch = (k + 15) / 16;
-    const int nu = 4 + (graphs > 0 ? 2 * graphs + 1 : 0);
-    return k > 0 && nu <= nch && ntiles >= 2 * 8 * ws_bpx(ntiles);
+    return k > 0 && ntiles >= 2 * 8 * ws_bpx(ntiles);
 }
 
 static void launch_ws(hipStream_t st, const uint16_t* up, const uint16_t* vp, int nt, int k, const float* r, int ldr,
@@ -2695,7 +2725,7 @@ extern "C" int lds_theta_grad_direct_ws(const uint16_t* up, const uint16_t* vp, 
     const DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                       counter_offset, counter_base, graphs};
     if (handoff != nullptr && handoff_floats >= lds_theta_grad_ws_floats() && (((uintptr_t)handoff) & 15) == 0 &&
-        ws_applies(n, k, graphs))
+        ws_applies(n, k))
         launch_ws((hipStream_t)stream, up, vp, nt, k, r, ldr_row, nr, theta, n, grad, lr, ldr_col, gscale, handoff, dr);
     else  // form 10 (the same results)
         launch_dma((hipStream_t)stream, up, vp, nt, k, r, ldr_row, nr, theta, n, grad, 2, lr, ldr_col, gscale,
