@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 16
+#define LDS_ABI_VERSION 15
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -369,28 +369,6 @@ int lds_theta_grad_direct(const uint16_t* up, const uint16_t* vp, int k, const f
                           const void* scalars, float gscale, uint64_t seed, uint32_t tag,
                           const uint32_t* counter_base, uint32_t counter_offset, int graphs,
                           uint64_t* bits, int words, int* deg_ws, void* stream);
-/* lds_theta_grad_direct in mode 2 (SGD + clamp, with the next window's draw
- * of `graphs` graphs when graphs > 0) as a persistent warp-specialised
- * kernel (ABI 16): one block per CU walks its 128 × 128 tiles; eight waves
- * run the k-loop over the block's chunk stream without a break between
- * tiles and hand each finished tile's accumulators to the block's slots in
- * `handoff` (global memory, L2-resident), eight waves run the previous
- * tile's epilogue (θ update, Philox draw, bit rows, degree counts) on the
- * VALU meanwhile; the two kinds of waves synchronise through LDS counters,
- * so neither waits for the other's steps.  Taken at two or more tiles per
- * block (large n); otherwise, or with handoff == NULL / too small, the call
- * runs lds_theta_grad_direct (mode 2).  Same result bits either way.
- * handoff: >= lds_theta_grad_ws_floats() floats, 16-byte aligned, contents
- * unused between calls.  Replaces, fused: src/trainers/outer.py:77-81 and
- * src/models/sampling.py:68 (as lds_theta_grad_direct). */
-int lds_theta_grad_direct_ws(const uint16_t* up, const uint16_t* vp, int k, const float* r, int ldr_row,
-                             int ldr_col, int nr, float* theta, int n, float* grad, const void* scalars,
-                             float gscale, uint64_t seed, uint32_t tag, const uint32_t* counter_base,
-                             uint32_t counter_offset, int graphs, uint64_t* bits, int words, int* deg_ws,
-                             float* handoff, int64_t handoff_floats, void* stream);
-/* Floats of lds_theta_grad_direct_ws's hand-off buffer on the current device
- * (two 32 × 32-float slots per lane of each block's eight k-loop waves). */
-int64_t lds_theta_grad_ws_floats(void);
 /* uint16 count of the form-10 planes of `rows` rows × k columns:
  * ceil(k/16) · ceil(rows/128) · 6144.  Host-only. */
 int64_t lds_planes_t128_elems(int rows, int k);

@@ -1819,467 +1819,6 @@ static void launch_dma(hipStream_t st, const uint16_t* up, const uint16_t* vp, i
 #undef LDS_DMA_ARGS
 }
 
-// ---------------------------------------------------------------------------
-// Persistent warp-specialised form of the direct-staged θ-grad with the draw
-// (form 10 + DRAW at many tiles per CU; round 5).  Form 10 runs one 128 × 128
-// tile per block at a time: the Philox epilogue of the next window's draw
-// (VALU) follows the k-loop (MFMA) in the same waves, and with 144 KB of LDS
-// per block nothing else runs on the CU meanwhile.  Here one block per CU
-// walks its tiles with two kinds of waves:
-//  * waves 0-7 (M) run form 10's k-loop over the block's chunk stream without
-//    a break between tiles (the LDS-DMA ring continues into the next tile's
-//    chunks) and hand each finished tile's raw accumulators to a per-block
-//    slot in global memory (L2; two slots, alternating);
-//  * waves 8-15 (E) run the previous tile's epilogue meanwhile — w8_epilogue's
-//    arithmetic for the sub-tile of M wave e, then the draw graph by graph —
-//    on the VALU while the matrix pipe multiplies (separate pipes:
-//    MI355X_MICROARCH.md "Wave scheduling").
-// The two kinds never share an s_barrier: LDS counters carry the k-loop's
-// chunk barrier (M only), the hand-off (tile ready / slot free) and the
-// epilogue's own barrier (E only), so neither waits for the other's steps.
-// Same chunks, same MFMA order per accumulator and the same epilogue
-// arithmetic and Philox counters as form 10: identical θ, dθ, bits, degrees.
-// ---------------------------------------------------------------------------
-constexpr int kWsM = 8;                                // MFMA waves (form 10's 2 × 4 sub-tiles)
-constexpr int kWsE = 8;                                // epilogue waves: wave 8 + e owns M wave e's sub-tile
-constexpr int kWsThreads = 64 * (kWsM + kWsE);
-constexpr int kWsSlot = kWsM * 64 * 32;                // floats per hand-off slot (the 8 waves' accumulators)
-constexpr int kWsHandoff = 2 * kWsSlot;                // floats per block
-constexpr int kWsGraphLds = kT2 * 4 * 4 + 2 * kT2 * 8; // bytes per graph buffer: row segments + column words
-constexpr int kWsLds = kDmaLds + 2 * kWsGraphLds + 2 * 2 * kT2 * 4 + 16;  // ring, graph buffers, R sums ×2, counters
-
-// The hand-off slot's values: plain 16-byte loads.  The slot is written and
-// read by waves of one workgroup (one CU's L1, write-through: no cache
-// maintenance within a workgroup), and the loads are the compiler's, so its
-// waits cover them.  (Loads issued from asm with a register binding read
-// stale thresholds in the first test runs.)
-__device__ __forceinline__ void ws_ld16(uint32_t* v, const float* p) {
-#pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-        const u32x4 x = *reinterpret_cast<const u32x4*>(p + 4 * e4);
-        v[4 * e4] = x[0];
-        v[4 * e4 + 1] = x[1];
-        v[4 * e4 + 2] = x[2];
-        v[4 * e4 + 3] = x[3];
-    }
-}
-#ifndef LDS_WS_ABL
-#define LDS_WS_ABL 0  // timing-only ablations of the persistent form (experiment builds only)
-#endif
-
-// The two kinds of waves synchronise through monotonic LDS counters, never a
-// shared s_barrier (which would tie every k-loop chunk to the slowest
-// epilogue step: measured 3.2 ms against 1.76 for the k-loop alone at
-// n = 20 000): one wave per group of eight adds 1, the others wait for a
-// target.  Every wait is bounded (a broken protocol gives wrong results, never
-// a hung GPU).
-__device__ __forceinline__ void ws_signal(uint32_t* c) {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void ws_signal_relaxed(uint32_t* c) {
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-template <bool kAcquire = true>
-__device__ __forceinline__ void ws_wait(uint32_t* c, uint32_t target) {
-    for (int it = 0; it < (1 << 20); ++it) {
-        const uint32_t v = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(c, kAcquire ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (v >= target) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-template <bool SMALL>
-__global__ __launch_bounds__(kWsThreads, 1) void theta_grad_ws_kernel(
-    const uint16_t* __restrict__ up, const uint16_t* __restrict__ vp, int nt, int k,
-    const float* __restrict__ r, int ldr, int nr, float* __restrict__ theta, int n,
-    float* __restrict__ grad, const double* __restrict__ lr_dev, int ldrc, float gscale, int group,
-    int per_xcd, int bpx, float* __restrict__ handoff, DrawArgs dr) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    const int nb = (n + kT2 - 1) / kT2;
-    const int ntiles = nb * (nb + 1) / 2;
-    // this block's tiles: L0 + q + bpx·i within its XCD's range of the grouped order
-    const int q = (int)blockIdx.x >> 3;
-    const int L0 = ((int)blockIdx.x & 7) * per_xcd;
-    const int Lend = min(L0 + per_xcd, ntiles);
-    if (L0 + q >= Lend) return;  // whole block: no barrier reached
-    const int T = (Lend - (L0 + q) + bpx - 1) / bpx;
-    const int nch = (k + 15) / 16;
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int64_t nn = n;
-    float* const slots = handoff + (int64_t)blockIdx.x * kWsHandoff;
-    auto tile_of = [&](int ti, int& bi, int& bj) { grouped_tile(L0 + q + bpx * ti, nb, group, bi, bj); };
-    // LDS counters: k-loop chunk barrier, tiles handed off, tiles whose slot
-    // the epilogue no longer reads, epilogue barrier
-    uint32_t* const ctr = lds_dyn + (kWsLds - 16) / 4;
-    if (t < 4) ctr[t] = 0u;  // (the first __syncthreads below publishes them)
-
-    if (wave < kWsM && LDS_WS_ABL == 3) {  // (timing only: the epilogue waves alone, zero accumulators)
-        __syncthreads();
-        for (int ti = 0; ti < T; ++ti) {
-            if (ti >= 2) ws_wait(&ctr[2], (uint32_t)kWsM * (ti - 1));
-            float* const sl = slots + (ti & 1) * kWsSlot + (wave * 64 + lane) * 32;
-            for (int q = 0; q < 32; q += 4) *reinterpret_cast<float4*>(sl + q) = make_float4(0.f, 0.f, 0.f, 0.f);
-            __builtin_amdgcn_s_waitcnt(0x0070);
-            ws_signal(&ctr[1]);
-        }
-        return;
-    }
-    if (wave < kWsM) {
-        // ---- M: form 10's k-loop over the block's chunk stream -------------
-        const int wr = wave >> 2, wc = wave & 3;
-        const int G = T * nch;  // chunks of the stream
-        const uint32_t lds_base =
-            (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)lds_dyn);
-        const int64_t cstride = (int64_t)nt * kTileBlk;
-        auto fill = [&](int gc) {
-            const int ti = gc / nch, c = gc - ti * nch;
-            int bi, bj;
-            tile_of(ti, bi, bj);
-            const uint16_t* const opb[4] = {up + (int64_t)bi * kTileBlk, vp + (int64_t)bi * kTileBlk,
-                                            up + (int64_t)bj * kTileBlk, vp + (int64_t)bj * kTileBlk};
-            const int buf = gc % kDmaStages;
-#pragma unroll
-            for (int qq = 0; qq < 6; ++qq) {
-                const int b = wave + 8 * qq;
-                const int a = b / 12, p = b - 12 * a;
-                const uint16_t* src = (a == 0 ? opb[0] : a == 1 ? opb[1] : a == 2 ? opb[2] : opb[3]) +
-                                      c * cstride + 512 * p + 8 * lane;
-                lds_dma16(src, lds_base + (uint32_t)(buf * kDmaStageBytes + 1024 * b));
-            }
-        };
-        if (G > 0) fill(0);
-        if (G > 1) fill(1);
-        if (G > 2) fill(2);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the asm loads are not counted by the compiler
-        __syncthreads();                     // (the first barrier; E waves meet it too)
-
-        const int fo = 4 * ((lane >> 5) ^ ((lane >> 3) & 1));
-        const int ra0 = (wr * 64 + (lane & 31)) * kS2 + fo, ra1 = ra0 + 32 * kS2;
-        const int rb = (wc * 32 + (lane & 31)) * kS2 + fo;
-        f32x16 acc[2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
-        typedef bf16x8 Half[2][3 + 3];
-        auto read_half = [&](int gc, int pr, Half& f) {
-            const uint32_t* cur = lds_dyn + (gc % kDmaStages) * (kDmaStageBytes / 4);
-            const int pa = pr == 0 ? 0 : 3, pb = pr == 0 ? 9 : 6;
-#pragma unroll
-            for (int s = 0; s < 3; ++s) {
-                f[0][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra0));
-                f[1][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pa + s) * kPL2 + ra1));
-                f[0][3 + s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + (pb + s) * kPL2 + rb));
-            }
-        };
-        auto mfmas = [&](const Half& f) {
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const bf16x8* a = f[m];
-                const bf16x8* b = f[0] + 3;
-                f32x16 cc = acc[m];
-                cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], cc, 0, 0, 0);
-                cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], cc, 0, 0, 0);
-                cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], cc, 0, 0, 0);
-                cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], cc, 0, 0, 0);
-                cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], cc, 0, 0, 0);
-                cc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], cc, 0, 0, 0);
-                acc[m] = cc;
-            }
-        };
-        Half h0, h1;
-        if (G > 0) read_half(0, 0, h0);
-        for (int gc = 0; gc < G; ++gc) {
-            const int c = gc % nch;
-            read_half(gc, 1, h1);
-            mfmas(h0);
-            if (gc + 1 < G) {
-                // chunk gc + 1 landed (this wave's loads; the counter: every
-                // wave's) and this wave's reads of chunk gc returned, so its
-                // buffer may take chunk gc + 3
-                if (gc + 2 < G) __builtin_amdgcn_s_waitcnt(0x0076);  // vmcnt(6) lgkmcnt(0)
-                else __builtin_amdgcn_s_waitcnt(0x0070);             // vmcnt(0) lgkmcnt(0)
-                ws_signal_relaxed(&ctr[0]);
-                // (relaxed: an acquire would wait for the ring's loads in flight;
-                // the stage reads below depend on the loop's exit)
-                ws_wait<false>(&ctr[0], (uint32_t)kWsM * (gc + 1));
-                asm volatile("" ::: "memory");
-                if (gc + 3 < G) fill(gc + 3);
-                read_half(gc + 1, 0, h0);
-            }
-            mfmas(h1);
-            if (c == nch - 1) {  // tile done: its accumulators to slot (tile & 1), lane-major
-                const int ti = gc / nch;
-                if (ti >= 2) ws_wait(&ctr[2], (uint32_t)kWsM * (ti - 1));  // tile ti - 2 left the slot
-                float* const sl = slots + (ti & 1) * kWsSlot + (wave * 64 + lane) * 32;
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int e4 = 0; e4 < 4; ++e4)
-                        *reinterpret_cast<float4*>(sl + m * 16 + 4 * e4) =
-                            make_float4(acc[m][4 * e4], acc[m][4 * e4 + 1], acc[m][4 * e4 + 2], acc[m][4 * e4 + 3]);
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
-                __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the stores (and the ring's loads) done
-                ws_signal(&ctr[1]);                  // tile ti handed off
-            }
-        }
-        return;
-    }
-
-    // ---- E: the epilogue of tile ti during the nch intervals after its hand-off
-    // Units of a tile, one per interval (the host checks graphs + 3 <= nch):
-    // two updates (accumulator m of the wave's sub-tile), one draw per graph
-    // (both halves of the tile: all eight waves), the last graph's store.  A
-    // unit's memory operands are loaded by the unit before it (the accumulators
-    // and θ of the second update, the thresholds, kept in the hand-off slot
-    // over the consumed accumulators), and the R sums of the next tile go to
-    // LDS one tile ahead: an exposed round trip per unit would set the pace of
-    // the k-loop waves.
-    const int e = wave - kWsM;  // the M wave whose sub-tile this wave finishes
-    const int wr = e >> 2, wc = e & 3;
-    const int te = t - 64 * kWsM;
-    const int jl = wc * 32 + (lane & 31);
-    const float lr = (float)(*lr_dev);
-    const uint32_t cb = dr.counter_base != nullptr ? *dr.counter_base : 0u;
-    uint32_t* const gbuf = lds_dyn + kDmaLds / 4;  // two graph buffers
-    const int G = dr.graphs;
-    int i0 = 0, j0 = 0;
-    __syncthreads();  // the first barrier (the counters are zero)
-    auto row_of = [&](int m, int ee) { return wr * 64 + m * 32 + (ee & 3) + 8 * (ee >> 2) + 4 * (lane >> 5); };
-    // this lane's 16 values of accumulator m in tile ti's slot
-    auto slot_of = [&](int ti, int m) { return slots + (ti & 1) * kWsSlot + (e * 64 + lane) * 32 + m * 16; };
-    struct Upd {
-        uint32_t v[16];
-        float th[16];
-    };
-    Upd ua, ub;
-    // the R sums of a tile's rows (I) and columns (J), double-buffered by tile
-    float* const rbuf = reinterpret_cast<float*>(lds_dyn + (kDmaLds + 2 * kWsGraphLds) / 4);
-    auto load_r = [&](int ti) {
-        if (te >= 2 * kT2) return;
-        int bi, bj;
-        tile_of(ti, bi, bj);
-        const int row = (te < kT2 ? bi * kT2 : bj * kT2) + (te & (kT2 - 1));
-        rbuf[(ti & 1) * 2 * kT2 + te] = row < n ? row_r_sum(r, (int64_t)row * ldr, ldrc, nr) : 0.f;
-    };
-    auto issue_update = [&](int ti, int m, Upd& d) {
-        ws_ld16(d.v, slot_of(ti, m));
-        const int j = j0 + jl;
-#pragma unroll
-        for (int ee = 0; ee < 16; ++ee) {
-            const int i = i0 + row_of(m, ee);
-            const bool in = i < n && j < n && j >= i;
-            d.th[ee] = in ? theta[in ? tri_at_t<SMALL>(i, j, nn) : 0] : 0.f;
-        }
-    };
-    // w8_epilogue's update (mode 2) of accumulator m (operands from
-    // issue_update): θ (and dθ) stored, the draw's thresholds written over the
-    // consumed accumulators
-    auto finish_update = [&](int ti, int m, const Upd& d) {
-        float* const sl = slot_of(ti, m);
-        const int j = j0 + jl;
-        const float* const Rt = rbuf + (ti & 1) * 2 * kT2;
-        const float rj = Rt[kT2 + jl];
-        uint32_t thr[16];
-#pragma unroll
-        for (int ee = 0; ee < 16; ++ee) {
-            const int li = row_of(m, ee);
-            const int i = i0 + li;
-            thr[ee] = 0u;
-            if (i >= n || j >= n || j < i) continue;
-            const int64_t id = tri_at_t<SMALL>(i, j, nn);
-            const float t0 = d.th[ee];
-            float g = 0.f;
-            if (j > i) {
-                g = gscale * (__uint_as_float(d.v[ee]) + Rt[li] + rj);
-                if (!(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
-            }
-            if (grad != nullptr) grad[id] = g;
-            const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-            theta[id] = tn;
-            if (j > i) thr[ee] = (uint32_t)ceilf(tn * 16777216.0f);
-        }
-        if (G > 0) {
-#pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4)
-                *reinterpret_cast<u32x4*>(sl + 4 * e4) = u32x4{thr[4 * e4], thr[4 * e4 + 1], thr[4 * e4 + 2], thr[4 * e4 + 3]};
-        }
-    };
-    // graph g of the wave's sub-tile: Philox words, ballots -> row segments /
-    // column words of buffer g & 1 (w8_epilogue's draw)
-    auto draw_sub = [&](int ti, int g) {
-        uint32_t* const rwb = gbuf + (g & 1) * (kWsGraphLds / 4);
-        uint64_t* const cwb = reinterpret_cast<uint64_t*>(rwb + kT2 * 4);
-        const uint32_t ctr = dr.counter + cb + (uint32_t)g;
-        const int j = j0 + jl;
-        uint64_t colw = 0;
-#pragma unroll 1
-        for (int m = 0; m < 2; ++m) {
-            // the thresholds (L2: the slot), in flight beside the Philox rounds
-            uint32_t th[16];
-            ws_ld16(th, slot_of(ti, m));
-            uint32_t x[16];
-            const int rq0 = (i0 + wr * 64 + m * 32 + 4 * (lane >> 5)) >> 2;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)(rq0 + 2 * qd), dr.tag, ctr}, dr.k0, dr.k1);
-                x[4 * qd] = o.x;
-                x[4 * qd + 1] = o.y;
-                x[4 * qd + 2] = o.z;
-                x[4 * qd + 3] = o.w;
-            }
-            uint32_t mylo = 0, myhi = 0;
-#pragma unroll
-            for (int ee = 0; ee < 16; ++ee) {
-                const bool bit = (x[ee] >> 8) < th[ee];
-                const uint64_t w = __ballot(bit);
-                mylo = lane == ee ? (uint32_t)w : mylo;
-                myhi = lane == ee ? (uint32_t)(w >> 32) : myhi;
-                colw |= (uint64_t)bit << (m * 32 + (ee & 3) + 8 * (ee >> 2) + 4 * (lane >> 5));
-            }
-            if (lane < 16) {
-                const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
-                rwb[rr * 4 + wc] = mylo;
-                rwb[(rr + 4) * 4 + wc] = myhi;
-            }
-        }
-        colw |= __shfl_xor(colw, 32);
-        if (lane < 32) cwb[wr * 128 + wc * 32 + lane] = colw;
-    };
-    // graph g's words and degrees: one (row, two words) item per E thread
-    auto store_graph = [&](int g) {
-        int tt = te;
-        asm volatile("" : "+v"(tt));  // (addresses rebuilt here, not kept live across the graph loop)
-        if (tt >= 2 * kT2) return;
-        const uint32_t* const rwb = gbuf + (g & 1) * (kWsGraphLds / 4);
-        const uint64_t* const cwb = reinterpret_cast<const uint64_t*>(rwb + kT2 * 4);
-        const bool diag = i0 == j0;
-        const int part1 = tt >> 7, x = tt & 127;
-        if (diag && part1) return;
-        const int row = (part1 ? j0 : i0) + x;
-        if (row >= n) return;
-        uint64_t* __restrict__ gb = dr.bits + (int64_t)g * n * dr.words;
-        int* __restrict__ da = dr.dacc + (int64_t)g * dr.wsi;
-        uint64_t w0, w1;
-        int wbase;
-        if (part1) {
-            w0 = cwb[x];
-            w1 = cwb[128 + x];
-            wbase = i0 >> 6;
-        } else {
-            const uint32_t* rws = rwb + x * 4;
-            w0 = (uint64_t)rws[0] | ((uint64_t)rws[1] << 32);
-            w1 = (uint64_t)rws[2] | ((uint64_t)rws[3] << 32);
-            wbase = j0 >> 6;
-            if (diag) {
-                w0 |= cwb[x];
-                w1 |= cwb[128 + x];
-                if (x < 64) w0 |= 1ull << x;
-                else w1 |= 1ull << (x - 64);
-            }
-        }
-        *reinterpret_cast<ulonglong2*>(gb + (int64_t)row * dr.words + wbase) = ulonglong2{w0, w1};
-        const int pc = __popcll(w0) + __popcll(w1);
-        if (pc != 0) atomicAdd(&da[row], pc);
-    };
-    // the epilogue waves' own barrier, over their LDS work only (a release
-    // would also wait for the graph words' global stores and degree atomics in
-    // flight)
-    uint32_t ebars = 0;
-    auto ebar = [&]() {
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS reads / writes done
-        ws_signal_relaxed(&ctr[3]);
-        ++ebars;
-        ws_wait<false>(&ctr[3], (uint32_t)kWsE * ebars);
-        asm volatile("" ::: "memory");
-    };
-    load_r(0);
-    const bool draw = G > 0 && LDS_WS_ABL != 2;
-    for (int ti = 0; ti < T; ++ti) {
-        ws_wait(&ctr[1], (uint32_t)kWsM * (ti + 1));  // the tile's accumulators are in its slot
-        if (LDS_WS_ABL == 1) {  // (timing only: the k-loop waves alone)
-            ws_signal(&ctr[2]);
-            continue;
-        }
-        ebar();  // (the R sums of the tile, and every read of the previous tile's graph buffers, done)
-        {
-            int bi, bj;
-            tile_of(ti, bi, bj);
-            i0 = bi * kT2;
-            j0 = bj * kT2;
-        }
-        issue_update(ti, 0, ua);
-        issue_update(ti, 1, ub);
-        finish_update(ti, 0, ua);
-        finish_update(ti, 1, ub);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the thresholds stored
-        if (ti + 1 < T) load_r(ti + 1);  // the other buffer: read after the next tile's first barrier
-        if (draw) {
-            draw_sub(ti, 0);
-            for (int g = 1; g < G; ++g) {
-                ebar();
-                store_graph(g - 1);
-                draw_sub(ti, g);
-            }
-            ebar();
-            store_graph(G - 1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every read of the slot returned
-        ws_signal(&ctr[2]);                                // the slot may take tile ti + 2
-    }
-}
-
-
-
-
-static int ws_cus() {
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return cus >= 8 ? cus : 256;
-}
-
-// Blocks of the persistent form: 8 XCDs × bpx, at most one per CU and tile.
-static int ws_bpx(int ntiles) {
-    const int per_xcd = (ntiles + 7) / 8;
-    const int cap = ws_cus() / 8;
-    return per_xcd < cap ? per_xcd : cap;
-}
-
-// The persistent form applies (mode 2, any draw) when the grid has at least
-// two tiles per block (one tile per CU: form 10 itself, which has no second
-// tile to overlap).
-static bool ws_applies(int n, int k) {
-    const int nb = (n + kT2 - 1) / kT2;
-    const int ntiles = nb * (nb + 1) / 2;
-    return k > 0 && ntiles >= 2 * 8 * ws_bpx(ntiles);
-}
-
-static void launch_ws(hipStream_t st, const uint16_t* up, const uint16_t* vp, int nt, int k, const float* r, int ldr,
-                      int nr, float* theta, int n, float* grad, const double* lr, int ldrc, float gscale,
-                      float* handoff, const DrawArgs& dr) {
-    const int nb = (n + kT2 - 1) / kT2;
-    const int ntiles = nb * (nb + 1) / 2;
-    const int per = (ntiles + 7) / 8;
-    const int bpx = ws_bpx(ntiles);
-    const bool small = n <= 46340;
-#define LDS_WS_LAUNCH(SM)                                                                                        \
-    do {                                                                                                         \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&theta_grad_ws_kernel<SM>),                      \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kWsLds);                           \
-        hipLaunchKernelGGL(theta_grad_ws_kernel<SM>, dim3(8 * bpx), dim3(kWsThreads), kWsLds, st, up, vp, nt, k, \
-                           r, ldr, nr, theta, n, grad, lr, ldrc, gscale, 8, per, bpx, handoff, dr);               \
-    } while (0)
-    if (small) LDS_WS_LAUNCH(true);
-    else LDS_WS_LAUNCH(false);
-#undef LDS_WS_LAUNCH
-}
-
 // Assembly form: 0 = fp32 MFMA (v_mfma_f32_32x32x2_f32); split-bf16: 1 = by
 // shape (below), 2 = 64-tile with 16-wide k chunks, 3 = 64-tile with 32-wide
 // k chunks, 4 = 128-tile in plain triangle order, 5 = 128-tile in XCD-grouped
@@ -2704,32 +2243,6 @@ extern "C" int lds_theta_grad_direct(const uint16_t* up, const uint16_t* vp, int
                       counter_offset, counter_base, graphs};
     launch_dma((hipStream_t)stream, up, vp, nt, k, r, ldr_row, nr, theta, n, grad, mode, lr, ldr_col, gscale,
                graphs > 0 ? &dr : nullptr);
-    LDS_RETURN_LAST_ERROR();
-}
-
-// Hand-off floats of lds_theta_grad_direct_ws on this device (two 64-KB
-// accumulator slots per block of the persistent form).
-extern "C" int64_t lds_theta_grad_ws_floats(void) { return (int64_t)ws_cus() * kWsHandoff; }
-
-extern "C" int lds_theta_grad_direct_ws(const uint16_t* up, const uint16_t* vp, int k, const float* r, int ldr_row,
-                                        int ldr_col, int nr, float* theta, int n, float* grad, const void* scalars,
-                                        float gscale, uint64_t seed, uint32_t tag, const uint32_t* counter_base,
-                                        uint32_t counter_offset, int graphs, uint64_t* bits, int words, int* deg_ws,
-                                        float* handoff, int64_t handoff_floats, void* stream) {
-    LDS_CHECK_ARG(n > 0 && k >= 0 && nr >= 0 && graphs >= 0 && graphs <= 65535 && theta && scalars);
-    LDS_CHECK_ARG(k == 0 || (up != nullptr && vp != nullptr && ((((uintptr_t)up) | ((uintptr_t)vp)) & 15) == 0));
-    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
-    LDS_CHECK_ARG(graphs == 0 || (bits && deg_ws && (words & 1) == 0 && words >= 2 * ((n + 127) / 128)));
-    const double* lr = reinterpret_cast<const double*>((const char*)scalars + 16);
-    const int nt = (n + kT2 - 1) / kT2;
-    const DrawArgs dr{bits, words, deg_ws, lds_sample_ws_ints(n), (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                      counter_offset, counter_base, graphs};
-    if (handoff != nullptr && handoff_floats >= lds_theta_grad_ws_floats() && (((uintptr_t)handoff) & 15) == 0 &&
-        ws_applies(n, k))
-        launch_ws((hipStream_t)stream, up, vp, nt, k, r, ldr_row, nr, theta, n, grad, lr, ldr_col, gscale, handoff, dr);
-    else  // form 10 (the same results)
-        launch_dma((hipStream_t)stream, up, vp, nt, k, r, ldr_row, nr, theta, n, grad, 2, lr, ldr_col, gscale,
-                   graphs > 0 ? &dr : nullptr);
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -14,15 +14,14 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 16
+ABI_VERSION = 15
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
 P = c_void_p  # device pointers travel as integers
 
 # name -> argtypes (restype is always int = hipError_t, except where noted)
-_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset", "lds_planes_t128_elems", "lds_spmm_dense_ws_bytes",
-                "lds_theta_grad_ws_floats"}  # byte counts
+_RESTYPE_I64 = {"lds_bitmask_agg_ws_bytes", "lds_bitmask_agg_part_offset", "lds_planes_t128_elems", "lds_spmm_dense_ws_bytes"}  # byte counts
 SIGNATURES = {
     "lds_abi_version": [],
     "lds_graph_node_census": [P, P, c_int],
@@ -50,9 +49,6 @@ SIGNATURES = {
     "lds_split_planes_t128": [P, c_int, c_int, c_int, P, P],
     "lds_theta_grad_direct": [P, P, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_uint64, c_uint32,
                               P, c_uint32, c_int, P, c_int, P, P],
-    "lds_theta_grad_ws_floats": [],
-    "lds_theta_grad_direct_ws": [P, P, c_int, P, c_int, c_int, c_int, P, c_int, P, P, c_float, c_uint64, c_uint32,
-                                 P, c_uint32, c_int, P, c_int, P, P, c_int64, P],
     "lds_bitmask_fill_csr_ell": [P, c_int, c_int, P, P, c_int64, P, P, P, P],
     "lds_sample_graph": [P, c_int, c_uint64, c_uint32, c_uint32, P, P, c_int, P, P, P, c_int64, P,
                          P, P],

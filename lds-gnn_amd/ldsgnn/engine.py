@@ -344,10 +344,6 @@ class LdsEngine:
         # the by-shape default on Cora-sized grids): see _planes_window
         self.uv_planes = True
         self._planes_now = False
-        # many tiles per CU (large n): the persistent warp-specialised θ-grad
-        # with the draw (lds_theta_grad_direct_ws; _ws_shape), its hand-off buffer
-        self.theta_ws = True
-        self._handoff = None
         # θ-grad assembly form of this engine's launches (ldsgnn.ops.THETA_GRAD_FORMS
         # name; None: the module default ops.theta_grad_form() at launch time)
         self.theta_form = None
@@ -949,28 +945,7 @@ class LdsEngine:
         if self.outer_update is not None or self.theta_fn is not None or self.split_theta_grad:
             return False
         nb = (self.n + 127) // 128
-        return form == "bf16x3-direct" or (form == "bf16x3" and (nb * (nb + 1) // 2 <= 256 or self._ws_shape()))
-
-    def _ws_shape(self) -> bool:
-        """The persistent warp-specialised θ-grad (lds_theta_grad_direct_ws)
-        takes this shape: two or more 128-tiles per CU (large n; n = 20 000:
-        12 403 tiles).  Its fused draw then replaces the two-blocks-per-CU
-        128-tile form the by-shape rule picks there."""
-        if not self.theta_ws:
-            return False
-        nb = (self.n + 127) // 128
-        cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
-        return nb * (nb + 1) // 2 >= 2 * cus
-
-    def _handoff_ptr(self) -> int:
-        """The persistent θ-grad's hand-off buffer (allocated on first use), or
-        0 where the shape does not take that form."""
-        if not self._ws_shape():
-            return 0
-        if self._handoff is None:
-            self._handoff = torch.empty(int(nat.lib.lds_theta_grad_ws_floats()), dtype=torch.float32,
-                                        device=self.dev)
-        return nat.ptr(self._handoff)
+        return form == "bf16x3-direct" or (form == "bf16x3" and nb * (nb + 1) // 2 <= 256)
 
     def _uv(self):
         """(U, V, ld) of the factor producers' launches: fp32 rows (ld > 0) or,
@@ -1102,17 +1077,10 @@ class LdsEngine:
                     graphs = self.gbatch.count
                     bits, deg = nat.ptr(self.gbatch.bits), nat.ptr(self._deg_next)
                     drew = True
-                hp = self._handoff_ptr()
-                if hp:  # many tiles per CU: the persistent warp-specialised form (same bits)
-                    nat.call("lds_theta_grad_direct_ws", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1,
-                             1, 1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0,
-                             nat.ptr(self.scalars), 1.0, self.seed, self.tag_graph, nat.ptr(self.scalars),
-                             self.pending_graph, graphs, bits, self.words, deg, hp, self._handoff.numel(), st)
-                else:
-                    nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1,
-                             1, nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0, 2,
-                             nat.ptr(self.scalars), 1.0, self.seed, self.tag_graph, nat.ptr(self.scalars),
-                             self.pending_graph, graphs, bits, self.words, deg, st)
+                nat.call("lds_theta_grad_direct", nat.ptr(self.Up), nat.ptr(self.Vp), k0, nat.ptr(self.R), 1, 1, 1,
+                         nat.ptr(self.theta), n, nat.ptr(self.grad) if self.keep_grad else 0, 2,
+                         nat.ptr(self.scalars), 1.0, self.seed, self.tag_graph, nat.ptr(self.scalars),
+                         self.pending_graph, graphs, bits, self.words, deg, st)
             elif presampled and self._prefetch_ok(T, k0):  # + the next window's draw, from the θ written here
                 if self._deg_next is None:
                     self._deg_next = torch.zeros_like(self.gbatch.deg)

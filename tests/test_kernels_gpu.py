@@ -809,61 +809,6 @@ def test_theta_grad_direct_draw_equals_sgd_draw(device, n, k, graphs):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("n,k,graphs,keep", [(4100, 264, 6, False), (4100, 264, 0, True), (4500, 168, 2, True),
-                                               (3000, 264, 6, False)])
-def test_theta_grad_persistent_equals_direct(device, n, k, graphs, keep):
-    """The persistent warp-specialised form (lds_theta_grad_direct_ws: k-loop
-    waves hand each tile's accumulators to epilogue waves through the block's
-    L2 slots) against form 10 (lds_theta_grad_direct, mode 2): identical θ,
-    dθ, bit rows and degree counts.  Ragged n (rows past n in the last tile
-    row), with and without the draw and the dθ store; n = 3000 has fewer than
-    two tiles per block on a 256-CU device (the call then runs form 10)."""
-    g = torch.Generator().manual_seed(n + k + graphs)
-    u = torch.randn(n, k, generator=g).to(device)
-    v = (torch.randn(n, k, generator=g) * 0.3).to(device)
-    r = torch.randn(n, generator=g).to(device)
-    theta = (torch.rand(n * (n + 1) // 2, generator=g) * 1.2 - 0.1).to(device)  # some entries outside [0, 1]
-    scal = torch.zeros(64, dtype=torch.uint8, device=device)
-    scal[16:24].view(torch.float64).fill_(0.05)
-    st = nat.stream_of(torch.device(device))
-    words = nat.lib.lds_bitmask_words(n)
-    wsi = nat.lib.lds_sample_ws_ints(n)
-    base = torch.tensor([5, 0, 0, 0], dtype=torch.int32, device=device)
-    seed, tag, off = 777, tag_for(TAG_GRAPH, 1), 3
-    ne = nat.lib.lds_planes_t128_elems(n, k)
-    up = torch.empty(ne, dtype=torch.int16, device=device)
-    vp = torch.empty(ne, dtype=torch.int16, device=device)
-    nat.call("lds_split_planes_t128", nat.ptr(u), n, k, k, nat.ptr(up), st)
-    nat.call("lds_split_planes_t128", nat.ptr(v), n, k, k, nat.ptr(vp), st)
-    hf = int(nat.lib.lds_theta_grad_ws_floats())
-    handoff = torch.full((hf,), float("nan"), device=device)
-    res = []
-    for ws in (False, True):
-        th = theta.clone()
-        grad = torch.full_like(theta, float("nan")) if keep else None
-        bits = torch.zeros((max(graphs, 1), n, words), dtype=torch.int64, device=device)
-        deg = torch.zeros((max(graphs, 1), wsi), dtype=torch.int32, device=device)
-        gp = nat.ptr(grad) if keep else 0
-        if ws:
-            nat.call("lds_theta_grad_direct_ws", nat.ptr(up), nat.ptr(vp), k, nat.ptr(r), 1, 1, 1, nat.ptr(th), n, gp,
-                     nat.ptr(scal), 0.5, seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words, nat.ptr(deg),
-                     nat.ptr(handoff), hf, st)
-        else:
-            nat.call("lds_theta_grad_direct", nat.ptr(up), nat.ptr(vp), k, nat.ptr(r), 1, 1, 1, nat.ptr(th), n, gp,
-                     2, nat.ptr(scal), 0.5, seed, tag, nat.ptr(base), off, graphs, nat.ptr(bits), words,
-                     nat.ptr(deg), st)
-        torch.cuda.synchronize()
-        res.append((th, grad, bits, deg))
-    (ta, ga, ba, da), (tb, gb, bb, db) = res
-    assert not torch.equal(ta, theta)
-    assert torch.equal(ta, tb)
-    if keep:
-        assert torch.equal(ga, gb)
-    assert torch.equal(ba, bb) and torch.equal(da, db)
-    if graphs:
-        assert int(da.sum()) > 0
-
-
 def _spmm_dense(graph_rp, graph_col, s, n, z, ldz=16, out=None, ldy=16, beta=0, grid=0, expect_err=0, checked=True):
     """lds_spmm_norm_dense into `out` (or a new n × 16); the checked form
     (an error word) must read `expect_err` afterwards; checked=False runs the

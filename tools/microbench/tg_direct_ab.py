@@ -74,15 +74,10 @@ def run(name, n, k, graphs):
         torch.cuda.synchronize()
         return theta.clone(), grad.clone(), bits.clone(), deg.clone()
 
-    if os.environ.get("TG_WS_ONLY"):  # only the persistent form against form 10 (below)
-        graphs_only = True
-    else:
-        graphs_only = False
     ref_plain = state(lambda: plain(FORM9))
     out["plain_identical"] = all(bool(torch.equal(a, b)) for a, b in zip(ref_plain[:2], state(lambda: direct(0))[:2]))
-    for label, fn in (() if graphs_only else (("plain_form9", lambda: plain(FORM9)),
-                                              ("plain_by_shape", lambda: plain(FORM_BY_SHAPE)),
-                                              ("plain_form10", lambda: direct(0)))):
+    for label, fn in (("plain_form9", lambda: plain(FORM9)), ("plain_by_shape", lambda: plain(FORM_BY_SHAPE)),
+                      ("plain_form10", lambda: direct(0))):
         t = chain_us(fn, dev)
         out[label] = {"chain_us": t, "bf16_frac": flop / t / 1e6 / BF16_PEAK_TF}
     out["split_planes_us"] = chain_us(split, dev)
@@ -90,30 +85,12 @@ def run(name, n, k, graphs):
         ref = state(lambda: drawcall(FORM_BY_SHAPE))
         out["draw_identical"] = all(bool(torch.equal(a, b)) for a, b in zip(ref, state(lambda: direct(graphs))))
         zt = chain_us(lambda: deg.zero_(), dev)
-        for label, fn in (() if graphs_only else (("draw_by_shape", lambda: drawcall(FORM_BY_SHAPE)),
-                                                  ("draw_form10", lambda: direct(graphs)))):
+        for label, fn in (("draw_by_shape", lambda: drawcall(FORM_BY_SHAPE)), ("draw_form10", lambda: direct(graphs))):
             def f2(fn=fn):
                 fn()
                 deg.zero_()
             t = chain_us(f2, dev) - zt
             out[label] = {"chain_us": t, "bf16_frac": flop / t / 1e6 / BF16_PEAK_TF}
-    if graphs > 0 and os.environ.get("TG_WS"):  # the persistent warp-specialised form (lds_theta_grad_direct_ws)
-        hf = int(nat.lib.lds_theta_grad_ws_floats())
-        handoff = torch.empty(hf, device=dev)
-
-        def wscall():
-            nat.call("lds_theta_grad_direct_ws", nat.ptr(up), nat.ptr(vp), k, nat.ptr(r), 1, n, 1, nat.ptr(theta), n,
-                     nat.ptr(grad), nat.ptr(scal), 1.0, seed, tag, nat.ptr(base), 0, graphs, nat.ptr(bits), words,
-                     nat.ptr(deg), nat.ptr(handoff), hf, nat.stream_of(dev))
-        ref = state(lambda: direct(graphs))
-        out["ws_identical"] = all(bool(torch.equal(a, b)) for a, b in zip(ref, state(wscall)))
-        zt = chain_us(lambda: deg.zero_(), dev)
-
-        def f3():
-            wscall()
-            deg.zero_()
-        t = chain_us(f3, dev) - zt
-        out["draw_ws"] = {"chain_us": t, "bf16_frac": flop / t / 1e6 / BF16_PEAK_TF}
     print(json.dumps(out), flush=True)
 
 
