@@ -646,6 +646,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--theta-form", default=None, help="θ-grad assembly form (ldsgnn.ops.THETA_GRAD_FORMS; "
                     "default: bf16x3, the split-bf16 MFMA form picked by shape)")
+    ap.add_argument("--two-hop-outer", type=int, default=1, choices=[0, 1], help="engine: the outer step's loss layer "
+                    "as one two-hop launch (lds_engine_fwd2_bwd2 over the opt rows; 1, the default) or as "
+                    "fwd_layer2 + bwd_layer2 (0)")
     ap.add_argument("--async-draw", action="store_true", help="engine: draw a window's graphs 1..τ on a side "
                     "stream beside inner step 0 (graph 0 on the main stream; without prefetched draws)")
     ap.add_argument("--xt-pair", type=int, default=0, choices=[0, 1, 2], help="engine: W0 products over pairs of "
@@ -753,6 +756,7 @@ def main():
             exchange_label = f"{args.backend}-allreduce-" + ("captured" if capture_exchange else "split")
         args.capture_exchange = capture_exchange  # (the strong-scaling leg's TN captures the same way)
         eng.async_draw = bool(args.async_draw)
+        eng.two_hop_outer = bool(args.two_hop_outer)
         if not args.keep_theta_grad:  # θ.grad not materialised (the fused update consumes dθ)
             eng.keep_grad = False
             runner.outer_trainer.model.probs.grad = None
@@ -848,6 +852,7 @@ def main():
             window["bitmask_aggregation"]["share_of_window"] = agg_rows[0]["us_per_window"] / total
 
     prefetched = bool(use_engine and eng.prefetch_draw)  # (the strong leg below frees the engine)
+    two_hop_outer = bool(use_engine and eng.two_hop_outer)
     form_name = eng._form_name() if use_engine else ldsops.theta_grad_form()
     strong = None
     if use_engine and args.strong_total and not param_theta:
@@ -874,6 +879,7 @@ def main():
                        "windows_per_graph": (args.graph_windows if whole else 1)
                        if use_engine and use_graph else None,
                        "prefetched_draw": prefetched, "async_draw": bool(args.async_draw),
+                       "two_hop_outer": two_hop_outer if use_engine else None,
                        "theta_grad_written": bool(args.keep_theta_grad) or reducer is not None
                        if use_engine else True,
                        "xt_pair": args.xt_pair, "exchange": exchange_label if use_engine else None},

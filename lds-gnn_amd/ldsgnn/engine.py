@@ -234,9 +234,13 @@ class LdsEngine:
         # two-hop loss kernels (lds_engine_fwd2_bwd2 / lds_engine_rev_bc): need the
         # ELL head with node flags, i.e. in-kernel aggregation (short rows)
         self.two_hop = not self.long_rows
-        # the outer step's loss (opt mask, ~2x the train rows): separate launches
-        # measured faster (more masked neighbours per row -> more rounds)
-        self.two_hop_outer = False
+        # the outer step's loss (opt mask, ~2x the train rows) as one two-hop
+        # launch too.  Round 2 measured the separate launches faster (more
+        # masked neighbours per row -> more rounds); with the two-hop kernels'
+        # own row plan (rows with many masked neighbours on blocks of their own)
+        # the one launch now wins by ≈2 µs per window at Cora (round 5: 14.52k
+        # against 14.48k steps/s, 56 launches per window; bench --two-hop-outer)
+        self.two_hop_outer = True
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
         if long_rows_kernel not in ("bitmask", "csr", "blocked"):
