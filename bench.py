@@ -401,6 +401,18 @@ def window_breakdown(eng, reducer, args, device, k=20, reps=10, rounds=5):
 
 
 def roofline_of(row, args):
+    """The roofline entry of the window's dominant kernel.  Its duration is the
+    call's time as a dependent chain of copies in one HIP graph (HIP events on
+    the launch stream: the kernel plus the graph's launch gap, the figure a
+    rocprofv3 --kernel-trace --stats average of the same launch matches); the
+    in-window marginal cost, which also carries the wait for the previous
+    launch's writes, is kept beside it (in_window_us)."""
+    us = row["chain_avg_us"]
+    scale = row["avg_us"] / us  # in-window rates -> chain rates
+    row = dict(row)
+    for key in ("achieved_tops", "achieved_tflops", "achieved_GBs"):
+        if key in row:
+            row[key] = row[key] * scale
     if row["bound"] == "mfma_i8":  # the config-5 bitmask aggregation: int8 MFMA, HBM fraction alongside
         achieved = row["achieved_tops"]
         roof = {"bound": "mfma", "achieved": achieved, "peak": INT8_PEAK_TOPS, "unit": "TOP/s (int8)",
@@ -417,8 +429,8 @@ def roofline_of(row, args):
         achieved = row.get("achieved_GBs", 0.0)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS}
-    roof.update(kernel=row["entry"], avg_us=row["avg_us"], launches_per_window=row["launches_per_window"],
-                share_of_window=None)
+    roof.update(kernel=row["entry"], avg_us=us, in_window_us=row["avg_us"],
+                launches_per_window=row["launches_per_window"], share_of_window=None)
     if row["entry"] in ("lds_theta_grad_sgd_draw", "lds_theta_grad_direct"):  # priced on the assembly's flops alone
         roof["includes"] = "the next window's graph draw (tau+1 graphs, Philox VALU) in the epilogue"
     if row["entry"] == "lds_theta_grad_direct":
