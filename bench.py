@@ -661,6 +661,9 @@ def main():
     ap.add_argument("--two-hop-outer", type=int, default=1, choices=[0, 1], help="engine: the outer step's loss layer "
                     "as one two-hop launch (lds_engine_fwd2_bwd2 over the opt rows; 1, the default) or as "
                     "fwd_layer2 + bwd_layer2 (0)")
+    ap.add_argument("--sgd-draw-split", type=int, default=1, choices=[0, 1], help="engine, exchange path: the "
+                    "SGD + next-window draw (lds_sgd_sample_graphs) with the replica samples split over more "
+                    "blocks (1, the default) or one block per tile (0)")
     ap.add_argument("--async-draw", action="store_true", help="engine: draw a window's graphs 1..τ on a side "
                     "stream beside inner step 0 (graph 0 on the main stream; without prefetched draws)")
     ap.add_argument("--xt-pair", type=int, default=0, choices=[0, 1, 2], help="engine: W0 products over pairs of "
@@ -769,6 +772,7 @@ def main():
         args.capture_exchange = capture_exchange  # (the strong-scaling leg's TN captures the same way)
         eng.async_draw = bool(args.async_draw)
         eng.two_hop_outer = bool(args.two_hop_outer)
+        eng.sgd_draw_split = bool(args.sgd_draw_split)
         if not args.keep_theta_grad:  # θ.grad not materialised (the fused update consumes dθ)
             eng.keep_grad = False
             runner.outer_trainer.model.probs.grad = None

@@ -135,11 +135,16 @@ int lds_sample_ws_ints(int n);
  * counters / tags as lds_sample_graphs_multi, the graph counter and the f64
  * lr read from the engine's `scalars`); bits and degree counts as
  * lds_sample_graphs_multi's tile kernel (deg_ws zero on entry), no fill.
+ * tile_ctr (NULL or lds_sgd_tile_ints(n) ints, zero on entry and left zero):
+ * per-tile counters that let the replica samples split over more blocks
+ * (the tile's last block writes the new θ); same θ and draws either way.
  * Replaces, fused: src/trainers/outer.py:78-81 (SGD + clamp after the
  * all-reduce) and the next window's src/models/sampling.py:68 draws. */
 int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, int n, uint64_t seed,
                           uint32_t tag, uint32_t tag_step, uint32_t counter_offset, int count,
-                          int samples, uint64_t* bits, int words, int* deg_ws, void* stream);
+                          int samples, uint64_t* bits, int words, int* deg_ws, int* tile_ctr, void* stream);
+/* Ints of lds_sgd_sample_graphs' tile counters: the triangle's 64×64 tiles. */
+int lds_sgd_tile_ints(int n);
 
 /* The fill launch of lds_sample_graphs_multi alone (CSR, s, ELL head of
  * `graphs` graphs whose bits and degree counts are already drawn, e.g. by

@@ -40,17 +40,24 @@ namespace lds {
 // on entry.  (Per-64-row-block totals kept the same way cost 2x the kernel's
 // time: ~10^4 atomics per graph on three cache lines serialise at the memory
 // side.)
-// kSgd (lds_sgd_sample_graphs, one block per tile, kLoop): the tile first
-// applies the outer SGD step θ <- clamp(θ - lr·g, 0, 1) (lr = the engine's
-// device f64 at lr_dev; the arithmetic of lds_engine_sgd_clamp) to every
-// packed entry it owns (i <= j) and writes it back, then draws from the new θ.
+// kSgd (lds_sgd_sample_graphs, kLoop): the tile computes the outer SGD step
+// θ <- clamp(θ - lr·g, 0, 1) (lr = the engine's device f64 at lr_dev; the
+// arithmetic of lds_engine_sgd_clamp) of every packed entry it owns (i <= j)
+// and draws from the new θ.  With the samples split over grid.z, every block
+// of the tile reads the OLD θ, so the new one is written by the tile's last
+// block to finish (tile_ctr[tile] counts them; that block recomputes the
+// update from θ and g — nobody else writes them — and resets the counter):
+// a block counts itself only after its draws, i.e. after its θ loads
+// returned, so no block can read a θ already updated.  grid.z = 1: the one
+// block writes at its end.
 template <bool kInj, bool kLoop, bool kDeg, bool kSgd = false>
 __global__ __launch_bounds__(256) void sample_tiles_kernel(
     const float* __restrict__ theta, int n, uint32_t k0, uint32_t k1, uint32_t tag,
     uint32_t counter, const uint32_t* __restrict__ counter_base, const float* __restrict__ u_inj,
     uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs,
     int* __restrict__ dacc, int wsi, float* __restrict__ theta_w = nullptr,
-    const float* __restrict__ grad = nullptr, const double* __restrict__ lr_dev = nullptr) {
+    const float* __restrict__ grad = nullptr, const double* __restrict__ lr_dev = nullptr,
+    int* __restrict__ tile_ctr = nullptr) {
     // items are drawn in groups of kGrp: per item wave w leaves its column bits
     // (rows 16w .. 16w+15 of the tile) here, then wave q assembles item q's
     // column words — one barrier pair per group instead of per item
@@ -86,7 +93,6 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
             if (i <= j && j < n) {
                 const int64_t idx = tri_index(i, j, nn);
                 const float t = fminf(fmaxf(fmaf(-lr, grad[idx], theta_w[idx]), 0.f), 1.f);  // θ via theta_w only
-                theta_w[idx] = t;
                 if (i < j) th[r] = t;
             }
         }
@@ -199,6 +205,30 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
             }
         }
         if (base + kGrp < z1) __syncthreads();  // colpart / rowword are reused by the next group
+    }
+    if constexpr (kSgd) {
+        __shared__ int last_sh;
+        bool last = true;
+        if (gridDim.z > 1) {
+            __syncthreads();  // every thread's θ loads have returned (their draws are done)
+            if (threadIdx.x == 0) {
+                last_sh = atomicAdd(tile_ctr + tile, 1) == (int)gridDim.z - 1;
+                if (last_sh) tile_ctr[tile] = 0;
+            }
+            __syncthreads();
+            last = last_sh != 0;
+        }
+        if (last) {
+            const float lr = (float)*lr_dev;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = r0 + r;
+                if (i <= j && j < n) {
+                    const int64_t idx = tri_index(i, j, nn);
+                    theta_w[idx] = fminf(fmaxf(fmaf(-lr, grad[idx], theta_w[idx]), 0.f), 1.f);
+                }
+            }
+        }
     }
 }
 
@@ -480,25 +510,43 @@ __global__ void __launch_bounds__(256) zero_ints_kernel(int* __restrict__ p, int
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) p[i] = 0;
 }
 
+// the batched draw's target block count (16 waves per SIMD-slot's worth on
+// 256 CUs at 4 waves per block).  MI355X, window draw per call (sample
+// splits): Cora S = 16 358 µs unsplit, 317 at 2048 blocks, 310 at 4096, 314
+// at 8192; Citeseer S = 16 475 / 429 / 423 / 415; Cora S = 8 189 / 177 /
+// 175 / 180 (profiles/r03_draw_split.jsonl)
+constexpr int kDrawBlocks = 4096;
+
 // The outer SGD step + clamp (lds_engine_sgd_clamp) and the NEXT window's
 // draw of `count` graphs × `samples` replicas from the θ it writes, in one
 // pass over the triangle: graph g, sample b takes counter counter_offset + g
 // + the scalars' graph counter and tag + b·tag_step, as lds_sample_graphs_multi;
 // bits and degree counts as its tile kernel (deg_ws zero on entry); the fill
 // is left to the caller (lds_sample_fill_csr).  `scalars`: the engine's
-// EngineScalars (graph counter at byte 0, f64 lr at byte 16).
+// EngineScalars (graph counter at byte 0, f64 lr at byte 16).  tile_ctr
+// (optional): lds_sgd_tile_ints(n) ints, zero on entry and left zero — the
+// per-tile counters that let the samples split over grid.z (see the kernel).
+extern "C" int lds_sgd_tile_ints(int n) {
+    const int nb = (n + 63) / 64;
+    return nb * (nb + 1) / 2;
+}
+
 extern "C" int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, int n, uint64_t seed,
                                      uint32_t tag, uint32_t tag_step, uint32_t counter_offset, int count,
-                                     int samples, uint64_t* bits, int words, int* deg_ws, void* stream) {
+                                     int samples, uint64_t* bits, int words, int* deg_ws, int* tile_ctr,
+                                     void* stream) {
     LDS_CHECK_ARG(theta && grad && scalars && bits && deg_ws && n > 0 && n <= (1 << 20));
     LDS_CHECK_ARG(count > 0 && samples > 0 && (int64_t)count * samples <= 65535 && words >= (n + 63) / 64);
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
     const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true, true>), dim3(ntiles, 1, 1), dim3(256),
-                       0, (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag, counter_offset,
-                       (const uint32_t*)scalars, (const float*)nullptr, bits, words, ntiles, tag_step, samples, count,
-                       deg_ws, lds_sample_ws_ints(n), theta, grad, lr);
+    // samples split over grid.z as lds_sample_graphs_multi's draw (same draws)
+    // when the caller gives the per-tile counters; one block per tile without
+    const int zsplit = tile_ctr == nullptr ? 1 : std::max(1, std::min(samples, (kDrawBlocks + ntiles - 1) / ntiles));
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true, true>), dim3(ntiles, 1, zsplit),
+                       dim3(256), 0, (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                       counter_offset, (const uint32_t*)scalars, (const float*)nullptr, bits, words, ntiles, tag_step,
+                       samples, count, deg_ws, lds_sample_ws_ints(n), theta, grad, lr, tile_ctr);
     LDS_RETURN_LAST_ERROR();
 }
 
@@ -530,13 +578,6 @@ extern "C" int lds_sample_fill_csr(const uint64_t* bits, int n, int words, const
                        err);
     LDS_RETURN_LAST_ERROR();
 }
-
-// the batched draw's target block count (16 waves per SIMD-slot's worth on
-// 256 CUs at 4 waves per block).  MI355X, window draw per call (sample
-// splits): Cora S = 16 358 µs unsplit, 317 at 2048 blocks, 310 at 4096, 314
-// at 8192; Citeseer S = 16 475 / 429 / 423 / 415; Cora S = 8 189 / 177 /
-// 175 / 180 (profiles/r03_draw_split.jsonl)
-constexpr int kDrawBlocks = 4096;
 
 extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed, uint32_t tag,
                                        uint32_t tag_step, const uint32_t* counter_base,

@@ -40,7 +40,8 @@ SIGNATURES = {
     "lds_sample_ws_ints": [c_int],
     "lds_sample_fill_csr": [P, c_int, c_int, P, c_int, P, P, c_int64, P, P, P, P, P],
     "lds_sgd_sample_graphs": [P, P, P, c_int, c_uint64, c_uint32, c_uint32, c_uint32, c_int, c_int, P, c_int, P,
-                              P],
+                              P, P],
+    "lds_sgd_tile_ints": [c_int],
     "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int, P],
     "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int,
                               P],

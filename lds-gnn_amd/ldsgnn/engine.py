@@ -241,6 +241,11 @@ class LdsEngine:
         # the one launch now wins by ≈2 µs per window at Cora (round 5: 14.52k
         # against 14.48k steps/s, 56 launches per window; bench --two-hop-outer)
         self.two_hop_outer = True
+        # the exchange path's SGD + next-window draw (lds_sgd_sample_graphs)
+        # with the replica samples split over more blocks (per-tile counters;
+        # same θ and draws): False = one block per tile, the round-4 form
+        self.sgd_draw_split = True
+        self._sgd_tiles = None
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
         if long_rows_kernel not in ("bitmask", "csr", "blocked"):
@@ -1139,9 +1144,12 @@ class LdsEngine:
             if self._deg_next is None:
                 self._deg_next = torch.zeros_like(self.gbatch.deg)
             gb = self.gbatch
+            if self.sgd_draw_split and self._sgd_tiles is None:  # zero, and every call leaves it zero
+                self._sgd_tiles = torch.zeros(int(nat.lib.lds_sgd_tile_ints(self.n)), dtype=torch.int32,
+                                              device=self.theta.device)
             nat.call("lds_sgd_sample_graphs", P(self.theta), P(self.grad), P(self.scalars), self.n, self.seed,
                      self.tag_graph, 1, self.pending_graph, gb.count, self.S, P(gb.bits), self.words,
-                     P(self._deg_next), st)
+                     P(self._deg_next), P(self._sgd_tiles) if self.sgd_draw_split else 0, st)
             return True
         nat.call("lds_engine_sgd_clamp", P(self.theta), P(self.grad), self.theta.numel(), P(self.scalars), st)
         return False

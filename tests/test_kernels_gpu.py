@@ -423,6 +423,50 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
                     pc += (x >> k) & 1
             assert torch.equal(deg[gi, b, :n].long(), pc), (gi, b)
 
+@pytest.mark.parametrize("n,count,samples", [(300, 2, 3), (2708, 1, 8), (2708, 2, 5)])
+def test_sgd_sample_split_equals_one_block_per_tile(device, n, count, samples):
+    """lds_sgd_sample_graphs with the replica samples split over grid.z (tile
+    counters given; at Cora n, S = 8: five blocks per tile, ranges of two
+    samples and one empty block) against one block per tile (tile_ctr NULL):
+    bit-identical θ, bits and degree counts over two chained calls, θ equal to
+    lds_engine_sgd_clamp's, and the counters left zero."""
+    g = torch.Generator().manual_seed(n + samples)
+    m = n * (n + 1) // 2
+    theta0 = torch.rand(m, generator=g).to(device)
+    grads = [(torch.randn(m, generator=g) * 0.3).to(device) for _ in range(2)]
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    st = nat.stream_of(theta0.device)
+    scalars = torch.zeros(nat.lib.lds_engine_scalars_size(), dtype=torch.uint8, device=device)
+    scalars[:4].view(torch.int32).fill_(9)  # graph counter
+    scalars[16:24].view(torch.float64).fill_(0.37)  # lr
+    G = count * samples
+    tiles = torch.zeros(nat.lib.lds_sgd_tile_ints(n), dtype=torch.int32, device=device)
+    outs = []
+    for split in (False, True):
+        theta = theta0.clone()
+        got = []
+        for k, gr in enumerate(grads):
+            bits = torch.zeros((G, n, words), dtype=torch.int64, device=device)
+            deg = torch.zeros((G, wsi), dtype=torch.int32, device=device)
+            nat.call("lds_sgd_sample_graphs", nat.ptr(theta), nat.ptr(gr), nat.ptr(scalars), n, 4321,
+                     tag_for(TAG_GRAPH, 3), 1, 2 + 5 * k, count, samples, nat.ptr(bits), words, nat.ptr(deg),
+                     nat.ptr(tiles) if split else 0, st)
+            got.append((theta.clone(), bits, deg))
+        torch.cuda.synchronize()
+        assert int(tiles.abs().sum()) == 0
+        outs.append(got)
+    for (ta, ba, da), (tb, bb, db) in zip(*outs):
+        assert torch.equal(ta, tb)
+        assert torch.equal(ba, bb)
+        assert torch.equal(da, db)
+    want = theta0.clone()
+    for gr in grads:
+        nat.call("lds_engine_sgd_clamp", nat.ptr(want), nat.ptr(gr), m, nat.ptr(scalars), st)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[1][-1][0], want)
+
+
 def test_fill_guard_pads_inflated_degrees(device):
     """lds_sample_graphs_multi promised a zero degree workspace (ws_zeroed =
     1) that is not: every row's count exceeds its drawn bits.  The fill
