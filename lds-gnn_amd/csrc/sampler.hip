@@ -116,17 +116,28 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     // this one θ tile load (graph blockIdx.y + g draws counter + g); with
     // grid.z > 1 the samples are split into grid.z consecutive ranges, one per
     // block (more waves per SIMD to hide the Philox chains and the stores; the
-    // tile's θ is then loaded once per range — the same draws either way)
+    // tile's θ is then loaded once per range — the same draws either way).
+    // kSgd splits the flattened (graph, sample) items instead, so one sample
+    // (the N > 1 path's default) splits its graphs as well.
     const int zper = kLoop ? (samples + (int)gridDim.z - 1) / (int)gridDim.z : 1;
     const int zs = kLoop ? (int)blockIdx.z * zper : 0;
     const int zc = kLoop ? max(0, min(samples, zs + zper) - zs) : 1;
+    const int fper = (samples * graphs + (int)gridDim.z - 1) / (int)gridDim.z;  // kSgd: items per block
+    const int f0 = (int)blockIdx.z * fper;
     const int z0 = kLoop ? 0 : (int)blockIdx.z;
-    const int z1 = kLoop ? zc * graphs : z0 + 1;
+    const int z1 = kSgd ? max(0, min(samples * graphs, f0 + fper) - f0) : kLoop ? zc * graphs : z0 + 1;
     const bool rvalid = lane < 16 && r0 + lane < n;  // lane r stores row r0 + r's word
     // item -> (graph index, sample, counter, tag, its bits / degree slices)
     auto item = [&](int it, int& gidx, int& z) {
-        const int gl = kLoop ? it / zc : 0;
-        z = kLoop ? zs + (it - gl * zc) : it;
+        int gl;
+        if constexpr (kSgd) {
+            const int ig = f0 + it;
+            gl = ig / samples;
+            z = ig - gl * samples;
+        } else {
+            gl = kLoop ? it / zc : 0;
+            z = kLoop ? zs + (it - gl * zc) : it;
+        }
         gidx = (int)blockIdx.y + gl;
         return gl;
     };
@@ -540,9 +551,21 @@ extern "C" int lds_sgd_sample_graphs(float* theta, const float* grad, const void
     const int nb = (n + 63) / 64;
     const int ntiles = nb * (nb + 1) / 2;
     const double* lr = reinterpret_cast<const double*>(reinterpret_cast<const char*>(scalars) + 16);
-    // samples split over grid.z as lds_sample_graphs_multi's draw (same draws)
-    // when the caller gives the per-tile counters; one block per tile without
-    const int zsplit = tile_ctr == nullptr ? 1 : std::max(1, std::min(samples, (kDrawBlocks + ntiles - 1) / ntiles));
+    // with replica samples and the per-tile counters: the (graph, sample)
+    // items split over grid.z towards kDrawBlocks blocks, at most one block per
+    // sample, as lds_sample_graphs_multi's draw splits its samples (same
+    // draws); one block per tile otherwise.  Measured at Cora (no-op exchange
+    // captured): S = 8 0.2748 / 0.2745 ms per step unsplit, 0.2716 / 0.2712
+    // with five blocks of ten items; S = 1 split into three blocks of two
+    // graphs LOST (13.5k against 13.9k steps/s: the extra θ and dθ reads and
+    // the counters cost more than the parallelism gains at six items a tile)
+    int zsplit = 1;
+    if (tile_ctr != nullptr) {
+        const int total = count * samples;
+        const int want = std::max(1, std::min(samples, (kDrawBlocks + ntiles - 1) / ntiles));
+        const int per = (total + want - 1) / want;
+        zsplit = (total + per - 1) / per;  // no empty block
+    }
     hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true, true>), dim3(ntiles, 1, zsplit),
                        dim3(256), 0, (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
                        counter_offset, (const uint32_t*)scalars, (const float*)nullptr, bits, words, ntiles, tag_step,

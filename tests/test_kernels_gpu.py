@@ -423,11 +423,12 @@ def test_batched_sampler_equals_single_draws(device, n, count, samples):
                     pc += (x >> k) & 1
             assert torch.equal(deg[gi, b, :n].long(), pc), (gi, b)
 
-@pytest.mark.parametrize("n,count,samples", [(300, 2, 3), (2708, 1, 8), (2708, 2, 5)])
+@pytest.mark.parametrize("n,count,samples", [(300, 2, 3), (2708, 1, 8), (2708, 2, 5), (2708, 6, 1), (300, 6, 1)])
 def test_sgd_sample_split_equals_one_block_per_tile(device, n, count, samples):
-    """lds_sgd_sample_graphs with the replica samples split over grid.z (tile
-    counters given; at Cora n, S = 8: five blocks per tile, ranges of two
-    samples and one empty block) against one block per tile (tile_ctr NULL):
+    """lds_sgd_sample_graphs with its (graph, sample) items split over grid.z
+    (tile counters given; at Cora n, 6 graphs × 8 samples: five blocks per
+    tile of ten items; one sample: one block, the counters unused) against
+    one block per tile (tile_ctr NULL):
     bit-identical θ, bits and degree counts over two chained calls, θ equal to
     lds_engine_sgd_clamp's, and the counters left zero."""
     g = torch.Generator().manual_seed(n + samples)
