@@ -117,26 +117,22 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     // grid.z > 1 the samples are split into grid.z consecutive ranges, one per
     // block (more waves per SIMD to hide the Philox chains and the stores; the
     // tile's θ is then loaded once per range — the same draws either way).
-    // kSgd splits the flattened (graph, sample) items instead, so one sample
-    // (the N > 1 path's default) splits its graphs as well.
-    const int zper = kLoop ? (samples + (int)gridDim.z - 1) / (int)gridDim.z : 1;
-    const int zs = kLoop ? (int)blockIdx.z * zper : 0;
-    const int zc = kLoop ? max(0, min(samples, zs + zper) - zs) : 1;
-    const int fper = (samples * graphs + (int)gridDim.z - 1) / (int)gridDim.z;  // kSgd: items per block
-    const int f0 = (int)blockIdx.z * fper;
+    // The ranges are of the flattened (graph, sample) items, g-major, so the
+    // blocks of a tile get equal shares (±1) whatever divides what.
+    const int fper = kLoop ? (samples * graphs + (int)gridDim.z - 1) / (int)gridDim.z : 1;  // items per block
+    const int f0 = kLoop ? (int)blockIdx.z * fper : 0;
     const int z0 = kLoop ? 0 : (int)blockIdx.z;
-    const int z1 = kSgd ? max(0, min(samples * graphs, f0 + fper) - f0) : kLoop ? zc * graphs : z0 + 1;
+    const int z1 = kLoop ? max(0, min(samples * graphs, f0 + fper) - f0) : z0 + 1;
     const bool rvalid = lane < 16 && r0 + lane < n;  // lane r stores row r0 + r's word
     // item -> (graph index, sample, counter, tag, its bits / degree slices)
     auto item = [&](int it, int& gidx, int& z) {
-        int gl;
-        if constexpr (kSgd) {
+        int gl = 0;
+        if constexpr (kLoop) {
             const int ig = f0 + it;
             gl = ig / samples;
             z = ig - gl * samples;
         } else {
-            gl = kLoop ? it / zc : 0;
-            z = kLoop ? zs + (it - gl * zc) : it;
+            z = it;
         }
         gidx = (int)blockIdx.y + gl;
         return gl;
@@ -635,9 +631,16 @@ extern "C" int lds_sample_graphs_multi(const float* theta, int n, uint64_t seed,
     // replica samples and the window's graphs loop inside the block over one
     // θ tile load (θ read once per window)
     const int loop_graphs = count;
-    // replica samples split over grid.z so the launch has >= kDrawBlocks blocks
-    // (one sample range per block; same draws)
-    const int zsplit = std::max(1, std::min(samples, (kDrawBlocks + ntiles - 1) / ntiles));
+    // with replica samples, the (graph, sample) items split over grid.z so the
+    // launch has >= kDrawBlocks blocks, at most one block per sample and none
+    // empty (one item range per block; same draws)
+    int zsplit = 1;
+    {
+        const int total = count * samples;
+        const int want = std::max(1, std::min(samples, (kDrawBlocks + ntiles - 1) / ntiles));
+        const int per = (total + want - 1) / want;
+        zsplit = (total + per - 1) / per;
+    }
     if (samples > 1 || (loop_graphs > 1 && count > 1)) {
         if (fused)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, true>), dim3(ntiles, count / loop_graphs, zsplit),
