@@ -245,7 +245,9 @@ class LdsEngine:
         # with the replica samples split over more blocks (per-tile counters;
         # same θ and draws): False = one block per tile, the round-4 form
         self.sgd_draw_split = True
-        self._sgd_tiles = None
+        # its per-tile counters (zero, and every call leaves them zero), allocated
+        # here rather than on first use, which may fall inside a graph capture
+        self._sgd_tiles = torch.zeros(int(nat.lib.lds_sgd_tile_ints(n)), dtype=torch.int32, device=theta.device)
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
         if long_rows_kernel not in ("bitmask", "csr", "blocked"):
@@ -1144,9 +1146,6 @@ class LdsEngine:
             if self._deg_next is None:
                 self._deg_next = torch.zeros_like(self.gbatch.deg)
             gb = self.gbatch
-            if self.sgd_draw_split and self._sgd_tiles is None:  # zero, and every call leaves it zero
-                self._sgd_tiles = torch.zeros(int(nat.lib.lds_sgd_tile_ints(self.n)), dtype=torch.int32,
-                                              device=self.theta.device)
             nat.call("lds_sgd_sample_graphs", P(self.theta), P(self.grad), P(self.scalars), self.n, self.seed,
                      self.tag_graph, 1, self.pending_graph, gb.count, self.S, P(gb.bits), self.words,
                      P(self._deg_next), P(self._sgd_tiles) if self.sgd_draw_split else 0, st)
