@@ -661,6 +661,9 @@ def main():
     ap.add_argument("--two-hop-outer", type=int, default=1, choices=[0, 1], help="engine: the outer step's loss layer "
                     "as one two-hop launch (lds_engine_fwd2_bwd2 over the opt rows; 1, the default) or as "
                     "fwd_layer2 + bwd_layer2 (0)")
+    ap.add_argument("--fuse-fill", type=int, default=1, choices=[0, 1], help="engine, prefetched draws: the "
+                    "window's CSR fill in the first X-product launch (lds_engine_fill_x_linear; 1, the default) or "
+                    "as its own launch (0)")
     ap.add_argument("--sgd-draw-split", type=int, default=1, choices=[0, 1], help="engine, exchange path: the "
                     "SGD + next-window draw (lds_sgd_sample_graphs) with the replica samples split over more "
                     "blocks (1, the default) or one block per tile (0)")
@@ -773,6 +776,7 @@ def main():
         eng.async_draw = bool(args.async_draw)
         eng.two_hop_outer = bool(args.two_hop_outer)
         eng.sgd_draw_split = bool(args.sgd_draw_split)
+        eng.fuse_fill = bool(args.fuse_fill)
         if not args.keep_theta_grad:  # θ.grad not materialised (the fused update consumes dθ)
             eng.keep_grad = False
             runner.outer_trainer.model.probs.grad = None

@@ -533,7 +533,7 @@ int lds_engine_x_linear(const int* xrp, const int* xcol, const float* xval, int 
                         const int* csr2csc, const int* xhead, const int* xinfo, int head_vals,
                         const LdsBatch* batch, void* stream);
 /* lds_sample_fill_csr (CSR, s, ELL head of `graphs` drawn graphs) and
- * lds_engine_x_linear (one replica sample) in ONE launch: the first inner
+ * lds_engine_x_linear (every replica sample of `batch`) in ONE launch: the first inner
  * step's X product does not read the window's graphs, so a window that starts
  * from prefetched draws runs both halves side by side (blocks split by role)
  * with one dependent boundary instead of two.  Arguments as the two calls;

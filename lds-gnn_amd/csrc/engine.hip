@@ -582,8 +582,9 @@ __device__ __forceinline__ float x_wave_dot(const int* __restrict__ ptr, const i
 
 // out[i][h] = bias[h] + Σ_f Xd[i][f] · Wt[f][h]      (H0 = Xd W0ᵀ + b0)
 // Xd = dropout(X) with key (tag_x, fwd counter) when `train`, else X.
+// (row block bx of replica sample smp)
 template <bool kB>
-__device__ __forceinline__ void x_linear_rows(int bx,
+__device__ __forceinline__ void x_linear_rows(int bx, int smp,
     const int* __restrict__ xrp, const int* __restrict__ xcol, const float* __restrict__ xval, int n,
     const float* __restrict__ wt, const float* __restrict__ bias, float* __restrict__ out, Keys keys,
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
@@ -591,13 +592,13 @@ __device__ __forceinline__ void x_linear_rows(int bx,
     const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
     const int row = bx * 4 + wave_id();
     if (row >= n) return;
-    xval = boff<kB>(xval, bt.xval);
-    wt = boff<kB>(wt, bt.par);
-    bias = boff<kB>(bias, bt.par);
-    out = boff<kB>(out, bt.act);
-    xd_csr = boff<kB>(xd_csr, bt.xd);
-    xd_csc = boff<kB>(xd_csc, bt.xd);
-    bkeys<kB>(keys, bt);
+    xval = boffs<kB>(smp, xval, bt.xval);
+    wt = boffs<kB>(smp, wt, bt.par);
+    bias = boffs<kB>(smp, bias, bt.par);
+    out = boffs<kB>(smp, out, bt.act);
+    xd_csr = boffs<kB>(smp, xd_csr, bt.xd);
+    xd_csc = boffs<kB>(smp, xd_csc, bt.xd);
+    bkeys_s<kB>(smp, keys, bt);
     const int lane = threadIdx.x & 63;
     const float bl = (bias != nullptr && lane < HID) ? bias[lane] : 0.f;
     const uint32_t ctr = sc->fwd_ctr + fwd_off;
@@ -623,14 +624,17 @@ __global__ __launch_bounds__(256) void x_linear_kernel(
     const EngineScalars* __restrict__ sc, int fwd_off, int train, float keep, float scale,
     float* __restrict__ xd_csr, float* __restrict__ xd_csc, const int* __restrict__ csr2csc,
     const int* __restrict__ xhead, const int2* __restrict__ xinfo, int head_vals, Batch bt) {
-    x_linear_rows<kB>(blockIdx.x, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep, scale, xd_csr,
-                      xd_csc, csr2csc, xhead, xinfo, head_vals, bt);
+    x_linear_rows<kB>(blockIdx.x, blockIdx.y, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep,
+                      scale, xd_csr, xd_csc, csr2csc, xhead, xinfo, head_vals, bt);
 }
 
 // A window's first launch with prefetched draws: the CSR / s / ELL fill of its
 // graphs (fill.hpp; blocks [0, fill_blocks)) and the first inner step's
 // dropout(X)·W0ᵀ (the rest), which does not read the graphs — one launch and
-// one dependent boundary instead of two.
+// one dependent boundary instead of two.  kB: the X product of every replica
+// sample, sample-major after the fill blocks (one grid dimension, so no fill
+// block is repeated per sample).
+template <bool kB>
 __global__ __launch_bounds__(256) void fill_x_linear_kernel(
     const uint64_t* __restrict__ bits, int words, const int* __restrict__ dacc, int wsi, int graphs,
     int* __restrict__ row_ptr, int* __restrict__ gcol, int64_t capacity, float* __restrict__ gs,
@@ -647,8 +651,10 @@ __global__ __launch_bounds__(256) void fill_x_linear_kernel(
         fill_csr_block(b % fb, b / fb, bits, n, words, dacc, wsi, row_ptr, gcol, capacity, gs, ell, flags, err);
         return;
     }
-    x_linear_rows<false>(b - fb * graphs, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep, scale,
-                         xd_csr, xd_csc, csr2csc, xhead, xinfo, head_vals, bt);
+    const int xb = (n + 3) / 4, bx = b - fb * graphs;
+    const int smp = kB ? bx / xb : 0;
+    x_linear_rows<kB>(bx - smp * xb, smp, xrp, xcol, xval, n, wt, bias, out, keys, sc, fwd_off, train, keep, scale,
+                      xd_csr, xd_csc, csr2csc, xhead, xinfo, head_vals, bt);
 }
 
 // out[f][h] (= or +=) Σ_i Xd[i][f] · D[i][h]  (+ wd · w[f][h])   via CSC of X.
@@ -2467,10 +2473,9 @@ extern "C" int lds_engine_fill_x_linear(const uint64_t* bits, int words, const i
     LDS_CHECK_ARG(xhead == nullptr || xinfo != nullptr);
     Batch bt;
     const int ns = mk_batch(batch, bt);
-    LDS_CHECK_ARG(ns == 1);  // one replica sample (the prefetched-draw path)
-    const int64_t blocks = (int64_t)((n + 15) / 16) * graphs + (n + 3) / 4;
+    const int64_t blocks = (int64_t)((n + 15) / 16) * graphs + (int64_t)((n + 3) / 4) * ns;
     LDS_CHECK_ARG(blocks < (1ll << 31));
-    hipLaunchKernelGGL(fill_x_linear_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, bits, words,
+    LDS_LAUNCH_B(fill_x_linear_kernel, ns, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, bits, words,
                        deg_ws, lds_sample_ws_ints(n), graphs, row_ptr, col, col_stride, s, (int2*)ell, node_flags,
                        xrp, xcol, xval, n, wt, bias, out, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars,
                        fwd_off, train, keep, scale, xd_csr, xd_csc, csr2csc, xhead, (const int2*)xinfo, head_vals,

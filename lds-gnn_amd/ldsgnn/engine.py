@@ -881,7 +881,7 @@ class LdsEngine:
         if self._prefetched:  # bits + degrees drawn by the last hyper step (lds_theta_grad_sgd_draw)
             fill = (nat.ptr(gb.bits), self.words, nat.ptr(gb.deg), count * self.S, nat.ptr(gb.row_ptr),
                     self._col_arg(gb.col), max(self.cap, 1), nat.ptr(gb.s), nat.ptr(gb.ell), nat.ptr(self.nflag))
-            if self.fuse_fill and self.S == 1 and not self.long_rows:
+            if self.fuse_fill and not self.long_rows:
                 # deferred: the first inner step's X product launches it (lds_engine_fill_x_linear)
                 self._pending_fill = fill
             else:
