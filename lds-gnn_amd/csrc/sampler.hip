@@ -140,37 +140,13 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
 #pragma unroll 1
     for (int base = z0; base < z1; base += kGrp) {
         const int gn = min(kGrp, z1 - base);
-#pragma unroll 1
-        for (int q = 0; q < gn; ++q) {
+        // one item's words out of its draws e[16]: row words (lane r keeps row
+        // r's, from ballots), column bits per lane
+        auto emit = [&](int q, const bool (&e)[16]) {
             int gidx, z;
-            const int gl = item(base + q, gidx, z);
-            const uint32_t ctr = counter + (uint32_t)gl;
-            const uint32_t tg = tag + (uint32_t)z * tag_step;
+            item(base + q, gidx, z);
             uint64_t* __restrict__ gb = bits + ((int64_t)gidx * nsamp + z) * n * words;
             int* __restrict__ da = kDeg ? dacc + ((int64_t)gidx * nsamp + z) * wsi : nullptr;
-            // the draws of all 16 rows first: four independent Philox chains per lane
-            bool e[16];
-            if constexpr (kInj) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int i = r0 + r;
-                    const float u = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
-                    e[r] = th[r] >= 0.0f && u < fminf(th[r], 1.0f);
-                }
-            } else {
-                uint32_t x[16];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)((r0 >> 2) + m), tg, ctr}, k0, k1);
-                    x[4 * m] = o.x;
-                    x[4 * m + 1] = o.y;
-                    x[4 * m + 2] = o.z;
-                    x[4 * m + 3] = o.w;
-                }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) e[r] = (x[r] >> 8) < thr[r];
-            }
-            // row words out of ballots (lane r keeps row r's), column bits per lane
             uint32_t row_lo = 0, row_hi = 0, cw = 0;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -192,6 +168,43 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                 rowword[q][wave * 16 + lane] = myrow;
             }
             colpart[q][wave][lane] = cw;
+        };
+        if constexpr (kInj) {
+#pragma unroll 1
+            for (int q = 0; q < gn; ++q) {
+                bool e[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = r0 + r;
+                    const float u = (i < n && j < n) ? u_inj[(int64_t)i * nn + j] : 1.0f;
+                    e[r] = th[r] >= 0.0f && u < fminf(th[r], 1.0f);
+                }
+                emit(q, e);
+            }
+        } else {
+            // the draws of two items at a time: eight independent Philox chains
+            // per lane (an odd group's last pair draws its item twice, unused)
+#pragma unroll 1
+            for (int q = 0; q < gn; q += 2) {
+                bool e[2][16];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    int gidx, z;
+                    const int gl = item(base + min(q + h, gn - 1), gidx, z);
+                    const uint32_t ctr = counter + (uint32_t)gl;
+                    const uint32_t tg = tag + (uint32_t)z * tag_step;
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const U32x4 o = philox4x32_10(U32x4{(uint32_t)j, (uint32_t)((r0 >> 2) + m), tg, ctr}, k0, k1);
+                        e[h][4 * m] = (o.x >> 8) < thr[4 * m];
+                        e[h][4 * m + 1] = (o.y >> 8) < thr[4 * m + 1];
+                        e[h][4 * m + 2] = (o.z >> 8) < thr[4 * m + 2];
+                        e[h][4 * m + 3] = (o.w >> 8) < thr[4 * m + 3];
+                    }
+                }
+                emit(q, e[0]);
+                if (q + 1 < gn) emit(q + 1, e[1]);
+            }
         }
         __syncthreads();
         if (wave < gn) {  // wave q: the column words of item base + q
