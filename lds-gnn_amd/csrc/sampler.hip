@@ -182,13 +182,14 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                 emit(q, e);
             }
         } else {
-            // the draws of two items at a time: eight independent Philox chains
-            // per lane (an odd group's last pair draws its item twice, unused)
+            // the draws of kPar items at a time: 4·kPar independent Philox chains
+            // per lane (a short group's last pass redraws its last item, unused)
+            constexpr int kPar = 2;
 #pragma unroll 1
-            for (int q = 0; q < gn; q += 2) {
-                bool e[2][16];
+            for (int q = 0; q < gn; q += kPar) {
+                bool e[kPar][16];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
+                for (int h = 0; h < kPar; ++h) {
                     int gidx, z;
                     const int gl = item(base + min(q + h, gn - 1), gidx, z);
                     const uint32_t ctr = counter + (uint32_t)gl;
@@ -202,8 +203,9 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                         e[h][4 * m + 3] = (o.w >> 8) < thr[4 * m + 3];
                     }
                 }
-                emit(q, e[0]);
-                if (q + 1 < gn) emit(q + 1, e[1]);
+#pragma unroll
+                for (int h = 0; h < kPar; ++h)
+                    if (q + h < gn) emit(q + h, e[h]);
             }
         }
         __syncthreads();
