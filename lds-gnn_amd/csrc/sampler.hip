@@ -183,8 +183,9 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
             }
         } else {
             // the draws of kPar items at a time: 4·kPar independent Philox chains
-            // per lane (a short group's last pass redraws its last item, unused)
-            constexpr int kPar = 2;
+            // per lane (a short group's last pass redraws its last item, unused;
+            // one item per block without kLoop draws it alone)
+            constexpr int kPar = kLoop ? 2 : 1;
 #pragma unroll 1
             for (int q = 0; q < gn; q += kPar) {
                 bool e[kPar][16];
