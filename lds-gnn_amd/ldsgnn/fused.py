@@ -9,7 +9,7 @@ from __future__ import annotations
 
 from . import replicas as _replicas
 from . import rng as _rng
-from .engine import LdsEngine
+from .engine import LdsEngine, capture_into
 
 
 def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator" = None,
@@ -357,11 +357,14 @@ class FixedGraphGcn:
                 s = torch.cuda.Stream(eng.dev)
                 s.wait_stream(torch.cuda.current_stream(eng.dev))
                 g = nat.new_graph()
-                with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s):
-                        self._train_step()
-                        self._evaluate()
-                torch.cuda.current_stream(eng.dev).wait_stream(s)
+
+                def body():
+                    self._train_step()
+                    self._evaluate()
+                try:  # (an error inside the capture is raised alone, the stream left usable)
+                    capture_into(g, s, body, joins=(eng.side,))
+                finally:
+                    torch.cuda.current_stream(eng.dev).wait_stream(s)
                 self._graph = nat.seal_graph(g, "fixed-graph epoch")
             self._graph.replay()
         host = self._res.double().cpu().numpy()
