@@ -756,10 +756,14 @@ def main():
             if args.exchange == "rccl1":
                 from ldsgnn.replicas import collective_capture_probe, exchange_capturable
 
-                def reducer(grad):  # the N > 1 all-reduce mean, on the world-size-1 group
+                def reducer(grad, prescaled=False):  # the N > 1 all-reduce mean, on the world-size-1 group
                     dist.all_reduce(grad, op=dist.ReduceOp.SUM)
-                    grad.div_(dist.get_world_size())
+                    if not prescaled:
+                        grad.div_(dist.get_world_size())
                 reducer.capturable = exchange_capturable
+                # as at N > 1 over a power-of-two world (ldsgnn.fused, replicas.mean_prescale):
+                # the assembly scales dθ by 1/world, the exchange is the all-reduce SUM alone
+                reducer.prescale = lambda: dist.get_world_size()
                 capture_exchange = collective_capture_probe(device)
                 exchange_label = "nccl-allreduce-ws1-" + ("captured" if capture_exchange else "split")
             else:
@@ -886,8 +890,10 @@ def main():
     prefetched = bool(use_engine and eng.prefetch_draw)  # (the strong leg below frees the engine)
     two_hop_outer = bool(use_engine and eng.two_hop_outer)
     form_name = eng._form_name() if use_engine else ldsops.theta_grad_form()
+    long_rows = bool(use_engine and eng.long_rows)
     strong = None
-    if use_engine and args.strong_total and not param_theta:
+    # (config 5's long-row engine runs one replica sample per engine: no S_total split)
+    if use_engine and args.strong_total and not param_theta and not long_rows:
         del eng
         torch.cuda.empty_cache()
         strong = strong_scaling_leg(args, world, rank, device, barrier_sync)

@@ -812,6 +812,66 @@ def g_hypergrad_citeseer_s16(out, seed=13, samples=16):
     _store_vec(out, "theta1", theta1, pick)
 
 
+def g_hypergrad_citeseer_s16_wellcond(out, seed=13, samples=16):
+    """BASELINE config 3's shape (real Citeseer, θ₀ = the given graph, S = 16
+    replicas, replica b on the keyed stream of replica b) without dropout, in
+    the two well-conditioned hyper steps of hypergrad_cora_wellcond:
+      outer:  a hyper step from θ₀ with NO inner step before it (NLL on the
+              opt mask through each replica's sampled outer graph, the initial
+              weights as leaves); θ₁ = clamp(θ₀ − 0.1 · mean_b dθ_b, 0, 1);
+      window: from θ₁ (every replica's θ set to it, as the engine's shared θ
+              is), a dropout-free τ = 5 window per replica (5 inner steps +
+              its hyper step, lr 0.1 · 0.99); θ₂ from the mean.
+    Two passes over the replicas: the outer-only step of all 16 first (θ₁
+    needs their mean), then each replica re-run from its start through the
+    same outer-only step (same draw counters) with θ overwritten by θ₁
+    before its window."""
+    data = _planetoid("citeseer")
+    val, opt = _opt_split(data, seed)
+    prob = dict(x=data.x, y=data.y, train=data.train_mask, val=val, opt=opt, test=data.test_mask,
+                adj=data.dense_adj)
+    theta0, mean_outer, outer_losses = None, None, []
+    for b in range(samples):
+        patch_reference(KeyedRandomness(seed=seed, replica=b))
+        runner = build_reference(prob, seed=seed, dropout=0.0)
+        if theta0 is None:
+            theta0 = runner.outer_trainer.model.probs.detach().clone()
+        grads = []
+        _spy_grads(runner, grads)
+        outer_losses.append(runner.outer_trainer.train_step(runner.inner_trainer.model_forward).loss)
+        mean_outer = grads[0] if mean_outer is None else mean_outer + grads[0]
+    mean_outer /= samples
+    theta1 = (theta0 - 0.1 * torch.from_numpy(mean_outer).float()).clamp(0.0, 1.0)
+    mean_win, losses, win_outer = None, [], []
+    for b in range(samples):
+        patch_reference(KeyedRandomness(seed=seed, replica=b))
+        runner = build_reference(prob, seed=seed, dropout=0.0)
+        runner.hyper_opt_step(0)  # the outer-only step again: its draw counter, its lr decay, the detach
+        with torch.no_grad():
+            runner.outer_trainer.model.probs.data.copy_(theta1)
+        grads = []
+        _spy_grads(runner, grads)
+        losses.append([runner.inner_opt_step().loss for _ in range(5)])
+        win_outer.append(runner.outer_trainer.train_step(runner.inner_trainer.model_forward).loss)
+        mean_win = grads[0] if mean_win is None else mean_win + grads[0]
+        print(f"  citeseer nd replica {b}: inner {losses[-1][-1]:.6f} outer {win_outer[-1]:.6f}", flush=True)
+    mean_win /= samples
+    theta2 = (theta1 - np.float32(0.1 * 0.99) * torch.from_numpy(mean_win).float()).clamp(0.0, 1.0)
+    pick = np.random.default_rng(seed).choice(mean_win.size, 20000, replace=False)
+    out["seed"] = np.int64(seed)
+    out["samples"] = np.int64(samples)
+    out["opt_mask"] = opt.numpy()
+    out["val_mask"] = val.numpy()
+    out["outer_losses"] = np.array(outer_losses)       # [S], the outer-only step
+    out["window_inner_losses"] = np.array(losses)      # [S, 5]
+    out["window_outer_losses"] = np.array(win_outer)   # [S]
+    out["idx"] = pick.astype(np.int64)
+    _store_vec(out, "grad_outer", mean_outer, pick)
+    _store_vec(out, "theta_outer", theta1.numpy(), pick)
+    _store_vec(out, "grad_window", mean_win, pick)
+    _store_vec(out, "theta_window", theta2.numpy(), pick)
+
+
 def g_gcn_fixed_cora(out, seed=17, epochs=200, patience=10):
     """BASELINE config 1: the reference's fixed-graph GCN training loop
     (src/scripts/gcn.py:56-99 statement for statement: Adam groups 62-67,
@@ -957,7 +1017,7 @@ def main():
             ("hypergrad_citeseer_s16", g_hypergrad_citeseer_s16),
             ("hypergrad_citeseer_s16_probe", g_hypergrad_citeseer_s16_probe), ("gcn_fixed_cora", g_gcn_fixed_cora),
             ("pretrainer", g_pretrainer), ("hypergrad_cora_wellcond", g_hypergrad_cora_wellcond),
-            ("graph_models", g_graph_models)]
+            ("graph_models", g_graph_models), ("hypergrad_citeseer_s16_wellcond", g_hypergrad_citeseer_s16_wellcond)]
     only = set(sys.argv[1:])
     for name, fn in jobs:
         if only and name not in only:

@@ -227,7 +227,7 @@ def run_engine_samples_and_oracle(samples=3, n=96, f_in=24, classes=4, steps=6, 
         ep = eng.get_params(b)
         perr = max(perr, max(float((ep[k].cpu() - orc.params[k].detach()).abs().max()) for k in ep))
     terr = max(float((eng.theta.cpu() - orc.theta.detach()).abs().max()) for orc in oracles)
-    return dict(max_loss_err=float(max(lerr)), max_param_err=perr, max_grad_rel=max(grel) if grel else 0.0,
+    return dict(max_loss_err=float(max(lerr)) if lerr else 0.0, max_param_err=perr, max_grad_rel=max(grel) if grel else 0.0,
                 max_theta_err=terr,
                 theta_changed=float((oracles[0].theta.detach() - O.get_triu_values(prob["adj"])).abs().max()),
                 engine=eng, oracles=oracles)

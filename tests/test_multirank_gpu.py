@@ -56,14 +56,14 @@ def _trainers(samples, replica0, reducer):
     return engine_from_trainers(inner, outer, tau=5, generator=ldsgnn.rng.default_generator, samples=samples)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, per_rank=1):
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "lds-gnn_amd")]
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ldsgnn.replicas import allreduce_mean
-    eng = _trainers(1, rank, allreduce_mean)
+    eng = _trainers(per_rank, rank * per_rank, allreduce_mean)
     assert eng.grad_reducer is not None
     eng.inner_step()
     eng.hyper_step()            # step 0: dθ → all-reduce → SGD
@@ -78,14 +78,18 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_ranks_over_gloo_match_batched_replicas():
+@pytest.mark.parametrize("per_rank", [1, 8])
+def test_two_ranks_over_gloo_match_batched_replicas(per_rank):
+    """per_rank = 8: BASELINE config 4's split (8 Monte-Carlo samples per
+    GPU, replicas 8·rank … 8·rank + 7) against one process batching all 16."""
     world = 2
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     out = mgr.dict()
-    mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), out, per_rank), nprocs=world, join=True,
+                       start_method="spawn")
     r0, r1 = out[0], out[1]
-    eng = _trainers(2, 0, None)     # one process, replicas 0 and 1 batched
+    eng = _trainers(world * per_rank, 0, None)     # one process, replicas 0 .. world·per_rank - 1 batched
     eng.inner_step()
     eng.hyper_step()
     ref = [eng.theta.cpu().clone()]
@@ -99,12 +103,112 @@ def test_two_ranks_over_gloo_match_batched_replicas():
     for w, (a, b, c) in enumerate(zip(r0, r1, ref)):
         assert torch.equal(a, b), w                      # replicas in sync, bit for bit
         err = float((a - c).abs().max())
-        rows.append({"window": w, "ranks_bit_identical": True, "max_abs_vs_batched_S2": err})
+        rows.append({"window": w, "ranks_bit_identical": True, f"max_abs_vs_batched_S{world * per_rank}": err})
         assert err < 1e-5, (w, err)
     assert moved > 1e-4
     d = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(d):
-        with open(os.path.join(d, "multirank_gloo.json"), "w") as f:
+        with open(os.path.join(d, f"multirank_gloo_s{per_rank}.json"), "w") as f:
             json.dump({"test": "tests/test_multirank_gpu.py", "world": world, "backend": "gloo (one device)",
+                       "samples_per_rank": per_rank,
                        "workload": "cora kNN theta0, tau=5, replica = rank", "theta_moved": moved,
+                       "windows": rows}, f, indent=1)
+
+
+LR_N, LR_SEED, LR_WINDOWS = 1100, 6, 2
+
+
+def _long_row_problem():
+    from tests.parity_harness import synthetic_problem
+    from oracle import lds_oracle as O
+    prob = synthetic_problem(LR_N, 32, 5, LR_SEED)
+    # dense θ ~ U(0, 1): ≈ 550 expected neighbours per row, so the engine takes
+    # the long-row (bitmask-aggregation) path by itself, as at config 5
+    theta0 = torch.rand(LR_N * (LR_N + 1) // 2, generator=torch.Generator().manual_seed(LR_SEED + 1))
+    torch.manual_seed(LR_SEED)
+    from ldsgnn.models.gcn import MetaDenseGCN
+    gcn = MetaDenseGCN(32, 16, 5, dropout=0.5)
+    params = {k: v.detach().clone() for k, v in gcn.named_parameters()}
+    return prob, theta0, params, O
+
+
+def _long_row_worker(rank, world, port, out, kernel):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "lds-gnn_amd")]
+    from collections import OrderedDict
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ldsgnn
+    from ldsgnn.engine import LdsEngine
+    from ldsgnn.replicas import exchange_capturable
+    prob, theta0, params, _ = _long_row_problem()
+    dev = "cuda"
+
+    def reducer(grad):  # the replicas' all-reduce mean of dθ (800 MB per window at config 5)
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM)
+        grad.div_(world)
+    reducer.capturable = exchange_capturable  # (gloo: not capturable -> split graphs, capture outcome agreed)
+    eng = LdsEngine(prob["x"].to(dev), prob["y"].to(dev), prob["train"].to(dev), prob["opt"].to(dev),
+                    theta0.clone().to(dev), 5, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99,
+                    tau=5, generator=ldsgnn.rng.Generator(LR_SEED, rank),
+                    params=OrderedDict((k, v.to(dev)) for k, v in params.items()), long_rows_kernel=kernel)
+    assert eng.long_rows and eng.bitmask_agg == (kernel == "bitmask")
+    eng.grad_reducer = reducer
+    eng.inner_step()
+    eng.hyper_step()  # step 0: dθ -> all-reduce -> SGD + clamp
+    thetas = [eng.theta.cpu().clone()]
+    head_tail = eng.capture_window(5)
+    assert isinstance(head_tail, tuple) and len(head_tail) == 2
+    for _ in range(LR_WINDOWS):
+        eng.replay(1)
+        torch.cuda.synchronize()
+        thetas.append(eng.theta.cpu().clone())
+    eng.check_device_error()
+    out[rank] = thetas
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kernel", ["bitmask", "csr"])
+def test_two_ranks_long_row_engine_with_exchange(kernel):
+    """BASELINE config 5's multi-GPU half at a test size: the long-row engine
+    (dense θ, n = 1 100, the bitmask aggregation chosen by the engine itself,
+    or the CSR spill-pass SpMM) with the replicas' exchange — dθ all-reduced
+    (mean) between the split window graphs — on two ranks over gloo.  θ is
+    bit-identical on both ranks after every window and within 1e-5 of the
+    oracle's two replicas updated by their mean hypergradient
+    (oracle.replica_hyper_step).  Reference: src/trainers/outer.py:77-84."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    mp.start_processes(_long_row_worker, args=(world, _free_port(), out, kernel), nprocs=world, join=True,
+                       start_method="spawn")
+    r0, r1 = out[0], out[1]
+    prob, theta0, params, O = _long_row_problem()
+    from collections import OrderedDict
+    oracles = [O.LdsProblem(prob["x"], prob["y"], prob["train"], prob["val"], prob["test"], prob["opt"],
+                            theta0.clone(), hidden=16, dropout_p=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1,
+                            lr_decay=0.99, rnd=O.Randomness(LR_SEED, b), params=OrderedDict(params))
+               for b in range(world)]
+    ref = []
+    for w in range(LR_WINDOWS + 1):
+        for _ in range(1 if w == 0 else 5):
+            for orc in oracles:
+                orc.inner_step(orc.sample())
+        O.replica_hyper_step(oracles)
+        ref.append(oracles[0].theta.detach().clone())
+    rows = []
+    for w, (a, b, c) in enumerate(zip(r0, r1, ref)):
+        assert torch.equal(a, b), w
+        err = float((a - c).abs().max())
+        rows.append({"window": w, "ranks_bit_identical": True, "max_abs_vs_oracle_replica_mean": err})
+        assert err < 1e-5, (w, err)
+    assert float((ref[-1] - theta0).abs().max()) > 1e-4
+    d = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, f"multirank_gloo_long_rows_{kernel}.json"), "w") as f:
+            json.dump({"test": "tests/test_multirank_gpu.py::test_two_ranks_long_row_engine_with_exchange",
+                       "world": world, "backend": "gloo (one device)", "n": LR_N, "kernel": kernel,
                        "windows": rows}, f, indent=1)
