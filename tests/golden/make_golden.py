@@ -815,61 +815,65 @@ def g_hypergrad_citeseer_s16(out, seed=13, samples=16):
 def g_hypergrad_citeseer_s16_wellcond(out, seed=13, samples=16):
     """BASELINE config 3's shape (real Citeseer, θ₀ = the given graph, S = 16
     replicas, replica b on the keyed stream of replica b) without dropout, in
-    the two well-conditioned hyper steps of hypergrad_cora_wellcond:
-      outer:  a hyper step from θ₀ with NO inner step before it (NLL on the
-              opt mask through each replica's sampled outer graph, the initial
-              weights as leaves); θ₁ = clamp(θ₀ − 0.1 · mean_b dθ_b, 0, 1);
-      window: from θ₁ (every replica's θ set to it, as the engine's shared θ
-              is), a dropout-free τ = 5 window per replica (5 inner steps +
-              its hyper step, lr 0.1 · 0.99); θ₂ from the mean.
-    Two passes over the replicas: the outer-only step of all 16 first (θ₁
-    needs their mean), then each replica re-run from its start through the
-    same outer-only step (same draw counters) with θ overwritten by θ₁
-    before its window."""
+    the construction of hypergrad_cora_wellcond's dropout-free run:
+      step0:  the step-0 window (one inner step, its hyper step);
+      outer:  a hyper step with NO inner step before it (NLL on the opt mask
+              through each replica's sampled outer graph, the weights as
+              leaves): no Adam step between θ and the loss;
+      window: a dropout-free τ = 5 window.
+    The 16 reference runners are kept side by side, each with its own keyed
+    stream (patched in before each of its steps); after every hyper step all
+    replicas' θ are set to clamp(θ − lr · mean_b dθ_b, 0, 1) — the shared θ of
+    the engine's batched replicas — with lr the SGD rate that step used."""
     data = _planetoid("citeseer")
     val, opt = _opt_split(data, seed)
     prob = dict(x=data.x, y=data.y, train=data.train_mask, val=val, opt=opt, test=data.test_mask,
                 adj=data.dense_adj)
-    theta0, mean_outer, outer_losses = None, None, []
+    rnds = [KeyedRandomness(seed=seed, replica=b) for b in range(samples)]
+    runners, grads = [], [[] for _ in range(samples)]
     for b in range(samples):
-        patch_reference(KeyedRandomness(seed=seed, replica=b))
-        runner = build_reference(prob, seed=seed, dropout=0.0)
-        if theta0 is None:
-            theta0 = runner.outer_trainer.model.probs.detach().clone()
-        grads = []
-        _spy_grads(runner, grads)
-        outer_losses.append(runner.outer_trainer.train_step(runner.inner_trainer.model_forward).loss)
-        mean_outer = grads[0] if mean_outer is None else mean_outer + grads[0]
-    mean_outer /= samples
-    theta1 = (theta0 - 0.1 * torch.from_numpy(mean_outer).float()).clamp(0.0, 1.0)
-    mean_win, losses, win_outer = None, [], []
-    for b in range(samples):
-        patch_reference(KeyedRandomness(seed=seed, replica=b))
-        runner = build_reference(prob, seed=seed, dropout=0.0)
-        runner.hyper_opt_step(0)  # the outer-only step again: its draw counter, its lr decay, the detach
-        with torch.no_grad():
-            runner.outer_trainer.model.probs.data.copy_(theta1)
-        grads = []
-        _spy_grads(runner, grads)
-        losses.append([runner.inner_opt_step().loss for _ in range(5)])
-        win_outer.append(runner.outer_trainer.train_step(runner.inner_trainer.model_forward).loss)
-        mean_win = grads[0] if mean_win is None else mean_win + grads[0]
-        print(f"  citeseer nd replica {b}: inner {losses[-1][-1]:.6f} outer {win_outer[-1]:.6f}", flush=True)
-    mean_win /= samples
-    theta2 = (theta1 - np.float32(0.1 * 0.99) * torch.from_numpy(mean_win).float()).clamp(0.0, 1.0)
-    pick = np.random.default_rng(seed).choice(mean_win.size, 20000, replace=False)
+        patch_reference(rnds[b])
+        runners.append(build_reference(prob, seed=seed, dropout=0.0))
+        _spy_grads(runners[b], grads[b])
+
+    def synced_hyper(tag):
+        theta_old = runners[0].outer_trainer.model.probs.detach().clone()
+        lr = runners[0].outer_trainer.optimizer.param_groups[0]["lr"]
+        losses = []
+        for b in range(samples):
+            patch_reference(rnds[b])
+            r = runners[b]  # BilevelProblemRunner.hyper_opt_step (src/trainers/bilevel.py:109-113), its loss kept
+            losses.append(r.outer_trainer.train_step(r.inner_trainer.model_forward).loss)
+            r.inner_trainer.detach()
+            r.outer_trainer.detach()
+        mean = sum(gb[-1] for gb in grads) / samples
+        theta_new = theta_old.add(torch.from_numpy(mean).float(), alpha=-lr).clamp_(0.0, 1.0)
+        for r in runners:
+            with torch.no_grad():
+                r.outer_trainer.model.probs.data.copy_(theta_new)
+        if "idx" not in out:
+            out["idx"] = np.random.default_rng(seed).choice(mean.size, 20000, replace=False).astype(np.int64)
+        _store_vec(out, "grad_" + tag, mean, out["idx"])
+        _store_vec(out, "theta_" + tag, theta_new.numpy(), out["idx"])
+        out[tag + "_outer_losses"] = np.array(losses)
+
+    def inner_steps(k, tag):
+        rows = []
+        for b in range(samples):
+            patch_reference(rnds[b])
+            rows.append([runners[b].inner_opt_step().loss for _ in range(k)])
+        out[tag + "_inner_losses"] = np.array(rows)  # [S, k]
+
+    inner_steps(1, "step0")
+    synced_hyper("step0")
+    synced_hyper("outer")      # no inner step in this window
+    inner_steps(5, "window")
+    synced_hyper("window")
+    print("  citeseer nd window outer losses", out["window_outer_losses"][:4], flush=True)
     out["seed"] = np.int64(seed)
     out["samples"] = np.int64(samples)
     out["opt_mask"] = opt.numpy()
     out["val_mask"] = val.numpy()
-    out["outer_losses"] = np.array(outer_losses)       # [S], the outer-only step
-    out["window_inner_losses"] = np.array(losses)      # [S, 5]
-    out["window_outer_losses"] = np.array(win_outer)   # [S]
-    out["idx"] = pick.astype(np.int64)
-    _store_vec(out, "grad_outer", mean_outer, pick)
-    _store_vec(out, "theta_outer", theta1.numpy(), pick)
-    _store_vec(out, "grad_window", mean_win, pick)
-    _store_vec(out, "theta_window", theta2.numpy(), pick)
 
 
 def g_gcn_fixed_cora(out, seed=17, epochs=200, patience=10):
