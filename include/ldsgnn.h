@@ -62,6 +62,13 @@ const char* lds_error_string(int err);
  *     order only within the window the kernel places exactly give exact
  *     results without the flag. */
 #define LDS_DEVERR_CSR_COLUMNS 2u
+/*   LDS_DEVERR_SGD_TILE_COUNTER (round 6) — lds_sgd_sample_graphs with its
+ *     samples split over several blocks per tile found a per-tile counter
+ *     (tile_ctr) that was not zero on entry: a block counted past the tile's
+ *     block count.  That block does not write θ; the tile's update may have
+ *     been written early or not at all, so θ and the draws must not be used.
+ *     The word is the engine's EngineScalars.error (the `scalars` argument). */
+#define LDS_DEVERR_SGD_TILE_COUNTER 4u
 
 /* Number of uint64 words per bitmask row for n nodes (ceil(n/64) rounded up
  * to an even count so every row starts 16-byte aligned). Host-only. */

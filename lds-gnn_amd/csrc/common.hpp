@@ -22,6 +22,7 @@ constexpr int kEllFlagShift = 24;
 // Device error word bits (include/ldsgnn.h LDS_DEVERR_*).
 constexpr uint32_t kDevErrFillDegree = 1u;
 constexpr uint32_t kDevErrCsrColumns = 2u;
+constexpr uint32_t kDevErrSgdTileCounter = 4u;
 
 // Packed upper-triangle index of (i, j), i <= j, of an n×n matrix in
 // torch.triu_indices(n, n) row-major order (src/utils/graph.py:41-45).

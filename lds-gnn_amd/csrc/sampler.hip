@@ -235,8 +235,14 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
         if (gridDim.z > 1) {
             __syncthreads();  // every thread's θ loads have returned (their draws are done)
             if (threadIdx.x == 0) {
-                last_sh = atomicAdd(tile_ctr + tile, 1) == (int)gridDim.z - 1;
+                const int prev = atomicAdd(tile_ctr + tile, 1);
+                last_sh = prev == (int)gridDim.z - 1;
                 if (last_sh) tile_ctr[tile] = 0;
+                // a counter that was not zero on entry (stale or shared workspace):
+                // some block counts past the tile's blocks; report it (the engine's
+                // error word, EngineScalars.error at byte 32 of `counter_base`)
+                if (prev >= (int)gridDim.z && counter_base != nullptr)
+                    atomicOr(const_cast<uint32_t*>(counter_base) + 8, kDevErrSgdTileCounter);
             }
             __syncthreads();
             last = last_sh != 0;

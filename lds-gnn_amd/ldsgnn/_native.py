@@ -139,13 +139,17 @@ class DeviceError(RuntimeError):
 
 DEVERR_FILL_DEGREE = 1  # LDS_DEVERR_FILL_DEGREE
 DEVERR_CSR_COLUMNS = 2  # LDS_DEVERR_CSR_COLUMNS (ABI 14)
+DEVERR_SGD_TILE_COUNTER = 4  # LDS_DEVERR_SGD_TILE_COUNTER (round 6)
 
 _DEVERR_TEXT = {DEVERR_FILL_DEGREE: "a CSR fill found a row whose degree count differs from its drawn bits "
                                     "(degree workspace not zero on entry, or counts of another draw); its "
                                     "slots past the drawn entries hold the row's own index",
                 DEVERR_CSR_COLUMNS: "the dense CSR-SpMM (lds_spmm_norm_dense) met a row whose columns are not "
                                     "ascending in a way that changes its sum, or a column outside [0, n): the "
-                                    "aggregation is wrong"}
+                                    "aggregation is wrong",
+                DEVERR_SGD_TILE_COUNTER: "the SGD + draw pass (lds_sgd_sample_graphs) found a per-tile counter "
+                                         "that was not zero on entry: θ and the draws of that pass are not "
+                                         "trustworthy"}
 
 
 def raise_device_error(word: int, what: str) -> None:

@@ -331,6 +331,7 @@ class LdsEngine:
         # its per-tile counters (zero, and every call leaves them zero), allocated
         # here rather than on first use, which may fall inside a graph capture
         self._sgd_tiles = torch.zeros(int(nat.lib.lds_sgd_tile_ints(n)), dtype=torch.int32, device=theta.device)
+        self._sgd_tiles_checked = False
         if self.long_rows and self.S > 1:
             raise NotImplementedError("long-row (dense θ) mode runs one replica sample per engine")
         if long_rows_kernel not in ("bitmask", "csr", "blocked"):
@@ -1232,6 +1233,14 @@ class LdsEngine:
             nat.call("lds_sgd_sample_graphs", P(self.theta), P(self.grad), P(self.scalars), self.n, self.seed,
                      self.tag_graph, 1, self.pending_graph, gb.count, self.S, P(gb.bits), self.words,
                      P(self._deg_next), P(self._sgd_tiles) if self.sgd_draw_split else 0, st)
+            if self.sgd_draw_split and not self._sgd_tiles_checked and not torch.cuda.is_current_stream_capturing():
+                # the per-tile counters must come back to zero (their protocol
+                # assumes zero on entry); checked once, on the first eager call
+                # (round-5 ADVICE); later stale counters set
+                # LDS_DEVERR_SGD_TILE_COUNTER in the device error word
+                self._sgd_tiles_checked = True
+                if int(torch.count_nonzero(self._sgd_tiles).item()) != 0:
+                    nat.raise_device_error(nat.DEVERR_SGD_TILE_COUNTER, "LdsEngine (SGD + draw tile counters)")
             return True
         nat.call("lds_engine_sgd_clamp", P(self.theta), P(self.grad), self.theta.numel(), P(self.scalars), st)
         return False

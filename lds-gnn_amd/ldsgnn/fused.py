@@ -71,7 +71,10 @@ def engine_from_trainers(inner, outer, tau: int = 5, generator: "_rng.Generator"
         # graph-capturable exactly when the trainer's reducer is (RCCL all-reduce)
         reduce_engine_grad.capturable = getattr(reducer, "capturable", False)
         # the package's all-reduce mean: the engine may scale dθ by 1/world in
-        # the assembly (a power-of-two world: the same bits as sum-then-divide)
+        # the assembly (a power-of-two world: the same bits as sum-then-divide
+        # for every dθ entry above the subnormal range; entries near FLT_MIN
+        # may differ by up to world subnormal ulps, world · 2^-149 —
+        # tests/test_replicas_gloo.py)
         if reducer is _replicas.allreduce_mean:
             reduce_engine_grad.prescale = _replicas.mean_prescale
         eng.grad_reducer = reduce_engine_grad

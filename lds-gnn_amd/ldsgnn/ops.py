@@ -142,6 +142,13 @@ class CsrGraph:
             # order it cannot aggregate faithfully (a property of the CSR:
             # read on the graph's first call, one sync)
             checked = not self.canonical_columns
+            if checked and not getattr(self, "_dense_checked", False) and torch.cuda.is_current_stream_capturing():
+                # the check's error word is read on the host; inside a capture it
+                # never would be, so a wrong column order would give wrong sums
+                # silently on every replay (round-5 ADVICE): verify eagerly first
+                raise RuntimeError("CsrGraph.spmm: the column order of this CSR has not been checked yet; run one "
+                                   "eager spmm on it before capturing (canonical_columns=False graphs are checked "
+                                   "once, on the host)")
             nat.call("lds_spmm_norm_dense", nat.ptr(self.row_ptr), nat.ptr(self.col), nat.ptr(self.s), self.n,
                      nat.ptr(z), z.stride(0), nat.ptr(out), out.stride(0), beta, nat.ptr(ws), 0, 1,
                      nat.ptr(self._dense_err) if checked else 0, _stream(z))

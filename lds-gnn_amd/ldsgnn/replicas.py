@@ -53,7 +53,8 @@ def mean_prescale():
     gradients each rank has already scaled by 1/world: a process group of
     more than one rank whose size is a power of two (scaling by 2^-k commutes
     with fp32 rounding, so Σ_r (g_r / world) is bit for bit (Σ_r g_r) / world,
-    barring subnormals).  None otherwise (sum, then divide)."""
+    barring subnormals: entries near FLT_MIN may differ by up to
+    world · 2^-149, world subnormal ulps).  None otherwise (sum, then divide)."""
     if not _group_up():
         return None
     world = dist.get_world_size()

@@ -468,6 +468,34 @@ def test_sgd_sample_split_equals_one_block_per_tile(device, n, count, samples):
     assert torch.equal(outs[1][-1][0], want)
 
 
+def test_sgd_sample_split_stale_tile_counter_sets_device_error(device):
+    """Round-5 ADVICE: the split SGD + draw pass assumes its per-tile
+    counters are zero on entry.  With counters left at a value past the
+    tile's block count (a stale or shared workspace), a block counts past the
+    tile's blocks and sets LDS_DEVERR_SGD_TILE_COUNTER in the engine's error
+    word (EngineScalars.error, byte 32 of `scalars`) instead of passing
+    silently; with clean counters the word stays zero."""
+    n, count, samples = 600, 6, 8
+    g = torch.Generator().manual_seed(5)
+    m = n * (n + 1) // 2
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    st = nat.stream_of(torch.device(device))
+    for stale in (0, 1000):
+        theta = torch.rand(m, generator=g).to(device)
+        gr = (torch.randn(m, generator=g) * 0.3).to(device)
+        scalars = torch.zeros(nat.lib.lds_engine_scalars_size(), dtype=torch.uint8, device=device)
+        scalars[16:24].view(torch.float64).fill_(0.1)
+        tiles = torch.full((nat.lib.lds_sgd_tile_ints(n),), stale, dtype=torch.int32, device=device)
+        bits = torch.zeros((count * samples, n, words), dtype=torch.int64, device=device)
+        deg = torch.zeros((count * samples, wsi), dtype=torch.int32, device=device)
+        nat.call("lds_sgd_sample_graphs", nat.ptr(theta), nat.ptr(gr), nat.ptr(scalars), n, 99,
+                 tag_for(TAG_GRAPH, 0), 1, 0, count, samples, nat.ptr(bits), words, nat.ptr(deg), nat.ptr(tiles), st)
+        torch.cuda.synchronize()
+        word = int(scalars[32:36].view(torch.int32).item())
+        assert word == (nat.DEVERR_SGD_TILE_COUNTER if stale else 0), (stale, word)
+
+
 def test_fill_guard_pads_inflated_degrees(device):
     """lds_sample_graphs_multi promised a zero degree workspace (ws_zeroed =
     1) that is not: every row's count exceeds its drawn bits.  The fill

@@ -137,14 +137,14 @@ def test_library_exports_only_declared_entry_points():
 
 def test_variants_library_is_tools_only():
     """The variants library (built by __graft_entry__.build() for the
-    ablation tools) exports its two tools entry points and nothing of the
+    ablation tools) exports its tools entry points and nothing of the
     product's API."""
     import pytest
     path = os.path.join(ROOT, "tools", "variants", "libldsgnn_variants.so")
     if not os.path.exists(path):
         pytest.skip("tools/variants not built")
     assert _exported_lds_symbols(path) == ["lds_variants_spmm_dense", "lds_variants_spmm_dense_delayed",
-                                          "lds_variants_ws_bytes"]
+                                          "lds_variants_spmm_dense_e16", "lds_variants_ws_bytes"]
 
 
 def _kernel_metadata(lib_path, tmp_path):

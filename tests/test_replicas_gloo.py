@@ -46,12 +46,14 @@ def test_two_replicas_average_and_stay_in_sync():
     assert torch.allclose(out[0], out[1], atol=0) and torch.allclose(out[0], want, atol=1e-7)
 
 
-def _prescale_worker(rank, world, port, out):
+def _prescale_worker(rank, world, port, out, subnormal=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ldsgnn.replicas import allreduce_mean, allreduce_sum_, mean_prescale
     g = torch.Generator().manual_seed(200 + rank)
     grad = torch.randn(4099, generator=g) * torch.logspace(-20, 20, 4099)
+    if subnormal:  # around FLT_MIN: normal and subnormal dθ entries
+        grad = torch.randn(4099, generator=g) * (2.0 ** -126) * torch.logspace(-6, 1, 4099)
     model = torch.nn.Module()
     model.theta = torch.nn.Parameter(torch.zeros(4099))
     model.theta.grad = grad.clone()
@@ -78,3 +80,22 @@ def test_prescaled_sum_equals_mean_bit_for_bit():
         w, mean, pre = out[r]
         assert w == world
         assert torch.equal(mean, pre)
+
+
+def test_prescaled_sum_near_flt_min_within_one_subnormal_ulp():
+    """Round-5 ADVICE: scaling by 2^-k is exact only above the subnormal
+    range, so for dθ entries near FLT_MIN the prescaled exchange may differ
+    from SUM-then-divide.  Bounded: each rank's g/world rounds once (half a
+    subnormal ulp each) and the divide once, so |difference| <= world · 2^-149
+    (2^-149: one ulp of the subnormal range, far below any θ step lr·dθ can
+    make visible), as documented at ldsgnn.fused.engine_from_trainers."""
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_prescale_worker, args=(world, port, out, True), nprocs=world, join=True)
+    for r in range(world):
+        w, mean, pre = out[r]
+        diff = (mean.double() - pre.double()).abs()
+        assert float(diff.max()) <= world * 2.0 ** -149, float(diff.max())
+        assert float(diff.max()) > 0.0  # (the case the bound is about does occur)
