@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 16
+#define LDS_ABI_VERSION 17
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -152,6 +152,31 @@ int lds_sgd_sample_graphs(float* theta, const float* grad, const void* scalars, 
                           int samples, uint64_t* bits, int words, int* deg_ws, int* tile_ctr, void* stream);
 /* Ints of lds_sgd_sample_graphs' tile counters: the triangle's 64×64 tiles. */
 int lds_sgd_tile_ints(int n);
+
+/* ----- band-sharded replicas (BASELINE config 5 at N > 1, ABI 17) -----
+ * Rank b of N owns the rows [row0_b, row1_b) of the packed triangle: it
+ * assembles dθ of that band from EVERY rank's factors (all-gathered), applies
+ * SGD + clamp there, and draws the band's upper-triangle words of every
+ * replica's next graphs; the row bands go to their owners (all-to-all), which
+ * complete the lower triangle.  Replaces, sharded across ranks:
+ * src/trainers/outer.py:77-84 (dθ, SGD, clamp) and src/models/sampling.py:68
+ * (the next window's draws); the reference runs one replica per job
+ * (configs/seml/final/lds.yaml:1-13).
+ *
+ * lds_sample_band_bits: the draws of the tiles of 64-row blocks row0/64 …
+ * (row0 a multiple of 64, row1 too or n) for count graphs × samples
+ * replicas, counters / tags / storage as lds_sample_graphs_multi; writes the
+ * band's rows' words only (no transposed words below the band, no degree
+ * counts).  Every bit it writes equals lds_sample_graphs_multi's. */
+int lds_sample_band_bits(const float* theta, int n, uint64_t seed, uint32_t tag, uint32_t tag_step,
+                         const uint32_t* counter_base, uint32_t counter_offset, int count, int samples,
+                         int row0, int row1, uint64_t* bits, int words, void* stream);
+/* The strict lower triangle of `graphs` bitmasks from their upper triangle
+ * (diagonal words included), then degrees into deg_ws (lds_sample_ws_ints(n)
+ * ints per graph) and s = deg^-1/2 ([graphs][n]): the state
+ * lds_sample_graphs_multi leaves with col = NULL. */
+int lds_bitmask_mirror_degree(uint64_t* bits, int n, int words, int graphs, int* deg_ws, float* s,
+                              void* stream);
 
 /* The fill launch of lds_sample_graphs_multi alone (CSR, s, ELL head of
  * `graphs` graphs whose bits and degree counts are already drawn, e.g. by
@@ -354,6 +379,14 @@ int lds_theta_grad_sgd_draw(const float* u, const float* v, int ld, int k,
 int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, const float* r,
                       int ldr_row, int ldr_col, int nr, float* theta, int n, float* grad,
                       int mode, const void* scalars, float gscale, int form, void* stream);
+/* lds_theta_grad_ex over the packed triangle's rows [row0, row1) only (the
+ * band-sharded exchange, ABI 17): their 128-row block tiles, every column
+ * block from the diagonal on, in the plain split-bf16 128-tile form; row0 a
+ * multiple of 128, row1 too or n; mode 0 (dθ of the band) or 2 (fused SGD +
+ * clamp of the band).  Each entry gets the bits the full launch gives it. */
+int lds_theta_grad_band(const float* u, const float* v, int ld, int k, const float* r, int ldr_row,
+                        int ldr_col, int nr, float* theta, int n, float* grad, int mode,
+                        const void* scalars, float gscale, int row0, int row1, void* stream);
 /* lds_theta_grad_ex on pre-split operands: every fp32 value x of U and V as
  * its three truncation-split bf16 words x = hi + mid + lo (lds_split_planes
  * makes them from fp32; the engine's factor producers write them directly),

@@ -41,6 +41,20 @@ __device__ __forceinline__ void tri_tile(int t, int& a, int& b) {
     b = t - r * (r + 1) / 2;
 }
 
+// Linear id L of a row band's tiles -> upper-triangle block (bi <= bj): the
+// block rows b0, b0 + 1, … of the band in order, each from its diagonal block
+// to the last column block (lds_theta_grad_band, lds_sample_band_bits: the band-sharded exchange
+// of BASELINE config 5).
+__device__ __forceinline__ void band_tile(int L, int nb, int b0, int& bi, int& bj) {
+    int i = b0;
+    while (L >= nb - i) {
+        L -= nb - i;
+        ++i;
+    }
+    bi = i;
+    bj = i + L;
+}
+
 struct U32x4 {
     uint32_t x, y, z, w;
 };

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     uint64_t* __restrict__ bits, int words, int ntiles, uint32_t tag_step, int samples, int graphs,
     int* __restrict__ dacc, int wsi, float* __restrict__ theta_w = nullptr,
     const float* __restrict__ grad = nullptr, const double* __restrict__ lr_dev = nullptr,
-    int* __restrict__ tile_ctr = nullptr) {
+    int* __restrict__ tile_ctr = nullptr, int band0 = -1, int mirror = 1) {
     // items are drawn in groups of kGrp: per item wave w leaves its column bits
     // (rows 16w .. 16w+15 of the tile) here, then wave q assembles item q's
     // column words — one barrier pair per group instead of per item
@@ -75,9 +75,18 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
     (void)ntiles;
     const int lane = wave_lane();
     const int wave = wave_id();
-    int a, b;
-    tri_tile(tile, a, b);
-    const int bi = b, bj = a;  // bi <= bj
+    // band0 >= 0 (lds_sample_band_bits): the tiles of 64-row blocks band0, …
+    // in band order; mirror = 0: an off-diagonal tile writes its rows' words
+    // only, not the transposed words of the rows below the band
+    int bi, bj;  // bi <= bj
+    if (band0 >= 0) {
+        band_tile(tile, (n + 63) / 64, band0, bi, bj);
+    } else {
+        int a, b;
+        tri_tile(tile, a, b);
+        bi = b;
+        bj = a;
+    }
     const int j = bj * 64 + lane;
     const bool diag_tile = (bi == bj);
     const int64_t nn = n;
@@ -220,7 +229,7 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
                 uint64_t out = (uint64_t)colpart[wave][0][lane] | ((uint64_t)colpart[wave][1][lane] << 16) |
                                ((uint64_t)colpart[wave][2][lane] << 32) | ((uint64_t)colpart[wave][3][lane] << 48);
                 if (diag_tile) out |= rowword[wave][lane] | (1ull << lane);  // self-loop: diagonal set to 1
-                gb[(int64_t)j * words + bi] = out;
+                if (mirror || diag_tile) gb[(int64_t)j * words + bi] = out;
                 pc = __popcll(out);
             }
             if constexpr (kDeg) {
@@ -259,6 +268,29 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
             }
         }
     }
+}
+
+// The strict lower triangle of `graphs` bitmasks from their upper triangle
+// (lds_bitmask_mirror_degree): one wave per 64 × 64 block pair (bi > bj): lane l
+// holds row 64·bj + l's word bi; 64 ballots transpose it, lane c keeps the
+// word bj of row 64·bi + c.  Graph blockIdx.y.
+__global__ __launch_bounds__(256) void mirror_kernel(uint64_t* __restrict__ bits, int n, int words, int pairs) {
+    const int pair = blockIdx.x * 4 + wave_id();
+    if (pair >= pairs) return;
+    int a, b;
+    tri_tile(pair, a, b);  // b <= a: the block pair (a + 1, b)
+    const int bi = a + 1, bj = b;
+    const int lane = wave_lane();
+    bits += (int64_t)blockIdx.y * n * words;
+    const int src_row = bj * 64 + lane, dst_row = bi * 64 + lane;
+    const uint64_t src = src_row < n ? bits[(int64_t)src_row * words + bi] : 0ull;
+    uint64_t mine = 0ull;
+#pragma unroll
+    for (int c = 0; c < 64; ++c) {
+        const uint64_t t = __ballot((src >> c) & 1ull);
+        mine = lane == c ? t : mine;
+    }
+    if (dst_row < n) bits[(int64_t)dst_row * words + bj] = mine;
 }
 
 // One wave per row: popcount of the row's words.
@@ -713,4 +745,57 @@ extern "C" int lds_sample_graph(const float* theta, int n, uint64_t seed, uint32
     e = lds_exclusive_scan(deg_ws, n, row_ptr, stream);
     if (e) return e;
     return lds_bitmask_fill_csr(bits, n, words, row_ptr, col, col_capacity, overflow, stream);
+}
+
+// The band draw of the band-sharded exchange (BASELINE config 5 at N > 1,
+// DESIGN §5b): the Bernoulli draws of the upper-triangle tiles of the rows
+// [row0, row1) only — the tiles of 64-row blocks row0 / 64 … — for `count`
+// graphs × `samples` replicas (graph g, replica b: counter *counter_base +
+// counter_offset + g, tag + b·tag_step, stored as graph g·samples + b, as
+// lds_sample_graphs_multi), writing those rows' words and nothing below the
+// band (no transposed words, no degree counts).  Every (i, j), i < j, of the
+// band gets the bit lds_sample_graphs_multi gives it.  row0 a multiple of 64,
+// row1 too or n.
+extern "C" int lds_sample_band_bits(const float* theta, int n, uint64_t seed, uint32_t tag, uint32_t tag_step,
+                                    const uint32_t* counter_base, uint32_t counter_offset, int count, int samples,
+                                    int row0, int row1, uint64_t* bits, int words, void* stream) {
+    LDS_CHECK_ARG(theta && bits && n > 0 && n <= (1 << 20) && words >= (n + 63) / 64);
+    LDS_CHECK_ARG(count > 0 && samples > 0 && (int64_t)count * samples <= 65535);
+    LDS_CHECK_ARG(0 <= row0 && row0 < row1 && row1 <= n && row0 % 64 == 0 && (row1 % 64 == 0 || row1 == n));
+    const int nb = (n + 63) / 64, b0 = row0 / 64, b1 = (row1 + 63) / 64;
+    int64_t tiles = 0;
+    for (int b = b0; b < b1; ++b) tiles += nb - b;
+    LDS_CHECK_ARG(tiles > 0 && tiles < (1 << 30));
+    int zsplit = 1;  // as lds_sample_graphs_multi: the (graph, sample) items over grid.z
+    {
+        const int total = count * samples;
+        const int want = std::max(1, std::min(samples, (int)((kDrawBlocks + tiles - 1) / tiles)));
+        const int per = (total + want - 1) / want;
+        zsplit = (total + per - 1) / per;
+    }
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(sample_tiles_kernel<false, true, false>), dim3((unsigned)tiles, 1, zsplit),
+                       dim3(256), 0, (hipStream_t)stream, theta, n, (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                       counter_offset, counter_base, (const float*)nullptr, bits, words, (int)tiles, tag_step,
+                       samples, count, (int*)nullptr, 0, (float*)nullptr, (const float*)nullptr,
+                       (const double*)nullptr, (int*)nullptr, b0, 0);
+    LDS_RETURN_LAST_ERROR();
+}
+
+// Complete `graphs` bitmasks whose upper triangle (diagonal words included)
+// is drawn — e.g. assembled from the row bands of lds_sample_band_bits —
+// with their strict lower triangle (the transposed words), then their
+// degrees into deg_ws (lds_sample_ws_ints(n) ints per graph) and s = deg^-1/2
+// ([graphs][n]), as lds_sample_graphs_multi leaves them with col = NULL.
+extern "C" int lds_bitmask_mirror_degree(uint64_t* bits, int n, int words, int graphs, int* deg_ws, float* s,
+                                         void* stream) {
+    LDS_CHECK_ARG(bits && deg_ws && s && n > 0 && n <= (1 << 20) && words >= (n + 63) / 64 && graphs > 0 &&
+                  graphs <= 65535);
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = (n + 63) / 64;
+    const int pairs = nb * (nb - 1) / 2;
+    if (pairs > 0)
+        hipLaunchKernelGGL(mirror_kernel, dim3((pairs + 3) / 4, graphs), dim3(256), 0, st, bits, n, words, pairs);
+    hipLaunchKernelGGL(degree_kernel, dim3((n + 3) / 4, graphs), dim3(256), 0, st, (const uint64_t*)bits, n, words,
+                       deg_ws, s, lds_sample_ws_ints(n));
+    LDS_RETURN_LAST_ERROR();
 }

@@ -977,6 +977,8 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
         const int L = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
         if (L >= ntiles) return;  // whole block: no barrier reached
         grouped_tile(L, nb, group, bi, bj);
+    } else if (group < 0) {  // a row band's tiles: block rows -group - 1 … (the grid is the band's tile count)
+        band_tile((int)blockIdx.x, nb, -group - 1, bi, bj);
     } else {
         int a, b;
         tri_tile(blockIdx.x, a, b);
@@ -2113,6 +2115,42 @@ extern "C" int lds_theta_grad_ex(const float* u, const float* v, int ld, int k, 
     //  196 VGPRs and 66 KB LDS leave 2 waves per SIMD.  MFMA busy of this form
     //  at S = 16 is 63 % of the cycles at a 2.26 GHz DVFS clock, r01 PMC)
     launch_theta_grad(ntiles, (hipStream_t)stream, u, v, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale, form);
+    LDS_RETURN_LAST_ERROR();
+}
+
+// lds_theta_grad_ex over the rows [row0, row1) of the packed triangle only
+// (their 128-row block tiles, every column block from the diagonal on; the
+// plain split-bf16 128-tile form): the band-sharded exchange of BASELINE
+// config 5, where rank b assembles, updates and draws from its
+// own row band of θ with every rank's factors.  row0 a multiple of 128, row1
+// too or n; mode 0 (dθ of the band into grad) or 2 (fused SGD + clamp of the
+// band of θ, grad optional).  Same result bits per entry as the full launch.
+extern "C" int lds_theta_grad_band(const float* u, const float* v, int ld, int k, const float* r, int ldr_row,
+                                   int ldr_col, int nr, float* theta, int n, float* grad, int mode,
+                                   const void* scalars, float gscale, int row0, int row1, void* stream) {
+    LDS_CHECK_ARG(n > 0 && k > 0 && nr >= 0 && (mode == 0 || mode == 2));
+    LDS_CHECK_ARG(u != nullptr && v != nullptr && ld >= k);
+    LDS_CHECK_ARG(nr == 0 || (r != nullptr && ldr_row >= 0 && ldr_col >= 0));
+    LDS_CHECK_ARG(mode == 0 ? grad != nullptr : (theta != nullptr && scalars != nullptr));
+    LDS_CHECK_ARG(0 <= row0 && row0 < row1 && row1 <= n && row0 % kT2 == 0 && (row1 % kT2 == 0 || row1 == n));
+    const int nb = (n + kT2 - 1) / kT2;
+    const int b0 = row0 / kT2, b1 = (row1 + kT2 - 1) / kT2;
+    int64_t tiles = 0;
+    for (int b = b0; b < b1; ++b) tiles += nb - b;
+    LDS_CHECK_ARG(tiles > 0 && tiles < (1 << 30));
+    const int vec4 = ((ld & 3) == 0 && ((((uintptr_t)u) | ((uintptr_t)v)) & 15) == 0) ? 1 : 0;
+    const bool fast = vec4 && (k & 7) == 0, small = n <= 46340;
+    const double* lr = mode == 2 ? reinterpret_cast<const double*>((const char*)scalars + 16) : nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    const Planes none{nullptr, nullptr};
+#define LDS_TGB_ARGS u, v, ld, k, r, ldr_row, nr, theta, n, grad, mode, lr, vec4, ldr_col, gscale, -b0 - 1, 0, none
+    if (fast && small)
+        hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, true>), dim3((unsigned)tiles), dim3(256), 0, st, LDS_TGB_ARGS);
+    else if (fast)
+        hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<true, false>), dim3((unsigned)tiles), dim3(256), 0, st, LDS_TGB_ARGS);
+    else
+        hipLaunchKernelGGL((theta_grad_bf3_t128_kernel<false, false>), dim3((unsigned)tiles), dim3(256), 0, st, LDS_TGB_ARGS);
+#undef LDS_TGB_ARGS
     LDS_RETURN_LAST_ERROR();
 }
 

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -42,6 +42,11 @@ SIGNATURES = {
     "lds_sgd_sample_graphs": [P, P, P, c_int, c_uint64, c_uint32, c_uint32, c_uint32, c_int, c_int, P, c_int, P,
                               P, P],
     "lds_sgd_tile_ints": [c_int],
+    "lds_sample_band_bits": [P, c_int, c_uint64, c_uint32, c_uint32, P, c_uint32, c_int, c_int, c_int, c_int, P,
+                             c_int, P],
+    "lds_bitmask_mirror_degree": [P, c_int, c_int, c_int, P, P, P],
+    "lds_theta_grad_band": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int,
+                            c_int, P],
     "lds_theta_grad_ex": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int, P],
     "lds_theta_grad_planes": [P, P, c_int, c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, c_float, c_int,
                               P],

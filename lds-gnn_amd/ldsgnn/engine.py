@@ -421,6 +421,10 @@ class LdsEngine:
         # written, reduced, then SGD + clamp runs (the assembly is not fused
         # with the update), and captures split at it
         self.grad_reducer = None
+        # band-sharded replicas (set_band_shards): the long-row engine's
+        # exchange at N > 1 as factor all-gather + band update + band draws
+        self.shards = None
+        self._allbits = None
         # dθ assembly split per graph: chunks of finished graphs run on a side
         # stream beside the (latency-bound) reverse pass.  Off by default: on
         # MI355X the replayed graph did not overlap the branches and the
@@ -612,6 +616,9 @@ class LdsEngine:
         self._drop_prefetch()
         if self.S != 1:
             raise NotImplementedError("empirical_mean runs on single-sample engines")
+        if self.shards is not None and self.shards.world > 1 and not self._theta_whole:
+            raise RuntimeError("empirical_mean: band-sharded θ is current only in this rank's band; "
+                               "call sync_theta() first")
         if not self.long_rows:
             return self._empirical_mean_batched(flat, n_samples, val_mask, test_mask)
         return self._empirical_mean_seq(flat, n_samples, val_mask, test_mask)
@@ -740,6 +747,11 @@ class LdsEngine:
         """Draw the next graph of every replica sample into `g` (from `theta`,
         default self.theta)."""
         self._drop_prefetch()
+        if self.shards is not None and theta is None:
+            self._sharded_draw(g.bits, self.deg, g.s, (g.row_ptr, g.col, g.ell), 1, self.pending_graph)
+            self._block_ptrs([g])
+            self.pending_graph += 1
+            return
         nat.call("lds_sample_graphs_multi", nat.ptr(self.theta if theta is None else theta), self.n, self.seed, self.tag_graph, 1,
                  nat.ptr(self.scalars), self.pending_graph, 1, self.S, nat.ptr(g.bits), self.words,
                  nat.ptr(self.deg), nat.ptr(g.row_ptr), self._col_arg(g.col), self.cap, nat.ptr(g.s),
@@ -971,6 +983,8 @@ class LdsEngine:
             else:
                 nat.call("lds_sample_fill_csr", fill[0], self.n, *fill[1:], self._err_ptr(), self._stream())
             self._prefetched = False
+        elif self.shards is not None:
+            self._sharded_draw(gb.bits, gb.deg, gb.s, (gb.row_ptr, gb.col, gb.ell), count, self.pending_graph)
         elif self.async_draw and count > 1 and not self.long_rows:
             # graph 0 on the main stream; graphs 1 .. count-1 on the side stream,
             # beside inner step 0 (joined before step 1: _join_draw)
@@ -1037,7 +1051,8 @@ class LdsEngine:
         form = self._form_name()
         if not self.uv_planes or self.S != 1 or T != self.tau:
             return False
-        if self.outer_update is not None or self.theta_fn is not None or self.split_theta_grad:
+        if self.outer_update is not None or self.theta_fn is not None or self.split_theta_grad or \
+                self.shards is not None:
             return False
         nb = (self.n + 127) // 128
         return form == "bf16x3-direct" or (form == "bf16x3" and nb * (nb + 1) // 2 <= 256)
@@ -1158,7 +1173,9 @@ class LdsEngine:
             k0 = self.kg  # the last chunk (graph 0) + R on the main stream
         else:
             k0 = T * self.kg + HID + self.cw
-        if self.S > 1:
+        if self.shards is not None:  # band-sharded replicas: the exchange is in the update itself
+            self._sharded_update(k0)
+        elif self.S > 1:
             drew = self._assemble_samples(k0, grad_reducer, presampled)
         elif grad_reducer is None:  # dθ assembly (last chunk) fused with SGD + clamp
             if split:
@@ -1271,6 +1288,102 @@ class LdsEngine:
                 grad_reducer(self.grad)
             return self._sgd_step(self.tau if presampled else -1, k0, presampled)
         return False
+
+    # ------------------------------------------------ band-sharded replicas
+    def set_band_shards(self, shards) -> None:
+        """Run this long-row engine as rank `shards.rank` of band-sharded
+        replicas (ldsgnn.replicas.BandShards; BASELINE config 5 at N > 1,
+        DESIGN §5b): one replica per rank (replica = rank), θ current only in
+        this rank's row band between sync_theta() calls.  Every hyper step
+        all-gathers the ranks' θ-gradient factors and updates the band
+        (lds_theta_grad_band: the mean hypergradient, fused SGD + clamp);
+        every draw takes the band's rows of every replica's graphs
+        (lds_sample_band_bits), exchanges them (all-to-all) and completes
+        this replica's graphs (lds_bitmask_mirror_degree).  Windows run
+        eagerly (run_window).  With world 1 the results are bit-identical to
+        the engine's own exchange path (dθ, then SGD + clamp)."""
+        from .rng import TAG_GRAPH as _TG
+        if not self.long_rows or self.S != 1:
+            raise NotImplementedError("band-sharded replicas: the long-row engine, one sample per rank")
+        if self.theta_fn is not None or self.outer_update is not None:
+            raise NotImplementedError("band-sharded replicas: plain LDS θ")
+        if self.tag_graph != tag_for(_TG, shards.rank):
+            raise ValueError("band-sharded replicas: this engine's replica must equal its rank "
+                             "(ldsgnn.rng.manual_seed(seed, replica=rank))")
+        if shards.n != self.n:
+            raise ValueError("band-sharded replicas: bands built for another n")
+        self._drop_prefetch()
+        self.prefetch_draw = False
+        self.shards = shards
+        self._theta_whole = True
+
+    def sync_theta(self) -> None:
+        """Every rank's band of θ into every rank's copy (all-gather): the
+        full, identical θ on all ranks (evaluation, checkpoints, the drop-in
+        model's probs)."""
+        if self.shards is not None:
+            self.shards.gather_rows(self.theta.view(-1), self.n)
+            self._theta_whole = True
+
+    def _sharded_update(self, k0: int) -> None:
+        """The mean hypergradient of all ranks' replicas on this rank's band,
+        fused with SGD + clamp there: every rank's factors all-gathered and
+        side by side (replica q in columns [q·ldk, (q+1)·ldk)), R stacked,
+        gscale = 1/world — the arithmetic of a batched engine's rank-(S·K)
+        assembly.  θ.grad (if kept) holds the band's dθ."""
+        st, n, P, sh = self._stream(), self.n, nat.ptr, self.shards
+        if k0 < self.ldu:  # stale columns of a longer earlier window
+            self.U[:, k0:].zero_()
+            self.V[:, k0:].zero_()
+        N = sh.world
+        if N > 1:
+            uc = sh.all_gather(self.U).permute(1, 0, 2).contiguous()  # [n, N, ldk]
+            vc = sh.all_gather(self.V).permute(1, 0, 2).contiguous()
+            rg = sh.all_gather(self.R[0])  # [N, n]
+        else:
+            uc, vc, rg = self.U, self.V, self.R
+        ld = N * self.ldu
+        gs = float(np.float32(1.0) / np.float32(N))
+        row0, row1 = sh.band
+        nat.call("lds_theta_grad_band", P(uc), P(vc), ld, ld, P(rg), 1, n, N, P(self.theta), n,
+                 P(self.grad) if self.keep_grad else 0, 2, P(self.scalars), gs, row0, row1, st)
+        self._theta_whole = N == 1
+
+    def _sharded_draw(self, bits: torch.Tensor, deg: torch.Tensor, s: torch.Tensor, csr, count: int,
+                      counter_off: int) -> None:
+        """`count` graphs of this rank's replica (draw counters counter_off + g)
+        into bits [count, 1, n, words] with their degrees (deg [count, 1, wsi])
+        and s, and (CSR modes) row_ptr / col / ELL: this rank draws its band's
+        rows of EVERY replica's graphs, the bands meet at their owners
+        (all-to-all), the owner mirrors its graphs' lower triangle."""
+        from .rng import TAG_GRAPH as _TG
+        st, n, W, P, sh = self._stream(), self.n, self.words, nat.ptr, self.shards
+        N = sh.world
+        row0, row1 = sh.band
+        need = count * N * n * W
+        if self._allbits is None or self._allbits.numel() < need:
+            self._allbits = torch.empty(need, dtype=torch.int64, device=self.dev)
+        ab = self._allbits[:need].view(count, N, n, W)
+        nat.call("lds_sample_band_bits", P(self.theta), n, self.seed, tag_for(_TG, 0), 1, P(self.scalars),
+                 counter_off, count, N, row0, row1, P(ab), W, st)
+        dst = bits.view(count, n, W)
+        if N == 1:
+            dst.copy_(ab[:, 0])
+        else:
+            rows = [r1 - r0 for r0, r1 in sh.bounds]
+            send = ab[:, :, row0:row1, :].permute(1, 0, 2, 3).contiguous().view(-1)  # [dest, g, band rows, W]
+            recv = sh.all_to_all(send, [count * (row1 - row0) * W] * N, [count * r * W for r in rows])
+            off = 0
+            for q, (q0, q1) in enumerate(sh.bounds):
+                m = count * (q1 - q0) * W
+                dst[:, q0:q1, :] = recv[off:off + m].view(count, q1 - q0, W)
+                off += m
+        nat.call("lds_bitmask_mirror_degree", P(bits), n, W, count, P(deg), P(s), st)
+        self._ws_clean = False
+        if not self.bitmask_agg:  # CSR / s / ELL from the completed bits and their degree counts
+            row_ptr, col, ell = csr
+            nat.call("lds_sample_fill_csr", P(bits), n, W, P(deg), count, P(row_ptr), P(col), max(self.cap, 1),
+                     P(s), P(ell), P(self.nflag), self._err_ptr(), st)
 
     @staticmethod
     def _prescale(grad_reducer):
@@ -1540,6 +1653,9 @@ class LdsEngine:
                                       "side's counters: run windows eagerly")
         if tau != self.tau:
             raise ValueError(f"engine was built for tau={self.tau}; capture that window length")
+        if self.shards is not None:
+            raise NotImplementedError("band-sharded windows run eagerly (run_window): their exchange is two "
+                                      "collectives per window around host-sized buffers")
         if windows < 1:
             raise ValueError("windows >= 1")
         if grad_reducer is None:

@@ -15,6 +15,8 @@ window around an eager collective.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 import torch.distributed as dist
 
@@ -115,3 +117,85 @@ def collective_capture_probe(device: torch.device) -> bool:
     graph.replay()
     torch.cuda.synchronize(device)
     return agree(bool(torch.all(x == float(world)).item()))
+
+
+def band_bounds(n: int, world: int, align: int = 128):
+    """Row bands [(row0, row1)] of the packed upper triangle for `world`
+    ranks: boundaries on multiples of `align` (the θ-grad's 128-row tiles),
+    each band holding about 1/world of the triangle's entries (row i holds
+    n − i of them), none empty."""
+    if world < 1 or n < align * world:
+        raise NotImplementedError(f"band-sharded exchange: n >= {align}·world (n = {n}, world = {world})")
+    cum = lambda r: r * n - r * (r - 1) // 2  # noqa: E731  (entries of rows < r)
+    total = cum(n)
+    cuts = [0]
+    for b in range(1, world):
+        target = b * total / world
+        r = min(range(cuts[-1] + align, n - align * (world - b) + 1, align), key=lambda x: abs(cum(x) - target))
+        cuts.append(r)
+    cuts.append(n)
+    return [(cuts[b], cuts[b + 1]) for b in range(world)]
+
+
+class BandShards:
+    """The band-sharded exchange of the long-row engine (BASELINE config 5 at
+    N > 1; LdsEngine.set_band_shards).  Rank b owns the packed
+    triangle's rows [row0_b, row1_b): per hyper step it all-gathers every
+    rank's θ-gradient factors (U, V, R: 2·n·K + n floats per rank, against
+    the n(n+1)/2 floats of a dense dθ all-reduce), assembles, updates and
+    clamps its own band of θ (lds_theta_grad_band), and at each window start
+    draws its band's rows of EVERY replica's graphs (lds_sample_band_bits)
+    and sends each replica's rows to its rank (all-to-all); the owner
+    completes the lower triangle (lds_bitmask_mirror_degree).  Replica = rank
+    (one sample per rank).  Under gloo the collectives run on host copies."""
+
+    def __init__(self, n: int, world: Optional[int] = None, rank: Optional[int] = None):
+        up = _group_up()
+        self.world = int(world if world is not None else (dist.get_world_size() if up else 1))
+        self.rank = int(rank if rank is not None else (dist.get_rank() if up else 0))
+        if self.world > 1 and not up:
+            raise RuntimeError("BandShards: a process group is needed for world > 1")
+        self.n = n
+        self.bounds = band_bounds(n, self.world)
+        self.host = up and dist.get_backend() != "nccl"  # gloo: collectives on host copies
+
+    @property
+    def band(self):
+        return self.bounds[self.rank]
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape], rank order."""
+        if self.world == 1:
+            return t.unsqueeze(0)
+        src = t.contiguous().cpu() if self.host else t.contiguous()
+        # (concatenated along dim 0, the form every backend accepts, then viewed)
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src)
+        out = out.view((self.world,) + tuple(t.shape))
+        return out.to(t.device) if self.host else out
+
+    def all_to_all(self, send: torch.Tensor, send_splits, recv_splits) -> torch.Tensor:
+        """all_to_all_single of a flat buffer: send_splits[q] elements to rank q,
+        recv_splits[q] from rank q."""
+        if self.world == 1:
+            return send
+        src = send.cpu() if self.host else send
+        out = torch.empty(sum(recv_splits), dtype=send.dtype, device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=list(recv_splits), input_split_sizes=list(send_splits))
+        return out.to(send.device) if self.host else out
+
+    def gather_rows(self, flat: torch.Tensor, n: int) -> None:
+        """Every rank's band of a packed triangle (θ) into every rank's copy,
+        in place: after it all ranks hold the same full triangle."""
+        if self.world == 1:
+            return
+        offs = [r0 * n - r0 * (r0 - 1) // 2 for r0, _ in self.bounds] + [flat.numel()]
+        lens = [offs[b + 1] - offs[b] for b in range(self.world)]
+        m = max(lens)
+        mine = torch.zeros(m, dtype=flat.dtype, device=flat.device)
+        b = self.rank
+        mine[:lens[b]] = flat[offs[b]:offs[b + 1]]
+        allv = self.all_gather(mine)
+        for q in range(self.world):
+            if q != b:
+                flat[offs[q]:offs[q + 1]] = allv[q, :lens[q]]

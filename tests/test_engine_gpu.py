@@ -932,3 +932,34 @@ def test_engine_replica_samples_wellconditioned_at_north_star_tolerance(samples)
           f"(L2 {win_l2:.2e})")
     assert win_l2 <= 1e-5, (win_max, win_l2)
     assert th < TOL
+
+
+@pytest.mark.parametrize("kernel", ["bitmask", "csr"])
+def test_band_sharded_world1_equals_exchange_path(kernel):
+    """The band-sharded exchange (LdsEngine.set_band_shards, BASELINE config
+    5 at N > 1) at world size 1: the band is the whole triangle, the factor
+    all-gather and the band all-to-all are identities, so θ, the drawn
+    graphs and the weights must be bit-identical to the engine's own
+    exchange path (dθ, a reducer — here a no-op — then SGD + clamp): the
+    band θ-grad (lds_theta_grad_band, mode 2) against the full assembly, the
+    band draw without mirror + lds_bitmask_mirror_degree against the full
+    draw, over a step-0 window and two τ = 5 windows."""
+    from ldsgnn.replicas import BandShards
+
+    def noop(grad):
+        return None
+    mk = lambda: run_engine_and_oracle(n=700, f_in=24, classes=5, steps=1, tau=5, dropout=0.5, seed=31,  # noqa: E731
+                                       theta_uniform=1.0, long_rows=True, long_rows_kernel=kernel)["engine"]
+    a, b = mk(), mk()  # (run_engine_and_oracle ran step 0 on both: inner step + hyper step, no exchange)
+    a.set_band_shards(BandShards(a.n, world=1, rank=0))
+    for _ in range(2):
+        a.run_window(5)
+        b.run_window(5, grad_reducer=noop)
+    torch.cuda.synchronize()
+    a.check_device_error()
+    assert torch.equal(a.gbatch.bits, b.gbatch.bits)
+    assert torch.equal(a.gbatch.s, b.gbatch.s)
+    assert torch.equal(a.theta, b.theta)
+    for k, v in a.get_params().items():
+        assert torch.equal(v, b.get_params()[k]), k
+    assert a.scalars_host() == b.scalars_host()

@@ -116,6 +116,9 @@ def test_two_ranks_over_gloo_match_batched_replicas(per_rank):
 
 
 LR_N, LR_SEED, LR_WINDOWS = 1100, 6, 2
+# dθ of a dense graph is small (≈ 1/degree): a large outer rate makes θ move
+# well past the comparison tolerance in two windows
+LR_OUTER = 50.0
 
 
 def _long_row_problem():
@@ -132,7 +135,7 @@ def _long_row_problem():
     return prob, theta0, params, O
 
 
-def _long_row_worker(rank, world, port, out, kernel):
+def _long_row_worker(rank, world, port, out, kernel, sharded=False):
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "lds-gnn_amd")]
     from collections import OrderedDict
@@ -151,31 +154,54 @@ def _long_row_worker(rank, world, port, out, kernel):
         grad.div_(world)
     reducer.capturable = exchange_capturable  # (gloo: not capturable -> split graphs, capture outcome agreed)
     eng = LdsEngine(prob["x"].to(dev), prob["y"].to(dev), prob["train"].to(dev), prob["opt"].to(dev),
-                    theta0.clone().to(dev), 5, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1, lr_decay=0.99,
+                    theta0.clone().to(dev), 5, dropout=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=LR_OUTER, lr_decay=0.99,
                     tau=5, generator=ldsgnn.rng.Generator(LR_SEED, rank),
                     params=OrderedDict((k, v.to(dev)) for k, v in params.items()), long_rows_kernel=kernel)
     assert eng.long_rows and eng.bitmask_agg == (kernel == "bitmask")
-    eng.grad_reducer = reducer
+    if sharded:  # band-sharded replicas: factor all-gather, band update, band draws + all-to-all
+        from ldsgnn.replicas import BandShards
+        sh = BandShards(LR_N)
+        eng.set_band_shards(sh)
+
+        def snap():
+            eng.sync_theta()
+            sh.gather_rows(eng.grad, LR_N)  # (each rank's dθ band)
+            return eng.theta.cpu().clone(), eng.grad.cpu().clone()
+    else:
+        eng.grad_reducer = reducer
+
+        def snap():
+            return eng.theta.cpu().clone(), eng.grad.cpu().clone()
     eng.inner_step()
-    eng.hyper_step()  # step 0: dθ -> all-reduce -> SGD + clamp
-    thetas = [eng.theta.cpu().clone()]
-    head_tail = eng.capture_window(5)
-    assert isinstance(head_tail, tuple) and len(head_tail) == 2
+    eng.hyper_step()  # step 0: dθ -> all-reduce -> SGD + clamp (sharded: factors -> band update)
+    t0, g0 = snap()
+    thetas, grads = [t0], [g0]
+    if not sharded:
+        head_tail = eng.capture_window(5)
+        assert isinstance(head_tail, tuple) and len(head_tail) == 2
     for _ in range(LR_WINDOWS):
-        eng.replay(1)
+        if sharded:
+            eng.run_window(5)  # (eager: the sharded exchange is not captured)
+        else:
+            eng.replay(1)
         torch.cuda.synchronize()
-        thetas.append(eng.theta.cpu().clone())
+        t, g = snap()
+        thetas.append(t)
+        grads.append(g)
     eng.check_device_error()
-    out[rank] = thetas
+    out[rank] = (thetas, grads)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kernel", ["bitmask", "csr"])
-def test_two_ranks_long_row_engine_with_exchange(kernel):
+@pytest.mark.parametrize("kernel,sharded", [("bitmask", False), ("csr", False), ("bitmask", True), ("csr", True)])
+def test_two_ranks_long_row_engine_with_exchange(kernel, sharded):
     """BASELINE config 5's multi-GPU half at a test size: the long-row engine
     (dense θ, n = 1 100, the bitmask aggregation chosen by the engine itself,
     or the CSR spill-pass SpMM) with the replicas' exchange — dθ all-reduced
-    (mean) between the split window graphs — on two ranks over gloo.  θ is
+    (mean) between the split window graphs, or (`sharded`) the band-sharded
+    exchange (every rank's factors all-gathered, each rank updating and
+    drawing its own row band of θ for every replica, the bands exchanged
+    all-to-all; θ gathered for the check) — on two ranks over gloo.  θ is
     bit-identical on both ranks after every window and within 1e-5 of the
     oracle's two replicas updated by their mean hypergradient
     (oracle.replica_hyper_step).  Reference: src/trainers/outer.py:77-84."""
@@ -183,32 +209,38 @@ def test_two_ranks_long_row_engine_with_exchange(kernel):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     out = mgr.dict()
-    mp.start_processes(_long_row_worker, args=(world, _free_port(), out, kernel), nprocs=world, join=True,
+    mp.start_processes(_long_row_worker, args=(world, _free_port(), out, kernel, sharded), nprocs=world, join=True,
                        start_method="spawn")
-    r0, r1 = out[0], out[1]
+    (r0, g0), (r1, g1) = out[0], out[1]
     prob, theta0, params, O = _long_row_problem()
     from collections import OrderedDict
     oracles = [O.LdsProblem(prob["x"], prob["y"], prob["train"], prob["val"], prob["test"], prob["opt"],
-                            theta0.clone(), hidden=16, dropout_p=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=0.1,
+                            theta0.clone(), hidden=16, dropout_p=0.5, gcn_lr=0.01, gcn_wd=5e-4, outer_lr=LR_OUTER,
                             lr_decay=0.99, rnd=O.Randomness(LR_SEED, b), params=OrderedDict(params))
                for b in range(world)]
-    ref = []
+    ref, refg = [], []
     for w in range(LR_WINDOWS + 1):
         for _ in range(1 if w == 0 else 5):
             for orc in oracles:
                 orc.inner_step(orc.sample())
-        O.replica_hyper_step(oracles)
+        refg.append(O.replica_hyper_step(oracles)[1])
         ref.append(oracles[0].theta.detach().clone())
     rows = []
-    for w, (a, b, c) in enumerate(zip(r0, r1, ref)):
-        assert torch.equal(a, b), w
+    for w, (a, b, c, ga, gb, gc) in enumerate(zip(r0, r1, ref, g0, g1, refg)):
+        assert torch.equal(a, b) and torch.equal(ga, gb), w
         err = float((a - c).abs().max())
-        rows.append({"window": w, "ranks_bit_identical": True, "max_abs_vs_oracle_replica_mean": err})
+        grel = float((ga - gc).abs().max() / gc.abs().max())
+        rows.append({"window": w, "ranks_bit_identical": True, "max_abs_theta_vs_oracle_replica_mean": err,
+                     "max_grad_rel_vs_oracle_replica_mean": grel})
         assert err < 1e-5, (w, err)
-    assert float((ref[-1] - theta0).abs().max()) > 1e-4
+        assert grel < 1e-4, (w, grel)  # (the windows' Adam steps: test_engine_long_rows_match_oracle's bound)
+    assert float((ref[-1] - theta0).abs().max()) > 1e-3
     d = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(d):
-        with open(os.path.join(d, f"multirank_gloo_long_rows_{kernel}.json"), "w") as f:
+        tag = "sharded" if sharded else "allreduce"
+        with open(os.path.join(d, f"multirank_gloo_long_rows_{kernel}_{tag}.json"), "w") as f:
             json.dump({"test": "tests/test_multirank_gpu.py::test_two_ranks_long_row_engine_with_exchange",
                        "world": world, "backend": "gloo (one device)", "n": LR_N, "kernel": kernel,
+                       "exchange": "band-sharded (factor all-gather, band update, band draws + all-to-all)"
+                       if sharded else "dense dθ all-reduce (mean)",
                        "windows": rows}, f, indent=1)
