@@ -676,13 +676,17 @@ def main():
     ap.add_argument("--strong-total", type=int, default=None, help="config 4 leg: S_total samples split over "
                     "the ranks, against rank 0 alone (default 64 when N > 1, off at N = 1)")
     ap.add_argument("--strong-steps", type=int, default=50)
-    ap.add_argument("--exchange", default="auto", choices=["auto", "split", "noop", "noop-captured", "rccl1"],
+    ap.add_argument("--exchange", default="auto", choices=["auto", "split", "noop", "noop-captured", "rccl1",
+                                                           "sharded", "allreduce"],
                     help="auto: N > 1 captures the RCCL all-reduce into the window graph when every rank's "
                          "capture probe succeeds (ldsgnn.replicas.collective_capture_probe), else splits; split: "
                          "N > 1 with the round-4 two graphs per window around an eager all-reduce; one GPU: "
                          "noop = the N > 1 per-rank path with a no-op reducer (split graphs), noop-captured = "
                          "the same reducer captured into the window graph, rccl1 = a world-size-1 nccl (RCCL) "
-                         "group and its real all-reduce captured into the window graph (DESIGN §5b)")
+                         "group and its real all-reduce captured into the window graph (DESIGN §5b); the long-row "
+                         "engine (config 5): auto = sharded at N > 1 (band-sharded replicas: factor all-gather, "
+                         "band update, band draws + all-to-all, eager windows; at N = 1 a world-1 rehearsal), "
+                         "allreduce = the dense dθ all-reduce (split graphs)")
     ap.add_argument("--keep-theta-grad", type=int, default=0, choices=[0, 1],
                     help="engine, no exchange: 1 writes dθ to θ.grad beside the fused SGD update (the drop-in "
                          "trainer's state after its backward, what FusedBilevelRunner keeps); 0 (default: the "
@@ -750,7 +754,17 @@ def main():
         eng, reducer = make_engine(runner, args.tau, world, args.samples)
         exchange_label = args.exchange if world == 1 else None
         capture_exchange = False
-        if args.exchange in ("noop", "noop-captured", "rccl1"):
+        sharded = eng.long_rows and (args.exchange == "sharded" or (args.exchange == "auto" and world > 1))
+        if args.exchange == "sharded" and not eng.long_rows:
+            raise SystemExit("--exchange sharded: the long-row engine (config 5) only")
+        if sharded:  # band-sharded replicas: the exchange lives inside the hyper step
+            from ldsgnn.replicas import BandShards
+            eng.grad_reducer = None
+            reducer = None
+            eng.set_band_shards(BandShards(eng.n))
+            args.eager = True  # (two collectives per window around host-sized buffers: not captured)
+            exchange_label = f"band-sharded-{args.backend if world > 1 else 'world1'}"
+        elif args.exchange in ("noop", "noop-captured", "rccl1"):
             if world > 1:
                 raise SystemExit(f"--exchange {args.exchange} rehearses the N > 1 path on one GPU")
             if args.exchange == "rccl1":
@@ -774,7 +788,7 @@ def main():
         elif world > 1 and args.exchange == "auto" and args.backend == "nccl":
             from ldsgnn.replicas import collective_capture_probe
             capture_exchange = collective_capture_probe(device)
-        if world > 1:
+        if world > 1 and not sharded:
             exchange_label = f"{args.backend}-allreduce-" + ("captured" if capture_exchange else "split")
         args.capture_exchange = capture_exchange  # (the strong-scaling leg's TN captures the same way)
         eng.async_draw = bool(args.async_draw)
@@ -838,6 +852,8 @@ def main():
                   "ms_per_step": 1000.0 * el / (reps * args.tau)}
 
     in_sync = None
+    if use_engine and eng.shards is not None:
+        eng.sync_theta()  # (band-sharded: every rank's band into every copy, then the same check)
     if world > 1:  # replicas must hold bit-identical θ after every update
         th = eng.theta if use_engine else runner.outer_trainer.model.probs.data
         mine = torch.stack([th.double().sum(), th.double().square().sum()])  # on this rank's device
@@ -852,7 +868,7 @@ def main():
 
     nnz = eng.sampled_nnz_mean() if use_engine else None
     roof, window = None, None
-    if use_engine and not args.no_breakdown:
+    if use_engine and not args.no_breakdown and eng.shards is None:
         rows, ncalls, pre = window_breakdown(eng, reducer, args, device)
         total = sum(r["us_per_window"] for r in rows)
         wall_win = 1000.0 * (steady["ms_per_step"] if steady else 1000.0 * elapsed / args.steps) * args.tau

@@ -1362,7 +1362,8 @@ class LdsEngine:
         row0, row1 = sh.band
         need = count * N * n * W
         if self._allbits is None or self._allbits.numel() < need:
-            self._allbits = torch.empty(need, dtype=torch.int64, device=self.dev)
+            # zeroed once: a row's padding word past ceil(n/64) (words is even) is never drawn
+            self._allbits = torch.zeros(need, dtype=torch.int64, device=self.dev)
         ab = self._allbits[:need].view(count, N, n, W)
         nat.call("lds_sample_band_bits", P(self.theta), n, self.seed, tag_for(_TG, 0), 1, P(self.scalars),
                  counter_off, count, N, row0, row1, P(ab), W, st)

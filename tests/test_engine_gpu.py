@@ -957,7 +957,8 @@ def test_band_sharded_world1_equals_exchange_path(kernel):
         b.run_window(5, grad_reducer=noop)
     torch.cuda.synchronize()
     a.check_device_error()
-    assert torch.equal(a.gbatch.bits, b.gbatch.bits)
+    nbw = (a.n + 63) // 64  # (the padding word of an odd word count is never drawn)
+    assert torch.equal(a.gbatch.bits[..., :nbw], b.gbatch.bits[..., :nbw])
     assert torch.equal(a.gbatch.s, b.gbatch.s)
     assert torch.equal(a.theta, b.theta)
     for k, v in a.get_params().items():
