@@ -53,7 +53,7 @@ namespace spill {
 constexpr int kSpStream = 12;         // streaming waves 0-11; multiply waves 12-15
 constexpr int kSpMul = 16 - kSpStream;
 constexpr int kSpThreads = 1024;
-constexpr int kSpE = 8;               // entries per lane and step (the product; kernel template kE)
+constexpr int kSpE = 8;               // entries per lane and step
 constexpr int kSpStepEntries = 64 * kSpE;  // 512 entries (2 KB) per step
 constexpr int kSpDepth = 4;           // register ring slots per streaming wave (three steps in flight)
 constexpr int kSpMaxTiles = 6;
@@ -112,11 +112,10 @@ __device__ __forceinline__ int sp_ld(const int* p) {
 // OR of a lane's eight window offsets c_e - base (as unsigned: a column below
 // the base is huge): < 64 iff every column lies in [base, base + 64), and
 // base + it bounds the largest column from above.
-template <int kE>
-__device__ __forceinline__ uint32_t sp_offsets(const int (&c)[kE], int base, uint32_t (&r)[kE]) {
+__device__ __forceinline__ uint32_t sp_offsets(const int (&c)[kSpE], int base, uint32_t (&r)[kSpE]) {
     uint32_t o = 0u;
 #pragma unroll
-    for (int e = 0; e < kE; ++e) {
+    for (int e = 0; e < kSpE; ++e) {
         r[e] = (uint32_t)(c[e] - base);
         o |= r[e];
     }
@@ -131,16 +130,14 @@ __device__ __forceinline__ uint32_t sp_offsets(const int (&c)[kE], int base, uin
 // word is set as described above; without it (the caller guarantees
 // ascending columns in [0, n), as for every CSR this library builds) they test
 // a lane's first and last column only, as the round-4 product did.
-// kE: entries per lane and step (8: 2-KB steps, the product; 16: 4-KB steps,
-// twice the bytes in flight per ring slot)
-template <int kTiles, bool kCheck, int kDelay = 0, int kE = kSpE>
+template <int kTiles, bool kCheck, int kDelay = 0>
 __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
     int chunks, int cpp, int passes, int rowdw, const uint32_t* __restrict__ colmax, const float* __restrict__ s,
     float* __restrict__ y, int ldy, int beta, uint32_t* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sp_lds[];
-    constexpr int D = kSpDepth, kStep = 64 * kE, kLd = kE / 4;  // kLd 16-byte loads per lane and step
-    static_assert((D - 1) * kLd <= 15, "vmcnt field");
+    constexpr int D = kSpDepth, kStep = kSpStepEntries;
+    static_assert((D - 1) * (kSpE / 4) <= 15, "vmcnt field");
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int r0 = (int)blockIdx.x * rows_per_wg;
@@ -183,7 +180,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         // the ring: a step's start, row bounds and packed (row | pass << 8 |
         // first << 16 | last << 17), -1 for a null step; its columns in registers
         int ma[D], mlo[D], mup[D], mk[D];
-        v4i rg[D][kLd];
+        v4i rg[D][2];
         // process side: the pass the multiply waves wait for; (row, pass) of the
         // last step and its bounds / bit rows; the row's spill flag and first
         // entry past pass p + 1
@@ -241,17 +238,17 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         mup[J] = up_;                                                                                        \
         mk[J] = k_;                                                                                          \
         pending += k_ >= 0 ? 1 : 0;                                                                          \
-        _Pragma("unroll") for (int h_ = 0; h_ < kLd; ++h_) {                                                 \
-            const int aa_ = a_ + kE * lane + 4 * h_;                                                         \
+        _Pragma("unroll") for (int h_ = 0; h_ < 2; ++h_) {                                                   \
+            const int aa_ = a_ + kSpE * lane + 4 * h_;                                                       \
             const int* src_ = (a_ >= 0 && aa_ + 4 <= nnz) ? col + aa_ : dummy;                               \
             rb_gload(rg[J][h_], reinterpret_cast<const v4i*>(src_));                                         \
         }                                                                                                    \
     } while (0)
 #define LDS_SP_PROCESS(J)                                                                                    \
     do {                                                                                                     \
-        /* slot J's step landed: every iteration issues exactly kLd loads, so D - 1 younger steps stay */    \
+        /* slot J's step landed: every iteration issues exactly two loads, so D - 1 younger steps stay */    \
         /* in flight (the rare paths' plain loads are waited for where they are used: stricter) */           \
-        __builtin_amdgcn_s_waitcnt(0x0F70 | ((D - 1) * kLd));                                                \
+        __builtin_amdgcn_s_waitcnt(0x0F70 | ((D - 1) * 2));                                                  \
         asm volatile("" ::: "memory");                                                                       \
         const int k_ = mk[J];                                                                                \
         if (k_ >= 0) {                                                                                       \
@@ -277,16 +274,12 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
             uint32_t* const bp_ = pbp;                                                                       \
             uint32_t* const bq_ = pbq;                                                                       \
             const int a_ = ma[J], rlo_ = mlo[J], rup_ = mup[J];                                              \
-            _Pragma("unroll") for (int h_ = 0; h_ < kLd; h_ += 2) rb_bind(rg[J][h_], rg[J][h_ + 1]);      \
-            bool spill_ = false;                                                                             \
+            rb_bind(rg[J][0], rg[J][1]);                                                                     \
+            const int c_[kSpE] = {rg[J][0][0], rg[J][0][1], rg[J][0][2], rg[J][0][3],                        \
+                                  rg[J][1][0], rg[J][1][1], rg[J][1][2], rg[J][1][3]};                       \
+            const int i0_ = a_ + kSpE * lane;                                                                \
+            bool spill_ = false, fast_ = false;                                                              \
             int myx_ = kSpNone;                                                                              \
-            /* the lane's entries in groups of eight, each with its own 64-column window */                  \
-            _Pragma("unroll") for (int hh_ = 0; hh_ < kE / kSpE; ++hh_) {                                    \
-            const int c_[kSpE] = {rg[J][2 * hh_][0], rg[J][2 * hh_][1], rg[J][2 * hh_][2], rg[J][2 * hh_][3], \
-                                  rg[J][2 * hh_ + 1][0], rg[J][2 * hh_ + 1][1], rg[J][2 * hh_ + 1][2],       \
-                                  rg[J][2 * hh_ + 1][3]};                                                    \
-            const int i0_ = a_ + kE * lane + kSpE * hh_;                                                     \
-            bool fast_ = false;                                                                              \
             if (kCheck && a_ >= rlo_ && a_ + kStep <= rup_) { /* interior (uniform): every entry is the row's */       \
                 const uint32_t w0_ = (uint32_t)(c_[0] - lo_) >> 5;                                           \
                 const int base_ = lo_ + (int)(w0_ << 5);                                                     \
@@ -408,7 +401,6 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
                     }                                                                                        \
                 }                                                                                            \
             }                                                                                                \
-            } /* (the groups of eight) */                                                                    \
             if (__ballot(spill_) != 0ull) bnd = true;                                                        \
             const uint64_t xm_ = __ballot(myx_ != kSpNone);                                                  \
             if (xm_ != 0ull) estar = min(estar, __builtin_amdgcn_readlane(myx_, __builtin_ctzll(xm_)));      \
@@ -559,7 +551,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
 
 // Launch on grid g (0: one workgroup per CU; rows split evenly, at most
 // kSpMaxRows per workgroup).  err != NULL: the checked form.
-template <int kDelay, int kE = kSpE>
+template <int kDelay>
 inline int sp_launch(const int* row_ptr, const int* col, const float* s, int n, const Ws& w, float* y, int ldy,
                      int beta, int grid, uint32_t* err, hipStream_t st) {
     const int nc = chunks_of(n);
@@ -576,9 +568,9 @@ inline int sp_launch(const int* row_ptr, const int* col, const float* s, int n, 
     LDS_CHECK_ARG(lds <= 163840 && sg.passes <= 255);  // (the pass is an 8-bit field of a ring record)
 #define LDS_SP_LAUNCH1(TT, CK)                                                                                 \
     do {                                                                                                       \
-        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, CK, kDelay, kE>, lds);                        \
+        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, CK, kDelay>, lds);                            \
         if (e != hipSuccess) return (int)e;                                                                    \
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, CK, kDelay, kE>), dim3(g), dim3(kSpThreads), lds, st, \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, CK, kDelay>), dim3(g), dim3(kSpThreads), lds, st, \
                            row_ptr, col, n, R, (const int8_t*)w.zq, nc, sg.cpp, sg.passes, sg.rowdw,          \
                            (const uint32_t*)w.colmax, s, y, ldy, beta, err);                                   \
     } while (0)

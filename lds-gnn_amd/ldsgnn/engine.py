@@ -1367,18 +1367,7 @@ class LdsEngine:
         ab = self._allbits[:need].view(count, N, n, W)
         nat.call("lds_sample_band_bits", P(self.theta), n, self.seed, tag_for(_TG, 0), 1, P(self.scalars),
                  counter_off, count, N, row0, row1, P(ab), W, st)
-        dst = bits.view(count, n, W)
-        if N == 1:
-            dst.copy_(ab[:, 0])
-        else:
-            rows = [r1 - r0 for r0, r1 in sh.bounds]
-            send = ab[:, :, row0:row1, :].permute(1, 0, 2, 3).contiguous().view(-1)  # [dest, g, band rows, W]
-            recv = sh.all_to_all(send, [count * (row1 - row0) * W] * N, [count * r * W for r in rows])
-            off = 0
-            for q, (q0, q1) in enumerate(sh.bounds):
-                m = count * (q1 - q0) * W
-                dst[:, q0:q1, :] = recv[off:off + m].view(count, q1 - q0, W)
-                off += m
+        sh.exchange_rows(ab, bits.view(count, n, W))
         nat.call("lds_bitmask_mirror_degree", P(bits), n, W, count, P(deg), P(s), st)
         self._ws_clean = False
         if not self.bitmask_agg:  # CSR / s / ELL from the completed bits and their degree counts

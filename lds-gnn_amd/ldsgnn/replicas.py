@@ -184,6 +184,28 @@ class BandShards:
         dist.all_to_all_single(out, src, output_split_sizes=list(recv_splits), input_split_sizes=list(send_splits))
         return out.to(send.device) if self.host else out
 
+    def exchange_rows(self, ab: torch.Tensor, dst: torch.Tensor) -> None:
+        """The band all-to-all of the sharded draw: ab [count, world, n, W]
+        holds (in this rank's band rows) every replica's graphs; dst
+        [count, n, W] receives every band's rows of THIS rank's replica.  A
+        band's rows travel from word row0 / 64 on — the bounding box of their
+        upper-triangle words; the words below are lower triangle, which the
+        owner's mirror writes — so each rank sends about 1/world of the
+        triangle's bits (twice that for the last band, a triangle)."""
+        count, W = ab.shape[0], ab.shape[3]
+        if self.world == 1:
+            dst.copy_(ab[:, 0])
+            return
+        row0, row1 = self.band
+        box = [(q1 - q0) * (W - q0 // 64) for q0, q1 in self.bounds]
+        send = ab[:, :, row0:row1, row0 // 64:].permute(1, 0, 2, 3).contiguous().view(-1)  # [dest, g, rows, box W]
+        recv = self.all_to_all(send, [count * box[self.rank]] * self.world, [count * m for m in box])
+        off = 0
+        for q, (q0, q1) in enumerate(self.bounds):
+            m = count * box[q]
+            dst[:, q0:q1, q0 // 64:] = recv[off:off + m].view(count, q1 - q0, W - q0 // 64)
+            off += m
+
     def gather_rows(self, flat: torch.Tensor, n: int) -> None:
         """Every rank's band of a packed triangle (θ) into every rank's copy,
         in place: after it all ranks hold the same full triangle."""

@@ -48,25 +48,18 @@ def _worker(rank, world, port, n, out):
     g = sh.all_gather(u)
     assert g.shape == (world, n, 3) and all(float(g[q, 0, 0]) == q for q in range(world))
     # band rows of every replica's graphs to their owners (the engine's pack / unpack)
-    count, W = 2, 4
+    count, W = 2, (n + 63) // 64 + 1
     ab = torch.zeros((count, world, n, W), dtype=torch.int64)
     r0, r1 = sh.band
     for q in range(world):  # my band's rows of replica q's graphs: tagged (writer, replica, row)
         rows = torch.arange(r0, r1, dtype=torch.int64)
         ab[:, q, r0:r1, :] = (rank * 1000000 + q * 100000 + rows)[None, :, None]
-    send = ab[:, :, r0:r1, :].permute(1, 0, 2, 3).contiguous().view(-1)
-    rows = [b1 - b0 for b0, b1 in sh.bounds]
-    recv = sh.all_to_all(send, [count * (r1 - r0) * W] * world, [count * r * W for r in rows])
-    dst = torch.zeros((count, n, W), dtype=torch.int64)
-    off = 0
-    for q, (q0, q1) in enumerate(sh.bounds):
-        m = count * (q1 - q0) * W
-        dst[:, q0:q1, :] = recv[off:off + m].view(count, q1 - q0, W)
-        off += m
-    want = torch.zeros_like(dst)
-    for q, (q0, q1) in enumerate(sh.bounds):  # row i came from the rank owning it, for MY replica
-        rws = torch.arange(q0, q1, dtype=torch.int64)
-        want[:, q0:q1, :] = (q * 1000000 + rank * 100000 + rws)[None, :, None]
+    dst = torch.full((count, n, W), -7, dtype=torch.int64)
+    sh.exchange_rows(ab, dst)
+    want = torch.full_like(dst, -7)
+    for q, (q0, q1) in enumerate(sh.bounds):  # row i came from the rank owning it, for MY replica,
+        rws = torch.arange(q0, q1, dtype=torch.int64)  # from word q0 / 64 on (the band's box)
+        want[:, q0:q1, q0 // 64:] = (q * 1000000 + rank * 100000 + rws)[None, :, None]
     assert torch.equal(dst, want)
     # θ row gather: each rank's band into everyone's copy
     m = n * (n + 1) // 2

@@ -1611,16 +1611,3 @@ static int variants_launch(const int* row_ptr, const int* col, const float* s, i
 #undef LDS_CP_LAUNCH
     LDS_RETURN_LAST_ERROR();
 }
-
-// The product spill-pass kernel with 4-KB streaming steps (16 entries per lane,
-// four 16-byte loads, two windows of eight): twice the bytes in flight per
-// ring slot (round 6, tools/spmm_config5.py "spill-pass e16").  Operands as
-// lds_spmm_norm_dense after its quantisation (ws holds the digits).
-LDS_VAR_EXPORT int lds_variants_spmm_dense_e16(const int* row_ptr, const int* col, const float* s, int n,
-                                               float* y, int ldy, void* ws, int grid, uint32_t* err,
-                                               void* stream) {
-    LDS_CHECK_ARG(row_ptr && col && s && y && ws && n > 0 && n <= kDnMaxChunks * kChunk && ldy >= kF);
-    LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
-    const Ws w = carve(ws, n);
-    return lds::spill::sp_launch<0, 16>(row_ptr, col, s, n, w, y, ldy, 0, grid, err, (hipStream_t)stream);
-}

@@ -33,8 +33,6 @@ def lib():
         _lib.lds_variants_spmm_dense.restype = c_int
         _lib.lds_variants_spmm_dense_delayed.argtypes = [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P]
         _lib.lds_variants_spmm_dense_delayed.restype = c_int
-        _lib.lds_variants_spmm_dense_e16.argtypes = [P, P, P, c_int, P, c_int, P, c_int, P, P]
-        _lib.lds_variants_spmm_dense_e16.restype = c_int
     return _lib
 
 
@@ -55,10 +53,3 @@ def spmm_dense_delayed(rp, col, s, n, y, ldy, ws, grid, delay, err, stream):
     pass barrier (delay 1 or 4): the timing-independent buffer-clear check."""
     nat.check(lib().lds_variants_spmm_dense_delayed(rp, col, s, n, y, ldy, ws, grid, delay, err, stream),
               f"lds_variants_spmm_dense_delayed({delay})")
-
-
-def spmm_dense_e16(rp, col, s, n, y, ldy, ws, grid, err, stream):
-    """The product spill-pass kernel with 4-KB streaming steps (16 entries per
-    lane); the digits must be in ws (as spmm_dense)."""
-    nat.check(lib().lds_variants_spmm_dense_e16(rp, col, s, n, y, ldy, ws, grid, err, stream),
-              "lds_variants_spmm_dense_e16")
