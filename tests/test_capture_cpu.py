@@ -134,3 +134,39 @@ def test_collective_reducer_needs_a_group_of_more_than_one_rank():
     assert not E._collective_reducer(red)          # no `capturable`: not the replicas' collective
     red.capturable = lambda: True
     assert not E._collective_reducer(red)          # no process group in this process
+
+
+def _agree_worker(rank, world, port, statuses, out):
+    import os
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def red(grad):
+        return None
+    red.capturable = lambda: False
+    out[rank] = (E._collective_reducer(red), E._ranks_agree(statuses[rank], "cpu"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("statuses,want", [((2, 2), 2), ((2, 1), 1), ((0, 2), 0), ((1, 0), 0)])
+def test_ranks_agree_on_the_worst_capture_outcome(statuses, want):
+    """Round-5 ADVICE: with a collective exchange every rank learns the worst
+    capture outcome of any rank (an eager MIN all-reduce, before any replay),
+    so one rank's failed capture moves every rank to the split graphs
+    (RETRY_SPLIT) or makes every rank raise (FATAL) instead of leaving the
+    others replaying a graph that waits inside the collective."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_agree_worker, args=(2, port, statuses, out), nprocs=2, join=True)
+    for r in range(2):
+        collective, agreed = out[r]
+        assert collective  # the replicas' reducer over a 2-rank group: the agreement runs
+        assert agreed == want
