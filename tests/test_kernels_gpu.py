@@ -496,6 +496,40 @@ def test_sgd_sample_split_stale_tile_counter_sets_device_error(device):
         assert word == (nat.DEVERR_SGD_TILE_COUNTER if stale else 0), (stale, word)
 
 
+@pytest.mark.parametrize("n", [64, 130, 700, 1100])
+def test_bitmask_mirror_degree_completes_symmetric_graphs(device, n):
+    """lds_bitmask_mirror_degree (the band-sharded exchange's owner step):
+    from a symmetric bitmask with its strictly-lower words cleared it rebuilds
+    every lower word (8 × 8 super-blocks of 64 × 64 bit transposes, partial
+    super-blocks at the edge) and writes the degrees and s = deg^-1/2 the
+    sampler's popcount pass gives."""
+    g = torch.Generator().manual_seed(n)
+    graphs = 3
+    words = nat.lib.lds_bitmask_words(n)
+    wsi = nat.lib.lds_sample_ws_ints(n)
+    a = torch.rand((graphs, n, n), generator=g) < 0.3
+    a = a.triu(1)
+    a = a | a.transpose(1, 2) | torch.eye(n, dtype=torch.bool)[None]
+    pad = torch.zeros((graphs, n, 64 * words), dtype=torch.bool)
+    pad[:, :, :n] = a
+    wts = (1 << torch.arange(64, dtype=torch.int64))
+    full = (pad.view(graphs, n, words, 64).long() * wts).sum(-1)  # [graphs, n, words] (two's complement wraps)
+    upper = full.clone()
+    for r in range(n):
+        upper[:, r, :r // 64] = 0  # strictly-lower words
+    bits = upper.to(device)
+    deg = torch.zeros((graphs, wsi), dtype=torch.int32, device=device)
+    s = torch.zeros((graphs, n), device=device)
+    nat.call("lds_bitmask_mirror_degree", nat.ptr(bits), n, words, graphs, nat.ptr(deg), nat.ptr(s),
+             nat.stream_of(torch.device(device)))
+    torch.cuda.synchronize()
+    assert torch.equal(bits.cpu(), full)
+    want_deg = a.sum(-1).to(torch.int32)
+    assert torch.equal(deg[:, :n].cpu(), want_deg)
+    want_s = 1.0 / want_deg.float().sqrt()  # (torch CPU's fp32 1 / sqrt(degree), DESIGN §3)
+    assert torch.equal(s.cpu(), want_s)
+
+
 def test_fill_guard_pads_inflated_degrees(device):
     """lds_sample_graphs_multi promised a zero degree workspace (ws_zeroed =
     1) that is not: every row's count exceeds its drawn bits.  The fill
