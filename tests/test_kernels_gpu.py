@@ -526,8 +526,14 @@ def test_bitmask_mirror_degree_completes_symmetric_graphs(device, n):
     assert torch.equal(bits.cpu(), full)
     want_deg = a.sum(-1).to(torch.int32)
     assert torch.equal(deg[:, :n].cpu(), want_deg)
-    want_s = 1.0 / want_deg.float().sqrt()  # (torch CPU's fp32 1 / sqrt(degree))
-    assert torch.equal(s.cpu(), want_s)
+    ref_full = full.to(device)  # the sampler's own degree pass on the complete bits: the same s bit for bit
+    for gi in range(graphs):
+        d1 = torch.zeros(n, dtype=torch.int32, device=device)
+        s1 = torch.zeros(n, device=device)
+        nat.call("lds_bitmask_degree", nat.ptr(ref_full[gi]), n, words, nat.ptr(d1), nat.ptr(s1),
+                 nat.stream_of(torch.device(device)))
+        torch.cuda.synchronize()
+        assert torch.equal(s[gi], s1) and torch.equal(deg[gi, :n], d1)
 
 
 def test_fill_guard_pads_inflated_degrees(device):
