@@ -96,6 +96,10 @@ __device__ __forceinline__ void dn_or(uint32_t* p, uint32_t m) {
 __device__ __forceinline__ void rb_gload(v4i& v, const v4i* p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
 }
+// the same with the non-temporal cache policy (a once-read stream)
+__device__ __forceinline__ void rb_gload_nt(v4i& v, const v4i* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+}
 __device__ __forceinline__ void rb_bind(v4i& a, v4i& b) { asm volatile("" : "+v"(a), "+v"(b)); }
 
 inline int device_cus() {

@@ -274,10 +274,31 @@ __global__ __launch_bounds__(256) void sample_tiles_kernel(
 // (lds_bitmask_mirror_degree).  A workgroup takes an 8 × 8 super-block of
 // 64 × 64 bit blocks — source row blocks 8R … 8R + 7, words 8C … 8C + 7,
 // C >= R — loads its 512 rows × 64 bytes coalesced into LDS, transposes each
-// block (rb, w) with w > rb by 64 ballots (lane l holds row 64·rb + l's word
-// w; lane c keeps the word rb of row 64·w + c), and stores the 512 transposed
-// rows × 64 bytes coalesced.  (A wave per block with row-strided 8-byte
-// accesses measured 270 µs for six config-5 graphs.)  Graph blockIdx.y.
+// block (rb, w) with w > rb in registers (lane l holds row 64·rb + l's word
+// w; six butterfly stages, bit64_transpose, leave lane c with the word rb of
+// row 64·w + c), and stores the 512 transposed rows × 64 bytes coalesced.
+// (One wave per block with row-strided 8-byte accesses and 64 ballots: 270
+// µs for six config-5 graphs; super-blocks with the ballots: 230.)  Graph
+// blockIdx.y.
+// 64 × 64 bit transpose across a wave: lane l holds row l (bit c = column c);
+// afterwards lane l holds column l.  Stage s swaps, between lanes l and l ^ s,
+// the s × s sub-blocks off the diagonal of every 2s × 2s block.
+__device__ __forceinline__ uint64_t bit64_transpose(uint64_t v, int lane) {
+    const uint64_t masks[6] = {0xFFFFFFFF00000000ull, 0xFFFF0000FFFF0000ull, 0xFF00FF00FF00FF00ull,
+                               0xF0F0F0F0F0F0F0F0ull, 0xCCCCCCCCCCCCCCCCull, 0xAAAAAAAAAAAAAAAAull};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int s = 32 >> k;
+        const uint64_t m = masks[k];  // columns with bit s set
+        const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
+        const uint64_t x = ((uint64_t)hi << 32) | lo;
+        // lanes without bit s keep their columns without bit s and take the
+        // partner's such columns, shifted up; lanes with bit s the converse
+        v = (lane & s) ? ((v & m) | ((x >> s) & ~m)) : ((v & ~m) | ((x << s) & m));
+    }
+    return v;
+}
+
 constexpr int kMirSb = 8;                 // blocks per super-block side
 constexpr int kMirRows = 64 * kMirSb;     // 512 rows
 __global__ __launch_bounds__(256) void mirror_kernel(uint64_t* __restrict__ bits, int n, int words) {
@@ -302,13 +323,7 @@ __global__ __launch_bounds__(256) void mirror_kernel(uint64_t* __restrict__ bits
         const int rbl = blk >> 3, wl = blk & 7;  // block (row block 8R + rbl, word 8C + wl)
         if (kMirSb * C + wl <= kMirSb * R + rbl) continue;  // (uniform) not strictly upper
         const uint64_t v = src[64 * rbl + lane][wl ^ (lane & 7)];
-        uint64_t mine = 0ull;
-#pragma unroll
-        for (int c = 0; c < 64; ++c) {
-            const uint64_t b = __ballot((v >> c) & 1ull);
-            mine = lane == c ? b : mine;
-        }
-        dst[64 * wl + lane][rbl ^ (lane & 7)] = mine;
+        dst[64 * wl + lane][rbl ^ (lane & 7)] = bit64_transpose(v, lane);
     }
     __syncthreads();
     // destination: rows 512·C + r, words 8·R + q, where the block was transposed

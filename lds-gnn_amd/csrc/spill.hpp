@@ -130,7 +130,8 @@ __device__ __forceinline__ uint32_t sp_offsets(const int (&c)[kSpE], int base, u
 // word is set as described above; without it (the caller guarantees
 // ascending columns in [0, n), as for every CSR this library builds) they test
 // a lane's first and last column only, as the round-4 product did.
-template <int kTiles, bool kCheck, int kDelay = 0>
+// kNt (tools only): the column stream loaded with the non-temporal policy
+template <int kTiles, bool kCheck, int kDelay = 0, bool kNt = false>
 __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
     const int* __restrict__ rp, const int* __restrict__ col, int n, int rows_per_wg, const int8_t* __restrict__ zq,
     int chunks, int cpp, int passes, int rowdw, const uint32_t* __restrict__ colmax, const float* __restrict__ s,
@@ -241,7 +242,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
         _Pragma("unroll") for (int h_ = 0; h_ < 2; ++h_) {                                                   \
             const int aa_ = a_ + kSpE * lane + 4 * h_;                                                       \
             const int* src_ = (a_ >= 0 && aa_ + 4 <= nnz) ? col + aa_ : dummy;                               \
-            rb_gload(rg[J][h_], reinterpret_cast<const v4i*>(src_));                                         \
+            if constexpr (kNt) rb_gload_nt(rg[J][h_], reinterpret_cast<const v4i*>(src_));                   \
+            else rb_gload(rg[J][h_], reinterpret_cast<const v4i*>(src_));                                    \
         }                                                                                                    \
     } while (0)
 #define LDS_SP_PROCESS(J)                                                                                    \
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void csr_spill_agg_kernel(
 
 // Launch on grid g (0: one workgroup per CU; rows split evenly, at most
 // kSpMaxRows per workgroup).  err != NULL: the checked form.
-template <int kDelay>
+template <int kDelay, bool kNt = false>
 inline int sp_launch(const int* row_ptr, const int* col, const float* s, int n, const Ws& w, float* y, int ldy,
                      int beta, int grid, uint32_t* err, hipStream_t st) {
     const int nc = chunks_of(n);
@@ -568,9 +570,9 @@ inline int sp_launch(const int* row_ptr, const int* col, const float* s, int n, 
     LDS_CHECK_ARG(lds <= 163840 && sg.passes <= 255);  // (the pass is an 8-bit field of a ring record)
 #define LDS_SP_LAUNCH1(TT, CK)                                                                                 \
     do {                                                                                                       \
-        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, CK, kDelay>, lds);                            \
+        const hipError_t e = allow_lds(&csr_spill_agg_kernel<TT, CK, kDelay, kNt>, lds);                       \
         if (e != hipSuccess) return (int)e;                                                                    \
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, CK, kDelay>), dim3(g), dim3(kSpThreads), lds, st, \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(csr_spill_agg_kernel<TT, CK, kDelay, kNt>), dim3(g), dim3(kSpThreads), lds, st, \
                            row_ptr, col, n, R, (const int8_t*)w.zq, nc, sg.cpp, sg.passes, sg.rowdw,          \
                            (const uint32_t*)w.colmax, s, y, ldy, beta, err);                                   \
     } while (0)

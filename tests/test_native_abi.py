@@ -144,7 +144,7 @@ def test_variants_library_is_tools_only():
     if not os.path.exists(path):
         pytest.skip("tools/variants not built")
     assert _exported_lds_symbols(path) == ["lds_variants_spmm_dense", "lds_variants_spmm_dense_delayed",
-                                          "lds_variants_ws_bytes"]
+                                          "lds_variants_spmm_dense_nt", "lds_variants_ws_bytes"]
 
 
 def _kernel_metadata(lib_path, tmp_path):

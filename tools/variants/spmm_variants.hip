@@ -1611,3 +1611,14 @@ static int variants_launch(const int* row_ptr, const int* col, const float* s, i
 #undef LDS_CP_LAUNCH
     LDS_RETURN_LAST_ERROR();
 }
+
+// The product spill-pass kernel with its column stream loaded non-temporally
+// (global_load_dwordx4 ... nt; round 6 A/B, tools/microbench/spmm_nt_ab.py).
+// Operands as lds_spmm_norm_dense after its quantisation (ws holds the digits).
+LDS_VAR_EXPORT int lds_variants_spmm_dense_nt(const int* row_ptr, const int* col, const float* s, int n, float* y,
+                                              int ldy, void* ws, int grid, uint32_t* err, void* stream) {
+    LDS_CHECK_ARG(row_ptr && col && s && y && ws && n > 0 && n <= kDnMaxChunks * kChunk && ldy >= kF);
+    LDS_CHECK_ARG((((uintptr_t)col) & 15) == 0 && (((uintptr_t)ws) & 15) == 0);
+    const Ws w = carve(ws, n);
+    return lds::spill::sp_launch<0, true>(row_ptr, col, s, n, w, y, ldy, 0, grid, err, (hipStream_t)stream);
+}

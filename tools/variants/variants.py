@@ -33,6 +33,8 @@ def lib():
         _lib.lds_variants_spmm_dense.restype = c_int
         _lib.lds_variants_spmm_dense_delayed.argtypes = [P, P, P, c_int, P, c_int, P, c_int, c_int, P, P]
         _lib.lds_variants_spmm_dense_delayed.restype = c_int
+        _lib.lds_variants_spmm_dense_nt.argtypes = [P, P, P, c_int, P, c_int, P, c_int, P, P]
+        _lib.lds_variants_spmm_dense_nt.restype = c_int
     return _lib
 
 
@@ -53,3 +55,10 @@ def spmm_dense_delayed(rp, col, s, n, y, ldy, ws, grid, delay, err, stream):
     pass barrier (delay 1 or 4): the timing-independent buffer-clear check."""
     nat.check(lib().lds_variants_spmm_dense_delayed(rp, col, s, n, y, ldy, ws, grid, delay, err, stream),
               f"lds_variants_spmm_dense_delayed({delay})")
+
+
+def spmm_dense_nt(rp, col, s, n, y, ldy, ws, grid, err, stream):
+    """The product spill-pass kernel with its column stream loaded with the
+    non-temporal policy; the digits must be in ws (as spmm_dense)."""
+    nat.check(lib().lds_variants_spmm_dense_nt(rp, col, s, n, y, ldy, ws, grid, err, stream),
+              "lds_variants_spmm_dense_nt")
