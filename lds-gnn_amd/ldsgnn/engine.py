@@ -1336,7 +1336,7 @@ class LdsEngine:
             self.U[:, k0:].zero_()
             self.V[:, k0:].zero_()
         N = sh.world
-        if N > 1:
+        if not sh._skip:
             uc = sh.all_gather(self.U).permute(1, 0, 2).contiguous()  # [n, N, ldk]
             vc = sh.all_gather(self.V).permute(1, 0, 2).contiguous()
             rg = sh.all_gather(self.R[0])  # [N, n]

@@ -149,7 +149,9 @@ class BandShards:
     completes the lower triangle (lds_bitmask_mirror_degree).  Replica = rank
     (one sample per rank).  Under gloo the collectives run on host copies."""
 
-    def __init__(self, n: int, world: Optional[int] = None, rank: Optional[int] = None):
+    def __init__(self, n: int, world: Optional[int] = None, rank: Optional[int] = None, always: bool = False):
+        """`always`: run the collectives at world size 1 too (the world-size-1
+        RCCL rehearsal of tests/rccl_worker.py; a process group must be up)."""
         up = _group_up()
         self.world = int(world if world is not None else (dist.get_world_size() if up else 1))
         self.rank = int(rank if rank is not None else (dist.get_rank() if up else 0))
@@ -158,6 +160,8 @@ class BandShards:
         self.n = n
         self.bounds = band_bounds(n, self.world)
         self.host = up and dist.get_backend() != "nccl"  # gloo: collectives on host copies
+        self.always = bool(always) and up
+        self._skip = self.world == 1 and not self.always  # world size 1: the collectives are identities
 
     @property
     def band(self):
@@ -165,7 +169,7 @@ class BandShards:
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape], rank order."""
-        if self.world == 1:
+        if self._skip:
             return t.unsqueeze(0)
         src = t.contiguous().cpu() if self.host else t.contiguous()
         # (concatenated along dim 0, the form every backend accepts, then viewed)
@@ -177,7 +181,7 @@ class BandShards:
     def all_to_all(self, send: torch.Tensor, send_splits, recv_splits) -> torch.Tensor:
         """all_to_all_single of a flat buffer: send_splits[q] elements to rank q,
         recv_splits[q] from rank q."""
-        if self.world == 1:
+        if self._skip:
             return send
         src = send.cpu() if self.host else send
         out = torch.empty(sum(recv_splits), dtype=send.dtype, device=src.device)
@@ -193,7 +197,7 @@ class BandShards:
         owner's mirror writes — so each rank sends about 1/world of the
         triangle's bits (twice that for the last band, a triangle)."""
         count, W = ab.shape[0], ab.shape[3]
-        if self.world == 1:
+        if self._skip:
             dst.copy_(ab[:, 0])
             return
         row0, row1 = self.band
@@ -209,7 +213,7 @@ class BandShards:
     def gather_rows(self, flat: torch.Tensor, n: int) -> None:
         """Every rank's band of a packed triangle (θ) into every rank's copy,
         in place: after it all ranks hold the same full triangle."""
-        if self.world == 1:
+        if self._skip:
             return
         offs = [r0 * n - r0 * (r0 - 1) // 2 for r0, _ in self.bounds] + [flat.numel()]
         lens = [offs[b + 1] - offs[b] for b in range(self.world)]

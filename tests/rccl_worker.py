@@ -52,6 +52,33 @@ def trainers(reducer):
     return engine_from_trainers(inner, outer, tau=5, generator=ldsgnn.rng.default_generator, samples=SAMPLES)
 
 
+def band_sharded_rccl() -> bool:
+    """The band-sharded exchange's collectives on the nccl backend with
+    device tensors (factor all-gather, the band rows' all-to-all with split
+    sizes, θ's band gather), forced to run at world size 1: a long-row engine
+    with them against one whose world-size-1 collectives are identities —
+    θ, bits, s and weights bit-identical over a step-0 window and two τ = 5
+    windows."""
+    from ldsgnn.replicas import BandShards
+    from tests.parity_harness import run_engine_and_oracle
+    engs = []
+    for always in (True, False):
+        e = run_engine_and_oracle(n=700, f_in=24, classes=5, steps=1, tau=5, dropout=0.5, seed=31,
+                                  theta_uniform=1.0, long_rows=True)["engine"]
+        e.set_band_shards(BandShards(e.n, world=1, rank=0, always=always))
+        assert e.shards.always == always
+        for _ in range(2):
+            e.run_window(5)
+        e.sync_theta()
+        engs.append(e)
+    torch.cuda.synchronize()
+    a, b = engs
+    nbw = (a.n + 63) // 64
+    return bool(torch.equal(a.theta, b.theta) and torch.equal(a.gbatch.bits[..., :nbw], b.gbatch.bits[..., :nbw])
+                and torch.equal(a.gbatch.s, b.gbatch.s)
+                and all(torch.equal(v, b.get_params()[k]) for k, v in a.get_params().items()))
+
+
 def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -111,6 +138,7 @@ def main():
     torch.cuda.synchronize()
     out["group_replay_identical"] = bool(torch.equal(eng.theta, engines["noop"].theta) and
                                          torch.equal(eng.theta, engines["eager"].theta))
+    out["band_sharded_rccl_identical"] = band_sharded_rccl()
     dist.destroy_process_group()
     line = json.dumps(out)
     print(line)

@@ -38,3 +38,4 @@ def test_rccl_world_size_1_exchange_eager_and_captured():
     for w, row in enumerate(res["bit_identical_per_window"]):
         assert row["eager"] and row["capture"], (w, res)
     assert res["group_replay_identical"], res
+    assert res["band_sharded_rccl_identical"], res  # (the config-5 sharded exchange's RCCL collectives)
