@@ -48,3 +48,19 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["replicas_in_sync"] is True and d["config"]["prefetched_draw"] is True
     s = d["strong_scaling"]
     assert s["samples_total"] == 64 and s["samples_per_rank"] == 32 and s["speedup_vs_1gpu"] > 0
+
+
+def test_bench_two_ranks_gloo_config5_sharded():
+    """BASELINE config 5 at N > 1, rehearsed: the synthetic N = 20 000 dense-θ
+    line on two gloo ranks takes the band-sharded exchange by default
+    (factor all-gather, band update, band draws + all-to-all) and
+    ends with θ identical on both ranks after the bands are gathered."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--backend", "gloo",
+           "--dataset", "synthetic20k", "--steps", "5", "--warmup", "5", "--no-cpu-baseline", "--no-breakdown"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["config"]["workload"] == "synthetic20k-lds-S1-tau5"
+    assert d["config"]["exchange"] == "band-sharded-gloo" and d["config"]["replicas_in_sync"] is True
