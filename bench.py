@@ -54,8 +54,8 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
 METRIC = "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X"
 # committed rocprofv3 PMC records (2 x FETCH_SIZE + WRITE_SIZE per launch, separate passes) by workload
-PMC_RECORDS = {"cora-lds-S1-tau5": os.path.join(ROOT, "profiles", "r05_pmc_traffic.json"),
-               "synthetic20k-lds-S1-tau5": os.path.join(ROOT, "profiles", "r05_pmc_traffic_config5.json")}
+PMC_RECORDS = {"cora-lds-S1-tau5": os.path.join(ROOT, "profiles", "r06_pmc_traffic.json"),
+               "synthetic20k-lds-S1-tau5": os.path.join(ROOT, "profiles", "r06_pmc_traffic_config5.json")}
 
 
 def world_info():
