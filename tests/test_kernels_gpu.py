@@ -780,6 +780,46 @@ def test_theta_grad_pipe_bit_exact(device, n, k, mode):
         assert torch.equal(outs[0][1], o[1])
 
 
+@pytest.mark.parametrize("n,k,mode,cuts", [(700, 40, 0, (0, 384, 700)), (1100, 264, 2, (0, 384, 1100)),
+                                           (2708, 264, 2, (0, 384, 768, 1408, 2708)), (300, 24, 0, (0, 128, 256, 300))])
+def test_theta_grad_band_equals_full(device, n, k, mode, cuts):
+    """lds_theta_grad_band (the band-sharded exchange's assembly): the row
+    bands [cuts[b], cuts[b+1]) launched one by one give, on every band, the
+    bits of the full 128-tile assembly (dθ in mode 0; θ after the fused SGD +
+    clamp in mode 2, outside the bands θ untouched), multi-sample operands
+    (R of two samples summed), gscale 1/2."""
+    g = torch.Generator().manual_seed(7 * n + k + mode)
+    u = torch.randn(n, k, generator=g).to(device)
+    v = (torch.randn(n, k, generator=g) * 0.3).to(device)
+    r = torch.randn(2, n, generator=g).to(device)
+    theta = torch.rand(n * (n + 1) // 2, generator=g)
+    theta[::9] = -0.5
+    scal = torch.zeros(32, dtype=torch.uint8, device=device)
+    scal[16:24].view(torch.float64).fill_(0.05)
+    st = nat.stream_of(torch.device(device))
+    off = lambda r0: r0 * n - r0 * (r0 - 1) // 2  # noqa: E731  (packed index of row r0's first entry)
+    prev = ops.theta_grad_form("bf16x3-t128-grouped")
+    try:
+        th_full = theta.clone().to(device)
+        gr_full = torch.zeros_like(th_full)
+        nat.call("lds_theta_grad_ex", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, 2, nat.ptr(th_full), n,
+                 nat.ptr(gr_full), mode, nat.ptr(scal), 0.5, ops.form_code(), st)
+    finally:
+        ops.theta_grad_form(prev)
+    for b in range(len(cuts) - 1):
+        r0, r1 = cuts[b], cuts[b + 1]
+        th = theta.clone().to(device)
+        gr = torch.full_like(th, 7.0)
+        nat.call("lds_theta_grad_band", nat.ptr(u), nat.ptr(v), k, k, nat.ptr(r), 1, n, 2, nat.ptr(th), n,
+                 nat.ptr(gr), mode, nat.ptr(scal), 0.5, r0, r1, st)
+        torch.cuda.synchronize()
+        lo, hi = off(r0), off(r1)
+        assert torch.equal(gr[lo:hi], gr_full[lo:hi]), b
+        assert torch.equal(th[lo:hi], th_full[lo:hi]), b
+        assert bool((gr[:lo] == 7.0).all()) and bool((gr[hi:] == 7.0).all()), b  # nothing outside the band
+        assert torch.equal(th[:lo], theta[:lo].to(device)) and torch.equal(th[hi:], theta[hi:].to(device)), b
+
+
 @pytest.mark.parametrize("draw_form", ["bf16x3", "bf16x3-t64k16-grouped", "bf16x3-t128-grouped", "bf16x3-t128-w8"])
 @pytest.mark.parametrize("n,k,graphs", [(2708, 264, 6), (300, 40, 3), (130, 8, 1), (700, 24, 2), (1000, 16, 21),
                                         (64, 8, 2), (129, 24, 9)])
