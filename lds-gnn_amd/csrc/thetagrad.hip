@@ -1642,7 +1642,6 @@ __global__ __launch_bounds__(512, 1) void theta_grad_dma_kernel(
     const int lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int wr = wave >> 2, wc = wave & 3;
-    const int64_t nn = n;
     const int nch = (k + 15) / 16;
 
     // stage fill: wave w copies the 1-KB blocks w, w + 8, …, w + 40 of a chunk
@@ -1670,16 +1669,24 @@ __global__ __launch_bounds__(512, 1) void theta_grad_dma_kernel(
     const int jl = wc * 32 + (lane & 31);
     const int j = j0 + jl;
     auto row_of = [&](int m, int e) { return wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); };
+    // n in a VGPR, and the loads branch-free (entries outside the triangle
+    // read element 0; the epilogue skips them): under this kernel's SGPR
+    // pressure the compiler otherwise re-read n from the kernel arguments,
+    // with a wait, for each of the 32 loads behind an exec branch
+    int nv = n;
+    asm volatile("" : "+v"(nv));
     float th[2][16], part[2][16];
+    const bool has_theta = theta != nullptr;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int i = i0 + row_of(m, e);
-            const bool in = i < n && j < n && j >= i;
-            const int64_t id = in ? tri_at_t<SMALL>(i, j, nn) : 0;
-            th[m][e] = (in && theta != nullptr) ? theta[id] : 0.f;
-            part[m][e] = (PART && in) ? grad[id] : 0.f;
+            const bool in = i < nv && j < nv && j >= i;
+            const int64_t id0 = tri_at_t<SMALL>(i, j, (int64_t)nv);  // (any value outside the triangle)
+            const int64_t id = in ? id0 : 0;
+            th[m][e] = has_theta ? theta[id] : 0.f;
+            part[m][e] = PART ? grad[id] : 0.f;
         }
 
     if (t < 2 * kT2) {

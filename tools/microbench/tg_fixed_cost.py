@@ -3,7 +3,8 @@ mode 2, no dθ store as in the bench): µs per launch as a dependent chain of
 20 copies in one HIP graph, with and without the next window's six-graph
 draw, at k = 264 (17 chunks) and k = 16 (one chunk).  Run once per library
 (LDSGNN_LIB): the product, and timing-only builds of thetagrad.hip with
-tools/microbench/tg_fixed_cost.patch applied (`git apply`) and
+tools/microbench/tg_fixed_cost.patch applied (`git apply`, against the
+thetagrad.hip of commit 2bccbf0) and
 -DLDS_TG_EXPT=1 (no θ preload), 2 (no k-loop), 3 (no θ store), 5 (θ loaded
 after the k-loop), 6 (no in-loop ring refill), 7 (no MFMAs), 8 (refill kept,
 no load wait) — their results are wrong by construction; with
