@@ -804,6 +804,7 @@ __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const f
                                               int mode, const double* __restrict__ lr_dev, float gscale,
                                               int i0, int j0, int wr, int wc, int lane,
                                               uint32_t (*thr)[2][16] = nullptr) {
+    if constexpr (DRAW) mode = 2;  // (every DRAW launch is mode 2: the mode branches fold)
     const int64_t nn = n;
     auto tri_at = [](int i, int j, int64_t nn_) { return tri_at_t<SMALL>(i, j, nn_); };
     // Epilogue: every θ (and partial-grad) operand of the wave's 64 outputs is
@@ -829,39 +830,51 @@ __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const f
     __syncthreads();  // Ri / Rj written by other waves
 
     const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+    // R sums read outside the per-element branches: the column's two once,
+    // the rows' as one 16-byte read per run of four consecutive rows (shared
+    // by both column halves) — inside the branches every element paid an LDS
+    // round trip of its own
+    const float rj[2] = {Rj[wc * 64 + (lane & 31)], Rj[wc * 64 + 32 + (lane & 31)]};
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int lj = wc * 64 + q * 32 + (lane & 31);
-            const int j = j0 + lj;
+        for (int qd = 0; qd < 4; ++qd) {
+            const float4 r4 =
+                *reinterpret_cast<const float4*>(Ri + wr * 64 + m * 32 + 8 * qd + 4 * (lane >> 5));
+            const float ri4[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                const int i = i0 + li;
-                if constexpr (DRAW) thr[m][q][e] = 0u;
-                if (i >= n || j >= n || j < i) continue;
-                const int64_t id = tri_at(i, j, nn);
-                const float t0 = th[m][q][e];
-                float g = 0.f;
-                if (j > i) {
-                    const float gs = gscale * (acc[m][q][e] + Ri[li] + Rj[lj]);
-                    g = mode == 3 ? part[m][q][e] + gs : gs;
-                    if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
-                }
-                if (mode == 3) {
-                    grad[id] = g;
-                    theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                } else if (mode == 2) {
-                    if (grad != nullptr) grad[id] = g;
-                    const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                    theta[id] = tn;
-                    // the next draw's integer threshold (sampler.hip): bit iff (x >> 8) < ceil(θ·2^24)
-                    if constexpr (DRAW) thr[m][q][e] = j > i ? (uint32_t)ceilf(tn * 16777216.0f) : 0u;
-                } else if (mode == 1) {
-                    grad[id] = part[m][q][e] + g;
-                } else {
-                    grad[id] = g;
+            for (int q = 0; q < 2; ++q) {
+                const int lj = wc * 64 + q * 32 + (lane & 31);
+                const int j = j0 + lj;
+#pragma unroll
+                for (int e4 = 0; e4 < 4; ++e4) {
+                    const int e = 4 * qd + e4;
+                    const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                    const int i = i0 + li;
+                    if constexpr (DRAW) thr[m][q][e] = 0u;
+                    if (i >= n || j >= n || j < i) continue;
+                    const int64_t id = tri_at(i, j, nn);
+                    const float t0 = th[m][q][e];
+                    float g = 0.f;
+                    if (j > i) {
+                        const float gs = gscale * (acc[m][q][e] + ri4[e4] + rj[q]);
+                        g = mode == 3 ? part[m][q][e] + gs : gs;
+                        if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+                    }
+                    if (mode == 3) {
+                        grad[id] = g;
+                        theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                    } else if (mode == 2) {
+                        if (grad != nullptr) grad[id] = g;
+                        const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                        theta[id] = tn;
+                        // the next draw's integer threshold (sampler.hip): bit iff (x >> 8) < ceil(θ·2^24)
+                        if constexpr (DRAW) thr[m][q][e] = j > i ? (uint32_t)ceilf(tn * 16777216.0f) : 0u;
+                    } else if (mode == 1) {
+                        grad[id] = part[m][q][e] + g;
+                    } else {
+                        grad[id] = g;
+                    }
                 }
             }
         }
@@ -968,7 +981,7 @@ __global__ __launch_bounds__(256, 2) void theta_grad_bf3_t128_kernel(
     float gscale, int group, int per_xcd, Planes pl, DrawArgs dr = DrawArgs{}) {
     constexpr int kPL = kPL2 + (PRE ? 4 : 0);
     __shared__ __attribute__((aligned(16))) uint32_t lds[12 * kPL];
-    __shared__ float Ri[kT2], Rj[kT2];
+    __shared__ __attribute__((aligned(16))) float Ri[kT2], Rj[kT2];
 
     const int nb = (n + kT2 - 1) / kT2;
     const int ntiles = nb * (nb + 1) / 2;
@@ -1145,7 +1158,7 @@ __global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
     float gscale, int group, int per_xcd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    __shared__ float Ri[kT2], Rj[kT2];
+    __shared__ __attribute__((aligned(16))) float Ri[kT2], Rj[kT2];
 
     const int nb = (n + kT2 - 1) / kT2;
     const int ntiles = nb * (nb + 1) / 2;
@@ -1286,11 +1299,28 @@ __device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float 
                                             float* __restrict__ theta, float* __restrict__ grad, int n, int mode,
                                             const double* __restrict__ lr_dev, float gscale, int i0, int j0, int wr,
                                             int wc, int lane, int t, uint32_t* lds_dyn, const DrawArgs& dr) {
+    if constexpr (DRAW) mode = 2;  // (every DRAW launch is mode 2: the mode branches fold)
     const int64_t nn = n;
     const int jl = wc * 32 + (lane & 31);
     const int j = j0 + jl;
     auto row_of = [&](int m, int e) { return wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); };
     const float lr = mode >= 2 ? (float)(*lr_dev) : 0.f;
+    // the R sums of this lane's 32 rows (four runs of four consecutive rows
+    // per accumulator: 16-byte reads) and of its column, read together ahead
+    // of the element loop — inside it each element's two dependent reads sat
+    // behind its own branch, an LDS round trip per element
+    float ri[2][16];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 r4 = *reinterpret_cast<const float4*>(Ri + row_of(m, 4 * q));
+            ri[m][4 * q] = r4.x;
+            ri[m][4 * q + 1] = r4.y;
+            ri[m][4 * q + 2] = r4.z;
+            ri[m][4 * q + 3] = r4.w;
+        }
+    const float rj = Rj[jl];
     uint32_t thr[2][16];  // DRAW: the next draw's integer thresholds (sampler.hip)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -1304,7 +1334,7 @@ __device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float 
             const float t0 = th[m][e];
             float g = 0.f;
             if (j > i) {
-                const float gs = gscale * (acc[m][e] + Ri[li] + Rj[jl]);
+                const float gs = gscale * (acc[m][e] + ri[m][e] + rj);
                 g = mode == 3 ? part[m][e] + gs : gs;
                 if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
             }
@@ -1453,7 +1483,7 @@ __global__ __launch_bounds__(512, 1) void theta_grad_w8_kernel(
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
     float gscale, int group, int per_xcd, DrawArgs dr) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    __shared__ float Ri[kT2], Rj[kT2];
+    __shared__ __attribute__((aligned(16))) float Ri[kT2], Rj[kT2];
 
     const int nb = (n + kT2 - 1) / kT2;
     const int ntiles = nb * (nb + 1) / 2;
@@ -1627,7 +1657,7 @@ __global__ __launch_bounds__(512, 1) void theta_grad_dma_kernel(
     float* __restrict__ grad, int mode, const double* __restrict__ lr_dev, int ldrc,
     float gscale, int group, int per_xcd, DrawArgs dr) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_dyn[];
-    __shared__ float Ri[kT2], Rj[kT2];
+    __shared__ __attribute__((aligned(16))) float Ri[kT2], Rj[kT2];
 
     const int nb = (n + kT2 - 1) / kT2;
     const int ntiles = nb * (nb + 1) / 2;
