@@ -920,20 +920,21 @@ __device__ __forceinline__ void t128_draw(const uint32_t (&thr)[2][2][16], uint3
                         x[4 * qd + 2] = o.z;
                         x[4 * qd + 3] = o.w;
                     }
-                    uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+                    uint32_t cbits = 0;  // bit e: this lane's element e (as in w8_epilogue)
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) {
+                    for (int e = 15; e >= 0; --e) {
                         const bool bit = (x[e] >> 8) < thr[m][qq][e];
                         const uint64_t w = __ballot(bit);
-                        mylo = lane == e ? (uint32_t)w : mylo;
-                        myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
-                        colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                        cbits = (cbits << 1) + (uint32_t)bit;
+                        if (lane == 0) {  // the ballot's words: rows rr and rr + 4, column segment wc·2 + qq
+                            const int rr = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2);
+                            rwb[(q * 128 + rr) * 4 + wc * 2 + qq] = (uint32_t)w;
+                            rwb[(q * 128 + rr + 4) * 4 + wc * 2 + qq] = (uint32_t)(w >> 32);
+                        }
                     }
-                    if (lane < 16) {  // element e = lane: rows rr and rr + 4, column segment wc·2 + qq
-                        const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
-                        rwb[(q * 128 + rr) * 4 + wc * 2 + qq] = mylo;
-                        rwb[(q * 128 + rr + 4) * 4 + wc * 2 + qq] = myhi;
-                    }
+                    cbits = (cbits | (cbits << 8)) & 0x00FF00FFu;
+                    cbits = (cbits | (cbits << 4)) & 0x0F0F0F0Fu;
+                    colw |= (uint64_t)(cbits << (4 * (lane >> 5))) << (32 * m);
                 }
                 colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
                 if (lane < 32) cwb[(q * 2 + wr) * 128 + wc * 64 + qq * 32 + lane] = colw;
@@ -1396,20 +1397,27 @@ __device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float 
                     uint64_t colw = 0;
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {
-                        uint32_t mylo = 0, myhi = 0;  // lane e (< 16) keeps the ballot of element e
+                        uint32_t cb = 0;  // bit e: this lane's element e (shift-and-add chain)
 #pragma unroll
-                        for (int e = 0; e < 16; ++e) {
+                        for (int e = 15; e >= 0; --e) {
                             const bool bit = (x[gg][m][e] >> 8) < thr[m][e];
                             const uint64_t w = __ballot(bit);
-                            mylo = lane == e ? (uint32_t)w : mylo;
-                            myhi = lane == e ? (uint32_t)(w >> 32) : myhi;
-                            colw |= (uint64_t)bit << (m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5));
+                            cb = (cb << 1) + (uint32_t)bit;
+                            if (lane == 0) {  // the ballot's words: rows rr and rr + 4 of columns wc·32 …
+                                const int rr = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2);
+                                rwb[(qg * 128 + rr) * 4 + wc] = (uint32_t)w;
+                                rwb[(qg * 128 + rr + 4) * 4 + wc] = (uint32_t)(w >> 32);
+                            }
                         }
-                        if (lane < 16) {  // element e = lane: rows rr and rr + 4 of columns wc·32 …
-                            const int rr = wr * 64 + m * 32 + (lane & 3) + 8 * (lane >> 2);
-                            rwb[(qg * 128 + rr) * 4 + wc] = mylo;
-                            rwb[(qg * 128 + rr + 4) * 4 + wc] = myhi;
-                        }
+                        // element e is row (e & 3) + 8·(e >> 2) + 4·(lane >> 5) of the
+                        // accumulator: nibble t of cb to bits 8t … 8t + 3, then the
+                        // lane half's 4-row offset.  With the ballots stored by lane 0
+                        // as they come (no lane-select masks, no per-word v_mov +
+                        // v_cndmask) the draw's bit assembly is ≈ 1 µs shorter at Cora
+                        // (tools/microbench/tg_fixed_cost.py; bits unchanged)
+                        cb = (cb | (cb << 8)) & 0x00FF00FFu;
+                        cb = (cb | (cb << 4)) & 0x0F0F0F0Fu;
+                        colw |= (uint64_t)(cb << (4 * (lane >> 5))) << (32 * m);
                     }
                     colw |= __shfl_xor(colw, 32);  // the other row interleave of this column
                     if (lane < 32) cwb[(qg * 2 + wr) * 128 + wc * 32 + lane] = colw;
