@@ -55,6 +55,12 @@ __device__ __forceinline__ void band_tile(int L, int nb, int b0, int& bi, int& b
     bj = i + L;
 }
 
+// A compile-time bool as a value (for generic lambdas instantiated per case).
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
 struct U32x4 {
     uint32_t x, y, z, w;
 };

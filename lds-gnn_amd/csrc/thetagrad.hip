@@ -835,49 +835,55 @@ __device__ __forceinline__ void t128_epilogue(const f32x16 (&acc)[2][2], const f
     // by both column halves) — inside the branches every element paid an LDS
     // round trip of its own
     const float rj[2] = {Rj[wc * 64 + (lane & 31)], Rj[wc * 64 + 32 + (lane & 31)]};
+    // an off-diagonal tile inside the triangle takes the loop without bounds
+    // and diagonal tests (kIn); here in every launch — the lambda form, which
+    // the register allocator fits in 256 VGPRs without spilling (a function
+    // template spilled)
+    auto elements = [&](auto in_c) {
+        constexpr bool kIn = decltype(in_c)::value;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int qd = 0; qd < 4; ++qd) {
-            const float4 r4 =
-                *reinterpret_cast<const float4*>(Ri + wr * 64 + m * 32 + 8 * qd + 4 * (lane >> 5));
-            const float ri4[4] = {r4.x, r4.y, r4.z, r4.w};
+            for (int qd = 0; qd < 4; ++qd) {
+                const float4 r4 = *reinterpret_cast<const float4*>(Ri + wr * 64 + m * 32 + 8 * qd + 4 * (lane >> 5));
+                const float ri4[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int lj = wc * 64 + q * 32 + (lane & 31);
-                const int j = j0 + lj;
+                for (int q = 0; q < 2; ++q) {
+                    const int j = j0 + wc * 64 + q * 32 + (lane & 31);
 #pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                    const int e = 4 * qd + e4;
-                    const int li = wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                    const int i = i0 + li;
-                    if constexpr (DRAW) thr[m][q][e] = 0u;
-                    if (i >= n || j >= n || j < i) continue;
-                    const int64_t id = tri_at(i, j, nn);
-                    const float t0 = th[m][q][e];
-                    float g = 0.f;
-                    if (j > i) {
-                        const float gs = gscale * (acc[m][q][e] + ri4[e4] + rj[q]);
-                        g = mode == 3 ? part[m][q][e] + gs : gs;
-                        if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
-                    }
-                    if (mode == 3) {
-                        grad[id] = g;
-                        theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                    } else if (mode == 2) {
-                        if (grad != nullptr) grad[id] = g;
-                        const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                        theta[id] = tn;
-                        // the next draw's integer threshold (sampler.hip): bit iff (x >> 8) < ceil(θ·2^24)
-                        if constexpr (DRAW) thr[m][q][e] = j > i ? (uint32_t)ceilf(tn * 16777216.0f) : 0u;
-                    } else if (mode == 1) {
-                        grad[id] = part[m][q][e] + g;
-                    } else {
-                        grad[id] = g;
+                    for (int e4 = 0; e4 < 4; ++e4) {
+                        const int e = 4 * qd + e4;
+                        const int i = i0 + wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                        if constexpr (DRAW) thr[m][q][e] = 0u;
+                        if (!kIn && (i >= n || j >= n || j < i)) continue;
+                        const int64_t id = tri_at(i, j, nn);
+                        const float t0 = th[m][q][e];
+                        float g = 0.f;
+                        if (kIn || j > i) {
+                            const float gs = gscale * (acc[m][q][e] + ri4[e4] + rj[q]);
+                            g = mode == 3 ? part[m][q][e] + gs : gs;
+                            if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+                        }
+                        if (mode == 3) {
+                            grad[id] = g;
+                            theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                        } else if (mode == 2) {
+                            if (grad != nullptr) grad[id] = g;
+                            const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                            theta[id] = tn;
+                            // the next draw's integer threshold (sampler.hip): bit iff (x >> 8) < ceil(θ·2^24)
+                            if constexpr (DRAW) thr[m][q][e] = (kIn || j > i) ? (uint32_t)ceilf(tn * 16777216.0f) : 0u;
+                        } else if (mode == 1) {
+                            grad[id] = part[m][q][e] + g;
+                        } else {
+                            grad[id] = g;
+                        }
                     }
                 }
             }
-        }
+    };
+    if (i0 != j0 && j0 + kT2 <= n) elements(BoolC<true>{});
+    else elements(BoolC<false>{});
 }
 
 // The next window's draw from the θ a 128-tile epilogue just wrote (mode 2;
@@ -1289,6 +1295,48 @@ __global__ __launch_bounds__(256, 1) void theta_grad_bf3_pipe_kernel(
 constexpr int kW8Lds = 2 * 12 * kPL2 * 4;  // bytes of the two stage buffers (96 KB)
 constexpr int kW8Grp = 8;                  // graphs per draw group (4 KB of LDS each)
 
+// w8_epilogue's element loop: dθ = gscale·(acc + R_i + R_j) on the strict
+// upper triangle, clamp-backward mask, the mode's stores and (DRAW) the
+// next draw's thresholds.  IN: an off-diagonal tile inside the triangle, no
+// bounds or diagonal tests.
+template <bool SMALL, bool DRAW, bool IN>
+__device__ __forceinline__ void w8_elements(const f32x16 (&acc)[2], const float (&th)[2][16],
+                                            const float (&part)[2][16], const float (&ri)[2][16], float rj,
+                                            float* __restrict__ theta, float* __restrict__ grad, int n, int mode,
+                                            float lr, float gscale, int i0, int j, int wr, int lane,
+                                            uint32_t (&thr)[2][16]) {
+    const int64_t nn = n;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int i = i0 + wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            thr[m][e] = 0u;
+            if (!IN && (i >= n || j >= n || j < i)) continue;
+            const int64_t id = tri_at_t<SMALL>(i, j, nn);
+            const float t0 = th[m][e];
+            float g = 0.f;
+            if (IN || j > i) {
+                const float gs = gscale * (acc[m][e] + ri[m][e] + rj);
+                g = mode == 3 ? part[m][e] + gs : gs;
+                if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
+            }
+            if (mode == 3) {
+                grad[id] = g;
+                theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+            } else if (mode == 2) {
+                if (grad != nullptr) grad[id] = g;
+                const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
+                theta[id] = tn;
+                if (DRAW && (IN || j > i)) thr[m][e] = (uint32_t)ceilf(tn * 16777216.0f);
+            } else if (mode == 1) {
+                grad[id] = part[m][e] + g;
+            } else {
+                grad[id] = g;
+            }
+        }
+}
+
 // Epilogue of the eight-wave 128-tile kernels (forms 9 and 10; wave (wr, wc)
 // owns outputs wr·64 … + 63 × wc·32 … + 31 of the tile, lane column j): dθ =
 // gscale·(acc + R_i + R_j) on the strict upper triangle, clamp-backward mask,
@@ -1301,7 +1349,6 @@ __device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float 
                                             const double* __restrict__ lr_dev, float gscale, int i0, int j0, int wr,
                                             int wc, int lane, int t, uint32_t* lds_dyn, const DrawArgs& dr) {
     if constexpr (DRAW) mode = 2;  // (every DRAW launch is mode 2: the mode branches fold)
-    const int64_t nn = n;
     const int jl = wc * 32 + (lane & 31);
     const int j = j0 + jl;
     auto row_of = [&](int m, int e) { return wr * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); };
@@ -1323,36 +1370,17 @@ __device__ __forceinline__ void w8_epilogue(const f32x16 (&acc)[2], const float 
         }
     const float rj = Rj[jl];
     uint32_t thr[2][16];  // DRAW: the next draw's integer thresholds (sampler.hip)
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int li = row_of(m, e);
-            const int i = i0 + li;
-            thr[m][e] = 0u;
-            if (i >= n || j >= n || j < i) continue;
-            const int64_t id = tri_at_t<SMALL>(i, j, nn);
-            const float t0 = th[m][e];
-            float g = 0.f;
-            if (j > i) {
-                const float gs = gscale * (acc[m][e] + ri[m][e] + rj);
-                g = mode == 3 ? part[m][e] + gs : gs;
-                if (theta != nullptr && !(t0 >= 0.f && t0 <= 1.f)) g = 0.f;  // clamp backward
-            }
-            if (mode == 3) {
-                grad[id] = g;
-                theta[id] = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-            } else if (mode == 2) {
-                if (grad != nullptr) grad[id] = g;
-                const float tn = fminf(fmaxf(fmaf(-lr, g, t0), 0.f), 1.f);
-                theta[id] = tn;
-                if (DRAW && j > i) thr[m][e] = (uint32_t)ceilf(tn * 16777216.0f);
-            } else if (mode == 1) {
-                grad[id] = part[m][e] + g;
-            } else {
-                grad[id] = g;
-            }
-        }
+    // an off-diagonal tile inside the triangle (every i < j < n: all but the
+    // diagonal and the last column of tiles) takes the loop without bounds
+    // and diagonal tests — in draw launches only, where the mode is folded
+    if constexpr (DRAW) {
+        if (i0 != j0 && j0 + kT2 <= n)
+            w8_elements<SMALL, DRAW, true>(acc, th, part, ri, rj, theta, grad, n, mode, lr, gscale, i0, j, wr, lane, thr);
+        else
+            w8_elements<SMALL, DRAW, false>(acc, th, part, ri, rj, theta, grad, n, mode, lr, gscale, i0, j, wr, lane, thr);
+    } else {
+        w8_elements<SMALL, DRAW, false>(acc, th, part, ri, rj, theta, grad, n, mode, lr, gscale, i0, j, wr, lane, thr);
+    }
     if constexpr (DRAW) {
         // LDS (the dead stage buffers): per graph of a group, row segments
         // rw[row][wc] (uint32: 32 columns) and column words cw[h][col] (uint64:
