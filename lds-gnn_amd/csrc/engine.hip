@@ -2088,6 +2088,9 @@ __global__ __launch_bounds__(256) void xt_partials_kernel(
 // wave (a 16-lane group each): fewer waves for the same sums (Cora: 68 heavy,
 // 329 / 255 / 781 columns; 1,741 waves instead of 2,453 per sample).
 
+#ifndef LDS_XT_EXPT
+#define LDS_XT_EXPT 0
+#endif
 template <bool kB>
 __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
@@ -2117,6 +2120,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     // started after every other block of its sample had been dispatched)
     const int fb = fin_args.partials != nullptr ? 1 : 0;
     if (fb && blockIdx.x == 0) {
+        if (LDS_XT_EXPT == 4) return;  // timing-only builds (tools/microbench/xt_parts.py)
         final_block_1024<kB ? 16 : 64>(fin_args, adam, sc);
         return;
     }
@@ -2124,6 +2128,9 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
     const bool heavy = bx < n_heavy;
+    if (LDS_XT_EXPT == 1 && heavy) return;
+    if (LDS_XT_EXPT == 2 && !heavy && (bx - n_heavy) * 16 + wave < n_single) return;
+    if (LDS_XT_EXPT == 3 && !heavy && (bx - n_heavy) * 16 + wave >= n_single) return;
     {
         // light waves past the single-column ones: two or four short columns
         const int lw = (bx - n_heavy) * 16 + wave;  // light wave number
