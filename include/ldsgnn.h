@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LDS_ABI_VERSION 17
+#define LDS_ABI_VERSION 18
 
 /* ABI version of the loaded library (== LDS_ABI_VERSION). */
 int lds_abi_version(void);
@@ -752,8 +752,8 @@ int lds_engine_final(const float* partials, int nblocks, int c, float* dst, int 
  * range, partials summed in wave order), then every other column, one wave
  * each (n_heavy = 0 with xt_part).  xtinfo != NULL: per plan slot s,
  * xtinfo[s] = {column, p0, nnz, 0} (int4) replaces order[s] -> xcp loads,
- * and xthead[s] (64 ints, NULL allowed) holds the light column's first 64
- * row indices (values from xval[p0 + e]).  ABI 15: after the heavy slots,
+ * and xthead[s] (128 ints since ABI 18, NULL allowed) holds the column's
+ * first 128 row indices, zero past its end (values from xval[p0 + e]).  ABI 15: after the heavy slots,
  * n_single slots run one column per wave, the next n_pair (columns of at most
  * 32 entries) two per wave and the rest (at most 16 entries) four per wave —
  * the same sums; n_single = fin - n_heavy, n_pair = 0 is the one-per-wave

@@ -414,14 +414,17 @@ __device__ __forceinline__ float x_wave_dot_range(int beg, int end, const int* _
 // dependent row-pointer load: entries and the gathers they index are the
 // only round trips up to 64 entries; entries past 64 come from the CSR /
 // CSC arrays as in x_wave_dot_range.
-template <bool kCsc, int kHead>
+// kPre (kHead 2): the lane's head index was loaded by the caller (jpre), ahead
+// of the loads that give p0 / nnz.
+template <bool kCsc, int kHead, bool kPre = false>
 __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const int* __restrict__ head,
                                                  const int* __restrict__ idx, const float* __restrict__ val,
                                                  const float* __restrict__ src, const Keys& keys, uint32_t ctr,
                                                  int train, float keep, float scale,
                                                  float* __restrict__ xd_out = nullptr,
                                                  float* __restrict__ xd_perm_out = nullptr,
-                                                 const int* __restrict__ perm = nullptr) {
+                                                 const int* __restrict__ perm = nullptr, int jpre = 0, int jpre2 = 0) {
+    static_assert(!kPre || kHead == 2, "a preloaded head index is an index-only head");
     const int lane = threadIdx.x & (HID - 1);
     const int q = (threadIdx.x >> 4) & 3;
     float acc = 0.f;
@@ -435,7 +438,7 @@ __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const i
             j = hv.x;
             x = __int_as_float(hv.y);  // 0 past nnz
         } else {
-            j = kHead == 1 ? reinterpret_cast<const int2*>(head)[e].x : head[e];
+            j = kPre ? jpre : kHead == 1 ? reinterpret_cast<const int2*>(head)[e].x : head[e];
             x = v ? val[p0 + e] : 0.f;
         }
         if (v) {
@@ -457,7 +460,25 @@ __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const i
         }
     }
     const int end = p0 + nnz;
-    for (int pb = p0 + 64 + q * HID; pb < end; pb += 4 * HID) {
+    int pstart = p0 + 64;
+    if constexpr (kPre) {  // head entries 64..127 (jpre2): the same chunk order as the loop below
+        const int e = 64 + 16 * q + lane;
+        const bool v = e < nnz;
+        float x = v ? val[p0 + e] : 0.f;
+        if (v && train) x = u_at(keys, keys.tag_x, ctr, kCsc ? jpre2 : r, kCsc ? r : jpre2) < keep ? x * scale : 0.f;
+        if (64 + 16 * q < nnz) {
+            const int j = jpre2;
+            float sk[HID];
+#define LDS_G(K) sk[K] = src[rbc_i<K>(j) * HID + lane];
+            LDS_R16(LDS_G)
+#undef LDS_G
+#define LDS_F(K) acc = fmaf(rbc_f<K>(x), sk[K], acc);
+            LDS_R16(LDS_F)
+#undef LDS_F
+        }
+        pstart = p0 + 128;
+    }
+    for (int pb = pstart + q * HID; pb < end; pb += 4 * HID) {
         const int p = pb + lane;
         int j = 0;
         float x = 0.f;
@@ -549,12 +570,11 @@ __device__ __forceinline__ float x_wave_dot_head_pair(int p0, int nnz, const int
 // adds the groups of a two-group column with xor16_add.  Groups past a
 // column's entries contribute nothing there either, so the sums are the same
 // bits (up to the sign of a zero sum).  train = 0 (the stored Xd).
-__device__ __forceinline__ float x_group_dot_head(int qc, int p0, int nnz, const int* __restrict__ head,
+__device__ __forceinline__ float x_group_dot_head(int qc, int p0, int nnz, int j,
                                                   const float* __restrict__ val, const float* __restrict__ src) {
     const int lane = threadIdx.x & (HID - 1);
     float acc = 0.f;
     const int e = 16 * qc + lane;
-    const int j = head[e];
     const float x = e < nnz ? val[p0 + e] : 0.f;
     if (16 * qc < nnz) {  // group-uniform
         float sk[HID];
@@ -1645,6 +1665,11 @@ __global__ __launch_bounds__(256) void rev_bc_kernel(
 //     step) or reverse (hyper step) to b0 / W1 / b1, and xt_adam applies it
 //     to W0 right where each W0 gradient / adjoint is completed.
 // ---------------------------------------------------------------------------
+// timing-only builds of the W0 products (tools/microbench/xt_parts.py); 0 in the product
+#ifndef LDS_XT_EXPT
+#define LDS_XT_EXPT 0
+#endif
+
 struct AdamArgs {
     // mode 1 (forward): w0, m0, v0 -> w1, m1, v1, gp
     // mode 2 (reverse of the step whose post-state is m1, v1 and whose g' is
@@ -1676,6 +1701,7 @@ struct AdamOps {
 
 __device__ __forceinline__ AdamOps adam_load(const AdamArgs& a, int idx) {
     AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
+    if (LDS_XT_EXPT == 9) return AdamOps{1.f, 1.f, 1.f, 0.5f, 0.5f};  // timing only: no operand loads
     if (a.mode == 1) {
         o.p0 = a.w0[idx];
         o.p1 = a.m0[idx];
@@ -1695,6 +1721,11 @@ __device__ __forceinline__ AdamOps adam_load(const AdamArgs& a, int idx) {
 // x: mode 1 the data gradient g; mode 2 the complete adjoint of w1.
 __device__ __forceinline__ void adam_apply(const AdamArgs& a, int idx, float x, const AdamOps& o,
                                            float step_size, float c2) {
+    if (LDS_XT_EXPT == 10) {  // timing only: the operands loaded, no update computed or stored
+        float z = o.p0 + o.p1 + o.p2 + o.p3 + o.p4 + x * step_size * c2;
+        asm volatile("" : "+v"(z));
+        return;
+    }
     if (a.mode == 1) {
         const float w = o.p0;
         float gp = x;
@@ -1703,9 +1734,11 @@ __device__ __forceinline__ void adam_apply(const AdamArgs& a, int idx, float x, 
         const float v = o.p2 * a.hp.beta2 + (a.hp.omb2 * gp) * gp;
         const float denom = sqrtf(v) / c2 + a.hp.eps;
         a.w1[idx] = w + ((-step_size) * m) / denom;
-        a.m1[idx] = m;
-        a.v1[idx] = v;
-        a.gp[idx] = gp;
+        if (LDS_XT_EXPT != 8) {  // (timing-only build 8: no m / v / g' stores)
+            a.m1[idx] = m;
+            a.v1[idx] = v;
+            a.gp[idx] = gp;
+        }
     } else if (a.mode == 2) {
         const float wb = x;
         const float m = o.p0, v = o.p1, g = o.p2;
@@ -1724,15 +1757,19 @@ __device__ __forceinline__ void adam_apply(const AdamArgs& a, int idx, float x, 
     }
 }
 
+// {step_size, c2} = {0, 1} without an Adam step (mode 0: no table)
+__device__ const float kAdamNoStep[2] = {0.f, 1.f};
+
+// The step constants, loaded without a branch: with the load under `if
+// (a.mode)` the compiler waited for it (lgkmcnt(0)) at the branch merge, right
+// where it was issued — one more dependent round trip in front of every
+// wave's product loads (xt_adam: 4.95 -> ... us per launch, tools/microbench/xt_parts.py).
 __device__ __forceinline__ void adam_step_consts(const AdamArgs& a, const EngineScalars* __restrict__ sc,
                                                  float& step_size, float& c2) {
     (void)sc;
-    step_size = 0.f;
-    c2 = 1.f;
-    if (a.mode) {
-        step_size = a.tab[2 * a.step_off];
-        c2 = a.tab[2 * a.step_off + 1];
-    }
+    const float* t = a.mode ? a.tab + 2 * a.step_off : kAdamNoStep;
+    step_size = t[0];
+    c2 = t[1];
 }
 
 // {step_size, c2} of the Adam steps adam_step + 1 + k, k < count (one thread
@@ -1994,22 +2031,34 @@ __device__ __forceinline__ void final_pair(const FinalArgs& f, int e0, int e1, c
 // trip — the same sums either way.  The single-sample launch loads 64 at once
 // (its final block is on the critical path); the batched one 16, which keeps
 // xt_adam at 40 VGPRs instead of 86 (two 1024-thread blocks per CU, not one).
+//
+// The final stage runs as kFinParts such blocks, part p completing elements
+// [p·kFinPer, (p + 1)·kFinPer): the same sums per element, a quarter of the
+// 63-partial loads per block (one block issued ≈900 wave loads of 256 B, a
+// TA-bound ≈1.4 µs on one CU).
+constexpr int kFinParts = 4;
+constexpr int kFinPer = (kRedLen + kFinParts - 1) / kFinParts;
 template <int kBatch>
 __device__ __forceinline__ void final_block_1024(const FinalArgs& f, const AdamArgs& adam,
-                                                 const EngineScalars* __restrict__ sc) {
+                                                 const EngineScalars* __restrict__ sc, int part) {
     static_assert(kBatch % 16 == 0 && kBatch <= kRedBlocks, "groups of 16");
-    __shared__ float third[3][kRedLen];
+    static_assert(3 * kFinPer <= 1024, "three thirds per element in one block");
+    __shared__ float third[3][kFinPer];
     const int t = threadIdx.x;
-    const int q = t / kRedLen, e = t - q * kRedLen;
+    const int q = t / kFinPer, el = t - q * kFinPer;
+    const int e0 = part * kFinPer, e1 = min(kRedLen, e0 + kFinPer);
+    const int e = e0 + el;
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
     // the completing thread's Adam operands first (they overlap the sums)
-    const int idx = t < kRedLen ? final_index(f, t) : -1;
+    const int idx = t < kFinPer && e0 + t < e1 ? final_index(f, e0 + t) : -1;
     AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
     float prev = 0.f;
     if (idx >= 0) {
         o = adam_load(adam, idx);
         if (f.accumulate) prev = f.dst[idx];
     }
-    if (q < 3) {
+    if (q < 3 && e < e1) {
         const int per = (f.nblocks + 2) / 3;
         const int b0 = q * per, b1 = min(f.nblocks, b0 + per);
         float v = 0.f;
@@ -2028,13 +2077,11 @@ __device__ __forceinline__ void final_block_1024(const FinalArgs& f, const AdamA
                 v += y[0];
             }
         }
-        third[q][e] = v;
+        third[q][el] = v;
     }
     __syncthreads();
-    if (t >= kRedLen) return;
+    if (t >= kFinPer || e0 + t >= e1) return;
     const float tot = (third[0][t] + third[1][t]) + third[2][t];
-    float step_size, c2;
-    adam_step_consts(adam, sc, step_size, c2);
     if (idx >= 0) {
         const float val = f.accumulate ? prev + tot : tot;
         f.dst[idx] = val;
@@ -2088,9 +2135,11 @@ __global__ __launch_bounds__(256) void xt_partials_kernel(
 // wave (a 16-lane group each): fewer waves for the same sums (Cora: 68 heavy,
 // 329 / 255 / 781 columns; 1,741 waves instead of 2,453 per sample).
 
-#ifndef LDS_XT_EXPT
-#define LDS_XT_EXPT 0
-#endif
+// Column heads of the W0 products (xthead, ABI 18): the first kXtHead row
+// indices of every plan slot, so a one-wave column (at most 128 entries) needs
+// no index loads past its head.
+constexpr int kXtHead = 128;
+
 template <bool kB>
 __global__ __launch_bounds__(1024) void xt_adam_kernel(
     const int* __restrict__ xcp, const int* __restrict__ xrow, const float* __restrict__ xval, int fin,
@@ -2118,12 +2167,16 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     // the final reduction is block 0: dispatched first, so its chain of
     // partial-sum round trips overlaps the column blocks (as the last block it
     // started after every other block of its sample had been dispatched)
-    const int fb = fin_args.partials != nullptr ? 1 : 0;
-    if (fb && blockIdx.x == 0) {
+    if (LDS_XT_EXPT == 5) return;
+    if (LDS_XT_EXPT == 6) adam.mode = 0;  // no Adam loads or updates (the products and stores only)
+    const int fb = fin_args.partials != nullptr ? kFinParts : 0;
+    if ((int)blockIdx.x < fb) {
         if (LDS_XT_EXPT == 4) return;  // timing-only builds (tools/microbench/xt_parts.py)
-        final_block_1024<kB ? 16 : 64>(fin_args, adam, sc);
+        final_block_1024<kB ? 16 : 64>(fin_args, adam, sc, (int)blockIdx.x);
         return;
     }
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
     const int bx = (int)blockIdx.x - fb;
     const int wave = wave_id();
     const int lane = threadIdx.x & 63;
@@ -2144,20 +2197,22 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
             const int send = four ? fin : base + n_pair;
             if (__ballot(slot < send) == 0ull) return;  // light waves never reach a barrier
             const bool live = slot < send;
-            const int4 inf = xtinfo[live ? slot : base];
+            const int hs = live ? slot : base;
+            // the head entry first: it does not wait for the column's info,
+            // so the gathers need one round trip after it, not two
+            const int jh = xthead[(int64_t)hs * kXtHead + 16 * qc + (lane & (HID - 1))];
+            const int4 inf = xtinfo[hs];
             const int idx = inf.x * HID + (lane & (HID - 1));
             const bool owner = live && qc == 0;
             AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
             float prev = 0.f;
             if (owner) {
-                o = adam_load(adam, idx);
+                if (LDS_XT_EXPT != 7) o = adam_load(adam, idx);
                 if (fin_args.accumulate) prev = fin_args.dst[idx];
             }
-            float step_size, c2;
-            adam_step_consts(adam, sc, step_size, c2);
-            float acc = x_group_dot_head(qc, inf.y, live ? inf.z : 0, xthead + (int64_t)(live ? slot : base) * 64,
-                                         xval, d);
+            float acc = x_group_dot_head(qc, inf.y, live ? inf.z : 0, jh, xval, d);
             if (!four) acc = xor16_add(acc);  // the column's two groups, as groups_sum adds them
+            if (LDS_XT_EXPT == 7 && owner) o = adam_load(adam, idx);
             if (owner) {
                 const float val = fin_args.accumulate ? prev + acc : acc;
                 fin_args.dst[idx] = val;
@@ -2169,7 +2224,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     // with the column heads (xtinfo[slot] = {f, p0, nnz}, slot = position in
     // `order`) one load gives the column, its range and its first 64 rows;
     // without them: order[slot] -> xcp[f] -> entries, two dependent loads first
-    int f, beg, end, slot;
+    int f, beg, end, slot, jh = 0, jh2 = 0;
     if (heavy) {
         slot = bx;
         int cb, ce;
@@ -2189,6 +2244,13 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     } else {
         slot = n_heavy + (bx - n_heavy) * 16 + wave;
         if (slot >= fin) return;  // light blocks never reach a barrier
+        // the lane's head entry ahead of the column's info (the gathers then
+        // wait one round trip, not two)
+        if (xthead != nullptr && xt_part == nullptr) {
+            const int* hp = xthead + (int64_t)slot * kXtHead + 16 * ((threadIdx.x >> 4) & 3) + (lane & (HID - 1));
+            jh = hp[0];
+            jh2 = hp[64];
+        }
         if (xtinfo != nullptr) {
             const int4 inf = xtinfo[slot];
             f = inf.x;
@@ -2206,19 +2268,18 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
     float prev = 0.f;
     if (owner) {
-        o = adam_load(adam, idx);
+        if (LDS_XT_EXPT != 7) o = adam_load(adam, idx);
         if (fin_args.accumulate) prev = fin_args.dst[idx];
     }
-    float step_size, c2;
-    adam_step_consts(adam, sc, step_size, c2);
     float acc = 0.f;
     if (xt_part != nullptr) {   // partials of xt_partials_kernel, summed in range order (n_heavy = 0)
         if (kB) xt_part += (int64_t)blockIdx.y * xt_splits * fin * HID;
         if (lane < HID)
             for (int p = 0; p < xt_splits; ++p) acc += xt_part[((int64_t)p * fin + f) * HID + lane];
     } else if (xthead != nullptr && !heavy) {
-        acc = x_wave_dot_head<true, 2>(f, beg, end - beg, xthead + (int64_t)slot * 64, xrow, xval, d, keys,
-                                       sc->fwd_ctr + fwd_off, train, keep, scale);
+        acc = x_wave_dot_head<true, 2, true>(f, beg, end - beg, xthead + (int64_t)slot * kXtHead, xrow, xval, d,
+                                             keys, sc->fwd_ctr + fwd_off, train, keep, scale, nullptr, nullptr,
+                                             nullptr, jh, jh2);
     } else {
         acc = x_wave_dot_range<true>(beg, end, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
     }
@@ -2232,6 +2293,7 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
             for (int w = 0; w < 16; ++w) acc += part[w][lane];
         }
     }
+    if (LDS_XT_EXPT == 7 && owner) o = adam_load(adam, idx);
     if (owner) {
         const float val = fin_args.accumulate ? prev + acc : acc;
         fin_args.dst[idx] = val;
@@ -2273,10 +2335,10 @@ __global__ __launch_bounds__(1024) void xt_adam_pair_kernel(
     const EngineScalars* __restrict__ sc, FinalArgs fin_args, AdamArgs adam, const int4* __restrict__ xtinfo,
     const int* __restrict__ xthead, Batch bt) {
     const int s0 = 2 * (int)blockIdx.y;
-    const int fb = fin_args.partials != nullptr ? 2 : 0;  // the two final blocks first (as xt_adam_kernel)
+    const int fb = fin_args.partials != nullptr ? 2 * kFinParts : 0;  // the final blocks first (as xt_adam_kernel)
     if ((int)blockIdx.x < fb) {
-        sample_views(fin_args, adam, bt, s0 + (int)blockIdx.x);
-        final_block_1024<16>(fin_args, adam, sc);
+        sample_views(fin_args, adam, bt, s0 + (int)blockIdx.x / kFinParts);
+        final_block_1024<16>(fin_args, adam, sc, (int)blockIdx.x % kFinParts);
         return;
     }
     const int wave = wave_id();
@@ -2284,6 +2346,8 @@ __global__ __launch_bounds__(1024) void xt_adam_pair_kernel(
     const int slot = ((int)blockIdx.x - fb) * 16 + wave;
     if (slot >= fin) return;  // light blocks never reach a barrier
     sample_views(fin_args, adam, bt, s0 + (lane >> 5));
+    float step_size, c2;
+    adam_step_consts(adam, sc, step_size, c2);
     const int4 inf = xtinfo[slot];
     const int f = inf.x;
     const int idx = f * HID + (lane & (HID - 1));
@@ -2294,9 +2358,7 @@ __global__ __launch_bounds__(1024) void xt_adam_pair_kernel(
         o = adam_load(adam, idx);
         if (fin_args.accumulate) prev = fin_args.dst[idx];
     }
-    float step_size, c2;
-    adam_step_consts(adam, sc, step_size, c2);
-    const float acc = x_wave_dot_head_pair(inf.y, inf.z, xthead + (int64_t)slot * 64, xrow,
+    const float acc = x_wave_dot_head_pair(inf.y, inf.z, xthead + (int64_t)slot * kXtHead, xrow,
                                            soff(xval, bt.xval, s0), soff(xval, bt.xval, s0 + 1),
                                            soff(d, bt.act, s0), soff(d, bt.act, s0 + 1));
     if (owner) {
@@ -2836,7 +2898,7 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
                           train == 0;
     LDS_CHECK_ARG(mode != 2 || can_pair);
     if (can_pair && (mode == 2 || (mode == 0 && ns >= kXtPairMinSamples))) {
-        const int pblocks = (fin + 15) / 16 + (partials != nullptr ? 2 : 0);
+        const int pblocks = (fin + 15) / 16 + (partials != nullptr ? 2 * kFinParts : 0);
         hipLaunchKernelGGL(xt_adam_pair_kernel, dim3(pblocks, ns / 2), dim3(1024), 0, (hipStream_t)stream, xrow,
                            xval, fin, d, (const EngineScalars*)scalars, f, a, (const int4*)xtinfo, xthead, bt);
         LDS_RETURN_LAST_ERROR();
@@ -2847,7 +2909,7 @@ extern "C" int lds_engine_xt_adam(const int* xcp, const int* xrow, const float* 
     LDS_CHECK_ARG(n_heavy + n_single == fin || (xthead != nullptr && xt_part == nullptr && train == 0));
     const int n_four = fin - n_heavy - n_single - n_pair;
     const int lwaves = n_single + (n_pair + 1) / 2 + (n_four + 3) / 4;
-    const int blocks = n_heavy + (lwaves + 15) / 16 + (partials != nullptr ? 1 : 0);
+    const int blocks = n_heavy + (lwaves + 15) / 16 + (partials != nullptr ? kFinParts : 0);
     LDS_LAUNCH_B(xt_adam_kernel, ns, dim3(blocks, ns), dim3(1024), 0, (hipStream_t)stream, xcp, xrow, xval, fin,
                        d, mk_keys(seed, tag_x, 0), (const EngineScalars*)scalars, fwd_off, train, keep, scale, f,
                        a, xt_part, xt_splits, order, n_heavy, (const int4*)xtinfo, xthead, n_single, n_pair, bt);

@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL: shared HIP runtime)
 
 LIB_PATH = os.environ.get("LDSGNN_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libldsgnn.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 c_int, c_int64, c_uint32, c_uint64, c_float, c_void_p = (
     ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)

@@ -873,14 +873,16 @@ class LdsEngine:
         p0 = self.xcp[f].long()
         nz = (self.xcp[f + 1] - self.xcp[f]).long()
         self.xtinfo = torch.stack([f, p0, nz, torch.zeros_like(f)], 1).to(torch.int32).contiguous()
-        self.xthead = self._head_of(p0, nz, self.xrow, None)
+        # 128 row indices per slot (ABI 18): a one-wave column needs no index
+        # loads past its head
+        self.xthead = self._head_of(p0, nz, self.xrow, None, width=128)
 
     @staticmethod
-    def _head_of(p0: torch.Tensor, nz: torch.Tensor, idx: torch.Tensor, val):
-        """The first 64 entries of every row of a CSR (row starts p0, lengths
-        nz): indices [rows, 64] int32, or {index, value bits} pairs
-        [rows, 64, 2] when `val` is given; zero past each row's end."""
-        e = torch.arange(64, device=p0.device)
+    def _head_of(p0: torch.Tensor, nz: torch.Tensor, idx: torch.Tensor, val, width: int = 64):
+        """The first `width` entries of every row of a CSR (row starts p0,
+        lengths nz): indices [rows, width] int32, or {index, value bits} pairs
+        [rows, width, 2] when `val` is given; zero past each row's end."""
+        e = torch.arange(width, device=p0.device)
         ok = e[None, :] < nz[:, None]
         pos = torch.where(ok, p0[:, None] + e[None, :], torch.zeros_like(p0)[:, None])
         if idx.numel() == 0:

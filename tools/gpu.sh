@@ -10,6 +10,7 @@
 #   smoke      __graft_entry__.smoke()                      smoke_TAG.log
 #   bench      the default bench line (Cora, S = 1)          bench_TAG.json
 #   prof       rocprofv3 kernel-trace summary of the bench   prof_TAG/
+#   profnb     the same with --no-breakdown (per-window kernel shares)  profnb_TAG/
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the bench   pmc_TAG_{fetch,write}/
 #   pmc5       FETCH_SIZE / WRITE_SIZE passes of the config-5 line pmc5_TAG_{fetch,write}/
 #   config5    synthetic N = 20 000 line + its kernel trace c5_bench_TAG.json, c5_prof_TAG/
@@ -48,6 +49,9 @@ for step in "$@"; do
     prof)
         run 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$tag -o run -- \
             python3 bench.py --no-cpu-baseline --steps 100 > $O/prof_$tag.log 2>&1 || exit $? ;;
+    profnb)  # the same without the window breakdown (its prefix replays inflate the early calls' counts)
+        run 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/profnb_$tag -o run -- \
+            python3 bench.py --no-cpu-baseline --no-breakdown --steps 200 > $O/profnb_$tag.log 2>&1 || exit $? ;;
     pmc)
         for c in FETCH_SIZE WRITE_SIZE; do
             lc=$(echo $c | cut -d_ -f1 | tr 'A-Z' 'a-z')
