@@ -2262,8 +2262,21 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
             end = xcp[f + 1];
         }
     }
-    const int idx = f * HID + (lane & (HID - 1));
-    const bool owner = lane < HID && (!heavy || wave == 0);
+    // A block of sixteen one-column waves completes its columns' Adam steps on
+    // four waves, four columns (64 lanes) each, after one barrier: the Adam
+    // tail (a correctly rounded square root and two or more divisions per
+    // element) then costs each SIMD one wave's issue instead of four, where
+    // every wave used 16 of its 64 lanes.  The same operands and arithmetic.
+    const bool batched = !heavy && xthead != nullptr && xt_part == nullptr && (bx - n_heavy + 1) * 16 <= n_single;
+    int idx = f * HID + (lane & (HID - 1));
+    bool owner = lane < HID && (!heavy || wave == 0);
+    if (batched) {
+        owner = wave < 4;
+        if (owner) {  // column 4·wave + lane / 16 of the block, feature lane % 16
+            const int4 ainf = xtinfo[n_heavy + (bx - n_heavy) * 16 + 4 * wave + (lane >> 4)];
+            idx = ainf.x * HID + (lane & (HID - 1));
+        }
+    }
     // Adam operands and constants first: they overlap the product's loads
     AdamOps o{0.f, 0.f, 0.f, 0.f, 0.f};
     float prev = 0.f;
@@ -2283,8 +2296,8 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
     } else {
         acc = x_wave_dot_range<true>(beg, end, xrow, xval, f, d, keys, sc->fwd_ctr + fwd_off, train, keep, scale);
     }
+    __shared__ float part[16][HID];
     if (heavy) {
-        __shared__ float part[16][HID];
         if (lane < HID) part[wave][lane] = acc;
         __syncthreads();
         if (wave == 0 && lane < HID) {
@@ -2292,6 +2305,10 @@ __global__ __launch_bounds__(1024) void xt_adam_kernel(
 #pragma unroll
             for (int w = 0; w < 16; ++w) acc += part[w][lane];
         }
+    } else if (batched) {  // block-uniform: all sixteen waves have a column
+        if (lane < HID) part[wave][lane] = acc;
+        __syncthreads();
+        if (owner) acc = part[4 * wave + (lane >> 4)][lane & (HID - 1)];
     }
     if (LDS_XT_EXPT == 7 && owner) o = adam_load(adam, idx);
     if (owner) {
