@@ -414,9 +414,10 @@ __device__ __forceinline__ float x_wave_dot_range(int beg, int end, const int* _
 // dependent row-pointer load: entries and the gathers they index are the
 // only round trips up to 64 entries; entries past 64 come from the CSR /
 // CSC arrays as in x_wave_dot_range.
-// kPre (kHead 2): the lane's head index was loaded by the caller (jpre), ahead
-// of the loads that give p0 / nnz.
-template <bool kCsc, int kHead, bool kPre = false>
+// kPre (kHead 2): the lane's head indices (entries e and 64 + e) were loaded by
+// the caller (jpre, jpre2), ahead of the loads that give p0 / nnz; kPreP
+// (kHead 0 / 1): the lane's head pair {index, value bits} likewise (jpre, jpre2).
+template <bool kCsc, int kHead, bool kPre = false, bool kPreP = false>
 __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const int* __restrict__ head,
                                                  const int* __restrict__ idx, const float* __restrict__ val,
                                                  const float* __restrict__ src, const Keys& keys, uint32_t ctr,
@@ -425,6 +426,7 @@ __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const i
                                                  float* __restrict__ xd_perm_out = nullptr,
                                                  const int* __restrict__ perm = nullptr, int jpre = 0, int jpre2 = 0) {
     static_assert(!kPre || kHead == 2, "a preloaded head index is an index-only head");
+    static_assert(!kPreP || kHead != 2, "a preloaded head pair is a pair head");
     const int lane = threadIdx.x & (HID - 1);
     const int q = (threadIdx.x >> 4) & 3;
     float acc = 0.f;
@@ -434,9 +436,12 @@ __device__ __forceinline__ float x_wave_dot_head(int r, int p0, int nnz, const i
         int j;
         float x;
         if constexpr (kHead == 0) {
-            const int2 hv = reinterpret_cast<const int2*>(head)[e];
+            const int2 hv = kPreP ? make_int2(jpre, jpre2) : reinterpret_cast<const int2*>(head)[e];
             j = hv.x;
             x = __int_as_float(hv.y);  // 0 past nnz
+        } else if constexpr (kPreP) {
+            j = jpre;
+            x = v ? val[p0 + e] : 0.f;
         } else {
             j = kPre ? jpre : kHead == 1 ? reinterpret_cast<const int2*>(head)[e].x : head[e];
             x = v ? val[p0 + e] : 0.f;
@@ -624,13 +629,18 @@ __device__ __forceinline__ void x_linear_rows(int bx, int smp,
     const uint32_t ctr = sc->fwd_ctr + fwd_off;
     float acc;
     if (xhead != nullptr) {
+        // the lane's head pair first: it does not wait for the row's info
+        // (a scalar load the compiler waited for before issuing the head's)
+        const int2 hv = reinterpret_cast<const int2*>(xhead + (int64_t)row * 128)[16 * ((threadIdx.x >> 4) & 3) + (threadIdx.x & (HID - 1))];
         const int2 inf = xinfo[row];  // {p0, nnz}
         if (head_vals)  // X's own values from the head (forward)
-            acc = x_wave_dot_head<false, 0>(row, inf.x, inf.y, xhead + (int64_t)row * 128, xcol, xval, wt, keys,
-                                               ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
+            acc = x_wave_dot_head<false, 0, false, true>(row, inf.x, inf.y, xhead + (int64_t)row * 128, xcol, xval,
+                                                         wt, keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc,
+                                                         hv.x, hv.y);
         else            // values from xval (the Xd a training forward stored)
-            acc = x_wave_dot_head<false, 1>(row, inf.x, inf.y, xhead + (int64_t)row * 128, xcol, xval, wt,
-                                                keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
+            acc = x_wave_dot_head<false, 1, false, true>(row, inf.x, inf.y, xhead + (int64_t)row * 128, xcol, xval,
+                                                         wt, keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc,
+                                                         hv.x, hv.y);
     } else {
         acc = x_wave_dot<false>(xrp, xcol, xval, row, wt, keys, ctr, train, keep, scale, xd_csr, xd_csc, csr2csc);
     }

@@ -6,7 +6,8 @@ the product, and timing-only builds of engine.hip with -DLDS_XT_EXPT=k
 (tools/variants/xt/lib_xtk.so): 1 heavy-column blocks exit at once, 2 the
 one-column light waves exit, 3 the two- / four-column light waves exit,
 4 the final-reduction block exits — their results are wrong by construction.
-Usage (GPU box): LDSGNN_LIB=... python tools/microbench/xt_parts.py LABEL"""
+Usage (GPU box): LDSGNN_LIB=... python tools/microbench/xt_parts.py LABEL [ENTRY]
+(ENTRY: another engine entry point of the window, e.g. lds_engine_x_linear)"""
 import json
 import os
 import sys
@@ -21,6 +22,7 @@ import bench  # noqa: E402
 
 def main():
     label = sys.argv[1] if len(sys.argv) > 1 else "product"
+    entry = sys.argv[2] if len(sys.argv) > 2 else "lds_engine_xt_adam"  # any engine entry of the window
     dev = torch.device("cuda:0")
     args = types.SimpleNamespace(dataset="cora", seed=597905255 % (2 ** 31), samples=1, graph_model="lds",
                                  gae_dropout=0.0, tau=5)
@@ -40,10 +42,10 @@ def main():
     finally:
         nat.call = real
     torch.cuda.synchronize()
-    xt = [a for name, a in calls if name == "lds_engine_xt_adam"]
-    us = [min(bench.chain_us(lambda st, a=a: real("lds_engine_xt_adam", *(a[:-1] + (st,))), dev, 20)
+    xt = [a for name, a in calls if name == entry]
+    us = [min(bench.chain_us(lambda st, a=a: real(entry, *(a[:-1] + (st,))), dev, 20)
               for _ in range(3)) for a in xt]
-    print(json.dumps({"lib": label, "calls": len(us), "mean_us": round(sum(us) / len(us), 3),
+    print(json.dumps({"lib": label, "entry": entry, "calls": len(us), "mean_us": round(sum(us) / len(us), 3),
                       "us": [round(u, 3) for u in us]}), flush=True)
 
 
