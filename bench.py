@@ -54,8 +54,8 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (no sparsity)
 INT8_PEAK_TOPS = 5000.0    # dense int8 MFMA: 2x the bf16 rate (MI355X_MICROARCH.md, I8 row)
 METRIC = "inner-loop GCN steps/sec on Cora-sized LDS at 1/2/4/8 MI355X"
 # committed rocprofv3 PMC records (2 x FETCH_SIZE + WRITE_SIZE per launch, separate passes) by workload
-PMC_RECORDS = {"cora-lds-S1-tau5": os.path.join(ROOT, "profiles", "r06_pmc_traffic.json"),
-               "synthetic20k-lds-S1-tau5": os.path.join(ROOT, "profiles", "r06_pmc_traffic_config5.json")}
+PMC_RECORDS = {"cora-lds-S1-tau5": os.path.join(ROOT, "profiles", "r06b_pmc_traffic.json"),
+               "synthetic20k-lds-S1-tau5": os.path.join(ROOT, "profiles", "r06b_pmc_traffic_config5.json")}
 
 
 def world_info():
@@ -881,19 +881,22 @@ def main():
                   "replayed_window_us": wall_win,
                   "entries": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
                               for r in rows]}
-        # the dominant kernel: the largest in-window cost; two within 3 % of
-        # each other (the marginal costs' run-to-run noise: Cora's θ-grad and
-        # the ten xt_adam launches are both ≈17 % of the window) are ranked by
-        # their isolated time per window (chain average × launches, the
-        # rocprof figure) instead, so the pick does not flip between runs
+        # the dominant kernel: the largest in-window cost; two within 10 % of
+        # each other are ranked by their isolated time per window (chain
+        # average × launches) instead, so the pick does not flip between runs.
+        # The in-window marginal costs are the noisier measure: on the same
+        # code two boxes gave Cora's θ-grad / ten xt_adam launches 53.5 / 46.7
+        # and 49.0 / 52.5 µs, while their chain averages agreed within 2 %
+        # (51.9 / 45.5 µs per window) and rocprof put the two within 1 % of each
+        # other (profiles/r06b_kernel_stats.csv)
         top = rows[0]
-        if len(rows) > 1 and rows[1]["us_per_window"] >= 0.97 * top["us_per_window"]:
+        if len(rows) > 1 and rows[1]["us_per_window"] >= 0.90 * top["us_per_window"]:
             per_win = lambda r: r["chain_avg_us"] * r["launches_per_window"]  # noqa: E731
             if per_win(rows[1]) > per_win(top):
                 top = rows[1]
         roof = roofline_of(top, args)
         roof["share_of_window"] = top["us_per_window"] / total if total else None
-        roof["selected_by"] = ("largest in-window cost per window; within 3 % of the next, the larger isolated "
+        roof["selected_by"] = ("largest in-window cost per window; within 10 % of the next, the larger isolated "
                                "(chain) time per window")
         theta_rows = [r for r in rows if r["bound"] == "mfma"]
         if theta_rows:
