@@ -5,7 +5,11 @@ tools/microbench/xt_final.py does) and every xt_adam call is chain-timed
 the product, and timing-only builds of engine.hip with -DLDS_XT_EXPT=k
 (tools/variants/xt/lib_xtk.so): 1 heavy-column blocks exit at once, 2 the
 one-column light waves exit, 3 the two- / four-column light waves exit,
-4 the final-reduction block exits — their results are wrong by construction.
+4 the final-reduction blocks exit, 5 every block exits at entry (the grid's
+launch floor), 6 no Adam (mode 0), 7 the Adam operands loaded after the
+product, 8 no m / v / g' stores, 9 no Adam operand loads, 10 the operands
+loaded but no update computed or stored — their results are wrong by
+construction (profiles/r06_xt_parts.jsonl).
 Usage (GPU box): LDSGNN_LIB=... python tools/microbench/xt_parts.py LABEL [ENTRY]
 (ENTRY: another engine entry point of the window, e.g. lds_engine_x_linear)"""
 import json
