@@ -123,9 +123,13 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
     const int nbw = (n + 63) / 64;
     const bool live = row < n;
     const uint64_t* rb_bits = bits + (int64_t)row * words;
-    // the row's own operands first (independent of the block prefix)
+    // the row's own operands first (independent of the block prefix): its
+    // degree and its first 64 bit words (four per lane), so that rows of up
+    // to 4 096 columns walk their words without a load per 16-word step
     const int deg = live ? dacc[row] : 0;
-    const uint64_t word0 = (live && h < nbw) ? rb_bits[h] : 0ull;
+    uint64_t wpre[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wpre[q] = (live && 16 * q + h < nbw) ? rb_bits[16 * q + h] : 0ull;
     // head entries past the row's drawn count read as the row itself: a degree
     // workspace that was not zero on entry (deg above the bits' count) then
     // yields wrong weights, never an index outside the graph
@@ -135,17 +139,18 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
         const int d = row0 + lane < n ? dacc[row0 + lane] : 0;
         dblk[lane] = row16_incl_scan_int(d) - d;
     }
-    // degrees of the rows before the block: 8 independent loads per thread per round
+    // degrees of the rows before the block: 16 independent loads per thread
+    // per round (one round up to 4 096 rows)
     int acc = 0;
-    for (int r0b = 0; r0b < row0; r0b += 8 * 256) {
-        int v[8];
+    for (int r0b = 0; r0b < row0; r0b += 16 * 256) {
+        int v[16];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < 16; ++q) {
             const int r = r0b + q * 256 + (int)threadIdx.x;
             v[q] = r < row0 ? dacc[r] : 0;
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc += v[q];
+        for (int q = 0; q < 16; ++q) acc += v[q];
     }
     acc = wave_sum_int(acc);
     if (lane == 0) red[wave] = acc;
@@ -160,9 +165,8 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
     if (__ballot(live && deg >= kDenseRowFill) == 0) {
         int64_t base = pre;
         const int64_t lim = min(capacity, (int64_t)pre + deg);  // this row's slots only
-        for (int w0 = 0; w0 < nbw; w0 += 16) {  // uniform: every group walks the same word count
+        auto step = [&](int w0, uint64_t word) {  // 16 words of the row, one per lane
             const int w = w0 + h;
-            uint64_t word = w0 == 0 ? word0 : ((live && w < nbw) ? rb_bits[w] : 0ull);
             const int cnt = __popcll(word);
             const int incl = row16_incl_scan_int(cnt);
             int64_t pos = base + (incl - cnt);
@@ -175,7 +179,12 @@ __device__ __forceinline__ void fill_csr_block(int bx, int by, const uint64_t* _
                 word &= word - 1;
             }
             base += row16_last_int(incl);
-        }
+        };
+        // uniform: every group walks the same word count
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (16 * q < nbw) step(16 * q, wpre[q]);
+        for (int w0 = 64; w0 < nbw; w0 += 16) step(w0, (live && w0 + h < nbw) ? rb_bits[w0 + h] : 0ull);
         if (live) fill_degree_guard(pre, base - pre, deg, row, col, capacity, h, 16, err);
     } else {
 #pragma unroll 1
