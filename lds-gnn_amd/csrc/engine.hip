@@ -2043,10 +2043,11 @@ __device__ __forceinline__ void final_pair(const FinalArgs& f, int e0, int e1, c
 // xt_adam at 40 VGPRs instead of 86 (two 1024-thread blocks per CU, not one).
 //
 // The final stage runs as kFinParts such blocks, part p completing elements
-// [p·kFinPer, (p + 1)·kFinPer): the same sums per element, a quarter of the
+// [p·kFinPer, (p + 1)·kFinPer): the same sums per element, an eighth of the
 // 63-partial loads per block (one block issued ≈900 wave loads of 256 B, a
-// TA-bound ≈1.4 µs on one CU).
-constexpr int kFinParts = 4;
+// TA-bound ≈1.4 µs on one CU; 4 parts 4.57, 8 parts 4.50, 16 parts 4.55-4.59
+// µs per xt_adam launch).
+constexpr int kFinParts = 8;
 constexpr int kFinPer = (kRedLen + kFinParts - 1) / kFinParts;
 template <int kBatch>
 __device__ __forceinline__ void final_block_1024(const FinalArgs& f, const AdamArgs& adam,
