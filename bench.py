@@ -881,23 +881,18 @@ def main():
                   "replayed_window_us": wall_win,
                   "entries": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
                               for r in rows]}
-        # the dominant kernel: the largest in-window cost; two within 10 % of
-        # each other are ranked by their isolated time per window (chain
-        # average × launches) instead, so the pick does not flip between runs.
-        # The in-window marginal costs are the noisier measure: on the same
-        # code two boxes gave Cora's θ-grad / ten xt_adam launches 53.5 / 46.7
-        # and 49.0 / 52.5 µs, while their chain averages agreed within 2 %
-        # (51.9 / 45.5 µs per window) and rocprof put the two within 1 % of each
-        # other (profiles/r06b_kernel_stats.csv)
-        top = rows[0]
-        if len(rows) > 1 and rows[1]["us_per_window"] >= 0.90 * top["us_per_window"]:
-            per_win = lambda r: r["chain_avg_us"] * r["launches_per_window"]  # noqa: E731
-            if per_win(rows[1]) > per_win(top):
-                top = rows[1]
+        # the dominant kernel: the largest isolated time per window (the
+        # call's chain average × its launches per window: the same per-launch
+        # time the roofline entry divides by).  The in-window marginal costs
+        # rank the window's entries but are too noisy to pick one: on the same
+        # code, runs on different boxes gave the ten xt_adam launches 46.7-55.3
+        # µs against the θ-grad's 49.0-53.5, while the chain averages held
+        # within 2 % (≈45 against ≈51 µs per window)
+        per_win = lambda r: r["chain_avg_us"] * r["launches_per_window"]  # noqa: E731
+        top = max(rows, key=per_win)
         roof = roofline_of(top, args)
         roof["share_of_window"] = top["us_per_window"] / total if total else None
-        roof["selected_by"] = ("largest in-window cost per window; within 10 % of the next, the larger isolated "
-                               "(chain) time per window")
+        roof["selected_by"] = "largest isolated time per window (chain average x launches per window)"
         theta_rows = [r for r in rows if r["bound"] == "mfma"]
         if theta_rows:
             window["theta_grad"] = roofline_of(theta_rows[0], args)
