@@ -187,3 +187,29 @@ def test_register_ring_kernels_have_no_scratch(tmp_path):
     assert len(ring) == 6, sorted(ring)  # 2 / 4 / 6 tiles × checked / unchecked
     for k, (private, spills) in ring.items():
         assert private == 0 and spills == 0, (k, private, spills)
+
+
+def test_abi_version_matches_the_header():
+    import ldsgnn._native as nat
+    src = open(os.path.join(ROOT, "include", "ldsgnn.h")).read()
+    m = re.search(r"#define LDS_ABI_VERSION (\d+)", src)
+    assert m and int(m.group(1)) == nat.ABI_VERSION == nat.lib.lds_abi_version()
+
+
+def test_xt_column_heads_are_128_wide():
+    """ABI 18: lds_engine_xt_adam's `xthead` holds the first 128 row indices of
+    every plan slot, zero past the column's end (the host builds it with
+    LdsEngine._head_of); a one-wave column (<= 128 entries) then needs no index
+    loads past its head."""
+    import torch
+    from ldsgnn.engine import LdsEngine
+    g = torch.Generator().manual_seed(3)
+    lens = torch.tensor([0, 1, 17, 64, 65, 128, 129, 300])
+    p0 = torch.cat([torch.zeros(1, dtype=torch.long), lens.cumsum(0)[:-1]])
+    rows = torch.randint(0, 5000, (int(lens.sum()),), generator=g, dtype=torch.int32)
+    head = LdsEngine._head_of(p0, lens, rows, None, width=128)
+    assert head.shape == (len(lens), 128) and head.dtype == torch.int32
+    for c in range(len(lens)):
+        k = min(int(lens[c]), 128)
+        assert torch.equal(head[c, :k], rows[int(p0[c]):int(p0[c]) + k])
+        assert int(head[c, k:].abs().sum()) == 0
